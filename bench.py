@@ -1,0 +1,154 @@
+"""Flagship benchmark: epochs/sec of the 3-phase GAN (BASELINE.json config 2/3).
+
+Config: real-sized synthetic panel, T = 600 months split 240 / 60 / 300 (train / valid / test,
+the paper's split), N = 3000 stocks, F = 46 characteristics, M = 178 macro series; the paper
+architecture (LSTM [4] macro encoder, SDF FFN [64, 64], 8 tanh moments, dropout 0.05),
+random init, bf16 tower GEMMs with fp32 accumulation / master weights / losses.
+
+One timed "step" = one training epoch of the 3-phase schedule, drawn in the reference's
+256 : 64 : 1024 proportion (phase 1 and 3 epochs include the valid + test evaluation, as in
+`/root/reference/src/train.py:238-394`). Each rank (one per GPU) trains ``--models-per-gpu``
+independently seeded models (ensemble members) batched through the native engine; the
+reported value is the whole-job aggregate model-epochs per second (weak scaling: fixed work
+per GPU). Usage:
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+BENCH = dict(T_train=240, T_valid=60, T_test=300, N=3000, F=46, M=178)
+# reference CPU epochs/sec on this exact config and schedule mix (tools/ref_baseline.py,
+# 8-core Xeon, torch 2.10 CPU; see BASELINE.md "Measured on this box")
+REF_EPOCHS_PER_S = float(os.environ.get("DLAP_REF_EPOCHS_PER_S", "0.2488"))
+
+
+def make_panel(seed: int = 0, device: str = "cpu", T=None, N=None, F=None, M=None):
+    """Synthetic real-sized panel split 240/60/300 with the reference's macro standardisation."""
+    from deeplearninginassetpricing_paperreplication_amd.data.synthetic import generate_panel_fast
+    Tt, Tv, Te = BENCH["T_train"], BENCH["T_valid"], BENCH["T_test"]
+    T = T or Tt + Tv + Te
+    N, F, M = N or BENCH["N"], F or BENCH["F"], M or BENCH["M"]
+    ret, feats, mask, mac = generate_panel_fast(T, N, F, M, seed=seed, device=device)
+    ret, feats, mask, mac = ret.cpu(), feats.cpu(), mask.cpu(), mac.cpu()
+    mu = mac[:Tt].mean(0, keepdim=True)
+    sd = mac[:Tt].std(0, unbiased=False, keepdim=True) + 1e-8
+    mac = (mac - mu) / sd
+    cuts = [(0, Tt), (Tt, Tt + Tv), (Tt + Tv, T)]
+    return tuple({"returns": ret[a:b].contiguous(), "individual_features": feats[a:b].contiguous(),
+                  "mask": mask[a:b].contiguous(), "macro_features": mac[a:b].contiguous()} for a, b in cuts)
+
+
+def schedule_split(k: int):
+    """Split k epochs into the 256:64:1024 phase proportion (each >= 1 when k >= 3)."""
+    n1 = max(1, round(k * 256 / 1344))
+    n2 = max(1, round(k * 64 / 1344))
+    n3 = max(1, k - n1 - n2)
+    return n1, n2, n3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=210)
+    ap.add_argument("--warmup", type=int, default=21)
+    ap.add_argument("--models-per-gpu", type=int, default=1)
+    ap.add_argument("--no-graph", action="store_true")
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    torch.cuda.set_device(local)
+    if dist:
+        import torch.distributed as tdist
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from deeplearninginassetpricing_paperreplication_amd.config import default_cli_config
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import GANEngine
+    from deeplearninginassetpricing_paperreplication_amd.models.gan import AssetPricingGAN
+
+    tr, va, te = make_panel(seed=0, device=f"cuda:{local}")
+    cfg = default_cli_config(BENCH["M"], BENCH["F"])
+    G = a.models_per_gpu
+    n1, n2, n3 = schedule_split(a.steps)
+    w1, w2, w3 = schedule_split(max(a.warmup, 3))
+    eng = GANEngine(AssetPricingGAN(cfg).spec, n_models=G, max_epochs=n1 + n2 + n3 + w1 + w2 + w3 + 8)
+    eng.set_data(tr, va, te)
+    for g in range(G):
+        seed = 1000 * rank + g
+        torch.manual_seed(seed)
+        eng.set_model(g, AssetPricingGAN(cfg), seed)
+    use_graph = not a.no_graph
+
+    def run(k1, k2, k3):
+        for ph, k in ((1, k1), (2, k2), (3, k3)):
+            if k:
+                eng.eng.begin_phase(ph)
+                eng.run(ph, k, 1e-3, 64, 1.0, use_graph)
+
+    run(w1, w2, w3)                       # warmup (also captures the three phase graphs)
+    eng.eng.sync()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    t0 = time.perf_counter()
+    phase_t = []
+    for ph, k in ((1, n1), (2, n2), (3, n3)):
+        tp = time.perf_counter()
+        eng.eng.begin_phase(ph)
+        eng.run(ph, k, 1e-3, 64, 1.0, use_graph)
+        eng.eng.sync()
+        phase_t.append((time.perf_counter() - tp) / k)
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    dt = time.perf_counter() - t0
+    hist = eng.history_rows(0)
+    finite = bool(np.isfinite(hist[:, 1]).all())
+    K = n1 + n2 + n3
+    if dist:
+        t = torch.tensor([dt], device="cuda")
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms_per_step = dt / K * 1e3
+    value = world * G * K / dt
+    # time for one model's full 256/64/1024 schedule at the measured per-phase rates
+    full_s = 256 * phase_t[0] + 64 * phase_t[1] + 1024 * phase_t[2]
+    if rank == 0:
+        out = {
+            "metric": "epochs/sec (3-phase GAN)",
+            "value": round(value, 3), "unit": "model-epochs/s", "n_gpus": world, "steps": K,
+            "warmup": a.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": round(value / REF_EPOCHS_PER_S, 1) if REF_EPOCHS_PER_S else None,
+            "dtype": "bf16", "data": "synthetic (factor-model panel, random-init weights)",
+            "config": {"model": "Chen-Pelger-Zhu GAN: LSTM[4] + SDF FFN[64,64] + 8 tanh moments",
+                       "global_batch": world * G, "seq_len": BENCH["T_train"],
+                       "panel": f"T={BENCH['T_train']}/{BENCH['T_valid']}/{BENCH['T_test']} "
+                                f"N={BENCH['N']} F={BENCH['F']} M={BENCH['M']}",
+                       "models_per_gpu": G, "parallelism": f"ensemble-dp{world}",
+                       "schedule_mix": [n1, n2, n3]},
+            "ms_per_epoch_phase": [round(x * 1e3 / G * G, 4) for x in phase_t],
+            "full_schedule_s_per_model_batch": round(full_s, 3),
+            "hipgraph": use_graph, "finite": finite,
+        }
+        print(json.dumps(out))
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,109 @@
+// Shared device helpers for the DLAP CDNA4 (gfx950) kernels.
+//
+// Conventions used by every kernel in this directory
+//  * wave64: lane = threadIdx.x & 63; cross-lane reductions use __shfl_xor over 64 lanes.
+//  * MFMA tile = v_mfma_f32_16x16x32_bf16. Operand maps (gfx950, see
+//    /opt/skills/guides/cdna_hip_programming.md §3):
+//       A (16x32):  lane l holds A[m = l&15][k = 8*(l>>4) + j],  j = 0..7
+//       B (32x16):  lane l holds B[k = 8*(l>>4) + j][n = l&15]
+//       C (16x16):  lane l holds C[m = 4*(l>>4) + r][n = l&15],  r = 0..3
+//    The A and B maps are mirror images, so swapping the two operand registers of one
+//    MFMA yields C^T. The MLP kernels exploit this (see k_mlp.hip).
+//  * All reductions are fixed-order (no float atomics): results are bitwise reproducible.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+
+#define DLAP_DEV __device__ __forceinline__
+#define DLAP_MAXL 6   // max MFMA layers per tower
+
+#define HIP_OK(expr)                                                                        \
+  do {                                                                                      \
+    hipError_t _e = (expr);                                                                 \
+    if (_e != hipSuccess) dlap_throw_hip(_e, #expr, __FILE__, __LINE__);                    \
+  } while (0)
+
+void dlap_throw_hip(hipError_t e, const char* what, const char* file, int line);
+
+DLAP_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+DLAP_DEV f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
+
+DLAP_DEV __bf16 to_bf16(float x) { return (__bf16)x; }
+
+// Pack two C-layout blocks (4 floats each) into one 8-element operand fragment.
+DLAP_DEV bf16x8 pack8(const f32x4& lo, const f32x4& hi) {
+  bf16x8 r;
+  r[0] = (__bf16)lo[0]; r[1] = (__bf16)lo[1]; r[2] = (__bf16)lo[2]; r[3] = (__bf16)lo[3];
+  r[4] = (__bf16)hi[0]; r[5] = (__bf16)hi[1]; r[6] = (__bf16)hi[2]; r[7] = (__bf16)hi[3];
+  return r;
+}
+
+DLAP_DEV bf16x8 zero8() {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (__bf16)0.f;
+  return r;
+}
+
+// ---- counter-based RNG for dropout (murmur3 finaliser on a mixed counter) -------------
+DLAP_DEV uint32_t fmix32(uint32_t h) {
+  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+  return h;
+}
+__host__ __device__ inline uint32_t fmix32_h(uint32_t h) {
+  h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;
+  return h;
+}
+// Stream key for (model seed, optimisation step, layer).
+DLAP_DEV uint32_t dropout_key(uint32_t seed, uint32_t step, uint32_t layer) {
+  return fmix32(seed * 0x9E3779B1u ^ fmix32(step * 0x632BE59Bu + layer * 0x1B873593u + 0x5bd1e995u));
+}
+// keep(row, unit): independent Bernoulli(1-p) per (dense row, unit) for a given key.
+// thr = round(p * 2^24); keep iff top 24 bits of the hash >= thr.
+DLAP_DEV bool dropout_keep(uint32_t key, uint32_t row, uint32_t unit, uint32_t thr) {
+  uint32_t h = fmix32(key ^ (row * 0xcc9e2d51u) ^ (unit * 0x27d4eb2fu) ^ (row >> 16));
+  return (h >> 8) >= thr;
+}
+
+// ---- wave / block reductions (fixed order) --------------------------------------------
+DLAP_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+DLAP_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+DLAP_DEV float wave_min(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Block-wide sum for blockDim.x == NT (multiple of 64). `red` needs NT/64 floats.
+template <int NT>
+DLAP_DEV float block_sum(float v, float* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) s += red[i];
+  return s;
+}
+
+DLAP_DEV float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
+DLAP_DEV float tanhf_(float x) { return tanhf(x); }
+
+DLAP_DEV int ceil_div(int a, int b) { return (a + b - 1) / b; }

@@ -1,0 +1,741 @@
+// DLAP native engine: device-resident 3-phase GAN training / evaluation for G models at once.
+//
+// This is the MI355X runtime behind `train_3phase` on a GPU (the reference runs the same
+// schedule eagerly on the CPU, `/root/reference/src/train.py:156-426`):
+//   * the panel of every split lives in HBM for the whole run, compacted to valid rows
+//     (bf16 [R][KP] features + int32 dense index), with dense [T*N] fp32 returns/mask;
+//   * G models (ensemble members / sweep configs of one architecture) are batched into the
+//     same launches (grid.y = job), so a 9-seed ensemble costs the launches of one model;
+//   * an epoch is a fixed launch plan (prologue -> towers -> loss passes -> tower backward ->
+//     finalize -> update -> evaluation -> bookkeeping) that reads every step-varying value
+//     from device counters, so it is captured ONCE per phase into a hipGraph and replayed;
+//   * history, best-epoch tracking and checkpoint snapshots are device-side: the host only
+//     synchronises at print intervals / phase boundaries.
+#include <hip/hip_runtime.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "layout.h"
+#include "loss.h"
+#include "mlp.h"
+#include "rnn.h"
+#include "update.h"
+
+namespace py = pybind11;
+
+void dlap_throw_hip(hipError_t e, const char* what, const char* file, int line) {
+  throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e) + " at " + file + ":" +
+                           std::to_string(line) + " (" + what + ")");
+}
+
+namespace {
+
+template <typename T>
+struct DevBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  void alloc(size_t count, bool zero = true) {
+    free();
+    n = count;
+    if (count == 0) return;
+    HIP_OK(hipMalloc(&p, count * sizeof(T)));
+    if (zero) HIP_OK(hipMemset(p, 0, count * sizeof(T)));
+  }
+  void free() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  ~DevBuf() { free(); }
+};
+
+struct SplitDev {
+  int T = 0, N = 0, R = 0;
+  float Nbar = 0.f;
+  DevBuf<uint16_t> X;
+  DevBuf<int> row_dense, row_ptr;
+  DevBuf<float> Rm, mask, invNt, Nt, meanR, RR, invT, macro;
+  bool set = false;
+};
+
+struct ModelSplitWS {   // per (model, split)
+  DevBuf<float> pp, abias, xg, xin, sg, sc, sh;
+  DevBuf<float> w, wn, h, P, port, sdf, E, Eu, dE, dEu, part, dw, rstat, scal;
+  DevBuf<float> u, v, dpp, dab, dg, dx;
+};
+
+struct ModelState {
+  DevBuf<float> params, grads, m, v, snap_loss, snap_sharpe, gnorm, best, aux, hist;
+  DevBuf<int> adam_step, drop_step, snap_flags, ep;
+  DevBuf<uint16_t> blob;
+  unsigned seed = 0;
+};
+
+}  // namespace
+
+class Engine {
+ public:
+  Engine(int F, int M, int nrnn, int H, bool raw_macro_sdf, std::vector<int> hidden,
+         std::vector<int> mom_hidden, int K, float dropout, bool normalize_w, bool weighted,
+         float residual, int G, int max_epochs)
+      : G_(G), max_epochs_(max_epochs) {
+    HIP_OK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
+               residual);
+    d_desc_.alloc(sizeof(ModelDesc));
+    HIP_OK(hipMemcpy(d_desc_.p, &md_, sizeof(ModelDesc), hipMemcpyHostToDevice));
+    models_.resize(G);
+    for (int g = 0; g < G; ++g) {
+      ModelState& S = models_[g];
+      S.params.alloc(md_.P); S.grads.alloc(md_.P); S.m.alloc(md_.P); S.v.alloc(md_.P);
+      S.snap_loss.alloc(md_.P); S.snap_sharpe.alloc(md_.P);
+      S.gnorm.alloc(1); S.best.alloc(3); S.aux.alloc(md_.md.aux_floats);
+      S.hist.alloc((size_t)max_epochs_ * HIST_W);
+      S.adam_step.alloc(2); S.drop_step.alloc(1); S.snap_flags.alloc(2); S.ep.alloc(2);
+      S.blob.alloc((size_t)md_.md.blob_frags * 512);
+    }
+    ws_.resize((size_t)G * 3);
+  }
+  ~Engine() {
+    for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
+    if (st_) (void)hipStreamDestroy(st_);
+  }
+
+  // ---------------------------------------------------------------- description ----------
+  py::dict describe() const {
+    py::dict d;
+    d["P"] = md_.P; d["P_sdf"] = md_.P_sdf; d["KP"] = md_.KP; d["KS1"] = md_.KS1; d["WMB"] = md_.WMB;
+    d["Dm"] = md_.Dm; d["blob_frags"] = md_.md.blob_frags; d["aux_floats"] = md_.md.aux_floats;
+    d["ntile_s"] = md_.ntile_s; d["ntile_m"] = md_.ntile_m; d["G"] = G_;
+    return d;
+  }
+
+  // ---------------------------------------------------------------- data -----------------
+  void set_split(int s, py::array_t<uint16_t, py::array::c_style> X, py::array_t<int, py::array::c_style> row_dense,
+                 py::array_t<int, py::array::c_style> row_ptr, py::array_t<float, py::array::c_style> Rm,
+                 py::array_t<float, py::array::c_style> mask, py::array_t<float, py::array::c_style> macro,
+                 int T, int N) {
+    if (s < 0 || s > 2) throw std::invalid_argument("split must be 0, 1 or 2");
+    if (T > DLAP_MAX_T) throw std::invalid_argument("T exceeds DLAP_MAX_T");
+    SplitDev& D = splits_[s];
+    const int R = (int)row_dense.size();
+    if ((long)X.size() != (long)R * md_.KP) throw std::invalid_argument("X must be [R][KP] bf16 bits");
+    if ((long)Rm.size() != (long)T * N || (long)mask.size() != (long)T * N) throw std::invalid_argument("Rm/mask must be [T*N]");
+    if ((int)row_ptr.size() != T + 1) throw std::invalid_argument("row_ptr must be [T+1]");
+    if (md_.M > 0 && (long)macro.size() != (long)T * md_.M) throw std::invalid_argument("macro must be [T][M]");
+    D.T = T; D.N = N; D.R = R;
+    up(D.X, X.data(), X.size());
+    up(D.row_dense, row_dense.data(), R);
+    up(D.row_ptr, row_ptr.data(), T + 1);
+    up(D.Rm, Rm.data(), (size_t)T * N);
+    up(D.mask, mask.data(), (size_t)T * N);
+    if (md_.M > 0) up(D.macro, macro.data(), (size_t)T * md_.M);
+    // per-period / per-asset constants (host, double accumulation)
+    std::vector<float> nt(T), inv_nt(T), meanr(T), rr(T), invt(N);
+    std::vector<double> ti(N, 0.0);
+    const float* r = Rm.data();
+    const float* mk = mask.data();
+    double nbar = 0;
+    for (int t = 0; t < T; ++t) {
+      double n = 0, sr = 0, s2 = 0;
+      for (int i = 0; i < N; ++i) {
+        const float m = mk[(size_t)t * N + i];
+        n += m; sr += (double)r[(size_t)t * N + i] * m; s2 += (double)r[(size_t)t * N + i] * r[(size_t)t * N + i] * m;
+        ti[i] += m;
+      }
+      nt[t] = (float)n;
+      const double nc = n < 1 ? 1 : n;
+      inv_nt[t] = (float)(1.0 / nc);
+      meanr[t] = (float)(sr / nc);
+      rr[t] = (float)s2;
+      nbar += nc;
+    }
+    for (int i = 0; i < N; ++i) invt[i] = (float)(1.0 / (ti[i] < 1 ? 1 : ti[i]));
+    // N̄ = mean_t max(N_t, 1) in fp32 like torch's .mean()
+    float nb = 0.f;
+    {
+      double acc = 0;
+      for (int t = 0; t < T; ++t) acc += (nt[t] < 1.f ? 1.f : nt[t]);
+      nb = (float)(acc / T);
+    }
+    (void)nbar;
+    D.Nbar = nb;
+    up(D.Nt, nt.data(), T); up(D.invNt, inv_nt.data(), T); up(D.meanR, meanr.data(), T);
+    up(D.RR, rr.data(), T); up(D.invT, invt.data(), N);
+    D.set = true;
+    alloc_ws(s);
+    graphs_dirty_ = true;
+  }
+
+  // ---------------------------------------------------------------- parameters ----------
+  void set_params(int g, py::array_t<float, py::array::c_style> p) {
+    check_g(g);
+    if ((int)p.size() != md_.P) throw std::invalid_argument("params size mismatch");
+    HIP_OK(hipMemcpyAsync(models_[g].params.p, p.data(), md_.P * sizeof(float), hipMemcpyHostToDevice, st_));
+    pack(g);
+    sync();
+  }
+  py::array_t<float> get_params(int g) { return down(models_[check_g(g)].params); }
+  py::array_t<float> get_grads(int g) { return down(models_[check_g(g)].grads); }
+  py::array_t<float> get_snapshot(int g, int which) {
+    ModelState& S = models_[check_g(g)];
+    return down(which == 0 ? S.snap_loss : S.snap_sharpe);
+  }
+  void load_snapshot(int g, int which) {
+    ModelState& S = models_[check_g(g)];
+    HIP_OK(hipMemcpyAsync(S.params.p, (which == 0 ? S.snap_loss : S.snap_sharpe).p, md_.P * sizeof(float),
+                          hipMemcpyDeviceToDevice, st_));
+    pack(g);
+    sync();
+  }
+  void set_seed(int g, unsigned seed) { models_[check_g(g)].seed = seed; graphs_dirty_ = true; }
+  py::dict get_opt_state(int g) {
+    ModelState& S = models_[check_g(g)];
+    py::dict d;
+    d["m"] = down(S.m); d["v"] = down(S.v);
+    int hs[2], ds[1];
+    HIP_OK(hipMemcpy(hs, S.adam_step.p, sizeof(hs), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(ds, S.drop_step.p, sizeof(ds), hipMemcpyDeviceToHost));
+    d["step_sdf"] = hs[0]; d["step_moment"] = hs[1]; d["drop_step"] = ds[0];
+    return d;
+  }
+  void set_opt_state(int g, py::array_t<float, py::array::c_style> m, py::array_t<float, py::array::c_style> v,
+                     int step_sdf, int step_mom, int drop_step) {
+    ModelState& S = models_[check_g(g)];
+    HIP_OK(hipMemcpy(S.m.p, m.data(), md_.P * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(S.v.p, v.data(), md_.P * 4, hipMemcpyHostToDevice));
+    int hs[2] = {step_sdf, step_mom};
+    HIP_OK(hipMemcpy(S.adam_step.p, hs, sizeof(hs), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(S.drop_step.p, &drop_step, sizeof(int), hipMemcpyHostToDevice));
+  }
+
+  // ---------------------------------------------------------------- phase control -------
+  // Reset the per-phase trackers (reference: fresh best values per phase).
+  void begin_phase(int phase) {
+    for (int g = 0; g < G_; ++g) {
+      ModelState& S = models_[g];
+      const float inf = INFINITY;
+      float best[3] = {inf, -inf, -inf};
+      HIP_OK(hipMemcpyAsync(S.best.p, best, sizeof(best), hipMemcpyHostToDevice, st_));
+      HIP_OK(hipMemsetAsync(S.snap_flags.p, 0, 2 * sizeof(int), st_));
+      int ep[2];
+      HIP_OK(hipMemcpy(ep, S.ep.p, sizeof(ep), hipMemcpyDeviceToHost));
+      ep[1] = 0;
+      HIP_OK(hipMemcpy(S.ep.p, ep, sizeof(ep), hipMemcpyHostToDevice));
+    }
+    sync();
+    (void)phase;
+  }
+  py::array_t<int> snap_flags(int g) {
+    ModelState& S = models_[check_g(g)];
+    py::array_t<int> out(2);
+    HIP_OK(hipMemcpy(out.mutable_data(), S.snap_flags.p, 2 * sizeof(int), hipMemcpyDeviceToHost));
+    return out;
+  }
+  int epoch_count(int g) {
+    int ep[2];
+    HIP_OK(hipMemcpy(ep, models_[check_g(g)].ep.p, sizeof(ep), hipMemcpyDeviceToHost));
+    return ep[0];
+  }
+  py::array_t<float> history(int g) {
+    const int n = epoch_count(g);
+    py::array_t<float> out({n, (int)HIST_W});
+    if (n) HIP_OK(hipMemcpy(out.mutable_data(), models_[g].hist.p, (size_t)n * HIST_W * 4, hipMemcpyDeviceToHost));
+    return out;
+  }
+
+  // ---------------------------------------------------------------- execution -----------
+  // One epoch of `phase` (1, 2, 3): train step (+ valid/test evaluation in phases 1/3) and
+  // the device bookkeeping. `n` epochs are run by replaying the phase graph.
+  void run_epochs(int phase, int n, float lr, int ignore_epoch, float sel, bool use_graph) {
+    if (!splits_[0].set) throw std::runtime_error("train split not set");
+    if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
+    auto key = graph_key(phase, lr, ignore_epoch, sel);
+    if (!use_graph) {
+      for (int e = 0; e < n; ++e) enqueue_epoch(phase, lr, ignore_epoch, sel);
+      return;
+    }
+    auto it = graphs_.find(key);
+    if (it == graphs_.end()) {
+      hipGraph_t graph;
+      HIP_OK(hipStreamBeginCapture(st_, hipStreamCaptureModeThreadLocal));
+      enqueue_epoch(phase, lr, ignore_epoch, sel);
+      HIP_OK(hipStreamEndCapture(st_, &graph));
+      hipGraphExec_t exec;
+      HIP_OK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+      HIP_OK(hipGraphDestroy(graph));
+      it = graphs_.emplace(key, exec).first;
+    }
+    for (int e = 0; e < n; ++e) HIP_OK(hipGraphLaunch(it->second, st_));
+  }
+
+  // Pieces used by the module-level API / tests (no bookkeeping).
+  void forward_split(int s, bool train_mode, bool do_mom) {
+    if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
+    fwd_only(s, train_mode, do_mom);
+  }
+  void train_step(int phase, float lr) {
+    if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
+    enqueue_train(phase, lr);
+  }
+  void backward_only(int phase) {   // losses + gradients, no optimiser step
+    if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
+    enqueue_train_grads(phase);
+    launch_update(as<UpdJob>(j_upd_), G_, dd(), phase, 0.f, st_, 0);
+    sync();
+  }
+
+  py::array_t<float> read_ws(int g, int s, const std::string& name) {
+    ModelSplitWS& W = ws(g, s);
+    const std::map<std::string, DevBuf<float>*> m = {
+        {"pp", &W.pp}, {"abias", &W.abias}, {"w", &W.w}, {"wn", &W.wn}, {"h", &W.h}, {"P", &W.P},
+        {"port", &W.port}, {"sdf", &W.sdf}, {"E", &W.E}, {"Eu", &W.Eu}, {"dE", &W.dE}, {"dEu", &W.dEu},
+        {"dw", &W.dw}, {"scal", &W.scal}, {"u", &W.u}, {"v", &W.v}, {"dpp", &W.dpp}, {"dab", &W.dab},
+        {"sg", &W.sg}, {"sc", &W.sc}, {"sh", &W.sh}};
+    auto it = m.find(name);
+    if (it == m.end()) throw std::invalid_argument("unknown workspace buffer " + name);
+    sync();
+    return down(*it->second);
+  }
+  py::array_t<float> read_aux(int g) { sync(); return down(models_[check_g(g)].aux); }
+  py::array_t<uint16_t> read_blob(int g) {
+    sync();
+    ModelState& S = models_[check_g(g)];
+    py::array_t<uint16_t> out(S.blob.n);
+    HIP_OK(hipMemcpy(out.mutable_data(), S.blob.p, S.blob.n * 2, hipMemcpyDeviceToHost));
+    return out;
+  }
+  void sync() { HIP_OK(hipStreamSynchronize(st_)); }
+  uintptr_t stream() const { return (uintptr_t)st_; }
+
+ private:
+  int G_, max_epochs_;
+  hipStream_t st_ = nullptr;
+  ModelDesc md_{};
+  DevBuf<char> d_desc_;
+  SplitDev splits_[3];
+  std::vector<ModelState> models_;
+  std::vector<ModelSplitWS> ws_;
+  DevBuf<float> slab_;
+  int gx_bwd_ = 1, gx_fwd_[3] = {1, 1, 1};
+  bool graphs_dirty_ = true;
+  std::map<std::string, hipGraphExec_t> graphs_;
+  // device job tables
+  DevBuf<char> j_rnn_train_, j_rnn_eval_, j_mlp_train_[4], j_mlp_eval_, j_mlp_bwd_[4], j_loss_train_[4],
+      j_loss_eval_, j_fin_, j_upd_, j_epoch_[4];
+  int n_eval_jobs_ = 0;
+  int tmax_eval_ = 0, nmax_eval_ = 0;
+
+  static std::string graph_key(int phase, float lr, int ig, float sel) {
+    char b[128];
+    snprintf(b, sizeof b, "%d/%.9g/%d/%.3g", phase, lr, ig, sel);
+    return b;
+  }
+  int check_g(int g) const {
+    if (g < 0 || g >= G_) throw std::out_of_range("model index");
+    return g;
+  }
+  ModelSplitWS& ws(int g, int s) { return ws_[(size_t)g * 3 + s]; }
+
+  template <typename T>
+  void up(DevBuf<T>& b, const T* src, size_t n) {
+    b.alloc(n, false);
+    if (n) HIP_OK(hipMemcpy(b.p, src, n * sizeof(T), hipMemcpyHostToDevice));
+  }
+  py::array_t<float> down(const DevBuf<float>& b) {
+    sync();
+    py::array_t<float> out(b.n);
+    if (b.n) HIP_OK(hipMemcpy(out.mutable_data(), b.p, b.n * sizeof(float), hipMemcpyDeviceToHost));
+    return out;
+  }
+  template <typename T>
+  DevBuf<char>& upload(DevBuf<char>& b, const std::vector<T>& v) {
+    b.alloc(v.size() * sizeof(T), false);
+    if (!v.empty()) HIP_OK(hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return b;
+  }
+
+  void pack(int g) {
+    UpdJob J{};
+    J.params = models_[g].params.p;
+    J.blob = reinterpret_cast<bf16x8*>(models_[g].blob.p);
+    J.aux = models_[g].aux.p;
+    DevBuf<char> tmp;
+    std::vector<UpdJob> v{J};
+    upload(tmp, v);
+    launch_pack(nullptr, reinterpret_cast<const UpdJob*>(tmp.p), 1, reinterpret_cast<const ModelDesc*>(d_desc_.p), st_);
+    sync();
+  }
+
+  // ------------------------------------------------------------ model descriptor ------
+  void build_desc(int F, int M, int nrnn, int H, bool raw_macro_sdf, const std::vector<int>& hs,
+                  const std::vector<int>& hm, int K, float dropout, bool normalize_w, bool weighted,
+                  float residual) {
+    ModelDesc& d = md_;
+    std::memset(&d, 0, sizeof d);
+    if (hs.empty() || (int)hs.size() > 4) throw std::invalid_argument("native engine supports 1..4 SDF hidden layers");
+    for (int w : hs) if (w < 1 || w > 64) throw std::invalid_argument("SDF hidden widths must be in [1, 64]");
+    if ((int)hm.size() > 2) throw std::invalid_argument("native engine supports <= 2 moment hidden layers");
+    for (int w : hm) if (w < 1 || w > 64) throw std::invalid_argument("moment hidden widths must be in [1, 64]");
+    if (K < 1 || K > 64) throw std::invalid_argument("num_condition_moment must be in [1, 64]");
+    if (nrnn > DLAP_MAX_RNN || H > DLAP_MAX_H) throw std::invalid_argument("LSTM too large for the native engine");
+    d.F = F; d.M = M; d.nrnn = nrnn; d.H = nrnn > 0 ? H : 0; d.K = K;
+    d.Dm = nrnn > 0 ? H : (raw_macro_sdf ? M : 0);
+    d.KIN = F + d.Dm;
+    int ks = (d.KIN + 31) / 32;
+    if (ks > 4) throw std::invalid_argument("F + per-period inputs must be <= 128 for the native engine");
+    d.KS1 = ks <= 2 ? 2 : 4;
+    d.KP = 32 * d.KS1;
+    d.dropout = dropout; d.normalize_w = normalize_w; d.weighted_loss = weighted; d.residual_factor = residual;
+    int off = 0;
+    for (int l = 0; l < nrnn; ++l) {
+      const int in = l == 0 ? M : H;
+      d.lstm_w_ih[l] = off; off += 4 * H * in;
+      d.lstm_w_hh[l] = off; off += 4 * H * H;
+      d.lstm_b_ih[l] = off; off += 4 * H;
+      d.lstm_b_hh[l] = off; off += 4 * H;
+    }
+    d.nl_s = (int)hs.size();
+    for (int j = 0; j < d.nl_s; ++j) {
+      const int in = j == 0 ? d.KIN : hs[j - 1];
+      PackLayer& L = d.s[j];
+      L.w_off = off; L.b_off = off + hs[j] * in; L.out = hs[j]; L.in = in; L.ld = in; L.col0 = 0;
+      off += hs[j] * in + hs[j];
+    }
+    d.so_w = off; off += hs.back();
+    d.so_b = off; off += 1;
+    d.P_sdf = off;
+    std::vector<int> mw(hm);
+    mw.push_back(K);
+    d.nl_m = (int)mw.size();
+    int wmax = 0;
+    for (int j = 0; j < d.nl_m; ++j) {
+      const int in = j == 0 ? M + F : mw[j - 1];
+      PackLayer& L = d.m[j];
+      L.w_off = off; L.b_off = off + mw[j] * in; L.out = mw[j];
+      L.in = j == 0 ? F : in; L.ld = in; L.col0 = j == 0 ? M : 0;
+      off += mw[j] * in + mw[j];
+      wmax = std::max(wmax, mw[j]);
+    }
+    d.P = off;
+    d.cm1 = mw[0];
+    const int wb = (wmax + 15) / 16;
+    d.WMB = wb <= 1 ? 1 : (wb <= 2 ? 2 : 4);
+    const int KSM = (d.WMB + 1) / 2;
+    MlpDims& D = d.md;
+    D.F = F; D.Dm = d.Dm; D.K = K; D.cm1 = d.cm1; D.nrnn = nrnn;
+    D.nl_sdf = d.nl_s; D.nl_mom = d.nl_m; D.dropout = dropout;
+    D.s_fwd0 = 0; D.s_fwd = 4 * d.KS1; D.s_bwd = D.s_fwd + 8 * (d.nl_s - 1);
+    D.m_fwd0 = D.s_bwd + 8 * (d.nl_s - 1); D.m_fwd = D.m_fwd0 + d.WMB * d.KS1;
+    D.m_bwd = D.m_fwd + (d.nl_m - 1) * d.WMB * KSM;
+    D.blob_frags = D.m_bwd + (d.nl_m - 1) * d.WMB * KSM;
+    D.a_sb = 0; D.a_wo = 64 * d.nl_s; D.a_bo = D.a_wo + 64; D.a_pp = D.a_bo + 4;
+    D.a_mb = D.a_pp + 64 * d.Dm; D.aux_floats = D.a_mb + 64 * d.nl_m;
+    // gradient tiles: layer-0 chunks first, then one tile per later layer (slice = tile, TPS 1)
+    const int C0 = d.KS1 / 2;
+    int t = 0;
+    for (int c = 0; c < C0; ++c, ++t)
+      d.tile_s[t] = GradTile{d.s[0].w_off, d.s[0].ld, 0, d.s[0].out, d.s[0].in, c, t};
+    for (int j = 1; j < d.nl_s; ++j, ++t)
+      d.tile_s[t] = GradTile{d.s[j].w_off, d.s[j].ld, 0, d.s[j].out, d.s[j].in, 0, t};
+    d.ntile_s = d.nslice_s = t;
+    t = 0;
+    for (int c = 0; c < C0; ++c, ++t)
+      d.tile_m[t] = GradTile{d.m[0].w_off, d.m[0].ld, d.m[0].col0, d.m[0].out, d.m[0].in, c, t};
+    for (int j = 1; j < d.nl_m; ++j, ++t)
+      d.tile_m[t] = GradTile{d.m[j].w_off, d.m[j].ld, 0, d.m[j].out, d.m[j].in, 0, t};
+    d.ntile_m = d.nslice_m = t;
+    for (int e = 0; e < SLAB_EXTRA; ++e) { d.extra_s[e] = -1; d.extra_m[e] = -1; }
+    for (int j = 0; j < d.nl_s; ++j)
+      for (int o = 0; o < d.s[j].out; ++o) d.extra_s[j * 64 + o] = d.s[j].b_off + o;
+    for (int o = 0; o < hs.back(); ++o) d.extra_s[DLAP_MAXL * 64 + o] = d.so_w + o;
+    d.extra_s[DLAP_MAXL * 64 + 64] = d.so_b;
+    for (int j = 1; j < d.nl_m; ++j)
+      for (int o = 0; o < d.m[j].out; ++o) d.extra_m[j * 64 + o] = d.m[j].b_off + o;
+  }
+
+  int slab_stride() const { return 4096 + SLAB_EXTRA; }
+
+  void alloc_ws(int s) {
+    const SplitDev& D = splits_[s];
+    const int T = D.T, N = D.N, R = D.R, K = md_.K, H = md_.H;
+    for (int g = 0; g < G_; ++g) {
+      ModelSplitWS& W = ws(g, s);
+      W.pp.alloc((size_t)T * std::max(md_.Dm, 1));
+      W.abias.alloc((size_t)T * 64);
+      W.xg.alloc((size_t)T * std::max(4 * H, 1));
+      W.xin.alloc((size_t)T * std::max(H, 1));
+      W.w.alloc((size_t)T * N); W.wn.alloc((size_t)T * N); W.h.alloc((size_t)T * N * K);
+      W.P.alloc(T); W.port.alloc(T); W.sdf.alloc(T);
+      W.E.alloc((size_t)N * K); W.Eu.alloc(N); W.dE.alloc((size_t)N * K); W.dEu.alloc(N);
+      W.part.alloc(2 * ((N + 63) / 64));
+      W.scal.alloc(SC_NSCAL);
+      if (md_.residual_factor > 0.f) W.rstat.alloc((size_t)T * 4);
+      if (s == 0) {
+        W.dw.alloc((size_t)T * N);
+        W.u.alloc((size_t)R * std::max(md_.Dm, 1));
+        W.v.alloc((size_t)R * 64);
+        W.dpp.alloc((size_t)T * std::max(md_.Dm, 1));
+        W.dab.alloc((size_t)T * 64);
+        if (md_.nrnn > 0) {
+          W.sg.alloc((size_t)md_.nrnn * T * 4 * H);
+          W.sc.alloc((size_t)md_.nrnn * T * H);
+          W.sh.alloc((size_t)md_.nrnn * T * H);
+          W.dg.alloc((size_t)T * 4 * H);
+          W.dx.alloc((size_t)T * H);
+        }
+      }
+    }
+    if (s == 0) {
+      const int ntiles = (R + 31) / 32;
+      gx_bwd_ = std::max(1, std::min((ntiles + 3) / 4, 256));
+      const int nsl = std::max(md_.nslice_s, md_.nslice_m);
+      slab_.alloc((size_t)G_ * nsl * gx_bwd_ * slab_stride());
+    }
+    gx_fwd_[s] = std::max(1, std::min(((R + 31) / 32 + 3) / 4, 1024));
+  }
+
+  // ------------------------------------------------------------ job tables ------------
+  RnnJob rnn_job(int g, int s, bool train) {
+    ModelSplitWS& W = ws(g, s);
+    SplitDev& D = splits_[s];
+    RnnJob J{};
+    J.params = models_[g].params.p;
+    J.macro = D.macro.p;
+    J.T = D.T;
+    J.out = W.pp.p;
+    if (train && md_.nrnn > 0) { J.sg = W.sg.p; J.sc = W.sc.p; J.sh = W.sh.p; }
+    J.xg = W.xg.p; J.xin = W.xin.p;
+    J.abias = W.abias.p;
+    J.step = models_[g].drop_step.p;
+    J.seed = models_[g].seed;
+    J.train = train;
+    return J;
+  }
+  const float* pp_ptr(int g, int s) {
+    if (md_.nrnn > 0) return ws(g, s).pp.p;
+    if (md_.Dm > 0) return splits_[s].macro.p;   // raw macro feeds the SDF directly
+    return nullptr;
+  }
+  MlpJob mlp_job(int g, int s, bool train, bool do_sdf, bool do_mom) {
+    ModelSplitWS& W = ws(g, s);
+    SplitDev& D = splits_[s];
+    MlpJob J{};
+    J.X = reinterpret_cast<const bf16x8*>(D.X.p);
+    J.row_dense = D.row_dense.p;
+    J.pp = pp_ptr(g, s);
+    J.abias = W.abias.p;
+    J.blob = reinterpret_cast<const bf16x8*>(models_[g].blob.p);
+    J.aux = models_[g].aux.p;
+    J.w_out = W.w.p; J.h_out = W.h.p;
+    J.dw = W.dw.p; J.dE = W.dE.p; J.Rm = D.Rm.p; J.sdfv = W.sdf.p; J.invT = D.invT.p;
+    J.slab = slab_.p;
+    J.u_out = W.u.p; J.v_out = W.v.p;
+    J.step = models_[g].drop_step.p;
+    J.R = D.R; J.N = D.N;
+    J.seed = models_[g].seed;
+    J.train = train; J.do_sdf = do_sdf; J.do_mom = do_mom;
+    const int nsl = std::max(md_.nslice_s, md_.nslice_m);
+    J.slab_base = g * nsl * gx_bwd_;
+    return J;
+  }
+  LossJob loss_job(int g, int s, int phase) {
+    ModelSplitWS& W = ws(g, s);
+    SplitDev& D = splits_[s];
+    LossJob J{};
+    J.Rm = D.Rm.p; J.mask = D.mask.p; J.invNt = D.invNt.p; J.Nt = D.Nt.p; J.meanR = D.meanR.p;
+    J.RR = D.RR.p; J.invT = D.invT.p; J.Nbar = D.Nbar; J.T = D.T; J.N = D.N; J.K = md_.K;
+    J.normalize = md_.normalize_w; J.weighted = md_.weighted_loss; J.phase = phase;
+    J.res_factor = md_.residual_factor;
+    const float kn = (float)md_.K * (float)D.N;
+    J.coef_c = phase == 3 ? 2.f / kn : (phase == 2 ? -2.f / kn : 0.f);
+    J.coef_u = phase == 1 ? 2.f / (float)D.N : 0.f;
+    J.w = W.w.p; J.wn = W.wn.p; J.h = phase == 1 ? nullptr : W.h.p;
+    J.P = W.P.p; J.port = phase == 0 ? W.port.p : nullptr; J.sdfv = W.sdf.p;
+    J.E = W.E.p; J.Eu = W.Eu.p;
+    J.dE = (phase == 2 || phase == 3) ? W.dE.p : nullptr;
+    J.dEu = phase == 1 ? W.dEu.p : nullptr;
+    J.part = W.part.p; J.dw = W.dw.p; J.rstat = W.rstat.p; J.scal = W.scal.p;
+    return J;
+  }
+
+  void rebuild_jobs() {
+    for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
+    graphs_.clear();
+    std::vector<RnnJob> rt, re;
+    std::vector<LossJob> le;
+    std::vector<MlpJob> me;
+    std::vector<FinJob> fj;
+    std::vector<UpdJob> uj;
+    n_eval_jobs_ = 0; tmax_eval_ = 0; nmax_eval_ = 0;
+    for (int g = 0; g < G_; ++g) {
+      rt.push_back(rnn_job(g, 0, true));
+      for (int s = 1; s < 3; ++s) {
+        if (!splits_[s].set) continue;
+        re.push_back(rnn_job(g, s, false));
+        me.push_back(mlp_job(g, s, false, true, true));
+        le.push_back(loss_job(g, s, 0));
+        tmax_eval_ = std::max(tmax_eval_, splits_[s].T);
+        nmax_eval_ = std::max(nmax_eval_, splits_[s].N);
+      }
+      ModelSplitWS& W = ws(g, 0);
+      FinJob F{};
+      const int nsl = std::max(md_.nslice_s, md_.nslice_m);
+      F.slab = slab_.p + (size_t)g * nsl * gx_bwd_ * slab_stride();
+      F.grads = models_[g].grads.p; F.row_ptr = splits_[0].row_ptr.p;
+      F.u = W.u.p; F.dpp = W.dpp.p; F.v = W.v.p; F.dab = W.dab.p; F.T = splits_[0].T; F.nslab = gx_bwd_;
+      fj.push_back(F);
+      ModelState& S = models_[g];
+      UpdJob U{};
+      U.params = S.params.p; U.grads = S.grads.p; U.m = S.m.p; U.v = S.v.p;
+      U.adam_step = S.adam_step.p; U.drop_step = S.drop_step.p; U.gnorm = S.gnorm.p;
+      U.blob = reinterpret_cast<bf16x8*>(S.blob.p); U.aux = S.aux.p;
+      U.dpp = W.dpp.p; U.macro = splits_[0].macro.p; U.sg = W.sg.p; U.sc = W.sc.p; U.sh = W.sh.p;
+      U.dg = W.dg.p; U.dx = W.dx.p; U.dab = W.dab.p; U.T = splits_[0].T; U.seed = S.seed;
+      uj.push_back(U);
+    }
+    n_eval_jobs_ = (int)le.size();
+    upload(j_rnn_train_, rt); upload(j_rnn_eval_, re); upload(j_mlp_eval_, me); upload(j_loss_eval_, le);
+    upload(j_fin_, fj); upload(j_upd_, uj);
+    for (int phase = 1; phase <= 3; ++phase) {
+      std::vector<MlpJob> mt, mb;
+      std::vector<LossJob> lt;
+      std::vector<EpochJob> ej;
+      for (int g = 0; g < G_; ++g) {
+        mt.push_back(mlp_job(g, 0, true, true, phase != 1));
+        mb.push_back(mlp_job(g, 0, true, true, true));
+        lt.push_back(loss_job(g, 0, phase));
+        ModelState& S = models_[g];
+        EpochJob E{};
+        E.sc_train = ws(g, 0).scal.p;
+        E.sc_valid = (phase != 2 && splits_[1].set) ? ws(g, 1).scal.p : nullptr;
+        E.sc_test = (phase != 2 && splits_[2].set) ? ws(g, 2).scal.p : nullptr;
+        E.gnorm = S.gnorm.p; E.hist = S.hist.p; E.ep = S.ep.p; E.best = S.best.p;
+        E.snap_flags = S.snap_flags.p; E.params = S.params.p;
+        E.snap_loss = S.snap_loss.p; E.snap_sharpe = S.snap_sharpe.p;
+        ej.push_back(E);
+      }
+      upload(j_mlp_train_[phase], mt); upload(j_mlp_bwd_[phase], mb); upload(j_loss_train_[phase], lt);
+      upload(j_epoch_[phase], ej);
+    }
+    // evaluation-only jobs of the train split (module API / final evaluation)
+    {
+      std::vector<MlpJob> mt;
+      std::vector<LossJob> lt;
+      for (int g = 0; g < G_; ++g) {
+        mt.push_back(mlp_job(g, 0, false, true, true));
+        lt.push_back(loss_job(g, 0, 0));
+      }
+      upload(j_mlp_train_[0], mt);
+      upload(j_loss_train_[0], lt);
+    }
+  }
+
+  const ModelDesc* dd() const { return reinterpret_cast<const ModelDesc*>(d_desc_.p); }
+  template <typename T>
+  static const T* as(const DevBuf<char>& b) { return reinterpret_cast<const T*>(b.p); }
+
+  void enqueue_train_grads(int phase) {
+    const SplitDev& D = splits_[0];
+    launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), st_);
+    launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, gx_fwd_[0], md_.md, md_.KS1, md_.WMB, st_);
+    launch_period_fwd(as<LossJob>(j_loss_train_[phase]), G_, D.T, st_);
+    launch_asset(as<LossJob>(j_loss_train_[phase]), G_, D.N, st_);
+    launch_job_metrics(as<LossJob>(j_loss_train_[phase]), G_, st_);
+    if (phase == 2) {
+      launch_mlp_bwd_mom(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_m, 1, md_.md, md_.KS1,
+                         md_.WMB, slab_stride(), st_);
+    } else {
+      launch_period_bwd(as<LossJob>(j_loss_train_[phase]), G_, D.T, st_);
+      launch_mlp_bwd_sdf(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_s, 1, md_.md, md_.KS1,
+                         slab_stride(), st_);
+    }
+    launch_finalize(as<FinJob>(j_fin_), G_, dd(), md_, phase, slab_stride(), D.T, st_);
+  }
+  void enqueue_train(int phase, float lr) {
+    enqueue_train_grads(phase);
+    launch_update(as<UpdJob>(j_upd_), G_, dd(), phase, lr, st_);
+  }
+  void enqueue_eval() {
+    if (n_eval_jobs_ == 0) return;
+    launch_prologue(as<RnnJob>(j_rnn_eval_), n_eval_jobs_, tmax_eval_, dd(), st_);
+    int gx = std::max(gx_fwd_[1], gx_fwd_[2]);
+    launch_mlp_fwd(as<MlpJob>(j_mlp_eval_), n_eval_jobs_, gx, md_.md, md_.KS1, md_.WMB, st_);
+    launch_period_fwd(as<LossJob>(j_loss_eval_), n_eval_jobs_, tmax_eval_, st_);
+    launch_asset(as<LossJob>(j_loss_eval_), n_eval_jobs_, nmax_eval_, st_);
+    launch_job_metrics(as<LossJob>(j_loss_eval_), n_eval_jobs_, st_);
+  }
+  void enqueue_epoch(int phase, float lr, int ignore_epoch, float sel) {
+    enqueue_train(phase, lr);
+    if (phase != 2) enqueue_eval();
+    launch_epoch_end(as<EpochJob>(j_epoch_[phase]), G_, phase, ignore_epoch, sel, md_.residual_factor,
+                     md_.P, st_);
+  }
+  void fwd_only(int s, bool train_mode, bool do_mom) {
+    const SplitDev& D = splits_[s];
+    if (!D.set) throw std::runtime_error("split not set");
+    // build ad-hoc jobs for one split of every model
+    std::vector<RnnJob> rj;
+    std::vector<MlpJob> mj;
+    std::vector<LossJob> lj;
+    for (int g = 0; g < G_; ++g) {
+      rj.push_back(rnn_job(g, s, train_mode));
+      mj.push_back(mlp_job(g, s, train_mode, true, do_mom));
+      lj.push_back(loss_job(g, s, 0));
+      if (!do_mom) lj.back().h = nullptr;
+    }
+    DevBuf<char> a, b, c;
+    upload(a, rj); upload(b, mj); upload(c, lj);
+    launch_prologue(as<RnnJob>(a), G_, D.T, dd(), st_);
+    launch_mlp_fwd(as<MlpJob>(b), G_, gx_fwd_[s], md_.md, md_.KS1, md_.WMB, st_);
+    launch_period_fwd(as<LossJob>(c), G_, D.T, st_);
+    launch_asset(as<LossJob>(c), G_, D.N, st_);
+    launch_job_metrics(as<LossJob>(c), G_, st_);
+    sync();
+  }
+};
+
+PYBIND11_MODULE(_dlap_hip, m) {
+  m.doc() = "DLAP MI355X native engine (HIP kernels for gfx950 + hipGraph epoch executor)";
+  py::class_<Engine>(m, "Engine")
+      .def(py::init<int, int, int, int, bool, std::vector<int>, std::vector<int>, int, float, bool, bool,
+                    float, int, int>(),
+           py::arg("F"), py::arg("M"), py::arg("nrnn"), py::arg("H"), py::arg("raw_macro_sdf"),
+           py::arg("hidden"), py::arg("mom_hidden"), py::arg("K"), py::arg("dropout"),
+           py::arg("normalize_w"), py::arg("weighted"), py::arg("residual"), py::arg("G"),
+           py::arg("max_epochs"))
+      .def("describe", &Engine::describe)
+      .def("set_split", &Engine::set_split)
+      .def("set_params", &Engine::set_params)
+      .def("get_params", &Engine::get_params)
+      .def("get_grads", &Engine::get_grads)
+      .def("get_snapshot", &Engine::get_snapshot)
+      .def("load_snapshot", &Engine::load_snapshot)
+      .def("set_seed", &Engine::set_seed)
+      .def("get_opt_state", &Engine::get_opt_state)
+      .def("set_opt_state", &Engine::set_opt_state)
+      .def("begin_phase", &Engine::begin_phase)
+      .def("snap_flags", &Engine::snap_flags)
+      .def("epoch_count", &Engine::epoch_count)
+      .def("history", &Engine::history)
+      .def("run_epochs", &Engine::run_epochs, py::call_guard<py::gil_scoped_release>())
+      .def("forward_split", &Engine::forward_split)
+      .def("train_step", &Engine::train_step)
+      .def("backward_only", &Engine::backward_only)
+      .def("read_ws", &Engine::read_ws)
+      .def("read_aux", &Engine::read_aux)
+      .def("read_blob", &Engine::read_blob)
+      .def("sync", &Engine::sync, py::call_guard<py::gil_scoped_release>())
+      .def("stream", &Engine::stream);
+  m.attr("HIST_W") = (int)HIST_W;
+  m.attr("SC_NSCAL") = (int)SC_NSCAL;
+}

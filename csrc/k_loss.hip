@@ -1,0 +1,291 @@
+// Fused masked moment-loss kernels.
+//
+// Reference math (`/root/reference/src/model.py:346-483,565-594`, `src/train.py:29-42,106-153`):
+//   w'      = (w - mu_t) m                  mu_t = sum_i w m / max(N_t, 1)   (zero-mean)
+//   P_t     = (Nbar / max(N_t,1)) sum_i w' R m                              (weighted loss)
+//   E[k,i]  = sum_t h[k,t,i] R m (1 + P_t) / max(T_i, 1)
+//   L_cond  = mean_k mean_i E^2,   L_unc = the h == 1 case
+// Three passes, each a plain launch (no inter-workgroup hand-offs, fixed-order sums):
+//   k_period_fwd  one workgroup per (job, period): mu_t, w', P_t, SDF_t, the L1-normalised
+//                 portfolio return (evaluate), residual-loss statistics
+//   k_asset       one workgroup per (job, 64 stocks): E, E_unc, dL/dE and partial loss sums;
+//                 the 4 waves split the time axis, then reduce in LDS in a fixed order
+//   k_period_bwd  one workgroup per (job, period): dL/dSDF_t and the analytic gradient of
+//                 the zero-mean normalisation, dL/dw_raw = m c_t (R - mean_t R) (+ residual)
+//   k_job_metrics one workgroup per job: scalar losses, Sharpe (unbiased std, 1e-8 guard),
+//                 max drawdown (cumprod scan), mean/std of the evaluation returns
+#include "common.h"
+#include "loss.h"
+
+// ---------------------------------------------------------------- period forward -------
+__global__ __launch_bounds__(256) void k_period_fwd(const LossJob* __restrict__ jobs) {
+  const LossJob& J = jobs[blockIdx.y];
+  const int t = blockIdx.x;
+  if (t >= J.T) return;
+  __shared__ float red[4];
+  const int N = J.N;
+  const float* w = J.w + (size_t)t * N;
+  const float* m = J.mask + (size_t)t * N;
+  const float* R = J.Rm + (size_t)t * N;
+  float* wn = J.wn + (size_t)t * N;
+  float sw = 0.f;
+  if (J.normalize) {
+    for (int i = threadIdx.x; i < N; i += 256) sw += w[i] * m[i];
+    sw = block_sum<256>(sw, red);
+  }
+  const float mu = J.normalize ? sw * J.invNt[t] : 0.f;
+  float s_wr = 0.f, s_abs = 0.f, s_ww = 0.f;
+  for (int i = threadIdx.x; i < N; i += 256) {
+    const float v = (w[i] * m[i] - mu) * m[i];
+    wn[i] = v;
+    s_wr += v * R[i] * m[i];
+    s_abs += fabsf(v) * m[i];
+    s_ww += v * v * m[i];
+  }
+  s_wr = block_sum<256>(s_wr, red);
+  s_abs = block_sum<256>(s_abs, red);
+  if (J.rstat) s_ww = block_sum<256>(s_ww, red);
+  if (threadIdx.x == 0) {
+    const float p = J.weighted ? s_wr * J.invNt[t] * J.Nbar : s_wr;
+    J.P[t] = p;
+    J.sdfv[t] = 1.f + p;
+    if (J.port) J.port[t] = s_wr / fmaxf(s_abs, 1e-8f);
+    if (J.rstat) {
+      J.rstat[4 * t + 0] = s_ww;
+      J.rstat[4 * t + 1] = s_wr;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- asset pass ------------
+// grid (ceil(N/64), njobs); block 256 = 4 waves; lane -> stock, wave -> quarter of the time axis.
+__global__ __launch_bounds__(256) void k_asset(const LossJob* __restrict__ jobs) {
+  const LossJob& J = jobs[blockIdx.y];
+  const int nblk = (J.N + 63) >> 6;
+  if ((int)blockIdx.x >= nblk) return;
+  __shared__ float sdf[DLAP_MAX_T];
+  __shared__ float red[4][64][9];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int T = J.T, N = J.N, K = J.K;
+  for (int t = threadIdx.x; t < T; t += 256) sdf[t] = J.sdfv[t];
+  __syncthreads();
+  const int i = blockIdx.x * 64 + lane;
+  const bool ok = i < N;
+  const int t0 = (T * wave) / 4, t1 = (T * (wave + 1)) / 4;
+  const float invT = ok ? J.invT[i] : 0.f;
+  float loss_c = 0.f, loss_u = 0.f;
+  // unconditional moment (h == 1)
+  {
+    float e = 0.f;
+    if (ok)
+      for (int t = t0; t < t1; ++t) e += J.Rm[(size_t)t * N + i] * sdf[t];
+    red[wave][lane][8] = e;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    const float e = (red[0][lane][8] + red[1][lane][8] + red[2][lane][8] + red[3][lane][8]) * invT;
+    if (ok) {
+      J.Eu[i] = e;
+      if (J.dEu) J.dEu[i] = J.coef_u * e;
+    }
+    loss_u = ok ? e * e : 0.f;
+  }
+  // conditional moments, 8 at a time
+  if (J.h) {
+    for (int k0 = 0; k0 < K; k0 += 8) {
+      float e[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) e[k] = 0.f;
+      const int kn = min(8, K - k0);
+      if (ok) {
+        for (int t = t0; t < t1; ++t) {
+          const size_t d = (size_t)t * N + i;
+          const float q = J.Rm[d] * sdf[t];
+          const float* hp = J.h + d * K + k0;
+          if (kn == 8 && (K & 3) == 0) {
+            const f32x4 a = *reinterpret_cast<const f32x4*>(hp);
+            const f32x4 b = *reinterpret_cast<const f32x4*>(hp + 4);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) { e[k] += a[k] * q; e[4 + k] += b[k] * q; }
+          } else {
+            for (int k = 0; k < kn; ++k) e[k] += hp[k] * q;
+          }
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < 8; ++k) red[wave][lane][k] = e[k];
+      __syncthreads();
+      if (wave == 0 && ok) {
+        for (int k = 0; k < kn; ++k) {
+          const float v = (red[0][lane][k] + red[1][lane][k] + red[2][lane][k] + red[3][lane][k]) * invT;
+          J.E[(size_t)i * K + k0 + k] = v;
+          if (J.dE) J.dE[(size_t)i * K + k0 + k] = J.coef_c * v;
+          loss_c += v * v;
+        }
+      }
+    }
+  }
+  if (wave == 0) {
+    loss_c = wave_sum(loss_c);
+    loss_u = wave_sum(loss_u);
+    if (lane == 0) {
+      J.part[2 * blockIdx.x + 0] = loss_c;
+      J.part[2 * blockIdx.x + 1] = loss_u;
+    }
+  }
+}
+
+DLAP_DEV void final_losses(const LossJob& J, float& lc, float& lu) {
+  const int nblk = (J.N + 63) >> 6;
+  float a = 0.f, b = 0.f;
+  for (int k = 0; k < nblk; ++k) { a += J.part[2 * k]; b += J.part[2 * k + 1]; }
+  lc = J.h ? a / ((float)J.K * (float)J.N) : 0.f;
+  lu = b / (float)J.N;
+}
+
+// ---------------------------------------------------------------- residual loss --------
+// L_res = mean_{t in S1} resid_t / max(mean_{t in S2} Rsq_t, 1e-8)
+//   S2 = {n_t >= 2},  S1 = S2 and ww_t > 1e-8,  resid_t = (RR - Rw^2/ww)/n_t,  Rsq_t = RR/n_t.
+DLAP_DEV void residual_stats(const LossJob& J, float& lres, float& inv_b, float& n1) {
+  float a = 0.f, b = 0.f, c1 = 0.f, c2 = 0.f;
+  for (int t = 0; t < J.T; ++t) {
+    const float n = J.Nt[t];
+    if (n < 2.f) continue;
+    const float ww = J.rstat[4 * t + 0], rw = J.rstat[4 * t + 1], rr = J.RR[t];
+    b += rr / n; c2 += 1.f;
+    if (ww > 1e-8f) { a += (rr - rw * rw / ww) / n; c1 += 1.f; }
+  }
+  if (c1 == 0.f) { lres = 0.f; inv_b = 0.f; n1 = 0.f; return; }
+  const float B = fmaxf(b / c2, 1e-8f);
+  lres = (a / c1) / B;
+  inv_b = 1.f / B;
+  n1 = c1;
+}
+
+// ---------------------------------------------------------------- period backward ------
+__global__ __launch_bounds__(256) void k_period_bwd(const LossJob* __restrict__ jobs) {
+  const LossJob& J = jobs[blockIdx.y];
+  const int t = blockIdx.x;
+  if (t >= J.T) return;
+  __shared__ float red[4];
+  const int N = J.N, K = J.K;
+  const size_t base = (size_t)t * N;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < N; i += 256) {
+    const size_t d = base + i;
+    const float r = J.Rm[d];
+    if (r == 0.f) continue;
+    float g;
+    if (J.phase == 1) {
+      g = J.dEu[i];
+    } else {
+      g = 0.f;
+      const float* hp = J.h + d * K;
+      const float* de = J.dE + (size_t)i * K;
+      for (int k = 0; k < K; ++k) g += de[k] * hp[k];
+    }
+    s += g * r * J.invT[i];
+  }
+  s = block_sum<256>(s, red);
+  const float c = J.weighted ? s * J.Nbar * J.invNt[t] : s;   // dL/dS_t with S_t = sum w' R m
+  // optional residual-loss gradient wrt w' (valid stocks of period t)
+  float rcoef = 0.f, beta = 0.f;
+  if (J.res_factor > 0.f) {
+    float lres, inv_b, n1;
+    residual_stats(J, lres, inv_b, n1);
+    const float n = J.Nt[t], ww = J.rstat[4 * t + 0], rw = J.rstat[4 * t + 1];
+    if (n >= 2.f && ww > 1e-8f && n1 > 0.f) {
+      beta = rw / ww;
+      rcoef = J.res_factor * inv_b / n1 * (-2.f / n) * beta;   // d/dw'_i = rcoef * (R_i - beta w'_i)
+    }
+  }
+  // mean over valid stocks of the residual gradient (for the normalisation Jacobian)
+  float gres_mean = 0.f;
+  if (rcoef != 0.f && J.normalize) {
+    float sg = 0.f;
+    for (int i = threadIdx.x; i < N; i += 256) {
+      const size_t d = base + i;
+      if (J.mask[d] > 0.f) sg += J.Rm[d] - beta * J.wn[d];
+    }
+    sg = block_sum<256>(sg, red);
+    gres_mean = rcoef * sg * J.invNt[t];
+  }
+  const float mR = J.normalize ? J.meanR[t] : 0.f;
+  for (int i = threadIdx.x; i < N; i += 256) {
+    const size_t d = base + i;
+    const float m = J.mask[d];
+    float g = c * (J.Rm[d] - mR);
+    if (rcoef != 0.f) g += rcoef * (J.Rm[d] - beta * J.wn[d]) - gres_mean;
+    J.dw[d] = m * g;
+  }
+}
+
+// ---------------------------------------------------------------- per-job scalars -------
+// scal layout: see loss.h (SC_*).
+__global__ __launch_bounds__(256) void k_job_metrics(const LossJob* __restrict__ jobs) {
+  const LossJob& J = jobs[blockIdx.x];
+  __shared__ float red[4];
+  __shared__ float ret[DLAP_MAX_T];
+  const int T = J.T;
+  if (threadIdx.x == 0) {
+    float lc, lu;
+    final_losses(J, lc, lu);
+    float lres = 0.f, inv_b, n1;
+    if (J.res_factor > 0.f) residual_stats(J, lres, inv_b, n1);
+    J.scal[SC_LCOND] = lc;
+    J.scal[SC_LUNC] = lu;
+    J.scal[SC_LRES] = lres;
+  }
+  // Sharpe of the weighted training portfolio P (train monitor) and of the L1 portfolio.
+  for (int pass = 0; pass < 2; ++pass) {
+    const float* src = pass == 0 ? J.P : J.port;
+    if (!src) continue;
+    for (int t = threadIdx.x; t < T; t += 256) ret[t] = src[t];
+    __syncthreads();
+    float s = 0.f;
+    for (int t = threadIdx.x; t < T; t += 256) s += ret[t];
+    s = block_sum<256>(s, red);
+    const float mean = s / (float)T;
+    float v = 0.f;
+    for (int t = threadIdx.x; t < T; t += 256) { const float x = ret[t] - mean; v += x * x; }
+    v = block_sum<256>(v, red);
+    if (threadIdx.x == 0) {
+      const float sd_u = T > 1 ? sqrtf(v / (float)(T - 1)) : __builtin_nanf("");
+      const float sharpe = (sd_u < 1e-8f) ? 0.f : mean / sd_u;
+      if (pass == 0) {
+        J.scal[SC_TRAIN_SHARPE] = sharpe;
+      } else {
+        J.scal[SC_SHARPE] = sharpe;
+        J.scal[SC_MEAN] = mean;
+        J.scal[SC_STD] = sqrtf(v / (float)T);
+        float cum = 1.f, peak = 1.f, mdd = 0.f;
+        for (int t = 0; t < T; ++t) {
+          cum *= 1.f + ret[t];
+          peak = t == 0 ? cum : fmaxf(peak, cum);
+          mdd = fminf(mdd, (cum - peak) / peak);
+        }
+        J.scal[SC_MDD] = mdd;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------- launchers ------------
+void launch_period_fwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st) {
+  hipLaunchKernelGGL(k_period_fwd, dim3(tmax, njobs), dim3(256), 0, st, jobs);
+  HIP_OK(hipGetLastError());
+}
+void launch_asset(const LossJob* jobs, int njobs, int nmax, hipStream_t st) {
+  hipLaunchKernelGGL(k_asset, dim3((nmax + 63) / 64, njobs), dim3(256), 0, st, jobs);
+  HIP_OK(hipGetLastError());
+}
+void launch_period_bwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st) {
+  hipLaunchKernelGGL(k_period_bwd, dim3(tmax, njobs), dim3(256), 0, st, jobs);
+  HIP_OK(hipGetLastError());
+}
+void launch_job_metrics(const LossJob* jobs, int njobs, hipStream_t st) {
+  hipLaunchKernelGGL(k_job_metrics, dim3(njobs), dim3(256), 0, st, jobs);
+  HIP_OK(hipGetLastError());
+}

@@ -1,0 +1,694 @@
+// Fused SDF / moment "tower" kernels on the compacted panel (one row = one valid (t, i)).
+//
+// Replaces the reference hot path `SDFNetwork.forward` + `MomentNetwork.forward` and their
+// autograd (`/root/reference/src/model.py:132-161,221-281,513-521`, profile in SURVEY §2.3
+// K1/K2/K4/K12): macro tiling + cat + Linear/ReLU/Dropout x L + output projection + mask
+// become ONE kernel per direction; activations stay in registers; dropout masks come from a
+// counter hash (recomputed in backward, never stored).
+//
+// Widths are padded at pack time (zero weights/biases are exact no-ops through ReLU):
+//   SDF tower: every hidden layer is 64 units (4 blocks of 16);
+//   moment tower: every layer is WM = 16*WMB units (WMB in {1,2,4}, template).
+// Layer 0 reads KP = 32*KS1 panel columns (KS1 in {2,4}, template).
+//
+// ---- Data orientation -----------------------------------------------------------------
+// A wave owns a 32-row tile = 2 row blocks (b = 0, 1) of 16 rows. Everything is computed in
+// the "T" orientation: an activation block is a 16(units) x 16(rows) MFMA C tile,
+//      lane l holds  act[unit = 16u + 4*(l>>4) + r][row = l & 15],  r = 0..3.
+// Layer 0:   Z0^T = W0 . X^T           A = W0 frag (natural k), B = X frag
+//            (lane l: X[row l&15][k = 32s + 8q + j] -- a plain 16-byte load of the row).
+// Layer j:   Zj^T = Wj . A(j-1)^T      B = two C blocks packed (pack8): the k order inside a
+//            step is permuted, k(q, j) = j < 4 ? 4q + j : 16 + 4q + (j-4); the packed weight
+//            fragment uses the same permutation, so no lane movement is needed.
+// Backward chain dA(j-1)^T = Wj^T . dZj^T: the identical trick with the transposed blob.
+// Weight gradients dW = sum_rows dZ . A^T need rows on the k axis: the A and B operand maps
+// are mirror images, so an MFMA of a packed T fragment (as A) against a 0/1 selector (as B)
+// *transposes* a 16x16 block exactly (bf16 x 1.0, one non-zero term per output):
+//      N layout: lane l holds act[unit = 16c + (l&15)][row = 4*(l>>4) + r].
+// Packing the two row blocks' N tiles gives operands whose k axis is the tile's 32 rows
+// (k(q, j) = row 4q + (j&3) of block j>>2), so dW tiles accumulate in registers across the
+// whole persistent loop. Bias sums use the same rows-as-k operands against a one-hot
+// column selector: every layer's bias gradient shares 4 accumulator tiles.
+#include "common.h"
+#include "layout.h"
+#include "mlp.h"
+
+DLAP_DEV int lane_id() { return threadIdx.x & 63; }
+DLAP_DEV bf16x8 ldsf(const bf16x8* lds, int frag) { return lds[frag * 64 + lane_id()]; }
+DLAP_DEV int perm_unit(int q, int j) { return j < 4 ? 4 * q + j : 16 + 4 * q + (j - 4); }
+
+// 0/1 selectors (constant per lane) that transpose a packed T fragment (permuted k) or a
+// natural-k X fragment into N layout, and a one-hot column selector for bias sums.
+DLAP_DEV bf16x8 make_sel(bool permuted, int c) {
+  const int l = lane_id(), q = l >> 4, n = l & 15;
+  bf16x8 s;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    int k = permuted ? perm_unit(q, j) : 8 * q + j;
+    s[j] = (__bf16)((k == 16 * c + n) ? 1.f : 0.f);
+  }
+  return s;
+}
+DLAP_DEV bf16x8 make_onehot(int col) {
+  const bool on = (lane_id() & 15) == col;
+  bf16x8 s;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s[j] = (__bf16)(on ? 1.f : 0.f);
+  return s;
+}
+
+struct RowInfo {
+  int dense[2];   // dense index of this lane's row in block b (-1 beyond R)
+  int t[2], i[2];
+};
+
+DLAP_DEV RowInfo load_rows(const MlpJob& J, int tile) {
+  RowInfo ri;
+  const int l = lane_id();
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    int r = tile * 32 + 16 * b + (l & 15);
+    int d = r < J.R ? J.row_dense[r] : -1;
+    ri.dense[b] = d;
+    int t = d >= 0 ? d / J.N : 0;
+    ri.t[b] = t;
+    ri.i[b] = d >= 0 ? d - t * J.N : 0;
+  }
+  return ri;
+}
+
+template <int KS1>
+DLAP_DEV void load_x(const MlpJob& J, const MlpDims& D, int tile, const RowInfo& ri,
+                     bf16x8 (&xf)[2][KS1]) {
+  const int l = lane_id(), q = l >> 4;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    int r = tile * 32 + 16 * b + (l & 15);
+    bool ok = r < J.R;
+    const bf16x8* row = J.X + (size_t)(ok ? r : 0) * (4 * KS1);
+#pragma unroll
+    for (int s = 0; s < KS1; ++s) xf[b][s] = ok ? row[4 * s + q] : zero8();
+    if (D.Dm > 0 && ok) {
+      const float* pp = J.pp + ri.t[b] * D.Dm;
+#pragma unroll
+      for (int s = 0; s < KS1; ++s)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          int col = 32 * s + 8 * q + j - D.F;
+          if (col >= 0 && col < D.Dm) xf[b][s][j] = (__bf16)pp[col];
+        }
+    }
+  }
+}
+
+// acc[b][u] = W0 . X^T  (UB output blocks)
+template <int KS1, int UB>
+DLAP_DEV void layer0(const bf16x8* lds, int off, const bf16x8 (&xf)[2][KS1], f32x4 (&acc)[2][UB]) {
+#pragma unroll
+  for (int u = 0; u < UB; ++u) {
+    f32x4 c0 = zero4(), c1 = zero4();
+#pragma unroll
+    for (int s = 0; s < KS1; ++s) {
+      bf16x8 w = ldsf(lds, off + u * KS1 + s);
+      c0 = mfma16(w, xf[0][s], c0);
+      c1 = mfma16(w, xf[1][s], c1);
+    }
+    acc[0][u] = c0; acc[1][u] = c1;
+  }
+}
+
+// acc = W . prev^T, prev as KS packed fragments per row block, UB output blocks.
+template <int UB, int KS>
+DLAP_DEV void layer_chain(const bf16x8* lds, int off, const bf16x8 (&pf)[2][KS], f32x4 (&acc)[2][UB]) {
+#pragma unroll
+  for (int u = 0; u < UB; ++u) {
+    f32x4 c0 = zero4(), c1 = zero4();
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      bf16x8 w = ldsf(lds, off + u * KS + s);
+      c0 = mfma16(w, pf[0][s], c0);
+      c1 = mfma16(w, pf[1][s], c1);
+    }
+    acc[0][u] = c0; acc[1][u] = c1;
+  }
+}
+
+template <int UB>
+DLAP_DEV void pack_blocks(const f32x4 (&a)[2][UB], bf16x8 (&pf)[2][(UB + 1) / 2]) {
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int s = 0; s < (UB + 1) / 2; ++s)
+      pf[b][s] = pack8(a[b][2 * s], (2 * s + 1 < UB) ? a[b][2 * s + 1] : zero4());
+}
+
+struct DropCtx {
+  bool on; uint32_t thr; float scale; uint32_t seed, step;
+};
+
+// bias + ReLU + dropout in place; gate bit (u*4+r) per row block.
+template <int UB>
+DLAP_DEV void relu_dropout(f32x4 (&a)[2][UB], const float* bias0, const float* bias1,
+                           const DropCtx& dc, int layer_id, const RowInfo& ri, uint32_t (&gate)[2]) {
+  const int q = lane_id() >> 4;
+  const uint32_t key = dropout_key(dc.seed, dc.step, layer_id);
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const float* bp = b ? bias1 : bias0;
+    uint32_t g = 0;
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const f32x4 bb = *reinterpret_cast<const f32x4*>(bp + 16 * u + 4 * q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int unit = 16 * u + 4 * q + r;
+        float z = a[b][u][r] + bb[r];
+        bool on = z > 0.f;
+        if (dc.on) on = on && dropout_keep(key, (uint32_t)ri.dense[b], (uint32_t)unit, dc.thr);
+        a[b][u][r] = on ? z * dc.scale : 0.f;
+        g |= (on ? 1u : 0u) << (u * 4 + r);
+      }
+    }
+    gate[b] = g;
+  }
+}
+
+DLAP_DEV float reduce_q(float v) {  // sum over the 4 lane groups that share l & 15
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+DLAP_DEV DropCtx drop_ctx(const MlpJob& J, const MlpDims& D) {
+  DropCtx dc;
+  dc.on = J.train && D.dropout > 0.f;
+  dc.thr = (uint32_t)(D.dropout * 16777216.f + 0.5f);
+  dc.scale = dc.on ? 1.f / (1.f - D.dropout) : 1.f;
+  dc.seed = J.seed;
+  dc.step = J.step ? (uint32_t)*J.step : 0u;
+  return dc;
+}
+
+DLAP_DEV void stage_weights(const MlpJob& J, const MlpDims& D, bf16x8* lds, float* aux) {
+  for (int i = threadIdx.x; i < D.blob_frags * 64; i += blockDim.x) lds[i] = J.blob[i];
+  for (int i = threadIdx.x; i < D.aux_floats; i += blockDim.x) aux[i] = J.aux[i];
+  __syncthreads();
+}
+
+// SDF tower forward on one tile: the raw (pre-normalisation) weight of each row block.
+template <int KS1>
+DLAP_DEV void sdf_forward_tile(const bf16x8* lds, const float* aux, const MlpDims& D,
+                               const DropCtx& dc, const RowInfo& ri, const bf16x8 (&xf)[2][KS1],
+                               float (&w)[2]) {
+  f32x4 a[2][4];
+  bf16x8 pf[2][2];
+  uint32_t gate[2];
+  layer0<KS1, 4>(lds, D.s_fwd0, xf, a);
+  relu_dropout<4>(a, aux + D.a_sb, aux + D.a_sb, dc, 0, ri, gate);
+  for (int j = 1; j < D.nl_sdf; ++j) {
+    pack_blocks<4>(a, pf);
+    layer_chain<4, 2>(lds, D.s_fwd + (j - 1) * 8, pf, a);
+    relu_dropout<4>(a, aux + D.a_sb + 64 * j, aux + D.a_sb + 64 * j, dc, j, ri, gate);
+  }
+  const int q = lane_id() >> 4;
+  const float* wo = aux + D.a_wo;
+  const float bo = aux[D.a_bo];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    float s = 0.f;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const f32x4 ww = *reinterpret_cast<const f32x4*>(wo + 16 * u + 4 * q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s += a[b][u][r] * ww[r];
+    }
+    w[b] = reduce_q(s) + bo;
+  }
+}
+
+// Moment tower forward on one tile: writes the K tanh outputs of every valid row.
+template <int KS1, int WMB>
+DLAP_DEV void mom_forward_tile(const bf16x8* lds, const float* aux, const MlpDims& D,
+                               const MlpJob& J, const DropCtx& dc, const RowInfo& ri,
+                               const bf16x8 (&xf)[2][KS1]) {
+  constexpr int KSM = (WMB + 1) / 2;
+  f32x4 a[2][WMB];
+  bf16x8 pf[2][KSM];
+  uint32_t gate[2];
+  const int q = lane_id() >> 4;
+  layer0<KS1, WMB>(lds, D.m_fwd0, xf, a);
+  const float* pb0 = J.abias + ri.t[0] * 64;
+  const float* pb1 = J.abias + ri.t[1] * 64;
+  for (int j = 0; j + 1 < D.nl_mom; ++j) {
+    if (j > 0) pb0 = pb1 = aux + D.a_mb + 64 * j;
+    relu_dropout<WMB>(a, pb0, pb1, dc, 16 + j, ri, gate);
+    pack_blocks<WMB>(a, pf);
+    layer_chain<WMB, KSM>(lds, D.m_fwd + j * WMB * KSM, pf, a);
+  }
+  if (D.nl_mom > 1) pb0 = pb1 = aux + D.a_mb + 64 * (D.nl_mom - 1);
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    if (ri.dense[b] < 0) continue;
+    const float* bp = b ? pb1 : pb0;
+    float* dst = J.h_out + (size_t)ri.dense[b] * D.K;
+#pragma unroll
+    for (int u = 0; u < WMB; ++u)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int k = 16 * u + 4 * q + r;
+        if (k < D.K) dst[k] = tanhf(a[b][u][r] + bp[k]);
+      }
+  }
+}
+
+// ============================== forward ==================================================
+template <int KS1, int WMB>
+__global__ __launch_bounds__(256, 2) void k_mlp_fwd(const MlpJob* __restrict__ jobs, MlpDims D) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const MlpJob& J = jobs[blockIdx.y];
+  bf16x8* lds = reinterpret_cast<bf16x8*>(smem);
+  float* aux = reinterpret_cast<float*>(smem + (size_t)D.blob_frags * 1024);
+  stage_weights(J, D, lds, aux);
+  const DropCtx dc = drop_ctx(J, D);
+  const int wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  const int ntiles = (J.R + 31) >> 5;
+  const int q = lane_id() >> 4;
+  for (int tile = blockIdx.x * nwaves + wave; tile < ntiles; tile += gridDim.x * nwaves) {
+    const RowInfo ri = load_rows(J, tile);
+    bf16x8 xf[2][KS1];
+    load_x<KS1>(J, D, tile, ri, xf);
+    if (J.do_sdf) {
+      float w[2];
+      sdf_forward_tile<KS1>(lds, aux, D, dc, ri, xf, w);
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+        if (q == 0 && ri.dense[b] >= 0) J.w_out[ri.dense[b]] = w[b];
+    }
+    if (J.do_mom) mom_forward_tile<KS1, WMB>(lds, aux, D, J, dc, ri, xf);
+  }
+}
+
+// ============================== backward =================================================
+template <int UB>
+DLAP_DEV void to_rows_k(const bf16x8 (&pf)[2][(UB + 1) / 2], int blk, const bf16x8& s0,
+                        const bf16x8& s1, bf16x8& out) {
+  const bf16x8 sel = (blk & 1) ? s1 : s0;
+  out = pack8(mfma16(pf[0][blk >> 1], sel, zero4()), mfma16(pf[1][blk >> 1], sel, zero4()));
+}
+
+DLAP_DEV void x_rows_k(const bf16x8& x0, const bf16x8& x1, int blk, const bf16x8& s0,
+                       const bf16x8& s1, bf16x8& out) {
+  const bf16x8 sel = (blk & 1) ? s1 : s0;
+  out = pack8(mfma16(x0, sel, zero4()), mfma16(x1, sel, zero4()));
+}
+
+// One slab per workgroup: zero an LDS image (reusing the weight staging area), let the
+// waves add into it one after another (fixed order = deterministic), then store it.
+DLAP_DEV float* wg_slab_begin(char* smem, int slab_stride) {
+  __syncthreads();   // every wave is done with the staged weights
+  float* red = reinterpret_cast<float*>(smem);
+  for (int i = threadIdx.x; i < slab_stride; i += blockDim.x) red[i] = 0.f;
+  __syncthreads();
+  return red;
+}
+DLAP_DEV void wg_slab_store(const MlpJob& J, const float* red, int slab_stride) {
+  float* slab = J.slab + (size_t)(J.slab_base + blockIdx.z * gridDim.x + blockIdx.x) * slab_stride;
+  for (int i = threadIdx.x; i < slab_stride; i += blockDim.x) slab[i] = red[i];
+}
+
+// SDF backward. NL = number of hidden (MFMA) layers, all 64 wide.
+template <int KS1, int NL, int TPS>
+__global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict__ jobs, MlpDims D,
+                                                        int slab_stride) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const MlpJob& J = jobs[blockIdx.y];
+  bf16x8* lds = reinterpret_cast<bf16x8*>(smem);
+  float* aux = reinterpret_cast<float*>(smem + (size_t)D.blob_frags * 1024);
+  stage_weights(J, D, lds, aux);
+  const DropCtx dc = drop_ctx(J, D);
+  const int lane = lane_id(), q = lane >> 4, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  const int ntiles = (J.R + 31) >> 5;
+  const int slice = blockIdx.z;
+  constexpr int C0 = KS1 / 2;                // 64-column chunks of layer 0
+  const bf16x8 selP0 = make_sel(true, 0), selP1 = make_sel(true, 1);
+  const bf16x8 selN0 = make_sel(false, 0), selN1 = make_sel(false, 1);
+
+  f32x4 dW[TPS][4][4];
+#pragma unroll
+  for (int t = 0; t < TPS; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) dW[t][u][v] = zero4();
+  f32x4 gbias[4], gwo[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) { gbias[u] = zero4(); gwo[u] = zero4(); }
+  float gbo = 0.f;
+  int tl[TPS], tc[TPS];
+#pragma unroll
+  for (int t = 0; t < TPS; ++t) {
+    const int tid = slice * TPS + t;
+    tl[t] = tid < C0 ? 0 : tid - C0 + 1;
+    tc[t] = tid < C0 ? tid : 0;
+  }
+
+  for (int tile = blockIdx.x * nwaves + wave; tile < ntiles; tile += gridDim.x * nwaves) {
+    const RowInfo ri = load_rows(J, tile);
+    bf16x8 xf[2][KS1];
+    load_x<KS1>(J, D, tile, ri, xf);
+    // ---- forward recompute, keep packed activations + gates ----
+    bf16x8 act[NL][2][2];
+    uint32_t gates[NL][2];
+    f32x4 a[2][4];
+    layer0<KS1, 4>(lds, D.s_fwd0, xf, a);
+#pragma unroll
+    for (int j = 0; j < NL; ++j) {
+      if (j > 0) layer_chain<4, 2>(lds, D.s_fwd + (j - 1) * 8, act[j - 1], a);
+      relu_dropout<4>(a, aux + D.a_sb + 64 * j, aux + D.a_sb + 64 * j, dc, j, ri, gates[j]);
+      pack_blocks<4>(a, act[j]);
+    }
+    // ---- output layer: w = wo . a_last + bo ----
+    float dwr[2];
+#pragma unroll
+    for (int b = 0; b < 2; ++b) dwr[b] = ri.dense[b] >= 0 ? J.dw[ri.dense[b]] : 0.f;
+    f32x4 dz[2][4];
+    const float* wo = aux + D.a_wo;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const f32x4 ww = *reinterpret_cast<const f32x4*>(wo + 16 * u + 4 * q);
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        gwo[u] += dwr[b] * a[b][u];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool on = (gates[NL - 1][b] >> (u * 4 + r)) & 1u;
+          dz[b][u][r] = on ? dwr[b] * ww[r] * dc.scale : 0.f;
+        }
+      }
+    }
+    if (q == 0) gbo += dwr[0] + dwr[1];
+    // ---- backward chain ----
+#pragma unroll
+    for (int j = NL - 1; j >= 0; --j) {
+      bf16x8 dzf[2][2];
+      pack_blocks<4>(dz, dzf);
+      bf16x8 dzN[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) to_rows_k<4>(dzf, u, selP0, selP1, dzN[u]);
+      if (slice == 0) {
+        const bf16x8 oh = make_onehot(j);
+#pragma unroll
+        for (int u = 0; u < 4; ++u) gbias[u] = mfma16(dzN[u], oh, gbias[u]);
+      }
+#pragma unroll
+      for (int t = 0; t < TPS; ++t) {
+        if (tl[t] == j) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            bf16x8 aN;
+            if (j == 0) {
+              const int blk = 4 * tc[t] + v;
+              bf16x8 x0 = zero8(), x1 = zero8();
+#pragma unroll
+              for (int s = 0; s < KS1; ++s)
+                if (s == (blk >> 1)) { x0 = xf[0][s]; x1 = xf[1][s]; }
+              x_rows_k(x0, x1, blk, selN0, selN1, aN);
+            } else {
+              to_rows_k<4>(act[j > 0 ? j - 1 : 0], v, selP0, selP1, aN);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) dW[t][u][v] = mfma16(dzN[u], aN, dW[t][u][v]);
+          }
+        }
+      }
+      if (j > 0) {
+        f32x4 da[2][4];
+        layer_chain<4, 2>(lds, D.s_bwd + (j - 1) * 8, dzf, da);
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int u = 0; u < 4; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const bool on = (gates[j > 0 ? j - 1 : 0][b] >> (u * 4 + r)) & 1u;
+              dz[b][u][r] = on ? da[b][u][r] * dc.scale : 0.f;
+            }
+      } else if (D.nrnn > 0 && slice == 0) {
+        // dL/d(per-period input d) per row = sum_out W0[out][F + d] * dz0[out][row]
+        const float* wpp = aux + D.a_pp;
+        for (int d = 0; d < D.Dm; ++d) {
+#pragma unroll
+          for (int b = 0; b < 2; ++b) {
+            float s = 0.f;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              const f32x4 ww = *reinterpret_cast<const f32x4*>(wpp + d * 64 + 16 * u + 4 * q);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) s += dz[b][u][r] * ww[r];
+            }
+            s = reduce_q(s);
+            const int row = tile * 32 + 16 * b + (lane & 15);
+            if (q == 0 && row < J.R) J.u_out[(size_t)row * D.Dm + d] = s;
+          }
+        }
+      }
+    }
+  }
+  // ---- workgroup slab: waves add their partials into LDS in a fixed order ----
+  float* red = wg_slab_begin(smem, slab_stride);
+  for (int w = 0; w < nwaves; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int t = 0; t < TPS; ++t)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              red[t * 4096 + (16 * u + 4 * q + r) * 64 + 16 * v + (lane & 15)] += dW[t][u][v][r];
+      if (slice == 0) {
+        float* ex = red + TPS * 4096;
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            if ((lane & 15) < DLAP_MAXL) ex[(lane & 15) * 64 + 16 * u + 4 * q + r] += gbias[u][r];
+            float v = gwo[u][r];
+            v += __shfl_xor(v, 1, 64); v += __shfl_xor(v, 2, 64);
+            v += __shfl_xor(v, 4, 64); v += __shfl_xor(v, 8, 64);
+            if ((lane & 15) == 0) ex[DLAP_MAXL * 64 + 16 * u + 4 * q + r] += v;
+          }
+        const float sb = wave_sum(gbo);
+        if (lane == 0) ex[DLAP_MAXL * 64 + 64] += sb;
+      }
+    }
+    __syncthreads();
+  }
+  wg_slab_store(J, red, slab_stride);
+}
+
+// Moment backward (phase 2). NLM MFMA layers of WM = 16*WMB units; tanh on the last.
+template <int KS1, int WMB, int NLM, int TPS>
+__global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict__ jobs, MlpDims D,
+                                                        int slab_stride) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int KSM = (WMB + 1) / 2;
+  const MlpJob& J = jobs[blockIdx.y];
+  bf16x8* lds = reinterpret_cast<bf16x8*>(smem);
+  float* aux = reinterpret_cast<float*>(smem + (size_t)D.blob_frags * 1024);
+  stage_weights(J, D, lds, aux);
+  const DropCtx dc = drop_ctx(J, D);
+  const int lane = lane_id(), q = lane >> 4, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  const int ntiles = (J.R + 31) >> 5;
+  const int slice = blockIdx.z;
+  constexpr int C0 = KS1 / 2;
+  const bf16x8 selP0 = make_sel(true, 0), selP1 = make_sel(true, 1);
+  const bf16x8 selN0 = make_sel(false, 0), selN1 = make_sel(false, 1);
+
+  f32x4 dW[TPS][WMB][4];
+#pragma unroll
+  for (int t = 0; t < TPS; ++t)
+#pragma unroll
+    for (int u = 0; u < WMB; ++u)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) dW[t][u][v] = zero4();
+  f32x4 gbias[WMB];
+#pragma unroll
+  for (int u = 0; u < WMB; ++u) gbias[u] = zero4();
+  int tl[TPS], tc[TPS];
+#pragma unroll
+  for (int t = 0; t < TPS; ++t) {
+    const int tid = slice * TPS + t;
+    tl[t] = tid < C0 ? 0 : tid - C0 + 1;
+    tc[t] = tid < C0 ? tid : 0;
+  }
+
+  for (int tile = blockIdx.x * nwaves + wave; tile < ntiles; tile += gridDim.x * nwaves) {
+    const RowInfo ri = load_rows(J, tile);
+    bf16x8 xf[2][KS1];
+    load_x<KS1>(J, D, tile, ri, xf);
+    bf16x8 act[NLM][2][KSM];
+    uint32_t gates[NLM][2];
+    f32x4 a[2][WMB];
+    layer0<KS1, WMB>(lds, D.m_fwd0, xf, a);
+#pragma unroll
+    for (int j = 0; j < NLM; ++j) {
+      if (j > 0) layer_chain<WMB, KSM>(lds, D.m_fwd + (j - 1) * WMB * KSM, act[j - 1], a);
+      const float* b0 = j ? aux + D.a_mb + 64 * j : J.abias + ri.t[0] * 64;
+      const float* b1 = j ? aux + D.a_mb + 64 * j : J.abias + ri.t[1] * 64;
+      if (j + 1 < NLM) {
+        relu_dropout<WMB>(a, b0, b1, dc, 16 + j, ri, gates[j]);
+        pack_blocks<WMB>(a, act[j]);
+      } else {
+        // h = tanh(z); dz = dh (1 - h^2), dh = dE[i][k] R SDF_t / T_i
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const float* bp = b ? b1 : b0;
+          const int d = ri.dense[b];
+          const float cst = d >= 0 ? J.Rm[d] * J.sdfv[ri.t[b]] * J.invT[ri.i[b]] : 0.f;
+          const float* de = J.dE + (size_t)ri.i[b] * D.K;
+#pragma unroll
+          for (int u = 0; u < WMB; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int k = 16 * u + 4 * q + r;
+              const float h = tanhf(a[b][u][r] + bp[k]);
+              const float g = (d >= 0 && k < D.K) ? de[k] * cst : 0.f;
+              a[b][u][r] = g * (1.f - h * h);
+            }
+        }
+      }
+    }
+    f32x4 dz[2][WMB];
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int u = 0; u < WMB; ++u) dz[b][u] = a[b][u];
+#pragma unroll
+    for (int j = NLM - 1; j >= 0; --j) {
+      bf16x8 dzf[2][KSM];
+      pack_blocks<WMB>(dz, dzf);
+      bf16x8 dzN[WMB];
+#pragma unroll
+      for (int u = 0; u < WMB; ++u) to_rows_k<WMB>(dzf, u, selP0, selP1, dzN[u]);
+      if (slice == 0 && j > 0) {
+        const bf16x8 oh = make_onehot(j);
+#pragma unroll
+        for (int u = 0; u < WMB; ++u) gbias[u] = mfma16(dzN[u], oh, gbias[u]);
+      }
+#pragma unroll
+      for (int t = 0; t < TPS; ++t) {
+        if (tl[t] == j) {
+#pragma unroll
+          for (int v = 0; v < 4; ++v) {
+            if (j > 0 && v >= WMB) continue;
+            bf16x8 aN;
+            if (j == 0) {
+              const int blk = 4 * tc[t] + v;
+              bf16x8 x0 = zero8(), x1 = zero8();
+#pragma unroll
+              for (int s = 0; s < KS1; ++s)
+                if (s == (blk >> 1)) { x0 = xf[0][s]; x1 = xf[1][s]; }
+              x_rows_k(x0, x1, blk, selN0, selN1, aN);
+            } else {
+              to_rows_k<WMB>(act[j > 0 ? j - 1 : 0], v, selP0, selP1, aN);
+            }
+#pragma unroll
+            for (int u = 0; u < WMB; ++u) dW[t][u][v] = mfma16(dzN[u], aN, dW[t][u][v]);
+          }
+        }
+      }
+      if (j > 0) {
+        f32x4 da[2][WMB];
+        layer_chain<WMB, KSM>(lds, D.m_bwd + (j - 1) * WMB * KSM, dzf, da);
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int u = 0; u < WMB; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const bool on = (gates[j > 0 ? j - 1 : 0][b] >> (u * 4 + r)) & 1u;
+              dz[b][u][r] = on ? da[b][u][r] * dc.scale : 0.f;
+            }
+      } else if (slice == 0) {
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int row = tile * 32 + 16 * b + (lane & 15);
+          if (row < J.R) {
+#pragma unroll
+            for (int u = 0; u < WMB; ++u)
+              *reinterpret_cast<f32x4*>(J.v_out + (size_t)row * 64 + 16 * u + 4 * q) = dz[b][u];
+          }
+        }
+      }
+    }
+  }
+  float* red = wg_slab_begin(smem, slab_stride);
+  for (int w = 0; w < nwaves; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int t = 0; t < TPS; ++t)
+#pragma unroll
+        for (int u = 0; u < WMB; ++u)
+#pragma unroll
+          for (int v = 0; v < 4; ++v)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              red[t * 4096 + (16 * u + 4 * q + r) * 64 + 16 * v + (lane & 15)] += dW[t][u][v][r];
+      if (slice == 0) {
+        float* ex = red + TPS * 4096;
+#pragma unroll
+        for (int u = 0; u < WMB; ++u)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if ((lane & 15) < DLAP_MAXL) ex[(lane & 15) * 64 + 16 * u + 4 * q + r] += gbias[u][r];
+      }
+    }
+    __syncthreads();
+  }
+  wg_slab_store(J, red, slab_stride);
+}
+
+// ---- host launchers -------------------------------------------------------------------
+size_t mlp_lds_bytes(const MlpDims& D) { return (size_t)D.blob_frags * 1024 + (size_t)D.aux_floats * 4; }
+static size_t bwd_lds_bytes(const MlpDims& D, int slab_stride) {
+  size_t a = mlp_lds_bytes(D), b = (size_t)slab_stride * 4;
+  return a > b ? a : b;
+}
+
+void launch_mlp_fwd(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int KS1, int WMB,
+                    hipStream_t st) {
+  dim3 grid(gx, njobs), block(256);
+  size_t sh = mlp_lds_bytes(D);
+#define F_CASE(K, W) if (KS1 == K && WMB == W) { hipLaunchKernelGGL((k_mlp_fwd<K, W>), grid, block, sh, st, jobs, D); HIP_OK(hipGetLastError()); return; }
+  F_CASE(2, 1) F_CASE(2, 2) F_CASE(2, 4) F_CASE(4, 1) F_CASE(4, 2) F_CASE(4, 4)
+#undef F_CASE
+  dlap_throw_hip(hipErrorInvalidValue, "mlp_fwd: unsupported (KS1, WMB)", __FILE__, __LINE__);
+}
+
+void launch_mlp_bwd_sdf(const MlpJob* jobs, int njobs, int gx, int nslice, int tps, const MlpDims& D,
+                        int KS1, int slab_stride, hipStream_t st) {
+  dim3 grid(gx, njobs, nslice), block(256);
+  size_t sh = bwd_lds_bytes(D, slab_stride);
+#define S_CASE(K, N, T) if (KS1 == K && D.nl_sdf == N && tps == T) { hipLaunchKernelGGL((k_mlp_bwd_sdf<K, N, T>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
+  S_CASE(2, 1, 1) S_CASE(2, 2, 1) S_CASE(2, 3, 1) S_CASE(2, 4, 1)
+  S_CASE(2, 2, 2)
+  S_CASE(4, 1, 1) S_CASE(4, 2, 1) S_CASE(4, 3, 1) S_CASE(4, 4, 1)
+#undef S_CASE
+  dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_sdf: unsupported depth/tiling", __FILE__, __LINE__);
+}
+
+void launch_mlp_bwd_mom(const MlpJob* jobs, int njobs, int gx, int nslice, int tps, const MlpDims& D,
+                        int KS1, int WMB, int slab_stride, hipStream_t st) {
+  dim3 grid(gx, njobs, nslice), block(256);
+  size_t sh = bwd_lds_bytes(D, slab_stride);
+#define M_CASE(K, W, N) if (KS1 == K && WMB == W && D.nl_mom == N && tps == 1) { hipLaunchKernelGGL((k_mlp_bwd_mom<K, W, N, 1>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
+  M_CASE(2, 1, 1) M_CASE(2, 2, 1) M_CASE(2, 4, 1)
+  M_CASE(2, 1, 2) M_CASE(2, 2, 2) M_CASE(2, 4, 2)
+  M_CASE(2, 1, 3) M_CASE(2, 2, 3) M_CASE(2, 4, 3)
+  M_CASE(4, 1, 1) M_CASE(4, 2, 1) M_CASE(4, 4, 1)
+  M_CASE(4, 1, 2) M_CASE(4, 2, 2) M_CASE(4, 4, 2)
+#undef M_CASE
+  dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_mom: unsupported depth/width", __FILE__, __LINE__);
+}

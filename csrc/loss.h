@@ -1,0 +1,48 @@
+// Job record of the loss / metric kernels (k_loss.hip), shared with the engine.
+#pragma once
+#include "common.h"
+
+#define DLAP_MAX_T 2048   // max periods per split handled by the LDS-staged passes
+
+// Scalar slots written per job by k_job_metrics.
+enum {
+  SC_LCOND = 0, SC_LUNC = 1, SC_LRES = 2, SC_TRAIN_SHARPE = 3,
+  SC_SHARPE = 4, SC_MEAN = 5, SC_STD = 6, SC_MDD = 7, SC_NSCAL = 8
+};
+
+struct LossJob {
+  // panel constants of the split
+  const float* Rm;       // [T*N] returns, zero at invalid entries
+  const float* mask;     // [T*N] 0/1
+  const float* invNt;    // [T] 1 / max(N_t, 1)
+  const float* Nt;       // [T] N_t
+  const float* meanR;    // [T] sum_i R m / max(N_t, 1)
+  const float* RR;       // [T] sum_i R^2 m
+  const float* invT;     // [N] 1 / max(T_i, 1)
+  float Nbar;
+  int T, N, K;
+  int normalize, weighted;
+  int phase;             // 1: unconditional, 2: moment, 3: conditional, 0: evaluation
+  float res_factor;      // residual_loss_factor (gradient only in training jobs)
+  float coef_c, coef_u;  // dL/dE = coef * E (0 disables the write)
+  // per (model, split) workspace
+  const float* w;        // [T*N] raw SDF output
+  float* wn;             // [T*N] normalised weights w'
+  const float* h;        // [T*N*K] moments (nullptr: unconditional only)
+  float* P;              // [T] weighted portfolio return
+  float* port;           // [T] L1-normalised portfolio return (nullptr: skip)
+  float* sdfv;           // [T] 1 + P_t
+  float* E;              // [N*K]
+  float* Eu;             // [N]
+  float* dE;             // [N*K] (nullptr: skip)
+  float* dEu;            // [N]   (nullptr: skip)
+  float* part;           // [2 * ceil(N/64)] partial loss sums
+  float* dw;             // [T*N]
+  float* rstat;          // [T*4] residual statistics (nullptr: residual loss off)
+  float* scal;           // [SC_NSCAL]
+};
+
+void launch_period_fwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st);
+void launch_asset(const LossJob* jobs, int njobs, int nmax, hipStream_t st);
+void launch_period_bwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st);
+void launch_job_metrics(const LossJob* jobs, int njobs, hipStream_t st);

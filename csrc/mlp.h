@@ -1,0 +1,51 @@
+// Job / dimension records of the fused tower kernels (k_mlp.hip), shared with the engine.
+#pragma once
+#include "common.h"
+
+struct MlpJob {
+  const bf16x8* X;        // [R][KP/8] bf16 panel rows (cols [F, F+Dm) reserved, zero)
+  const int* row_dense;   // [R] dense index t*N + i
+  const float* pp;        // [T][Dm] per-period SDF inputs (LSTM output or raw macro)
+  const float* abias;     // [T][64] moment layer-0 per-period bias (W_macro . m_t + b)
+  const bf16x8* blob;     // packed weight fragments of this job's model
+  const float* aux;       // fp32 biases / output row of this job's model
+  float* w_out;           // fwd: dense [T*N] raw SDF weights (valid rows written)
+  float* h_out;           // fwd: dense [T*N][K] moments (valid rows written)
+  const float* dw;        // bwd sdf: dense [T*N] dL/dw_raw
+  const float* dE;        // bwd mom: [N][K] dL/dE
+  const float* Rm;        // dense [T*N] returns (zero-filled)
+  const float* sdfv;      // [T] SDF_t = 1 + P_t
+  const float* invT;      // [N] 1 / max(T_i, 1)
+  float* slab;            // bwd: per-wave gradient partials
+  float* u_out;           // bwd sdf: [R][Dm] dL/d(per-period inputs) per row
+  float* v_out;           // bwd mom: [R][64] dL/d(moment layer-0 pre-activation) per row
+  const int* step;        // device step counter (dropout stream)
+  int R, N;
+  unsigned seed;
+  int train;              // dropout active
+  int do_sdf, do_mom;     // fwd: towers to evaluate
+  int slab_base;          // bwd: first slab index of this job
+};
+
+// Scalars every tower kernel needs (small, passed by value).
+struct MlpDims {
+  int F, Dm, K, cm1;      // features, per-period cols, moments, moment layer-0 width
+  int nrnn;               // >0: an LSTM feeds the per-period columns (per-row dpp needed)
+  int nl_sdf, nl_mom;     // MFMA layers per tower
+  float dropout;
+  int s_fwd0, s_fwd, s_bwd;      // blob frag offsets: SDF layer 0, chain fwd base, chain bwd base
+  int m_fwd0, m_fwd, m_bwd;      // moment tower
+  int a_sb, a_wo, a_bo, a_pp, a_mb;   // aux offsets: SDF biases [nl][64], out row [64], out
+                                      // bias, W0 per-period cols [Dm][64], moment biases [nl][64]
+  int blob_frags, aux_floats;
+};
+
+#define SLAB_EXTRA (DLAP_MAXL * 64 + 64 + 64)
+
+size_t mlp_lds_bytes(const MlpDims& D);
+void launch_mlp_fwd(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int KS1, int WMB,
+                    hipStream_t st);
+void launch_mlp_bwd_sdf(const MlpJob* jobs, int njobs, int gx, int nslice, int tps, const MlpDims& D,
+                        int KS1, int slab_stride, hipStream_t st);
+void launch_mlp_bwd_mom(const MlpJob* jobs, int njobs, int gx, int nslice, int tps, const MlpDims& D,
+                        int KS1, int WMB, int slab_stride, hipStream_t st);

@@ -1,0 +1,23 @@
+// Job record of the LSTM / prologue kernel (k_rnn.hip).
+#pragma once
+#include "common.h"
+
+struct ModelDesc;
+
+struct RnnJob {
+  const float* params;   // flat parameters of this job's model
+  const float* macro;    // [T][M] standardised macro series of the split
+  int T;
+  float* out;            // [T][H] last-layer LSTM output (the SDF per-period inputs)
+  float* sg;             // train: saved post-activation gates [nrnn][T][4H] (else nullptr)
+  float* sc;             // train: saved cell states [nrnn][T][H]
+  float* sh;             // train: saved layer outputs [nrnn][T][H]
+  float* xg;             // scratch [T][4H]
+  float* xin;            // scratch [T][H]
+  float* abias;          // [T][64] moment layer-0 per-period bias (nullptr: skip)
+  const int* step;       // dropout stream counter
+  unsigned seed;
+  int train;
+};
+
+void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* md, hipStream_t st);

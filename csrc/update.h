@@ -1,0 +1,70 @@
+// Job records of the gradient-finalise / optimiser / bookkeeping kernels (k_update.hip).
+#pragma once
+#include "common.h"
+
+struct ModelDesc;
+
+struct FinJob {            // one model
+  const float* slab;       // first slab of this model (slices contiguous, gx slabs each)
+  float* grads;            // flat gradient vector [P]
+  const int* row_ptr;      // [T+1] compact-row offsets of the train split
+  const float* u;          // [R][Dm] per-row d(per-period SDF input)
+  float* dpp;              // [T][Dm]
+  const float* v;          // [R][64] per-row d(moment layer-0 pre-activation)
+  float* dab;              // [T][64]
+  int T;
+  int nslab;               // slabs per slice
+};
+
+struct UpdJob {            // one model
+  float* params;
+  float* grads;
+  float* m;                // Adam first moments [P]
+  float* v;                // Adam second moments [P]
+  int* adam_step;          // [2] optimiser step counts (sdf, moment)
+  int* drop_step;          // dropout stream counter
+  float* gnorm;            // [1] pre-clip gradient norm of the step
+  bf16x8* blob;
+  float* aux;
+  const float* dpp;        // [T][Dm] d(LSTM output)
+  const float* macro;      // [T][M] train macro series
+  const float* sg;         // [nrnn][T][4H] saved gates
+  const float* sc;         // [nrnn][T][H]  saved cells
+  const float* sh;         // [nrnn][T][H]  saved layer outputs
+  float* dg;               // scratch [T][4H]
+  float* dx;               // scratch [T][H]
+  const float* dab;        // [T][64]
+  int T;
+  unsigned seed;
+};
+
+// History row written per epoch by k_epoch_end (HIST_W floats).
+enum {
+  H_PHASE = 0, H_TRAIN_LOSS, H_TRAIN_SHARPE, H_VALID_LOSS, H_VALID_SHARPE, H_TEST_LOSS,
+  H_TEST_SHARPE, H_TRAIN_LUNC, H_TRAIN_LCOND, H_GNORM, H_VALID_LUNC, H_VALID_LCOND,
+  H_VALID_MDD, H_VALID_MEAN, H_VALID_STD, H_TEST_LUNC, H_TEST_LCOND, H_TEST_MDD,
+  H_TEST_MEAN, H_TEST_STD, H_TRAIN_LRES, H_BEST_LOSS, H_BEST_SR, H_SNAP, HIST_W = 24
+};
+
+struct EpochJob {          // one model
+  const float* sc_train;   // job scalars (SC_*) of the train job
+  const float* sc_valid;   // nullptr in phase 2
+  const float* sc_test;    // nullptr if no test split / phase 2
+  const float* gnorm;
+  float* hist;             // [max_epochs][HIST_W]
+  int* ep;                 // [2] global epoch index, epoch within the phase
+  float* best;             // [3] best valid loss, best (signed) valid Sharpe, best moment loss
+  int* snap_flags;         // [2] loss snapshot taken, Sharpe snapshot taken (this phase)
+  const float* params;
+  float* snap_loss;        // [P]
+  float* snap_sharpe;      // [P]
+};
+
+void launch_finalize(const FinJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
+                     int phase, int slab_stride, int tmax, hipStream_t st);
+void launch_update(const UpdJob* jobs, int njobs, const ModelDesc* md, int phase, float lr,
+                   hipStream_t st, int apply = 1);
+void launch_pack(float* const* params_unused, const UpdJob* jobs, int njobs, const ModelDesc* md,
+                 hipStream_t st);
+void launch_epoch_end(const EpochJob* jobs, int njobs, int phase, int ignore_epoch, float sel,
+                      float res_factor, int P, hipStream_t st);

@@ -1,0 +1,83 @@
+"""Build the native HIP extension ``_dlap_hip`` in-tree with hipcc (gfx950 only).
+
+Every ``csrc/*.hip`` kernel file and the C++ runtime ``csrc/engine.cpp`` are compiled as
+separate objects (in parallel, cached by source hash) and linked into
+``deeplearninginassetpricing_paperreplication_amd/_dlap_hip*.so``. No torch headers are
+involved: the runtime talks to Python through pybind11 and to the GPU through HIP directly.
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import hashlib
+import os
+import subprocess
+import sys
+import sysconfig
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parents[2]
+CSRC = ROOT / "csrc"
+PKG = ROOT / "deeplearninginassetpricing_paperreplication_amd"
+BUILD = ROOT / "build" / "native"
+ARCH = os.environ.get("DLAP_OFFLOAD_ARCH", "gfx950")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+
+
+def ext_path() -> Path:
+    suffix = sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+    return PKG / f"_dlap_hip{suffix}"
+
+
+def _includes():
+    import pybind11
+    return [f"-I{CSRC}", f"-I{pybind11.get_include()}", f"-I{sysconfig.get_paths()['include']}"]
+
+
+def _hash(files) -> str:
+    h = hashlib.sha256()
+    for f in sorted(files):
+        h.update(f.name.encode())
+        h.update(f.read_bytes())
+    h.update(ARCH.encode())
+    return h.hexdigest()[:16]
+
+
+def _compile(src: Path, obj: Path, flags):
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", *flags, "-c", str(src), "-o", str(obj)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src.name}:\n{r.stderr[-4000:]}")
+    return obj
+
+
+def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> Path:
+    srcs = sorted(CSRC.glob("*.hip")) + [CSRC / "engine.cpp"]
+    headers = sorted(CSRC.glob("*.h"))
+    out = ext_path()
+    stamp = BUILD / "stamp"
+    key = _hash(srcs + headers)
+    if not force and out.exists() and stamp.exists() and stamp.read_text() == key:
+        if verbose:
+            print(f"[dlap] native extension up to date: {out.name}")
+        return out
+    BUILD.mkdir(parents=True, exist_ok=True)
+    flags = _includes() + ["-Wno-unused-result"]
+    objs = []
+    with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(srcs)))) as ex:
+        futs = {ex.submit(_compile, s, BUILD / (s.stem + ".o"), flags): s for s in srcs}
+        for f in cf.as_completed(futs):
+            objs.append(f.result())
+            if verbose:
+                print(f"[dlap] compiled {futs[f].name}")
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, sorted(objs)), "-o", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
+    stamp.write_text(key)
+    if verbose:
+        print(f"[dlap] built {out}")
+    return out
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv)

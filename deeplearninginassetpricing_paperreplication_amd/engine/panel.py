@@ -1,0 +1,79 @@
+"""Host-side preparation of a split for the native engine.
+
+The reference keeps the full dense [T, N, F] panel on the CPU and copies it to the device
+every epoch (`/root/reference/src/train.py:69-75`). Here a split is uploaded once and kept in
+HBM in a compacted layout:
+
+  X         [R, KP] bf16   valid rows only, in (t, i) order; columns [F, F+Dm) are left zero
+                           (the kernels insert the per-period LSTM / macro inputs there)
+  row_dense [R]     int32  t*N + i of each compact row
+  row_ptr   [T+1]   int32  first compact row of each period
+  Rm, mask  [T*N]   fp32   dense returns (zero-filled) and 0/1 mask
+  macro     [T, M]  fp32   standardised macro series
+
+Masked rows never influence weights, losses or metrics (they are multiplied by the mask
+everywhere in the reference), so the compaction is exact and cuts tower work by the
+invalid fraction (~60% on the real data).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+
+def f32_to_bf16_bits(x: np.ndarray) -> np.ndarray:
+    """Round-to-nearest-even fp32 -> bf16 (as uint16 bit patterns)."""
+    u = np.ascontiguousarray(x, dtype=np.float32).view(np.uint32)
+    r = ((u + np.uint32(0x7FFF) + ((u >> np.uint32(16)) & np.uint32(1))) >> np.uint32(16)).astype(np.uint16)
+    return r
+
+
+def bf16_bits_to_f32(b: np.ndarray) -> np.ndarray:
+    return (b.astype(np.uint32) << np.uint32(16)).view(np.float32)
+
+
+@dataclass
+class PanelSplit:
+    T: int
+    N: int
+    R: int
+    X: np.ndarray          # uint16 [R, KP]
+    row_dense: np.ndarray  # int32 [R]
+    row_ptr: np.ndarray    # int32 [T+1]
+    Rm: np.ndarray         # float32 [T*N]
+    mask: np.ndarray       # float32 [T*N]
+    macro: np.ndarray      # float32 [T, M] (or empty)
+
+
+def _np(a) -> np.ndarray:
+    if isinstance(a, torch.Tensor):
+        return a.detach().cpu().numpy()
+    return np.asarray(a)
+
+
+def prepare_split(batch: Dict, KP: int) -> PanelSplit:
+    """Compact a ``get_full_batch()``-style dict (torch or numpy) for the engine."""
+    feats = _np(batch["individual_features"]).astype(np.float32, copy=False)
+    ret = _np(batch["returns"]).astype(np.float32, copy=False)
+    mask = _np(batch["mask"]).astype(bool, copy=False)
+    T, N, F = feats.shape
+    if F > KP:
+        raise ValueError(f"feature dim {F} exceeds engine row width {KP}")
+    tt, ii = np.nonzero(mask)                      # row-major: sorted by t then i
+    R = len(tt)
+    X = np.zeros((R, KP), dtype=np.uint16)
+    if R:
+        X[:, :F] = f32_to_bf16_bits(feats[tt, ii])
+    row_dense = (tt.astype(np.int64) * N + ii).astype(np.int32)
+    counts = mask.sum(axis=1)
+    row_ptr = np.zeros(T + 1, dtype=np.int32)
+    np.cumsum(counts, out=row_ptr[1:])
+    macro = batch.get("macro_features")
+    macro = np.zeros((T, 0), np.float32) if macro is None else _np(macro).astype(np.float32)
+    return PanelSplit(T, N, R, X, row_dense, row_ptr,
+                      np.ascontiguousarray(np.where(mask, ret, 0).reshape(-1), dtype=np.float32),
+                      np.ascontiguousarray(mask.reshape(-1), dtype=np.float32),
+                      np.ascontiguousarray(macro))

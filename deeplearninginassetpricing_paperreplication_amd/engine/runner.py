@@ -1,0 +1,259 @@
+"""Python driver of the native engine: model <-> flat parameters, the GPU ``train_3phase``.
+
+``GANEngine`` trains G models of one architecture at once on one GPU (ensemble members or
+sweep configurations that share a shape). The schedule is `/root/reference/src/train.py:156-426`
+executed as hipGraph replays of one captured epoch per phase; the host only synchronises at
+``print_freq`` boundaries and at phase ends, where it also writes the checkpoint files whose
+final on-disk state equals the reference's "last writer wins" sequence.
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..config import ModelSpec
+from ..ops.native import load as load_native
+from .panel import prepare_split
+
+HIST = dict(phase=0, train_loss=1, train_sharpe=2, valid_loss=3, valid_sharpe=4, test_loss=5,
+            test_sharpe=6, train_loss_unc=7, train_loss_cond=8, grad_norm=9, valid_loss_unc=10,
+            valid_loss_cond=11, valid_mdd=12, valid_mean=13, valid_std=14, test_loss_unc=15,
+            test_loss_cond=16, test_mdd=17, test_mean=18, test_std=19, train_loss_res=20,
+            best_loss=21, best_sharpe=22)
+SC = dict(loss_cond=0, loss_unc=1, loss_res=2, train_sharpe=3, sharpe=4, mean=5, std=6, mdd=7)
+
+
+def flatten_state(model_or_sd, spec: ModelSpec) -> np.ndarray:
+    sd = model_or_sd.state_dict() if hasattr(model_or_sd, "state_dict") else model_or_sd
+    parts = []
+    for k, shp in spec.param_layout():
+        t = sd[k].detach().float().cpu()
+        if tuple(t.shape) != tuple(shp):
+            raise ValueError(f"{k}: shape {tuple(t.shape)} != {shp}")
+        parts.append(t.reshape(-1).numpy())
+    return np.ascontiguousarray(np.concatenate(parts), dtype=np.float32)
+
+
+def unflatten_state(flat: np.ndarray, spec: ModelSpec) -> Dict[str, torch.Tensor]:
+    out, o = {}, 0
+    for k, shp in spec.param_layout():
+        n = int(np.prod(shp))
+        out[k] = torch.from_numpy(np.array(flat[o:o + n], dtype=np.float32).reshape(shp))
+        o += n
+    return out
+
+
+class GANEngine:
+    """Native multi-model trainer for one architecture (``spec``) on the current GPU."""
+
+    def __init__(self, spec: ModelSpec, n_models: int = 1, max_epochs: int = 4096):
+        nat = load_native()
+        self.spec = spec
+        self.G = n_models
+        self.eng = nat.Engine(
+            F=spec.individual_dim, M=spec.macro_dim, nrnn=spec.rnn_layers, H=spec.rnn_hidden,
+            raw_macro_sdf=(spec.rnn_layers == 0 and spec.macro_dim > 0),
+            hidden=list(spec.hidden), mom_hidden=list(spec.moment_hidden), K=spec.num_moments,
+            dropout=spec.dropout, normalize_w=spec.normalize_w, weighted=spec.weighted_loss,
+            residual=spec.residual_loss_factor, G=n_models, max_epochs=max_epochs)
+        self.desc = self.eng.describe()
+        self.KP = int(self.desc["KP"])
+        self.splits: Dict[int, object] = {}
+
+    # ---- data -----------------------------------------------------------------------
+    def set_data(self, train: Dict, valid: Optional[Dict] = None, test: Optional[Dict] = None):
+        for s, b in enumerate((train, valid, test)):
+            if b is None:
+                continue
+            ps = prepare_split(b, self.KP)
+            self.eng.set_split(s, ps.X.reshape(-1), ps.row_dense, ps.row_ptr, ps.Rm, ps.mask,
+                               ps.macro.reshape(-1), ps.T, ps.N)
+            self.splits[s] = ps
+
+    # ---- parameters -----------------------------------------------------------------
+    def set_model(self, g: int, model, seed: int):
+        self.eng.set_params(g, flatten_state(model, self.spec))
+        self.eng.set_seed(g, int(seed) & 0xFFFFFFFF)
+
+    def params(self, g: int, which: str = "current") -> np.ndarray:
+        if which == "current":
+            return self.eng.get_params(g)
+        return self.eng.get_snapshot(g, 0 if which == "loss" else 1)
+
+    def state_dict(self, g: int, which: str = "current") -> Dict[str, torch.Tensor]:
+        return unflatten_state(self.params(g, which), self.spec)
+
+    # ---- execution ------------------------------------------------------------------
+    def run(self, phase: int, n: int, lr: float, ignore_epoch: int, selection_sign: float = 1.0,
+            use_graph: bool = True):
+        self.eng.run_epochs(phase, n, lr, ignore_epoch, selection_sign, use_graph)
+
+    def history_rows(self, g: int) -> np.ndarray:
+        return self.eng.history(g)
+
+    def evaluate(self, s: int) -> List[Dict]:
+        """Eval-mode forward of split ``s`` for every model: metrics of `src/train.py:106-153`."""
+        self.eng.forward_split(s, False, True)
+        out = []
+        for g in range(self.G):
+            sc = self.eng.read_ws(g, s, "scal")
+            port = self.eng.read_ws(g, s, "port")
+            w = self.eng.read_ws(g, s, "wn")
+            ps = self.splits[s]
+            lres = sc[SC["loss_res"]] * self.spec.residual_loss_factor
+            sd_u = float(np.std(port, ddof=1)) if len(port) > 1 else float("nan")
+            sh = 0.0 if sd_u < 1e-8 else float(np.mean(port) / sd_u)
+            l1 = np.abs(w.reshape(ps.T, ps.N)).sum(axis=1, keepdims=True)
+            wn = w.reshape(ps.T, ps.N) / np.maximum(l1, 1e-8)
+            out.append({
+                "loss": float(sc[SC["loss_cond"]] + lres), "loss_unc": float(sc[SC["loss_unc"]]),
+                "loss_cond": float(sc[SC["loss_cond"]]), "sharpe": sh,
+                "max_drawdown": float(sc[SC["mdd"]]), "mean_return": float(np.mean(port)),
+                "std_return": float(np.std(port)), "weights": torch.from_numpy(wn.astype(np.float32)),
+                "portfolio_returns": port,
+            })
+        return out
+
+
+def _hist_to_dict(rows: np.ndarray, has_test: bool) -> Dict[str, list]:
+    keep = rows[rows[:, HIST["phase"]] != 2]
+    h = {
+        "train_loss": keep[:, HIST["train_loss"]].astype(np.float64).tolist(),
+        "train_sharpe": keep[:, HIST["train_sharpe"]].astype(np.float64).tolist(),
+        "valid_loss": keep[:, HIST["valid_loss"]].astype(np.float64).tolist(),
+        "valid_sharpe": keep[:, HIST["valid_sharpe"]].astype(np.float64).tolist(),
+        "test_loss": keep[:, HIST["test_loss"]].astype(np.float64).tolist() if has_test else [],
+        "test_sharpe": keep[:, HIST["test_sharpe"]].astype(np.float64).tolist() if has_test else [],
+        "phase": ["unc" if p == 1 else "cond" for p in keep[:, HIST["phase"]]],
+    }
+    return h
+
+
+def _save_sd(eng: GANEngine, g: int, which: str, path: str, template):
+    template.load_state_dict(eng.state_dict(g, which))
+    torch.save(template.state_dict(), path)
+
+
+def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None,
+                     num_epochs_unc=256, num_epochs_moment=64, num_epochs=1024, lr=1e-3,
+                     print_freq=128, save_dir=None, ignore_epoch=64, seed=None,
+                     precision="bf16", selection_sign=1.0, verbose=True, n_models=1,
+                     models=None, seeds=None, save_dirs=None):
+    """GPU executor of the 3-phase schedule; with ``n_models > 1`` trains an ensemble batch.
+
+    Returns ``(model, history)`` for a single model, or ``(models, histories)`` when
+    ``n_models > 1`` (``models``/``seeds``/``save_dirs`` give per-member inputs).
+    """
+    from ..models.gan import AssetPricingGAN
+    if precision != "bf16":
+        raise NotImplementedError("the native engine currently computes the tower GEMMs in bf16 "
+                                  "(fp32 accumulation / master weights); use the CPU path for fp32")
+    say = print if verbose else (lambda *a, **k: None)
+    dev = torch.device(device) if device is not None else torch.device("cuda")
+    if dev.index is not None:
+        torch.cuda.set_device(dev)
+    if models is None:
+        models = [AssetPricingGAN(config) for _ in range(n_models)]
+    n_models = len(models)
+    if seeds is None:
+        base = torch.initial_seed() if seed is None else seed
+        seeds = [int(base) + 7919 * g for g in range(n_models)]
+    if save_dirs is None:
+        save_dirs = [save_dir] * n_models if n_models == 1 else [None] * n_models
+    spec = models[0].spec
+    n_sdf, n_mom = spec.param_counts()
+    say(f"Model has {n_sdf + n_mom:,} trainable parameters")
+    say(f"  SDF network: {n_sdf:,}")
+    say(f"  Moment network: {n_mom:,}")
+    total = num_epochs_unc + num_epochs_moment + num_epochs
+    eng = GANEngine(spec, n_models, max_epochs=max(total, 1))
+    eng.set_data(train_data, valid_data, test_data)
+    for g, m in enumerate(models):
+        eng.set_model(g, m, seeds[g])
+    template = AssetPricingGAN(config)
+    t_start = time.time()
+    best_state = [False] * n_models
+
+    def run_phase(phase, n, title, tag):
+        if verbose:
+            print("\n" + "=" * 70 + f"\n{title}\nEpochs: {n}\n" + "=" * 70 + "\n")
+        eng.eng.begin_phase(phase)
+        done = 0
+        ep0 = eng.eng.epoch_count(0)
+        marks = sorted({0} | set(range(print_freq - 1, n, print_freq)) | {n - 1}) if n > 0 else []
+        for mk in marks:
+            k = mk + 1 - done
+            if k <= 0:
+                continue
+            t0 = time.time()
+            eng.run(phase, k, lr, ignore_epoch, selection_sign)
+            eng.eng.sync()
+            dt = (time.time() - t0) / k
+            done = mk + 1
+            if verbose and ((mk + 1) % print_freq == 0 or mk == 0):
+                r = eng.history_rows(0)[ep0 + mk]
+                if phase == 2:
+                    print(f"Epoch {mk + 1:4d}/{n} ({dt:.4f}s) | Conditional loss: {r[HIST['train_loss_cond']]:.6f}")
+                else:
+                    msg = (f"Epoch {mk + 1:4d}/{n} ({dt:.4f}s) | Train: loss={r[HIST['train_loss']]:.4f} "
+                           f"sharpe={r[HIST['train_sharpe']]:.2f} | Valid: loss={r[HIST['valid_loss']]:.4f} "
+                           f"sharpe={r[HIST['valid_sharpe']]:.2f}")
+                    if test_data is not None:
+                        msg += f" | Test sharpe={r[HIST['test_sharpe']]:.2f}"
+                    print(msg)
+        # checkpoint files (final state of the reference's per-improvement writes)
+        for g in range(n_models):
+            fl = eng.eng.snap_flags(g)
+            if fl[1]:
+                best_state[g] = True
+            d = save_dirs[g]
+            if d:
+                if fl[0]:
+                    _save_sd(eng, g, "loss", os.path.join(d, "best_model_loss.pt"), template)
+                if fl[1]:
+                    _save_sd(eng, g, "sharpe", os.path.join(d, "best_model_sharpe.pt"), template)
+
+    run_phase(1, num_epochs_unc, "PHASE 1: Training Unconditional Loss (E[w*R]^2)", "unc")
+    say("\nPhase 1 Complete!")
+    for g in range(n_models):
+        if best_state[g]:
+            eng.eng.load_snapshot(g, 1)
+    if best_state[0]:
+        say("Loaded best model from Phase 1")
+    run_phase(2, num_epochs_moment, "PHASE 2: Updating Moment Conditions", "mom")
+    say("\nPhase 2 Complete!")
+    run_phase(3, num_epochs, "PHASE 3: Training Conditional Loss (E[h*w*R]^2)", "cond")
+    elapsed = time.time() - t_start
+    for g in range(n_models):
+        if best_state[g]:
+            eng.eng.load_snapshot(g, 1)
+    say("\n" + "=" * 70 + "\nTraining Complete!")
+    say(f"Total time: {elapsed / 60:.1f} minutes")
+    say(f"Total epochs: {total} ({num_epochs_unc} + {num_epochs_moment} + {num_epochs})\n" + "=" * 70)
+    finals = {s: eng.evaluate(s) for s in eng.splits}
+    if verbose:
+        print("\nBest Model Performance (normalized weights):")
+        for s, name in ((0, "Train"), (1, "Valid"), (2, "Test ")):
+            if s in finals:
+                f = finals[s][0]
+                print(f"  {name} - Sharpe: {f['sharpe']:7.3f}, MaxDD: {f['max_drawdown']:7.2%}")
+        print("=" * 70)
+    out_models, hists = [], []
+    for g in range(n_models):
+        m = models[g]
+        m.load_state_dict(eng.state_dict(g, "current"))
+        m.to(dev)
+        m.engine_final_eval = {s: finals[s][g] for s in finals}
+        if save_dirs[g]:
+            torch.save(m.state_dict(), os.path.join(save_dirs[g], "final_model.pt"))
+        hists.append(_hist_to_dict(eng.history_rows(g), test_data is not None))
+        out_models.append(m)
+    train_3phase_gpu.last_engine = eng
+    train_3phase_gpu.last_elapsed = elapsed
+    if n_models == 1:
+        return out_models[0], hists[0]
+    return out_models, hists
