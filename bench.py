@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 BENCH = dict(T_train=240, T_valid=60, T_test=300, N=3000, F=46, M=178)
 # reference CPU epochs/sec on this exact config and schedule mix (tools/ref_baseline.py,
 # 8-core Xeon, torch 2.10 CPU; see BASELINE.md "Measured on this box")
-REF_EPOCHS_PER_S = float(os.environ.get("DLAP_REF_EPOCHS_PER_S", "0.2488"))
+REF_EPOCHS_PER_S = float(os.environ.get("DLAP_REF_EPOCHS_PER_S", "0.397"))
 
 
 def make_panel(seed: int = 0, device: str = "cpu", T=None, N=None, F=None, M=None):

@@ -66,10 +66,17 @@ DLAP_DEV uint32_t dropout_key(uint32_t seed, uint32_t step, uint32_t layer) {
   return fmix32(seed * 0x9E3779B1u ^ fmix32(step * 0x632BE59Bu + layer * 0x1B873593u + 0x5bd1e995u));
 }
 // keep(row, unit): independent Bernoulli(1-p) per (dense row, unit) for a given key.
-// thr = round(p * 2^24); keep iff top 24 bits of the hash >= thr.
+// thr = round(p * 2^24); keep iff top 24 bits of the hash >= thr. (Used where a single
+// decision is needed: LSTM inter-layer dropout.)
 DLAP_DEV bool dropout_keep(uint32_t key, uint32_t row, uint32_t unit, uint32_t thr) {
   uint32_t h = fmix32(key ^ (row * 0xcc9e2d51u) ^ (unit * 0x27d4eb2fu) ^ (row >> 16));
   return (h >> 8) >= thr;
+}
+// Two decisions from one hash for the unit pair (2*pair, 2*pair+1): 16-bit thresholds
+// thr16 = round(p * 2^16) (p = 0.05 -> 0.050003). rowmix = row * 0xcc9e2d51 ^ (row >> 16)
+// is hoisted per row by the caller. Branch-free: evaluated for every element.
+DLAP_DEV uint32_t dropout_pair(uint32_t key, uint32_t rowmix, uint32_t pair) {
+  return fmix32(key ^ rowmix ^ (pair * 0x27d4eb2fu));
 }
 
 // ---- wave / block reductions (fixed order) --------------------------------------------

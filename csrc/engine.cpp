@@ -62,14 +62,14 @@ struct SplitDev {
   int T = 0, N = 0, R = 0;
   float Nbar = 0.f;
   DevBuf<uint16_t> X;
-  DevBuf<int> row_dense, row_ptr;
-  DevBuf<float> Rm, mask, invNt, Nt, meanR, RR, invT, macro;
+  DevBuf<int> rowti, row_ptr;        // rowti: [R] (t, i) int2
+  DevBuf<float> Rm, mask, invNt, Nt, meanR, RR, invT, macro, Rc;
   bool set = false;
 };
 
 struct ModelSplitWS {   // per (model, split)
   DevBuf<float> pp, abias, xg, xin, sg, sc, sh;
-  DevBuf<float> w, wn, h, P, port, sdf, E, Eu, dE, dEu, part, dw, rstat, scal;
+  DevBuf<float> w, wn, h, P, port, sdf, mu, E, Eu, dE, dEu, part, pe, pu, dw, rstat, scal;
   DevBuf<float> u, v, dpp, dab, dg, dx;
 };
 
@@ -120,21 +120,27 @@ class Engine {
   }
 
   // ---------------------------------------------------------------- data -----------------
-  void set_split(int s, py::array_t<uint16_t, py::array::c_style> X, py::array_t<int, py::array::c_style> row_dense,
+  void set_split(int s, py::array_t<uint16_t, py::array::c_style> X, py::array_t<int, py::array::c_style> rowti,
                  py::array_t<int, py::array::c_style> row_ptr, py::array_t<float, py::array::c_style> Rm,
                  py::array_t<float, py::array::c_style> mask, py::array_t<float, py::array::c_style> macro,
                  int T, int N) {
     if (s < 0 || s > 2) throw std::invalid_argument("split must be 0, 1 or 2");
     if (T > DLAP_MAX_T) throw std::invalid_argument("T exceeds DLAP_MAX_T");
     SplitDev& D = splits_[s];
-    const int R = (int)row_dense.size();
+    const int R = (int)rowti.size() / 2;
     if ((long)X.size() != (long)R * md_.KP) throw std::invalid_argument("X must be [R][KP] bf16 bits");
     if ((long)Rm.size() != (long)T * N || (long)mask.size() != (long)T * N) throw std::invalid_argument("Rm/mask must be [T*N]");
     if ((int)row_ptr.size() != T + 1) throw std::invalid_argument("row_ptr must be [T+1]");
     if (md_.M > 0 && (long)macro.size() != (long)T * md_.M) throw std::invalid_argument("macro must be [T][M]");
     D.T = T; D.N = N; D.R = R;
     up(D.X, X.data(), X.size());
-    up(D.row_dense, row_dense.data(), R);
+    up(D.rowti, rowti.data(), (size_t)2 * R);
+    {
+      std::vector<float> rc(R);
+      const int* ti = rowti.data();
+      for (int r = 0; r < R; ++r) rc[r] = Rm.data()[(size_t)ti[2 * r] * N + ti[2 * r + 1]];
+      up(D.Rc, rc.data(), R);
+    }
     up(D.row_ptr, row_ptr.data(), T + 1);
     up(D.Rm, Rm.data(), (size_t)T * N);
     up(D.mask, mask.data(), (size_t)T * N);
@@ -290,14 +296,13 @@ class Engine {
   void backward_only(int phase) {   // losses + gradients, no optimiser step
     if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
     enqueue_train_grads(phase);
-    launch_update(as<UpdJob>(j_upd_), G_, dd(), phase, 0.f, st_, 0);
     sync();
   }
 
   py::array_t<float> read_ws(int g, int s, const std::string& name) {
     ModelSplitWS& W = ws(g, s);
     const std::map<std::string, DevBuf<float>*> m = {
-        {"pp", &W.pp}, {"abias", &W.abias}, {"w", &W.w}, {"wn", &W.wn}, {"h", &W.h}, {"P", &W.P},
+        {"pp", &W.pp}, {"abias", &W.abias}, {"w", &W.w}, {"wn", &W.wn}, {"mu", &W.mu}, {"h", &W.h}, {"P", &W.P},
         {"port", &W.port}, {"sdf", &W.sdf}, {"E", &W.E}, {"Eu", &W.Eu}, {"dE", &W.dE}, {"dEu", &W.dEu},
         {"dw", &W.dw}, {"scal", &W.scal}, {"u", &W.u}, {"v", &W.v}, {"dpp", &W.dpp}, {"dab", &W.dab},
         {"sg", &W.sg}, {"sc", &W.sc}, {"sh", &W.sh}};
@@ -474,14 +479,15 @@ class Engine {
       W.abias.alloc((size_t)T * 64);
       W.xg.alloc((size_t)T * std::max(4 * H, 1));
       W.xin.alloc((size_t)T * std::max(H, 1));
-      W.w.alloc((size_t)T * N); W.wn.alloc((size_t)T * N); W.h.alloc((size_t)T * N * K);
-      W.P.alloc(T); W.port.alloc(T); W.sdf.alloc(T);
+      W.w.alloc((size_t)std::max(R, 1)); W.wn.alloc((size_t)T * N); W.h.alloc((size_t)T * N * K);
+      W.P.alloc(T); W.port.alloc(T); W.sdf.alloc(T); W.mu.alloc(T);
       W.E.alloc((size_t)N * K); W.Eu.alloc(N); W.dE.alloc((size_t)N * K); W.dEu.alloc(N);
-      W.part.alloc(2 * ((N + 63) / 64));
+      W.part.alloc(2 * ((N + 255) / 256));
+      W.pe.alloc((size_t)DLAP_TCH * N * K); W.pu.alloc((size_t)DLAP_TCH * N);
       W.scal.alloc(SC_NSCAL);
       if (md_.residual_factor > 0.f) W.rstat.alloc((size_t)T * 4);
       if (s == 0) {
-        W.dw.alloc((size_t)T * N);
+        W.dw.alloc((size_t)std::max(R, 1));
         W.u.alloc((size_t)R * std::max(md_.Dm, 1));
         W.v.alloc((size_t)R * 64);
         W.dpp.alloc((size_t)T * std::max(md_.Dm, 1));
@@ -531,7 +537,7 @@ class Engine {
     SplitDev& D = splits_[s];
     MlpJob J{};
     J.X = reinterpret_cast<const bf16x8*>(D.X.p);
-    J.row_dense = D.row_dense.p;
+    J.rowti = reinterpret_cast<const int2*>(D.rowti.p);
     J.pp = pp_ptr(g, s);
     J.abias = W.abias.p;
     J.blob = reinterpret_cast<const bf16x8*>(models_[g].blob.p);
@@ -554,6 +560,7 @@ class Engine {
     LossJob J{};
     J.Rm = D.Rm.p; J.mask = D.mask.p; J.invNt = D.invNt.p; J.Nt = D.Nt.p; J.meanR = D.meanR.p;
     J.RR = D.RR.p; J.invT = D.invT.p; J.Nbar = D.Nbar; J.T = D.T; J.N = D.N; J.K = md_.K;
+    J.row_ptr = D.row_ptr.p; J.rowti = reinterpret_cast<const int2*>(D.rowti.p); J.Rc = D.Rc.p; J.mu = W.mu.p;
     J.normalize = md_.normalize_w; J.weighted = md_.weighted_loss; J.phase = phase;
     J.res_factor = md_.residual_factor;
     const float kn = (float)md_.K * (float)D.N;
@@ -564,7 +571,7 @@ class Engine {
     J.E = W.E.p; J.Eu = W.Eu.p;
     J.dE = (phase == 2 || phase == 3) ? W.dE.p : nullptr;
     J.dEu = phase == 1 ? W.dEu.p : nullptr;
-    J.part = W.part.p; J.dw = W.dw.p; J.rstat = W.rstat.p; J.scal = W.scal.p;
+    J.part = W.part.p; J.pe = W.pe.p; J.pu = W.pu.p; J.dw = W.dw.p; J.rstat = W.rstat.p; J.scal = W.scal.p;
     return J;
   }
 
@@ -646,7 +653,7 @@ class Engine {
 
   void enqueue_train_grads(int phase) {
     const SplitDev& D = splits_[0];
-    launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), st_);
+    launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_);
     launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, gx_fwd_[0], md_.md, md_.KS1, md_.WMB, st_);
     launch_period_fwd(as<LossJob>(j_loss_train_[phase]), G_, D.T, st_);
     launch_asset(as<LossJob>(j_loss_train_[phase]), G_, D.N, st_);
@@ -660,6 +667,7 @@ class Engine {
                          slab_stride(), st_);
     }
     launch_finalize(as<FinJob>(j_fin_), G_, dd(), md_, phase, slab_stride(), D.T, st_);
+    launch_lstm_bwd(as<UpdJob>(j_upd_), G_, dd(), md_, D.T, phase, st_);
   }
   void enqueue_train(int phase, float lr) {
     enqueue_train_grads(phase);
@@ -667,7 +675,7 @@ class Engine {
   }
   void enqueue_eval() {
     if (n_eval_jobs_ == 0) return;
-    launch_prologue(as<RnnJob>(j_rnn_eval_), n_eval_jobs_, tmax_eval_, dd(), st_);
+    launch_prologue(as<RnnJob>(j_rnn_eval_), n_eval_jobs_, tmax_eval_, dd(), md_, st_);
     int gx = std::max(gx_fwd_[1], gx_fwd_[2]);
     launch_mlp_fwd(as<MlpJob>(j_mlp_eval_), n_eval_jobs_, gx, md_.md, md_.KS1, md_.WMB, st_);
     launch_period_fwd(as<LossJob>(j_loss_eval_), n_eval_jobs_, tmax_eval_, st_);
@@ -695,7 +703,7 @@ class Engine {
     }
     DevBuf<char> a, b, c;
     upload(a, rj); upload(b, mj); upload(c, lj);
-    launch_prologue(as<RnnJob>(a), G_, D.T, dd(), st_);
+    launch_prologue(as<RnnJob>(a), G_, D.T, dd(), md_, st_);
     launch_mlp_fwd(as<MlpJob>(b), G_, gx_fwd_[s], md_.md, md_.KS1, md_.WMB, st_);
     launch_period_fwd(as<LossJob>(c), G_, D.T, st_);
     launch_asset(as<LossJob>(c), G_, D.N, st_);

@@ -24,24 +24,23 @@ __global__ __launch_bounds__(256) void k_period_fwd(const LossJob* __restrict__ 
   if (t >= J.T) return;
   __shared__ float red[4];
   const int N = J.N;
-  const float* w = J.w + (size_t)t * N;
-  const float* m = J.mask + (size_t)t * N;
-  const float* R = J.Rm + (size_t)t * N;
-  float* wn = J.wn + (size_t)t * N;
+  const int r0 = J.row_ptr[t], r1 = J.row_ptr[t + 1];   // this period's compact rows
   float sw = 0.f;
   if (J.normalize) {
-    for (int i = threadIdx.x; i < N; i += 256) sw += w[i] * m[i];
+    for (int r = r0 + threadIdx.x; r < r1; r += 256) sw += J.w[r];
     sw = block_sum<256>(sw, red);
   }
   const float mu = J.normalize ? sw * J.invNt[t] : 0.f;
   float s_wr = 0.f, s_abs = 0.f, s_ww = 0.f;
-  for (int i = threadIdx.x; i < N; i += 256) {
-    const float v = (w[i] * m[i] - mu) * m[i];
-    wn[i] = v;
-    s_wr += v * R[i] * m[i];
-    s_abs += fabsf(v) * m[i];
-    s_ww += v * v * m[i];
+  float* wn = J.wn + (size_t)t * N;
+  for (int r = r0 + threadIdx.x; r < r1; r += 256) {
+    const float v = J.w[r] - mu;
+    wn[J.rowti[r].y] = v;
+    s_wr += v * J.Rc[r];
+    s_abs += fabsf(v);
+    s_ww += v * v;
   }
+  if (threadIdx.x == 0) J.mu[t] = mu;
   s_wr = block_sum<256>(s_wr, red);
   s_abs = block_sum<256>(s_abs, red);
   if (J.rstat) s_ww = block_sum<256>(s_ww, red);
@@ -58,86 +57,98 @@ __global__ __launch_bounds__(256) void k_period_fwd(const LossJob* __restrict__ 
 }
 
 // ---------------------------------------------------------------- asset pass ------------
-// grid (ceil(N/64), njobs); block 256 = 4 waves; lane -> stock, wave -> quarter of the time axis.
-__global__ __launch_bounds__(256) void k_asset(const LossJob* __restrict__ jobs) {
-  const LossJob& J = jobs[blockIdx.y];
+// Pass 1, grid (ceil(N/64), TCH, jobs): block = 64 stocks x one time chunk; the 4 waves split
+// the chunk, reduce in LDS (fixed order) and write partial sums for the chunk:
+//   pe[ch][i][k] = sum_{t in chunk} h[t,i,k] R[t,i] SDF_t,  pu[ch][i] = sum R SDF_t.
+__global__ __launch_bounds__(256) void k_asset_part(const LossJob* __restrict__ jobs) {
+  const LossJob& J = jobs[blockIdx.z];
   const int nblk = (J.N + 63) >> 6;
   if ((int)blockIdx.x >= nblk) return;
-  __shared__ float sdf[DLAP_MAX_T];
   __shared__ float red[4][64][9];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int T = J.T, N = J.N, K = J.K;
-  for (int t = threadIdx.x; t < T; t += 256) sdf[t] = J.sdfv[t];
-  __syncthreads();
+  const int ch = blockIdx.y;
+  const int ca = (T * ch) / DLAP_TCH, cb = (T * (ch + 1)) / DLAP_TCH;
+  const int t0 = ca + ((cb - ca) * wave) / 4, t1 = ca + ((cb - ca) * (wave + 1)) / 4;
   const int i = blockIdx.x * 64 + lane;
   const bool ok = i < N;
-  const int t0 = (T * wave) / 4, t1 = (T * (wave + 1)) / 4;
-  const float invT = ok ? J.invT[i] : 0.f;
-  float loss_c = 0.f, loss_u = 0.f;
-  // unconditional moment (h == 1)
-  {
-    float e = 0.f;
-    if (ok)
-      for (int t = t0; t < t1; ++t) e += J.Rm[(size_t)t * N + i] * sdf[t];
-    red[wave][lane][8] = e;
-  }
-  __syncthreads();
-  if (wave == 0) {
-    const float e = (red[0][lane][8] + red[1][lane][8] + red[2][lane][8] + red[3][lane][8]) * invT;
+  float eu = 0.f;
+  float e[8];
+  const int kmax = J.h ? K : 0;
+  for (int k0 = 0; k0 < max(kmax, 1); k0 += 8) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e[k] = 0.f;
+    const int kn = J.h ? min(8, K - k0) : 0;
     if (ok) {
-      J.Eu[i] = e;
-      if (J.dEu) J.dEu[i] = J.coef_u * e;
-    }
-    loss_u = ok ? e * e : 0.f;
-  }
-  // conditional moments, 8 at a time
-  if (J.h) {
-    for (int k0 = 0; k0 < K; k0 += 8) {
-      float e[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) e[k] = 0.f;
-      const int kn = min(8, K - k0);
-      if (ok) {
-        for (int t = t0; t < t1; ++t) {
-          const size_t d = (size_t)t * N + i;
-          const float q = J.Rm[d] * sdf[t];
+#pragma unroll 4
+      for (int t = t0; t < t1; ++t) {
+        const size_t d = (size_t)t * N + i;
+        const float q = J.Rm[d] * J.sdfv[t];
+        if (k0 == 0) eu += q;
+        if (kn == 8 && (K & 3) == 0) {
           const float* hp = J.h + d * K + k0;
-          if (kn == 8 && (K & 3) == 0) {
-            const f32x4 a = *reinterpret_cast<const f32x4*>(hp);
-            const f32x4 b = *reinterpret_cast<const f32x4*>(hp + 4);
+          const f32x4 a = *reinterpret_cast<const f32x4*>(hp);
+          const f32x4 b = *reinterpret_cast<const f32x4*>(hp + 4);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) { e[k] += a[k] * q; e[4 + k] += b[k] * q; }
-          } else {
-            for (int k = 0; k < kn; ++k) e[k] += hp[k] * q;
-          }
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int k = 0; k < 8; ++k) red[wave][lane][k] = e[k];
-      __syncthreads();
-      if (wave == 0 && ok) {
-        for (int k = 0; k < kn; ++k) {
-          const float v = (red[0][lane][k] + red[1][lane][k] + red[2][lane][k] + red[3][lane][k]) * invT;
-          J.E[(size_t)i * K + k0 + k] = v;
-          if (J.dE) J.dE[(size_t)i * K + k0 + k] = J.coef_c * v;
-          loss_c += v * v;
+          for (int k = 0; k < 4; ++k) { e[k] += a[k] * q; e[4 + k] += b[k] * q; }
+        } else {
+          for (int k = 0; k < kn; ++k) e[k] += J.h[d * K + k0 + k] * q;
         }
       }
     }
-  }
-  if (wave == 0) {
-    loss_c = wave_sum(loss_c);
-    loss_u = wave_sum(loss_u);
-    if (lane == 0) {
-      J.part[2 * blockIdx.x + 0] = loss_c;
-      J.part[2 * blockIdx.x + 1] = loss_u;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[wave][lane][k] = e[k];
+    red[wave][lane][8] = eu;
+    __syncthreads();
+    if (wave == 0 && ok) {
+      float* pe = J.pe + ((size_t)ch * N + i) * K;
+      for (int k = 0; k < kn; ++k)
+        pe[k0 + k] = red[0][lane][k] + red[1][lane][k] + red[2][lane][k] + red[3][lane][k];
+      if (k0 == 0) J.pu[(size_t)ch * N + i] = red[0][lane][8] + red[1][lane][8] + red[2][lane][8] + red[3][lane][8];
     }
   }
 }
 
+// Pass 2, grid (ceil(N/256), jobs): thread per stock; sums the chunks in order, writes
+// E, E_unc, dL/dE and the block's loss partial sums.
+__global__ __launch_bounds__(256) void k_asset_red(const LossJob* __restrict__ jobs) {
+  const LossJob& J = jobs[blockIdx.y];
+  const int N = J.N, K = J.K;
+  if ((int)blockIdx.x * 256 >= N) return;
+  __shared__ float red[4];
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const bool ok = i < N;
+  float lc = 0.f, lu = 0.f;
+  if (ok) {
+    const float invT = J.invT[i];
+    float u = 0.f;
+    for (int ch = 0; ch < DLAP_TCH; ++ch) u += J.pu[(size_t)ch * N + i];
+    u *= invT;
+    J.Eu[i] = u;
+    if (J.dEu) J.dEu[i] = J.coef_u * u;
+    lu = u * u;
+    if (J.h) {
+      for (int k = 0; k < K; ++k) {
+        float v = 0.f;
+        for (int ch = 0; ch < DLAP_TCH; ++ch) v += J.pe[((size_t)ch * N + i) * K + k];
+        v *= invT;
+        J.E[(size_t)i * K + k] = v;
+        if (J.dE) J.dE[(size_t)i * K + k] = J.coef_c * v;
+        lc += v * v;
+      }
+    }
+  }
+  lc = block_sum<256>(lc, red);
+  lu = block_sum<256>(lu, red);
+  if (threadIdx.x == 0) {
+    J.part[2 * blockIdx.x + 0] = lc;
+    J.part[2 * blockIdx.x + 1] = lu;
+  }
+}
+
 DLAP_DEV void final_losses(const LossJob& J, float& lc, float& lu) {
-  const int nblk = (J.N + 63) >> 6;
+  const int nblk = (J.N + 255) >> 8;
   float a = 0.f, b = 0.f;
   for (int k = 0; k < nblk; ++k) { a += J.part[2 * k]; b += J.part[2 * k + 1]; }
   lc = J.h ? a / ((float)J.K * (float)J.N) : 0.f;
@@ -171,17 +182,17 @@ __global__ __launch_bounds__(256) void k_period_bwd(const LossJob* __restrict__ 
   __shared__ float red[4];
   const int N = J.N, K = J.K;
   const size_t base = (size_t)t * N;
+  const int r0 = J.row_ptr[t], r1 = J.row_ptr[t + 1];
   float s = 0.f;
-  for (int i = threadIdx.x; i < N; i += 256) {
-    const size_t d = base + i;
-    const float r = J.Rm[d];
-    if (r == 0.f) continue;
+  for (int rr = r0 + threadIdx.x; rr < r1; rr += 256) {
+    const int i = J.rowti[rr].y;
+    const float r = J.Rc[rr];
     float g;
     if (J.phase == 1) {
       g = J.dEu[i];
     } else {
       g = 0.f;
-      const float* hp = J.h + d * K;
+      const float* hp = J.h + (base + i) * K;
       const float* de = J.dE + (size_t)i * K;
       for (int k = 0; k < K; ++k) g += de[k] * hp[k];
     }
@@ -201,23 +212,20 @@ __global__ __launch_bounds__(256) void k_period_bwd(const LossJob* __restrict__ 
     }
   }
   // mean over valid stocks of the residual gradient (for the normalisation Jacobian)
+  const float mu = J.mu[t];
   float gres_mean = 0.f;
   if (rcoef != 0.f && J.normalize) {
     float sg = 0.f;
-    for (int i = threadIdx.x; i < N; i += 256) {
-      const size_t d = base + i;
-      if (J.mask[d] > 0.f) sg += J.Rm[d] - beta * J.wn[d];
-    }
+    for (int rr = r0 + threadIdx.x; rr < r1; rr += 256) sg += J.Rc[rr] - beta * (J.w[rr] - mu);
     sg = block_sum<256>(sg, red);
     gres_mean = rcoef * sg * J.invNt[t];
   }
   const float mR = J.normalize ? J.meanR[t] : 0.f;
-  for (int i = threadIdx.x; i < N; i += 256) {
-    const size_t d = base + i;
-    const float m = J.mask[d];
-    float g = c * (J.Rm[d] - mR);
-    if (rcoef != 0.f) g += rcoef * (J.Rm[d] - beta * J.wn[d]) - gres_mean;
-    J.dw[d] = m * g;
+  for (int rr = r0 + threadIdx.x; rr < r1; rr += 256) {
+    const float R = J.Rc[rr];
+    float g = c * (R - mR);
+    if (rcoef != 0.f) g += rcoef * (R - beta * (J.w[rr] - mu)) - gres_mean;
+    J.dw[rr] = g;
   }
 }
 
@@ -278,7 +286,9 @@ void launch_period_fwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st)
   HIP_OK(hipGetLastError());
 }
 void launch_asset(const LossJob* jobs, int njobs, int nmax, hipStream_t st) {
-  hipLaunchKernelGGL(k_asset, dim3((nmax + 63) / 64, njobs), dim3(256), 0, st, jobs);
+  hipLaunchKernelGGL(k_asset_part, dim3((nmax + 63) / 64, DLAP_TCH, njobs), dim3(256), 0, st, jobs);
+  HIP_OK(hipGetLastError());
+  hipLaunchKernelGGL(k_asset_red, dim3((nmax + 255) / 256, njobs), dim3(256), 0, st, jobs);
   HIP_OK(hipGetLastError());
 }
 void launch_period_bwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st) {

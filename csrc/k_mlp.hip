@@ -58,47 +58,67 @@ DLAP_DEV bf16x8 make_onehot(int col) {
 }
 
 struct RowInfo {
-  int dense[2];   // dense index of this lane's row in block b (-1 beyond R)
+  int dense[2];   // dense index t*N + i of this lane's row in block b (-1 beyond R)
   int t[2], i[2];
 };
 
-DLAP_DEV RowInfo load_rows(const MlpJob& J, int tile) {
-  RowInfo ri;
-  const int l = lane_id();
-#pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    int r = tile * 32 + 16 * b + (l & 15);
-    int d = r < J.R ? J.row_dense[r] : -1;
-    ri.dense[b] = d;
-    int t = d >= 0 ? d / J.N : 0;
-    ri.t[b] = t;
-    ri.i[b] = d >= 0 ? d - t * J.N : 0;
-  }
-  return ri;
-}
-
+// Per-tile data that does not depend on other loads: issued one tile ahead (software
+// prefetch) so the HBM latency hides behind the current tile's MFMA/VALU work.
 template <int KS1>
-DLAP_DEV void load_x(const MlpJob& J, const MlpDims& D, int tile, const RowInfo& ri,
-                     bf16x8 (&xf)[2][KS1]) {
+struct TileIn {
+  int2 ti[2];
+  bf16x8 x[2][KS1];
+  float dw[2];
+};
+
+template <int KS1, bool DW>
+DLAP_DEV void issue_tile(const MlpJob& J, int tile, TileIn<KS1>& in) {
   const int l = lane_id(), q = l >> 4;
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
-    int r = tile * 32 + 16 * b + (l & 15);
-    bool ok = r < J.R;
-    const bf16x8* row = J.X + (size_t)(ok ? r : 0) * (4 * KS1);
+    const int r = min(tile * 32 + 16 * b + (l & 15), J.R - 1);   // clamp: no divergent loads
+    in.ti[b] = J.rowti[r];
+    const bf16x8* row = J.X + (size_t)r * (4 * KS1);
 #pragma unroll
-    for (int s = 0; s < KS1; ++s) xf[b][s] = ok ? row[4 * s + q] : zero8();
-    if (D.Dm > 0 && ok) {
+    for (int s = 0; s < KS1; ++s) in.x[b][s] = row[4 * s + q];
+    if (DW) in.dw[b] = J.dw[r];
+  }
+}
+
+// Finish a prefetched tile: row info, zero rows beyond R, insert the per-period columns.
+template <int KS1>
+DLAP_DEV RowInfo finish_tile(const MlpJob& J, const MlpDims& D, int tile, TileIn<KS1>& in,
+                             bf16x8 (&xf)[2][KS1]) {
+  RowInfo ri;
+  const int l = lane_id(), q = l >> 4;
+  const int s_lo = D.F >> 5, s_hi = (D.F + D.Dm - 1) >> 5;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int r = tile * 32 + 16 * b + (l & 15);
+    const bool ok = r < J.R;
+    ri.t[b] = in.ti[b].x;
+    ri.i[b] = in.ti[b].y;
+    ri.dense[b] = ok ? in.ti[b].x * J.N + in.ti[b].y : -1;
+#pragma unroll
+    for (int s = 0; s < KS1; ++s) xf[b][s] = ok ? in.x[b][s] : zero8();
+    if (D.Dm > 0) {
       const float* pp = J.pp + ri.t[b] * D.Dm;
 #pragma unroll
-      for (int s = 0; s < KS1; ++s)
+      for (int s = 0; s < KS1; ++s) {
+        if (s >= s_lo && s <= s_hi) {                          // wave-uniform
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          int col = 32 * s + 8 * q + j - D.F;
-          if (col >= 0 && col < D.Dm) xf[b][s][j] = (__bf16)pp[col];
+          for (int j = 0; j < 8; ++j) {
+            const int col = 32 * s + 8 * q + j - D.F;
+            const bool in_rng = (unsigned)col < (unsigned)D.Dm;
+            const float v = pp[min(max(col, 0), D.Dm - 1)];
+            if (in_rng && ok) xf[b][s][j] = (__bf16)v;
+          }
         }
+      }
     }
+    if (!ok) in.dw[b] = 0.f;
   }
+  return ri;
 }
 
 // acc[b][u] = W0 . X^T  (UB output blocks)
@@ -143,10 +163,11 @@ DLAP_DEV void pack_blocks(const f32x4 (&a)[2][UB], bf16x8 (&pf)[2][(UB + 1) / 2]
 }
 
 struct DropCtx {
-  bool on; uint32_t thr; float scale; uint32_t seed, step;
+  bool on; uint32_t thr16; float scale; uint32_t seed, step;
 };
 
-// bias + ReLU + dropout in place; gate bit (u*4+r) per row block.
+// bias + ReLU + dropout in place; gate bit (u*4+r) per row block. Branch-free: one hash
+// per unit pair gives both keep decisions (see dropout_pair).
 template <int UB>
 DLAP_DEV void relu_dropout(f32x4 (&a)[2][UB], const float* bias0, const float* bias1,
                            const DropCtx& dc, int layer_id, const RowInfo& ri, uint32_t (&gate)[2]) {
@@ -155,16 +176,24 @@ DLAP_DEV void relu_dropout(f32x4 (&a)[2][UB], const float* bias0, const float* b
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
     const float* bp = b ? bias1 : bias0;
+    const uint32_t row = (uint32_t)ri.dense[b];
+    const uint32_t rowmix = row * 0xcc9e2d51u ^ (row >> 16);
     uint32_t g = 0;
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
       const f32x4 bb = *reinterpret_cast<const f32x4*>(bp + 16 * u + 4 * q);
+      uint32_t keep = 0xFu;
+      if (dc.on) {   // wave-uniform
+        const uint32_t pair0 = (uint32_t)(8 * u + 2 * q);
+        const uint32_t h0 = dropout_pair(key, rowmix, pair0);
+        const uint32_t h1 = dropout_pair(key, rowmix, pair0 + 1);
+        keep = ((h0 & 0xFFFFu) >= dc.thr16 ? 1u : 0u) | ((h0 >> 16) >= dc.thr16 ? 2u : 0u) |
+               ((h1 & 0xFFFFu) >= dc.thr16 ? 4u : 0u) | ((h1 >> 16) >= dc.thr16 ? 8u : 0u);
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int unit = 16 * u + 4 * q + r;
-        float z = a[b][u][r] + bb[r];
-        bool on = z > 0.f;
-        if (dc.on) on = on && dropout_keep(key, (uint32_t)ri.dense[b], (uint32_t)unit, dc.thr);
+        const float z = a[b][u][r] + bb[r];
+        const bool on = (z > 0.f) & (((keep >> r) & 1u) != 0u);
         a[b][u][r] = on ? z * dc.scale : 0.f;
         g |= (on ? 1u : 0u) << (u * 4 + r);
       }
@@ -182,7 +211,7 @@ DLAP_DEV float reduce_q(float v) {  // sum over the 4 lane groups that share l &
 DLAP_DEV DropCtx drop_ctx(const MlpJob& J, const MlpDims& D) {
   DropCtx dc;
   dc.on = J.train && D.dropout > 0.f;
-  dc.thr = (uint32_t)(D.dropout * 16777216.f + 0.5f);
+  dc.thr16 = (uint32_t)(D.dropout * 65536.f + 0.5f);
   dc.scale = dc.on ? 1.f / (1.f - D.dropout) : 1.f;
   dc.seed = J.seed;
   dc.step = J.step ? (uint32_t)*J.step : 0u;
@@ -272,19 +301,26 @@ __global__ __launch_bounds__(256, 2) void k_mlp_fwd(const MlpJob* __restrict__ j
   const DropCtx dc = drop_ctx(J, D);
   const int wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   const int ntiles = (J.R + 31) >> 5;
-  const int q = lane_id() >> 4;
-  for (int tile = blockIdx.x * nwaves + wave; tile < ntiles; tile += gridDim.x * nwaves) {
-    const RowInfo ri = load_rows(J, tile);
+  const int q = lane_id() >> 4, lane = lane_id();
+  const int stride = gridDim.x * nwaves;
+  int tile = blockIdx.x * nwaves + wave;
+  TileIn<KS1> cur, nxt;
+  if (tile < ntiles) issue_tile<KS1, false>(J, tile, cur);
+  for (; tile < ntiles; tile += stride) {
+    if (tile + stride < ntiles) issue_tile<KS1, false>(J, tile + stride, nxt);
     bf16x8 xf[2][KS1];
-    load_x<KS1>(J, D, tile, ri, xf);
+    const RowInfo ri = finish_tile<KS1>(J, D, tile, cur, xf);
     if (J.do_sdf) {
       float w[2];
       sdf_forward_tile<KS1>(lds, aux, D, dc, ri, xf, w);
 #pragma unroll
-      for (int b = 0; b < 2; ++b)
-        if (q == 0 && ri.dense[b] >= 0) J.w_out[ri.dense[b]] = w[b];
+      for (int b = 0; b < 2; ++b) {
+        const int r = tile * 32 + 16 * b + (lane & 15);
+        if (q == 0 && r < J.R) J.w_out[r] = w[b];
+      }
     }
     if (J.do_mom) mom_forward_tile<KS1, WMB>(lds, aux, D, J, dc, ri, xf);
+    cur = nxt;
   }
 }
 
@@ -352,10 +388,14 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
     tc[t] = tid < C0 ? tid : 0;
   }
 
-  for (int tile = blockIdx.x * nwaves + wave; tile < ntiles; tile += gridDim.x * nwaves) {
-    const RowInfo ri = load_rows(J, tile);
+  const int stride = gridDim.x * nwaves;
+  int tile = blockIdx.x * nwaves + wave;
+  TileIn<KS1> cur, nxt;
+  if (tile < ntiles) issue_tile<KS1, true>(J, tile, cur);
+  for (; tile < ntiles; tile += stride) {
+    if (tile + stride < ntiles) issue_tile<KS1, true>(J, tile + stride, nxt);
     bf16x8 xf[2][KS1];
-    load_x<KS1>(J, D, tile, ri, xf);
+    const RowInfo ri = finish_tile<KS1>(J, D, tile, cur, xf);
     // ---- forward recompute, keep packed activations + gates ----
     bf16x8 act[NL][2][2];
     uint32_t gates[NL][2];
@@ -368,9 +408,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
       pack_blocks<4>(a, act[j]);
     }
     // ---- output layer: w = wo . a_last + bo ----
-    float dwr[2];
-#pragma unroll
-    for (int b = 0; b < 2; ++b) dwr[b] = ri.dense[b] >= 0 ? J.dw[ri.dense[b]] : 0.f;
+    const float dwr[2] = {cur.dw[0], cur.dw[1]};
     f32x4 dz[2][4];
     const float* wo = aux + D.a_wo;
 #pragma unroll
@@ -453,6 +491,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
         }
       }
     }
+    cur = nxt;
   }
   // ---- workgroup slab: waves add their partials into LDS in a fixed order ----
   float* red = wg_slab_begin(smem, slab_stride);
@@ -524,10 +563,14 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
     tc[t] = tid < C0 ? tid : 0;
   }
 
-  for (int tile = blockIdx.x * nwaves + wave; tile < ntiles; tile += gridDim.x * nwaves) {
-    const RowInfo ri = load_rows(J, tile);
+  const int stride = gridDim.x * nwaves;
+  int tile = blockIdx.x * nwaves + wave;
+  TileIn<KS1> cur, nxt;
+  if (tile < ntiles) issue_tile<KS1, false>(J, tile, cur);
+  for (; tile < ntiles; tile += stride) {
+    if (tile + stride < ntiles) issue_tile<KS1, false>(J, tile + stride, nxt);
     bf16x8 xf[2][KS1];
-    load_x<KS1>(J, D, tile, ri, xf);
+    const RowInfo ri = finish_tile<KS1>(J, D, tile, cur, xf);
     bf16x8 act[NLM][2][KSM];
     uint32_t gates[NLM][2];
     f32x4 a[2][WMB];
@@ -623,6 +666,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
         }
       }
     }
+    cur = nxt;
   }
   float* red = wg_slab_begin(smem, slab_stride);
   for (int w = 0; w < nwaves; ++w) {

@@ -1,134 +1,384 @@
-// Macro-state LSTM (forward in the prologue, BPTT in the update kernel) and the moment
-// network's per-period bias.
+// Macro-state LSTM forward / backward and the moment network's per-period macro bias.
 //
-// Replaces `MacroLSTM.forward` = one nn.LSTM call over the whole T-sequence with batch 1
+// Replaces `MacroLSTM.forward` = one nn.LSTM over the whole T-sequence with batch 1
 // (`/root/reference/src/model.py:21-84`) and the macro half of the moment
 // input concatenation (`model.py:513-516`).
-//   * PyTorch gate order i, f, g, o and both biases (state_dict compatible).
-//   * Zero initial state for every split (the reference passes hidden=None everywhere).
-//   * Inter-layer dropout on every layer output but the last (torch semantics), train only.
-// The recurrence is latency-bound (T <= ~600 steps of a 4H x H mat-vec), so it runs on ONE
-// wave with W_hh rows in registers and h broadcast by lane shuffles (no barriers inside the
-// time loop); the input projections of all T steps are computed first by the whole
-// workgroup. Other workgroups of the same launch compute the moment layer-0 bias table
-//   abias[t][c] = sum_m W_m0[c][m] macro[t][m] + b_m0[c]      (zero-padded to 64 columns)
-// so the [T, N, M] macro tiling of the reference never exists.
+//   * PyTorch gate order i, f, g, o and both biases (state_dict compatible);
+//   * zero initial state for every split (the reference passes hidden=None everywhere);
+//   * inter-layer dropout on every layer output but the last (torch semantics), train only.
+//
+// Kernels
+//   k_proj      grid (ceil(T/4), jobs): the layer-0 input projection of every step
+//               xg[t] = W_ih x_t + b_ih + b_hh and the moment table
+//               abias[t][c] = W_m0[c, :M] . m_t + b_m0[c]  (zero-padded to 64 columns);
+//               the weights are staged in LDS, each thread owns one output for 4 periods.
+//   k_lstm      one wave per job: the recurrence. Lane k owns hidden unit k and keeps its
+//               4 rows of W_hh (and W_ih for layers > 0) in registers; h_{t-1} is broadcast
+//               with v_readlane (no LDS, no barrier); xg is staged in LDS when it fits.
+//   k_lstm_bwd  one workgroup per model: BPTT on wave 0 (same ownership, dgates broadcast
+//               with v_readlane), then every thread reduces the weight gradients over t
+//               from LDS-staged dgates (thread per macro column: 4H FMAs per load).
+//               Phase 2 instead builds the moment layer-0 macro-column / bias gradients.
 #include "common.h"
 #include "layout.h"
 #include "rnn.h"
+#include "update.h"
 
-DLAP_DEV float gate_act(float x, int type) {  // 0 i, 1 f, 2 g, 3 o
-  return type == 2 ? tanhf(x) : 1.f / (1.f + __expf(-x));
+#define DLAP_MAX_M 1024
+
+// Fast activations (v_exp + v_rcp): |err| < 1e-6 relative in the ranges that matter; tanh
+// switches to its cubic Taylor form near 0 where 2*sigm(2x)-1 would cancel.
+DLAP_DEV float sigm(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+DLAP_DEV float ftanh(float x) {
+  const float t = 2.f * sigm(2.f * x) - 1.f;
+  return fabsf(x) < 0.0125f ? x * (1.f - x * x * (1.f / 3.f)) : t;
 }
 
-__global__ __launch_bounds__(256) void k_prologue(const RnnJob* __restrict__ jobs,
-                                                  const ModelDesc* __restrict__ md) {
+// ------------------------------------------------------------------------ k_proj -------
+__global__ __launch_bounds__(256) void k_proj(const RnnJob* __restrict__ jobs,
+                                              const ModelDesc* __restrict__ md) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
   const RnnJob& J = jobs[blockIdx.y];
-  const int T = J.T;
-  const int M = md->M;
-  if (blockIdx.x > 0) {
-    // ---- moment layer-0 per-period bias ----
-    if (!J.abias) return;
-    const int t = (blockIdx.x - 1) * 4 + (threadIdx.x >> 6);
-    const int c = threadIdx.x & 63;
-    if (t >= T) return;
-    const PackLayer& L0 = md->m[0];
-    float s = 0.f;
-    if (c < L0.out) {
-      const float* w = J.params + L0.w_off + (size_t)c * L0.ld;
-      const float* x = J.macro + (size_t)t * M;
-      s = J.params[L0.b_off + c];
-      for (int m = 0; m < M; ++m) s += w[m] * x[m];
-    }
-    J.abias[t * 64 + c] = s;
-    return;
+  const int T = J.T, M = md->M;
+  const int t0 = blockIdx.x * 4;
+  if (t0 >= T) return;
+  const int G4 = md->nrnn > 0 ? 4 * md->H : 0;
+  const int cm1 = J.abias ? md->m[0].out : 0;
+  const int nout = G4 + (J.abias ? 64 : 0);
+  float* x = sm;                 // [4][M]
+  float* w = sm + 4 * M;         // [nout][M]
+  const int nt = min(4, T - t0);
+  for (int i = threadIdx.x; i < 4 * M; i += 256) {
+    const int tl = i / M;
+    x[i] = tl < nt ? J.macro[(size_t)(t0 + tl) * M + (i - tl * M)] : 0.f;
   }
+  const float* Wih = J.params + md->lstm_w_ih[0];
+  const PackLayer& L0 = md->m[0];
+  for (int i = threadIdx.x; i < nout * M; i += 256) {
+    const int o = i / M, m = i - o * M;
+    float v = 0.f;
+    if (o < G4) v = Wih[(size_t)o * M + m];
+    else if (o - G4 < cm1) v = J.params[L0.w_off + (size_t)(o - G4) * L0.ld + m];
+    w[i] = v;
+  }
+  __syncthreads();
+  const int o = threadIdx.x;
+  if (o >= nout) return;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  const float* wr = w + (size_t)o * M;
+#pragma unroll 4
+  for (int m = 0; m < M; ++m) {
+    const float wv = wr[m];
+    s0 += wv * x[m]; s1 += wv * x[M + m]; s2 += wv * x[2 * M + m]; s3 += wv * x[3 * M + m];
+  }
+  float b = 0.f;
+  if (o < G4) b = J.params[md->lstm_b_ih[0] + o] + J.params[md->lstm_b_hh[0] + o];
+  else if (o - G4 < cm1) b = J.params[L0.b_off + o - G4];
+  else b = 0.f;
+  const float s[4] = {s0, s1, s2, s3};
+  for (int tl = 0; tl < nt; ++tl) {
+    const int t = t0 + tl;
+    if (o < G4) J.xg[(size_t)t * G4 + o] = s[tl] + b;
+    else J.abias[t * 64 + (o - G4)] = (o - G4 < cm1) ? s[tl] + b : 0.f;
+  }
+}
+
+// ------------------------------------------------------------------------ k_lstm -------
+template <int HM>
+__global__ __launch_bounds__(64) void k_lstm(const RnnJob* __restrict__ jobs,
+                                             const ModelDesc* __restrict__ md) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const RnnJob& J = jobs[blockIdx.x];
   const int nrnn = md->nrnn;
   if (nrnn == 0) return;
-  const int H = md->H, G4 = 4 * H;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int T = J.T, H = md->H, G4 = 4 * H;
+  const int lane = threadIdx.x;
+  const int k = lane < H ? lane : 0;
+  const bool act = lane < H;
   const bool drop = J.train && md->dropout > 0.f;
   const uint32_t thr = (uint32_t)(md->dropout * 16777216.f + 0.5f);
   const float scale = drop ? 1.f / (1.f - md->dropout) : 1.f;
   const uint32_t step = J.step ? (uint32_t)*J.step : 0u;
+  const bool stage = T * G4 <= 12288;          // 48 KiB of LDS
   for (int l = 0; l < nrnn; ++l) {
-    const float* Wih = J.params + md->lstm_w_ih[l];
     const float* Whh = J.params + md->lstm_w_hh[l];
-    const float* bih = J.params + md->lstm_b_ih[l];
-    const float* bhh = J.params + md->lstm_b_hh[l];
-    const int in_dim = l == 0 ? M : H;
-    const float* x = l == 0 ? J.macro : J.xin;
-    // phase A: input projections of every step
-    for (int idx = threadIdx.x; idx < T * G4; idx += 256) {
-      const int t = idx / G4, g = idx - t * G4;
-      float s = bih[g] + bhh[g];
-      const float* w = Wih + (size_t)g * in_dim;
-      const float* xt = x + (size_t)t * in_dim;
-      for (int k = 0; k < in_dim; ++k) s += w[k] * xt[k];
-      J.xg[idx] = s;
-    }
-    __syncthreads();
-    // phase B: the recurrence on wave 0
-    float* hout = J.sh ? J.sh + (size_t)l * T * H : J.out;
-    if (wave == 0) {
-      const int g0 = lane, g1 = lane + 64;
-      float w0[DLAP_MAX_H], w1[DLAP_MAX_H];
+    float whh[4][HM], wih[4][HM], bias[4];
 #pragma unroll
-      for (int k = 0; k < DLAP_MAX_H; ++k) {
-        w0[k] = (k < H && g0 < G4) ? Whh[g0 * H + k] : 0.f;
-        w1[k] = (k < H && g1 < G4) ? Whh[g1 * H + k] : 0.f;
+    for (int q = 0; q < 4; ++q) {
+#pragma unroll
+      for (int j = 0; j < HM; ++j) {
+        whh[q][j] = j < H ? Whh[(q * H + k) * H + j] : 0.f;
+        wih[q][j] = (l > 0 && j < H) ? J.params[md->lstm_w_ih[l] + (q * H + k) * H + j] : 0.f;
       }
-      const int ty0 = g0 / H, ty1 = g1 / H;
-      float h = 0.f, c = 0.f;
-      for (int t = 0; t < T; ++t) {
-        float p0 = g0 < G4 ? J.xg[t * G4 + g0] : 0.f;
-        float p1 = g1 < G4 ? J.xg[t * G4 + g1] : 0.f;
+      bias[q] = l > 0 ? J.params[md->lstm_b_ih[l] + q * H + k] + J.params[md->lstm_b_hh[l] + q * H + k] : 0.f;
+    }
+    if (l == 0 && stage) {
+      for (int i = lane; i < T * G4; i += 64) sm[i] = J.xg[i];
+      __syncthreads();
+    }
+    float* hout = J.sh ? J.sh + (size_t)l * T * H : J.out;
+    const float* xin = J.xin;                      // layer l-1 output after dropout
+    const uint32_t key_in = l > 0 ? dropout_key(J.seed, step, 32 + (l - 1)) : 0u;
+    float h = 0.f, c = 0.f;
+    float nx[4];
+    if (l == 0) {
+      const float* xr = stage ? sm : J.xg;
 #pragma unroll
-        for (int k = 0; k < DLAP_MAX_H; ++k) {
-          if (k < H) {
-            const float hk = __shfl(h, k, 64);
-            p0 += w0[k] * hk;
-            p1 += w1[k] * hk;
+      for (int q = 0; q < 4; ++q) nx[q] = xr[q * H + k];
+    }
+    for (int t = 0; t < T; ++t) {
+      float p[4];
+      if (l == 0) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) p[q] = nx[q];
+        const int tn = t + 1 < T ? t + 1 : t;           // prefetch the next step's inputs
+        const float* xr = stage ? sm + tn * G4 : J.xg + (size_t)tn * G4;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) nx[q] = xr[q * H + k];
+      } else {
+        float xv = act ? xin[(size_t)t * H + k] : 0.f;
+        if (drop) xv = dropout_keep(key_in, (uint32_t)t, (uint32_t)k, thr) ? xv * scale : 0.f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) p[q] = bias[q];
+#pragma unroll
+        for (int j = 0; j < HM; ++j) {
+          if (j < H) {
+            const float xj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), j));
+#pragma unroll
+            for (int q = 0; q < 4; ++q) p[q] += wih[q][j] * xj;
           }
         }
-        const float a0 = gate_act(p0, ty0), a1 = gate_act(p1, ty1);
-        if (J.sg) {
-          float* sg = J.sg + ((size_t)l * T + t) * G4;
-          if (g0 < G4) sg[g0] = a0;
-          if (g1 < G4) sg[g1] = a1;
-        }
-        float gv[4];
+      }
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int G = q * H + (lane < H ? lane : 0);
-          const float v0 = __shfl(a0, G & 63, 64), v1 = __shfl(a1, G & 63, 64);
-          gv[q] = G < 64 ? v0 : v1;
+      for (int j = 0; j < HM; ++j) {
+        if (j < H) {
+          const float hj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(h), j));
+#pragma unroll
+          for (int q = 0; q < 4; ++q) p[q] += whh[q][j] * hj;
         }
-        c = gv[1] * c + gv[0] * gv[2];
-        h = gv[3] * tanhf(c);
-        if (lane < H) {
-          hout[t * H + lane] = h;
-          if (J.sc) J.sc[((size_t)l * T + t) * H + lane] = c;
+      }
+      const float gi = sigm(p[0]), gf = sigm(p[1]), gg = ftanh(p[2]), go = sigm(p[3]);
+      c = gf * c + gi * gg;
+      h = go * ftanh(c);
+      if (act) {
+        hout[(size_t)t * H + k] = h;
+        if (J.sc) {
+          J.sc[((size_t)l * T + t) * H + k] = c;
+          float* sg = J.sg + ((size_t)l * T + t) * G4;
+          sg[k] = gi; sg[H + k] = gf; sg[2 * H + k] = gg; sg[3 * H + k] = go;
         }
       }
     }
-    __syncthreads();
+    __threadfence_block();
     if (l + 1 < nrnn) {
-      // next layer input: dropout(h) in training
-      const uint32_t key = dropout_key(J.seed, step, 32 + l);
-      for (int idx = threadIdx.x; idx < T * H; idx += 256) {
-        float v = hout[idx];
-        if (drop) v = dropout_keep(key, (uint32_t)(idx / H), (uint32_t)(idx % H), thr) ? v * scale : 0.f;
-        J.xin[idx] = v;
-      }
-      __syncthreads();
+      for (int i = lane; i < T * H; i += 64) J.xin[i] = hout[i];   // dropout applied on read
+      __threadfence_block();
     } else if (J.sh) {
-      for (int idx = threadIdx.x; idx < T * H; idx += 256) J.out[idx] = hout[idx];
+      for (int i = lane; i < T * H; i += 64) J.out[i] = hout[i];
     }
   }
 }
 
-void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* md, hipStream_t st) {
-  hipLaunchKernelGGL(k_prologue, dim3(1 + (tmax + 3) / 4, njobs), dim3(256), 0, st, jobs, md);
+void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* md, const ModelDesc& mh,
+                     hipStream_t st) {
+  {
+    const int nout = (mh.nrnn > 0 ? 4 * mh.H : 0) + 64;
+    const size_t sh = (size_t)(4 * mh.M + nout * mh.M + 4) * sizeof(float);
+    if (sh > 160 * 1024) dlap_throw_hip(hipErrorInvalidValue, "k_proj: macro dim too large", __FILE__, __LINE__);
+    hipLaunchKernelGGL(k_proj, dim3((tmax + 3) / 4, njobs), dim3(256), sh, st, jobs, md);
+    HIP_OK(hipGetLastError());
+  }
+  if (mh.nrnn > 0) {
+    const size_t sh = 12288 * sizeof(float);
+    if (mh.H <= 4) hipLaunchKernelGGL((k_lstm<4>), dim3(njobs), dim3(64), sh, st, jobs, md);
+    else if (mh.H <= 8) hipLaunchKernelGGL((k_lstm<8>), dim3(njobs), dim3(64), sh, st, jobs, md);
+    else if (mh.H <= 16) hipLaunchKernelGGL((k_lstm<16>), dim3(njobs), dim3(64), sh, st, jobs, md);
+    else hipLaunchKernelGGL((k_lstm<32>), dim3(njobs), dim3(64), sh, st, jobs, md);
+    HIP_OK(hipGetLastError());
+  }
+}
+
+// -------------------------------------------------------------------- k_lstm_bwd -------
+// grid: models, 256 threads. BPTT through every LSTM layer (phases 1/3). Per layer the saved
+// gates / cells / outputs and the incoming gradient are staged in LDS, the recurrence runs
+// on wave 0 from LDS (next step prefetched), then all threads form the small gradients
+// (W_hh, biases, W_ih of layers > 0, d input of the layer below). The layer-0 W_ih
+// gradient (T x 4H x M) is left to k_wgrad, which has many workgroups.
+template <int HM>
+__global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ jobs,
+                                                  const ModelDesc* __restrict__ md) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const UpdJob& J = jobs[blockIdx.x];
+  if (md->nrnn == 0) return;
+  const int T = J.T, M = md->M, H = md->H, G4 = 4 * H;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const bool drop = md->dropout > 0.f;
+  const uint32_t thr = (uint32_t)(md->dropout * 16777216.f + 0.5f);
+  const float scale = drop ? 1.f / (1.f - md->dropout) : 1.f;
+  const uint32_t step = (uint32_t)*J.drop_step;
+  float* s_g = sm;                    // [T][4H] saved gates
+  float* s_c = s_g + T * G4;          // [T][H]  cells
+  float* s_h = s_c + T * H;           // [T][H]  layer outputs
+  float* s_d = s_h + T * H;           // [T][H]  incoming gradient
+  float* dgs = s_d + T * H;           // [T][4H] gate pre-activation gradients
+  for (int l = md->nrnn - 1; l >= 0; --l) {
+    const float* dout = l == md->nrnn - 1 ? J.dpp : J.dx;
+    __syncthreads();
+    for (int i = threadIdx.x; i < T * G4; i += 256) s_g[i] = J.sg[(size_t)l * T * G4 + i];
+    for (int i = threadIdx.x; i < T * H; i += 256) {
+      s_c[i] = J.sc[(size_t)l * T * H + i];
+      s_h[i] = J.sh[(size_t)l * T * H + i];
+      s_d[i] = dout[i];
+    }
+    __syncthreads();
+    if (wave == 0) {
+      const int k = lane < H ? lane : 0;
+      const bool act = lane < H;
+      const float* Whh = J.params + md->lstm_w_hh[l];
+      float wt[4][HM];            // wt[q][j] = W_hh[q*H + j][k]
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int j = 0; j < HM; ++j) wt[q][j] = j < H ? Whh[(q * H + j) * H + k] : 0.f;
+      float dh_next = 0.f, dc_next = 0.f;
+      for (int t = T - 1; t >= 0; --t) {
+        const float* g = s_g + t * G4;
+        const float gi = g[k], gf = g[H + k], gg = g[2 * H + k], go = g[3 * H + k];
+        const float c = s_c[t * H + k];
+        const float cp = t > 0 ? s_c[(t - 1) * H + k] : 0.f;
+        const float dh = (act ? s_d[t * H + k] : 0.f) + dh_next;
+        const float tc = ftanh(c);
+        const float dc = dh * go * (1.f - tc * tc) + dc_next;
+        float d[4];
+        d[0] = dc * gg * gi * (1.f - gi);
+        d[1] = dc * cp * gf * (1.f - gf);
+        d[2] = dc * gi * (1.f - gg * gg);
+        d[3] = dh * tc * go * (1.f - go);
+        dc_next = dc * gf;
+        if (act) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) dgs[t * G4 + q * H + k] = d[q];
+        }
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < HM; ++j) {
+          if (j < H) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              s += wt[q][j] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d[q]), j));
+          }
+        }
+        dh_next = act ? s : 0.f;
+      }
+    }
+    __syncthreads();
+    if (l == 0)
+      for (int i = threadIdx.x; i < T * G4; i += 256) J.dg[i] = dgs[i];   // for k_wgrad
+    // W_hh [4H][H] and the biases: thread per (gate, column)
+    const int in_dim = l == 0 ? M : H;
+    const uint32_t key_below = l > 0 ? dropout_key(J.seed, step, 32 + (l - 1)) : 0u;
+    const float* hb = l > 0 ? J.sh + (size_t)(l - 1) * T * H : nullptr;
+    const int ncol = H + 1 + (l > 0 ? H : 0);
+    for (int idx = threadIdx.x; idx < G4 * ncol; idx += 256) {
+      const int g = idx % G4, col = idx / G4;
+      float acc = 0.f;
+      if (col < H) {
+        for (int t = 1; t < T; ++t) acc += dgs[t * G4 + g] * s_h[(t - 1) * H + col];
+        J.grads[md->lstm_w_hh[l] + g * H + col] = acc;
+      } else if (col == H) {
+        for (int t = 0; t < T; ++t) acc += dgs[t * G4 + g];
+        J.grads[md->lstm_b_ih[l] + g] = acc;
+        J.grads[md->lstm_b_hh[l] + g] = acc;
+      } else {
+        const int m = col - H - 1;     // W_ih of layer l > 0 (input = dropout(h_{l-1}))
+        for (int t = 0; t < T; ++t) {
+          float x = hb[(size_t)t * H + m];
+          if (drop) x = dropout_keep(key_below, (uint32_t)t, (uint32_t)m, thr) ? x * scale : 0.f;
+          acc += dgs[t * G4 + g] * x;
+        }
+        J.grads[md->lstm_w_ih[l] + g * in_dim + m] = acc;
+      }
+    }
+    if (l > 0) {
+      const float* Wih = J.params + md->lstm_w_ih[l];
+      for (int idx = threadIdx.x; idx < T * H; idx += 256) {
+        const int t = idx / H, m = idx - t * H;
+        float s = 0.f;
+        for (int g = 0; g < G4; ++g) s += Wih[g * H + m] * dgs[t * G4 + g];
+        if (drop) s = dropout_keep(key_below, (uint32_t)t, (uint32_t)m, thr) ? s * scale : 0.f;
+        J.dx[idx] = s;
+      }
+      __threadfence_block();
+    }
+  }
+}
+
+// --------------------------------------------------------------------------- k_wgrad ---
+// out[g][col] = sum_t dG[t][g] * macro[t][col] (+ the bias column, x = 1) for the layer-0
+// LSTM input weights (phases 1/3, dG = gate gradients) or the moment layer-0 macro columns
+// (phase 2, dG = per-period sums of the pre-activation gradient). grid (ceil((M+1)/16), models):
+// 16 columns per block, 16 time groups; fixed-order LDS reduction over the time groups.
+template <int GM>
+__global__ __launch_bounds__(256) void k_wgrad(const UpdJob* __restrict__ jobs,
+                                               const ModelDesc* __restrict__ md, int phase) {
+  __shared__ float red[16][16][GM + 1];
+  const UpdJob& J = jobs[blockIdx.y];
+  const int T = J.T, M = md->M;
+  const bool mom = phase == 2;
+  const int G = mom ? md->m[0].out : 4 * md->H;
+  const int ldG = mom ? 64 : G;
+  const float* dG = mom ? J.dab : J.dg;
+  const int cl = threadIdx.x & 15, tg = threadIdx.x >> 4;
+  const int col = blockIdx.x * 16 + cl;
+  float acc[GM];
+#pragma unroll
+  for (int g = 0; g < GM; ++g) acc[g] = 0.f;
+  if (col <= M) {
+#pragma unroll 2
+    for (int t = tg; t < T; t += 16) {
+      const float x = col < M ? J.macro[(size_t)t * M + col] : 1.f;
+      const float* dr = dG + (size_t)t * ldG;
+#pragma unroll
+      for (int g = 0; g < GM; ++g) acc[g] += dr[g] * x;
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < GM; ++g) red[tg][cl][g] = acc[g];
+  __syncthreads();
+  // thread (cl, g-slice) sums the 16 time groups in order
+  for (int idx = threadIdx.x; idx < 16 * G; idx += 256) {
+    const int c = idx & 15, g = idx >> 4;
+    const int cc = blockIdx.x * 16 + c;
+    if (cc > M) continue;
+    float s = 0.f;
+    for (int q = 0; q < 16; ++q) s += red[q][c][g];
+    if (mom) {
+      const PackLayer& L0 = md->m[0];
+      if (cc < M) J.grads[L0.w_off + (size_t)g * L0.ld + cc] = s;
+      else J.grads[L0.b_off + g] = s;
+    } else if (cc < M) {
+      J.grads[md->lstm_w_ih[0] + (size_t)g * M + cc] = s;
+    }
+  }
+}
+
+void launch_lstm_bwd(const UpdJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
+                     int T, int phase, hipStream_t st) {
+  if (phase != 2 && mh.nrnn > 0) {
+    const size_t sh = (size_t)T * (8 * mh.H + 3 * mh.H) * sizeof(float);
+    if (sh > 160 * 1024) dlap_throw_hip(hipErrorInvalidValue, "lstm_bwd: T*H too large for LDS", __FILE__, __LINE__);
+    if (mh.H <= 4) hipLaunchKernelGGL((k_lstm_bwd<4>), dim3(njobs), dim3(256), sh, st, jobs, md);
+    else if (mh.H <= 8) hipLaunchKernelGGL((k_lstm_bwd<8>), dim3(njobs), dim3(256), sh, st, jobs, md);
+    else if (mh.H <= 16) hipLaunchKernelGGL((k_lstm_bwd<16>), dim3(njobs), dim3(256), sh, st, jobs, md);
+    else hipLaunchKernelGGL((k_lstm_bwd<32>), dim3(njobs), dim3(256), sh, st, jobs, md);
+    HIP_OK(hipGetLastError());
+  }
+  if (mh.M == 0) return;
+  if (phase != 2 && mh.nrnn == 0) return;
+  const int G = phase == 2 ? mh.m[0].out : 4 * mh.H;
+  dim3 grid((mh.M + 1 + 15) / 16, njobs);
+  if (G <= 16) hipLaunchKernelGGL((k_wgrad<16>), grid, dim3(256), 0, st, jobs, md, phase);
+  else if (G <= 32) hipLaunchKernelGGL((k_wgrad<32>), grid, dim3(256), 0, st, jobs, md, phase);
+  else hipLaunchKernelGGL((k_wgrad<64>), grid, dim3(256), 0, st, jobs, md, phase);
   HIP_OK(hipGetLastError());
 }

@@ -35,6 +35,7 @@ __global__ __launch_bounds__(256) void k_finalize(const FinJob* __restrict__ job
     const int tpos = ti - G.slice * tps;
     const float* src = J.slab + (size_t)G.slice * J.nslab * slab_stride + tpos * 4096 + e;
     float s = 0.f;
+#pragma unroll 16
     for (int k = 0; k < J.nslab; ++k) s += src[(size_t)k * slab_stride];
     J.grads[G.w_off + o * G.ld + G.col0 + i] = s;
     return;
@@ -47,22 +48,33 @@ __global__ __launch_bounds__(256) void k_finalize(const FinJob* __restrict__ job
     if (dst < 0) return;
     const float* src = J.slab + 1 * 4096 + e;   // slice-0 slabs (tps = 1)
     float s = 0.f;
+#pragma unroll 16
     for (int k = 0; k < J.nslab; ++k) s += src[(size_t)k * slab_stride];
     J.grads[dst] = s;
     return;
   }
   b -= nb_extra;
-  // per-period segment sums
+  // per-period segment sums: one block per period, threads = (column d, row group)
   const int D = mom ? 64 : (md->nrnn > 0 ? md->Dm : 0);
-  if (D == 0) return;
-  const int idx = b * 256 + threadIdx.x;
-  if (idx >= J.T * D) return;
-  const int t = idx / D, d = idx - t * D;
+  const int t = b;
+  if (D == 0 || t >= J.T) return;
+  __shared__ float red[256];
+  int Dp = 1;
+  while (Dp < D) Dp <<= 1;
+  const int nrg = 256 / Dp, d = threadIdx.x % Dp, rg = threadIdx.x / Dp;
   const float* src = mom ? J.v : J.u;
+  const int r0 = J.row_ptr[t], r1 = J.row_ptr[t + 1];
   float s = 0.f;
-  for (int r = J.row_ptr[t]; r < J.row_ptr[t + 1]; ++r) s += src[(size_t)r * D + d];
-  if (mom) J.dab[t * 64 + d] = s;
-  else J.dpp[t * D + d] = s;
+  if (d < D)
+    for (int r = r0 + rg; r < r1; r += nrg) s += src[(size_t)r * D + d];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (rg == 0 && d < D) {
+    float tot = 0.f;
+    for (int g = 0; g < nrg; ++g) tot += red[g * Dp + d];
+    if (mom) J.dab[t * 64 + d] = tot;
+    else J.dpp[t * D + d] = tot;
+  }
 }
 
 void launch_finalize(const FinJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
@@ -70,7 +82,7 @@ void launch_finalize(const FinJob* jobs, int njobs, const ModelDesc* md, const M
   const bool mom = phase == 2;
   const int ntile = mom ? mh.ntile_m : mh.ntile_s;
   const int D = mom ? 64 : (mh.nrnn > 0 ? mh.Dm : 0);
-  const int nb = ntile * 16 + (SLAB_EXTRA + 255) / 256 + (tmax * D + 255) / 256;
+  const int nb = ntile * 16 + (SLAB_EXTRA + 255) / 256 + (D > 0 ? tmax : 0);
   hipLaunchKernelGGL(k_finalize, dim3(nb, njobs), dim3(256), 0, st, jobs, md, phase, slab_stride);
   HIP_OK(hipGetLastError());
 }
@@ -156,129 +168,14 @@ void launch_pack(float* const*, const UpdJob* jobs, int njobs, const ModelDesc* 
   HIP_OK(hipGetLastError());
 }
 
-// ============================================================ LSTM BPTT =================
-DLAP_DEV void lstm_backward(const UpdJob& J, const ModelDesc* __restrict__ md, float* lds) {
-  const int T = J.T, H = md->H, G4 = 4 * H, M = md->M;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool drop = md->dropout > 0.f;
-  const uint32_t thr = (uint32_t)(md->dropout * 16777216.f + 0.5f);
-  const float scale = drop ? 1.f / (1.f - md->dropout) : 1.f;
-  const uint32_t step = (uint32_t)*J.drop_step;
-  float* whh = lds;                          // [4H][H]
-  for (int l = md->nrnn - 1; l >= 0; --l) {
-    const float* Wih = J.params + md->lstm_w_ih[l];
-    const float* Whh = J.params + md->lstm_w_hh[l];
-    const int in_dim = l == 0 ? M : H;
-    const float* sg = J.sg + (size_t)l * T * G4;
-    const float* sc = J.sc + (size_t)l * T * H;
-    const float* sh = J.sh + (size_t)l * T * H;
-    const float* dout = l == md->nrnn - 1 ? J.dpp : J.dx;
-    for (int i = threadIdx.x; i < G4 * H; i += 256) whh[i] = Whh[i];
-    __syncthreads();
-    if (wave == 0) {
-      float dh_next = 0.f, dc_next = 0.f;
-      const int k = lane < H ? lane : 0;
-      for (int t = T - 1; t >= 0; --t) {
-        const float* g = sg + (size_t)t * G4;
-        const float gi = g[k], gf = g[H + k], gg = g[2 * H + k], go = g[3 * H + k];
-        const float c = sc[(size_t)t * H + k];
-        const float cp = t > 0 ? sc[(size_t)(t - 1) * H + k] : 0.f;
-        const float dh = (lane < H ? dout[(size_t)t * H + k] : 0.f) + dh_next;
-        const float tc = tanhf(c);
-        const float dO = dh * tc;
-        const float dc = dh * go * (1.f - tc * tc) + dc_next;
-        const float pi = dc * gg * gi * (1.f - gi);
-        const float pf = dc * cp * gf * (1.f - gf);
-        const float pg = dc * gi * (1.f - gg * gg);
-        const float po = dO * go * (1.f - go);
-        dc_next = dc * gf;
-        if (lane < H) {
-          float* d = J.dg + (size_t)t * G4;
-          d[k] = pi; d[H + k] = pf; d[2 * H + k] = pg; d[3 * H + k] = po;
-        }
-        float s = 0.f;
-        for (int j = 0; j < H; ++j) {
-          const float a = __shfl(pi, j, 64), b = __shfl(pf, j, 64);
-          const float c2 = __shfl(pg, j, 64), d2 = __shfl(po, j, 64);
-          s += whh[(j) * H + k] * a + whh[(H + j) * H + k] * b + whh[(2 * H + j) * H + k] * c2 +
-               whh[(3 * H + j) * H + k] * d2;
-        }
-        dh_next = lane < H ? s : 0.f;
-      }
-    }
-    __syncthreads();
-    // weight / bias gradients (fixed-order sums over t)
-    float* gW_ih = J.grads + md->lstm_w_ih[l];
-    float* gW_hh = J.grads + md->lstm_w_hh[l];
-    float* gb_ih = J.grads + md->lstm_b_ih[l];
-    float* gb_hh = J.grads + md->lstm_b_hh[l];
-    const uint32_t key_below = l > 0 ? dropout_key(J.seed, step, 32 + (l - 1)) : 0u;
-    for (int idx = threadIdx.x; idx < G4 * (H + in_dim + 1); idx += 256) {
-      const int g = idx % G4, c = idx / G4;
-      float s = 0.f;
-      if (c < H) {                           // W_hh[g][c]: sum_t dg[t][g] h_{t-1}[c]
-        for (int t = 1; t < T; ++t) s += J.dg[(size_t)t * G4 + g] * sh[(size_t)(t - 1) * H + c];
-        gW_hh[g * H + c] = s;
-      } else if (c < H + in_dim) {           // W_ih[g][m]: sum_t dg[t][g] x_t[m]
-        const int m = c - H;
-        if (l == 0) {
-          for (int t = 0; t < T; ++t) s += J.dg[(size_t)t * G4 + g] * J.macro[(size_t)t * M + m];
-        } else {
-          const float* hb = J.sh + (size_t)(l - 1) * T * H;
-          for (int t = 0; t < T; ++t) {
-            float x = hb[(size_t)t * H + m];
-            if (drop) x = dropout_keep(key_below, (uint32_t)t, (uint32_t)m, thr) ? x * scale : 0.f;
-            s += J.dg[(size_t)t * G4 + g] * x;
-          }
-        }
-        gW_ih[g * in_dim + m] = s;
-      } else {
-        for (int t = 0; t < T; ++t) s += J.dg[(size_t)t * G4 + g];
-        gb_ih[g] = s;
-        gb_hh[g] = s;
-      }
-    }
-    if (l > 0) {
-      // d(input of layer l) -> d(output of layer l-1) through the inter-layer dropout
-      for (int idx = threadIdx.x; idx < T * H; idx += 256) {
-        const int t = idx / H, m = idx - t * H;
-        float s = 0.f;
-        for (int g = 0; g < G4; ++g) s += Wih[g * H + m] * J.dg[(size_t)t * G4 + g];
-        if (drop) s = dropout_keep(key_below, (uint32_t)t, (uint32_t)m, thr) ? s * scale : 0.f;
-        J.dx[idx] = s;
-      }
-    }
-    __syncthreads();
-  }
-}
-
 // ============================================================ update ====================
 __global__ __launch_bounds__(256) void k_update(const UpdJob* __restrict__ jobs,
                                                 const ModelDesc* __restrict__ md, int phase, float lr,
                                                 int apply) {
   const UpdJob& J = jobs[blockIdx.x];
-  __shared__ float lds[DLAP_MAX_H * 4 * DLAP_MAX_H];
   __shared__ float red[4];
   const bool mom = phase == 2;
-  if (!mom && md->nrnn > 0) lstm_backward(J, md, lds);
-  if (mom) {
-    // moment layer-0: macro columns and bias from the per-period sums
-    const PackLayer& L0 = md->m[0];
-    const int M = md->M;
-    for (int idx = threadIdx.x; idx < L0.out * (M + 1); idx += 256) {
-      const int c = idx / (M + 1), m = idx - c * (M + 1);
-      float s = 0.f;
-      if (m < M) {
-        for (int t = 0; t < J.T; ++t) s += J.dab[t * 64 + c] * J.macro[(size_t)t * M + m];
-        J.grads[L0.w_off + c * L0.ld + m] = s;
-      } else {
-        for (int t = 0; t < J.T; ++t) s += J.dab[t * 64 + c];
-        J.grads[L0.b_off + c] = s;
-      }
-    }
-  }
-  __syncthreads();
-  if (!apply) return;   // gradients only (tests / module API)
+  (void)apply;
   const int p0 = mom ? md->P_sdf : 0, p1 = mom ? md->P : md->P_sdf;
   float ss = 0.f;
   for (int i = p0 + threadIdx.x; i < p1; i += 256) { const float g = J.grads[i]; ss += g * g; }

@@ -3,6 +3,7 @@
 #include "common.h"
 
 #define DLAP_MAX_T 2048   // max periods per split handled by the LDS-staged passes
+#define DLAP_TCH 8        // time chunks of the asset pass
 
 // Scalar slots written per job by k_job_metrics.
 enum {
@@ -19,6 +20,10 @@ struct LossJob {
   const float* meanR;    // [T] sum_i R m / max(N_t, 1)
   const float* RR;       // [T] sum_i R^2 m
   const float* invT;     // [N] 1 / max(T_i, 1)
+  const int* row_ptr;    // [T+1] compact rows of each period
+  const int2* rowti;     // [R] (t, i) of each compact row
+  const float* Rc;       // [R] returns of the compact rows
+  float* mu;             // [T] cross-sectional mean of the raw weights
   float Nbar;
   int T, N, K;
   int normalize, weighted;
@@ -26,8 +31,8 @@ struct LossJob {
   float res_factor;      // residual_loss_factor (gradient only in training jobs)
   float coef_c, coef_u;  // dL/dE = coef * E (0 disables the write)
   // per (model, split) workspace
-  const float* w;        // [T*N] raw SDF output
-  float* wn;             // [T*N] normalised weights w'
+  const float* w;        // [R] raw SDF output (compact rows)
+  float* wn;             // [T*N] normalised weights w' (dense, zero at invalid entries)
   const float* h;        // [T*N*K] moments (nullptr: unconditional only)
   float* P;              // [T] weighted portfolio return
   float* port;           // [T] L1-normalised portfolio return (nullptr: skip)
@@ -36,8 +41,10 @@ struct LossJob {
   float* Eu;             // [N]
   float* dE;             // [N*K] (nullptr: skip)
   float* dEu;            // [N]   (nullptr: skip)
-  float* part;           // [2 * ceil(N/64)] partial loss sums
-  float* dw;             // [T*N]
+  float* part;           // [2 * ceil(N/256)] partial loss sums
+  float* pe;             // [DLAP_TCH][N][K] chunk partials of E
+  float* pu;             // [DLAP_TCH][N] chunk partials of E_unc
+  float* dw;             // [R] dL/dw_raw (compact rows)
   float* rstat;          // [T*4] residual statistics (nullptr: residual loss off)
   float* scal;           // [SC_NSCAL]
 };

@@ -20,4 +20,5 @@ struct RnnJob {
   int train;
 };
 
-void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* md, hipStream_t st);
+void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* md, const ModelDesc& mh,
+                     hipStream_t st);

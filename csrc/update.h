@@ -64,6 +64,8 @@ void launch_finalize(const FinJob* jobs, int njobs, const ModelDesc* md, const M
                      int phase, int slab_stride, int tmax, hipStream_t st);
 void launch_update(const UpdJob* jobs, int njobs, const ModelDesc* md, int phase, float lr,
                    hipStream_t st, int apply = 1);
+void launch_lstm_bwd(const UpdJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
+                     int T, int phase, hipStream_t st);
 void launch_pack(float* const* params_unused, const UpdJob* jobs, int njobs, const ModelDesc* md,
                  hipStream_t st);
 void launch_epoch_end(const EpochJob* jobs, int njobs, int phase, int ignore_epoch, float sel,

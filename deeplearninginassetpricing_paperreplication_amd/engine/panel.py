@@ -6,7 +6,7 @@ HBM in a compacted layout:
 
   X         [R, KP] bf16   valid rows only, in (t, i) order; columns [F, F+Dm) are left zero
                            (the kernels insert the per-period LSTM / macro inputs there)
-  row_dense [R]     int32  t*N + i of each compact row
+  rowti     [R, 2]  int32  (t, i) of each compact row
   row_ptr   [T+1]   int32  first compact row of each period
   Rm, mask  [T*N]   fp32   dense returns (zero-filled) and 0/1 mask
   macro     [T, M]  fp32   standardised macro series
@@ -41,7 +41,7 @@ class PanelSplit:
     N: int
     R: int
     X: np.ndarray          # uint16 [R, KP]
-    row_dense: np.ndarray  # int32 [R]
+    rowti: np.ndarray      # int32 [R, 2]
     row_ptr: np.ndarray    # int32 [T+1]
     Rm: np.ndarray         # float32 [T*N]
     mask: np.ndarray       # float32 [T*N]
@@ -67,13 +67,13 @@ def prepare_split(batch: Dict, KP: int) -> PanelSplit:
     X = np.zeros((R, KP), dtype=np.uint16)
     if R:
         X[:, :F] = f32_to_bf16_bits(feats[tt, ii])
-    row_dense = (tt.astype(np.int64) * N + ii).astype(np.int32)
+    rowti = np.ascontiguousarray(np.stack([tt, ii], axis=1).astype(np.int32))
     counts = mask.sum(axis=1)
     row_ptr = np.zeros(T + 1, dtype=np.int32)
     np.cumsum(counts, out=row_ptr[1:])
     macro = batch.get("macro_features")
     macro = np.zeros((T, 0), np.float32) if macro is None else _np(macro).astype(np.float32)
-    return PanelSplit(T, N, R, X, row_dense, row_ptr,
+    return PanelSplit(T, N, R, X, rowti, row_ptr,
                       np.ascontiguousarray(np.where(mask, ret, 0).reshape(-1), dtype=np.float32),
                       np.ascontiguousarray(mask.reshape(-1), dtype=np.float32),
                       np.ascontiguousarray(macro))

@@ -70,7 +70,7 @@ class GANEngine:
             if b is None:
                 continue
             ps = prepare_split(b, self.KP)
-            self.eng.set_split(s, ps.X.reshape(-1), ps.row_dense, ps.row_ptr, ps.Rm, ps.mask,
+            self.eng.set_split(s, ps.X.reshape(-1), ps.rowti.reshape(-1), ps.row_ptr, ps.Rm, ps.mask,
                                ps.macro.reshape(-1), ps.T, ps.N)
             self.splits[s] = ps
 
