@@ -19,6 +19,19 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16;
 
 #define DLAP_DEV __device__ __forceinline__
+
+// Pointers loaded from job records are generic (flat) to the compiler. A flat access counts
+// against both vmcnt and lgkmcnt, so every LDS wait would also wait for outstanding global
+// loads/stores (killing software prefetch). gp() re-qualifies a pointer as global memory so
+// the access compiles to global_load/global_store (vmcnt only).
+// (The host pass of a HIP compile only type-checks device code: the qualifier is empty there.)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define DLAP_GLOBAL __attribute__((address_space(1)))
+#else
+#define DLAP_GLOBAL
+#endif
+template <typename T>
+DLAP_DEV DLAP_GLOBAL T* gp(T* p) { return (DLAP_GLOBAL T*)p; }
 #define DLAP_MAXL 6   // max MFMA layers per tower
 
 #define HIP_OK(expr)                                                                        \
@@ -33,6 +46,11 @@ DLAP_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
+// 16-byte vector load through a float pointer, keeping its address space
+DLAP_DEV f32x4 ld4(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
+#if defined(__HIP_DEVICE_COMPILE__)
+DLAP_DEV f32x4 ld4(const DLAP_GLOBAL float* p) { return *(const DLAP_GLOBAL f32x4*)p; }
+#endif
 DLAP_DEV f32x4 zero4() { return f32x4{0.f, 0.f, 0.f, 0.f}; }
 
 DLAP_DEV __bf16 to_bf16(float x) { return (__bf16)x; }

@@ -11,6 +11,7 @@
 //     from device counters, so it is captured ONCE per phase into a hipGraph and replayed;
 //   * history, best-epoch tracking and checkpoint snapshots are device-side: the host only
 //     synchronises at print intervals / phase boundaries.
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
@@ -71,6 +72,8 @@ struct ModelSplitWS {   // per (model, split)
   DevBuf<float> pp, abias, xg, xin, sg, sc, sh;
   DevBuf<float> w, wn, h, P, port, sdf, mu, E, Eu, dE, dEu, part, pe, pu, dw, rstat, scal;
   DevBuf<float> u, v, dpp, dab, dg, dx;
+  DevBuf<uint32_t> gb, mgb;   // forward gate words of the train split (SDF / moment hidden)
+  DevBuf<float> scal_prev;    // train split: metrics of the last finished step (bookkeeping)
 };
 
 struct ModelState {
@@ -89,6 +92,9 @@ class Engine {
          float residual, int G, int max_epochs)
       : G_(G), max_epochs_(max_epochs) {
     HIP_OK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&st2_, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
                residual);
     d_desc_.alloc(sizeof(ModelDesc));
@@ -107,6 +113,9 @@ class Engine {
   }
   ~Engine() {
     for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
+    if (ev_fork_) (void)hipEventDestroy(ev_fork_);
+    if (ev_join_) (void)hipEventDestroy(ev_join_);
+    if (st2_) (void)hipStreamDestroy(st2_);
     if (st_) (void)hipStreamDestroy(st_);
   }
 
@@ -115,7 +124,7 @@ class Engine {
     py::dict d;
     d["P"] = md_.P; d["P_sdf"] = md_.P_sdf; d["KP"] = md_.KP; d["KS1"] = md_.KS1; d["WMB"] = md_.WMB;
     d["Dm"] = md_.Dm; d["blob_frags"] = md_.md.blob_frags; d["aux_floats"] = md_.md.aux_floats;
-    d["ntile_s"] = md_.ntile_s; d["ntile_m"] = md_.ntile_m; d["G"] = G_;
+    d["ntile_s"] = md_.ntile_s; d["tps_s"] = md_.tps_s; d["ntile_m"] = md_.ntile_m; d["G"] = G_;
     return d;
   }
 
@@ -227,12 +236,13 @@ class Engine {
   // ---------------------------------------------------------------- phase control -------
   // Reset the per-phase trackers (reference: fresh best values per phase).
   void begin_phase(int phase) {
+    sync();   // all queued epochs are done before the trackers are reset (synchronous copies)
     for (int g = 0; g < G_; ++g) {
       ModelState& S = models_[g];
       const float inf = INFINITY;
       float best[3] = {inf, -inf, -inf};
-      HIP_OK(hipMemcpyAsync(S.best.p, best, sizeof(best), hipMemcpyHostToDevice, st_));
-      HIP_OK(hipMemsetAsync(S.snap_flags.p, 0, 2 * sizeof(int), st_));
+      HIP_OK(hipMemcpy(S.best.p, best, sizeof(best), hipMemcpyHostToDevice));
+      HIP_OK(hipMemset(S.snap_flags.p, 0, 2 * sizeof(int)));
       int ep[2];
       HIP_OK(hipMemcpy(ep, S.ep.p, sizeof(ep), hipMemcpyDeviceToHost));
       ep[1] = 0;
@@ -243,11 +253,13 @@ class Engine {
   }
   py::array_t<int> snap_flags(int g) {
     ModelState& S = models_[check_g(g)];
+    sync();
     py::array_t<int> out(2);
     HIP_OK(hipMemcpy(out.mutable_data(), S.snap_flags.p, 2 * sizeof(int), hipMemcpyDeviceToHost));
     return out;
   }
   int epoch_count(int g) {
+    sync();
     int ep[2];
     HIP_OK(hipMemcpy(ep, models_[check_g(g)].ep.p, sizeof(ep), hipMemcpyDeviceToHost));
     return ep[0];
@@ -262,27 +274,35 @@ class Engine {
   // ---------------------------------------------------------------- execution -----------
   // One epoch of `phase` (1, 2, 3): train step (+ valid/test evaluation in phases 1/3) and
   // the device bookkeeping. `n` epochs are run by replaying the phase graph.
+  // Runs n epochs of a phase. With evaluation splits (phases 1 and 3) the epochs are
+  // software-pipelined: the evaluation + bookkeeping of epoch e-1 and the forward/backward of
+  // epoch e read the same parameters, so they run as two concurrent branches of one hipGraph
+  // and join before the Adam update:   head | pipe x (n-1) | tail.
   void run_epochs(int phase, int n, float lr, int ignore_epoch, float sel, bool use_graph) {
     if (!splits_[0].set) throw std::runtime_error("train split not set");
     if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
-    auto key = graph_key(phase, lr, ignore_epoch, sel);
+    if (n <= 0) return;
+    const bool pipe = phase != 2 && n_eval_jobs_ > 0 && pipeline_;
     if (!use_graph) {
       for (int e = 0; e < n; ++e) enqueue_epoch(phase, lr, ignore_epoch, sel);
       return;
     }
-    auto it = graphs_.find(key);
-    if (it == graphs_.end()) {
-      hipGraph_t graph;
-      HIP_OK(hipStreamBeginCapture(st_, hipStreamCaptureModeThreadLocal));
-      enqueue_epoch(phase, lr, ignore_epoch, sel);
-      HIP_OK(hipStreamEndCapture(st_, &graph));
-      hipGraphExec_t exec;
-      HIP_OK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
-      HIP_OK(hipGraphDestroy(graph));
-      it = graphs_.emplace(key, exec).first;
+    if (!pipe) {
+      hipGraphExec_t g = graph_for(graph_key(phase, lr, ignore_epoch, sel, 0),
+                                   [&] { enqueue_epoch(phase, lr, ignore_epoch, sel); });
+      for (int e = 0; e < n; ++e) HIP_OK(hipGraphLaunch(g, st_));
+      return;
     }
-    for (int e = 0; e < n; ++e) HIP_OK(hipGraphLaunch(it->second, st_));
+    hipGraphExec_t head = graph_for(graph_key(phase, lr, ignore_epoch, sel, 1), [&] { enqueue_head(phase, lr); });
+    hipGraphExec_t body = graph_for(graph_key(phase, lr, ignore_epoch, sel, 2),
+                                    [&] { enqueue_pipe(phase, lr, ignore_epoch, sel); });
+    hipGraphExec_t tail = graph_for(graph_key(phase, lr, ignore_epoch, sel, 3),
+                                    [&] { enqueue_tail(phase, ignore_epoch, sel); });
+    HIP_OK(hipGraphLaunch(head, st_));
+    for (int e = 1; e < n; ++e) HIP_OK(hipGraphLaunch(body, st_));
+    HIP_OK(hipGraphLaunch(tail, st_));
   }
+  void set_pipeline(bool on) { pipeline_ = on; }
 
   // Pieces used by the module-level API / tests (no bookkeeping).
   void forward_split(int s, bool train_mode, bool do_mom) {
@@ -313,7 +333,7 @@ class Engine {
   }
   py::array_t<float> read_aux(int g) { sync(); return down(models_[check_g(g)].aux); }
   py::array_t<uint16_t> read_blob(int g) {
-    sync();
+    sync();  // (already synchronous)
     ModelState& S = models_[check_g(g)];
     py::array_t<uint16_t> out(S.blob.n);
     HIP_OK(hipMemcpy(out.mutable_data(), S.blob.p, S.blob.n * 2, hipMemcpyDeviceToHost));
@@ -325,6 +345,8 @@ class Engine {
  private:
   int G_, max_epochs_;
   hipStream_t st_ = nullptr;
+  hipStream_t st2_ = nullptr;                // evaluation branch of the pipelined epoch graph
+  hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
   ModelDesc md_{};
   DevBuf<char> d_desc_;
   SplitDev splits_[3];
@@ -340,11 +362,12 @@ class Engine {
   int n_eval_jobs_ = 0;
   int tmax_eval_ = 0, nmax_eval_ = 0;
 
-  static std::string graph_key(int phase, float lr, int ig, float sel) {
-    char b[128];
-    snprintf(b, sizeof b, "%d/%.9g/%d/%.3g", phase, lr, ig, sel);
+  static std::string graph_key(int phase, float lr, int ig, float sel, int kind) {
+    char b[160];
+    snprintf(b, sizeof b, "%d/%.9g/%d/%.3g/%d", phase, lr, ig, sel, kind);
     return b;
   }
+  bool pipeline_ = true;
   int check_g(int g) const {
     if (g < 0 || g >= G_) throw std::out_of_range("model index");
     return g;
@@ -377,7 +400,7 @@ class Engine {
     DevBuf<char> tmp;
     std::vector<UpdJob> v{J};
     upload(tmp, v);
-    launch_pack(nullptr, reinterpret_cast<const UpdJob*>(tmp.p), 1, reinterpret_cast<const ModelDesc*>(d_desc_.p), st_);
+    launch_pack(nullptr, reinterpret_cast<const UpdJob*>(tmp.p), 1, reinterpret_cast<const ModelDesc*>(d_desc_.p), md_, st_);
     sync();
   }
 
@@ -442,7 +465,9 @@ class Engine {
     D.s_fwd0 = 0; D.s_fwd = 4 * d.KS1; D.s_bwd = D.s_fwd + 8 * (d.nl_s - 1);
     D.m_fwd0 = D.s_bwd + 8 * (d.nl_s - 1); D.m_fwd = D.m_fwd0 + d.WMB * d.KS1;
     D.m_bwd = D.m_fwd + (d.nl_m - 1) * d.WMB * KSM;
-    D.blob_frags = D.m_bwd + (d.nl_m - 1) * d.WMB * KSM;
+    D.s_upp = D.m_bwd + (d.nl_m - 1) * d.WMB * KSM;
+    D.ubpp = nrnn > 0 ? (d.Dm + 15) / 16 : 0;
+    D.blob_frags = D.s_upp + 2 * D.ubpp;
     D.a_sb = 0; D.a_wo = 64 * d.nl_s; D.a_bo = D.a_wo + 64; D.a_pp = D.a_bo + 4;
     D.a_mb = D.a_pp + 64 * d.Dm; D.aux_floats = D.a_mb + 64 * d.nl_m;
     // gradient tiles: layer-0 chunks first, then one tile per later layer (slice = tile, TPS 1)
@@ -452,13 +477,21 @@ class Engine {
       d.tile_s[t] = GradTile{d.s[0].w_off, d.s[0].ld, 0, d.s[0].out, d.s[0].in, c, t};
     for (int j = 1; j < d.nl_s; ++j, ++t)
       d.tile_s[t] = GradTile{d.s[j].w_off, d.s[j].ld, 0, d.s[j].out, d.s[j].in, 0, t};
-    d.ntile_s = d.nslice_s = t;
+    d.ntile_s = t;
+    // two gradient tiles per slice share one forward recompute (fits the 512-register
+    // budget of a single wave per SIMD); DLAP_TPS=1 forces one tile per slice
+    const char* tps_env = std::getenv("DLAP_TPS");
+    const bool tps2 = d.KS1 == 2 && d.ntile_s == 2 && !(tps_env && std::atoi(tps_env) == 1);
+    d.tps_s = tps2 ? 2 : 1;
+    d.nslice_s = (d.ntile_s + d.tps_s - 1) / d.tps_s;
+    for (int k = 0; k < d.ntile_s; ++k) d.tile_s[k].slice = k / d.tps_s;
     t = 0;
     for (int c = 0; c < C0; ++c, ++t)
       d.tile_m[t] = GradTile{d.m[0].w_off, d.m[0].ld, d.m[0].col0, d.m[0].out, d.m[0].in, c, t};
     for (int j = 1; j < d.nl_m; ++j, ++t)
       d.tile_m[t] = GradTile{d.m[j].w_off, d.m[j].ld, 0, d.m[j].out, d.m[j].in, 0, t};
     d.ntile_m = d.nslice_m = t;
+    d.tps_m = 1;
     for (int e = 0; e < SLAB_EXTRA; ++e) { d.extra_s[e] = -1; d.extra_m[e] = -1; }
     for (int j = 0; j < d.nl_s; ++j)
       for (int o = 0; o < d.s[j].out; ++o) d.extra_s[j * 64 + o] = d.s[j].b_off + o;
@@ -468,7 +501,7 @@ class Engine {
       for (int o = 0; o < d.m[j].out; ++o) d.extra_m[j * 64 + o] = d.m[j].b_off + o;
   }
 
-  int slab_stride() const { return 4096 + SLAB_EXTRA; }
+  int slab_stride() const { return std::max(md_.tps_s, md_.tps_m) * 4096 + SLAB_EXTRA; }
 
   void alloc_ws(int s) {
     const SplitDev& D = splits_[s];
@@ -485,6 +518,7 @@ class Engine {
       W.part.alloc(2 * ((N + 255) / 256));
       W.pe.alloc((size_t)DLAP_TCH * N * K); W.pu.alloc((size_t)DLAP_TCH * N);
       W.scal.alloc(SC_NSCAL);
+      if (s == 0) W.scal_prev.alloc(SC_NSCAL);
       if (md_.residual_factor > 0.f) W.rstat.alloc((size_t)T * 4);
       if (s == 0) {
         W.dw.alloc((size_t)std::max(R, 1));
@@ -492,6 +526,9 @@ class Engine {
         W.v.alloc((size_t)R * 64);
         W.dpp.alloc((size_t)T * std::max(md_.Dm, 1));
         W.dab.alloc((size_t)T * 64);
+        const size_t ntl = (size_t)(R + 31) / 32;
+        W.gb.alloc(std::max<size_t>(ntl * md_.nl_s * 64, 1), false);
+        W.mgb.alloc(std::max<size_t>(ntl * std::max(md_.nl_m - 1, 0) * 64, 1), false);
         if (md_.nrnn > 0) {
           W.sg.alloc((size_t)md_.nrnn * T * 4 * H);
           W.sc.alloc((size_t)md_.nrnn * T * H);
@@ -620,10 +657,16 @@ class Engine {
       for (int g = 0; g < G_; ++g) {
         mt.push_back(mlp_job(g, 0, true, true, phase != 1));
         mb.push_back(mlp_job(g, 0, true, true, true));
+        // the training forward stores the gate words its backward reuses
+        if (phase == 2) {
+          if (md_.nl_m > 1) mt.back().mgbits = mb.back().mgbits = ws(g, 0).mgb.p;
+        } else {
+          mt.back().gbits = mb.back().gbits = ws(g, 0).gb.p;
+        }
         lt.push_back(loss_job(g, 0, phase));
         ModelState& S = models_[g];
         EpochJob E{};
-        E.sc_train = ws(g, 0).scal.p;
+        E.sc_train = ws(g, 0).scal_prev.p;
         E.sc_valid = (phase != 2 && splits_[1].set) ? ws(g, 1).scal.p : nullptr;
         E.sc_test = (phase != 2 && splits_[2].set) ? ws(g, 2).scal.p : nullptr;
         E.gnorm = S.gnorm.p; E.hist = S.hist.p; E.ep = S.ep.p; E.best = S.best.p;
@@ -663,7 +706,7 @@ class Engine {
                          md_.WMB, slab_stride(), st_);
     } else {
       launch_period_bwd(as<LossJob>(j_loss_train_[phase]), G_, D.T, st_);
-      launch_mlp_bwd_sdf(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_s, 1, md_.md, md_.KS1,
+      launch_mlp_bwd_sdf(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_s, md_.tps_s, md_.md, md_.KS1,
                          slab_stride(), st_);
     }
     launch_finalize(as<FinJob>(j_fin_), G_, dd(), md_, phase, slab_stride(), D.T, st_);
@@ -671,22 +714,68 @@ class Engine {
   }
   void enqueue_train(int phase, float lr) {
     enqueue_train_grads(phase);
-    launch_update(as<UpdJob>(j_upd_), G_, dd(), phase, lr, st_);
+    copy_train_scal(st_);
+    launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);
   }
-  void enqueue_eval() {
+  void enqueue_eval(hipStream_t st) {
     if (n_eval_jobs_ == 0) return;
-    launch_prologue(as<RnnJob>(j_rnn_eval_), n_eval_jobs_, tmax_eval_, dd(), md_, st_);
+    launch_prologue(as<RnnJob>(j_rnn_eval_), n_eval_jobs_, tmax_eval_, dd(), md_, st);
     int gx = std::max(gx_fwd_[1], gx_fwd_[2]);
-    launch_mlp_fwd(as<MlpJob>(j_mlp_eval_), n_eval_jobs_, gx, md_.md, md_.KS1, md_.WMB, st_);
-    launch_period_fwd(as<LossJob>(j_loss_eval_), n_eval_jobs_, tmax_eval_, st_);
-    launch_asset(as<LossJob>(j_loss_eval_), n_eval_jobs_, nmax_eval_, st_);
-    launch_job_metrics(as<LossJob>(j_loss_eval_), n_eval_jobs_, st_);
+    launch_mlp_fwd(as<MlpJob>(j_mlp_eval_), n_eval_jobs_, gx, md_.md, md_.KS1, md_.WMB, st);
+    launch_period_fwd(as<LossJob>(j_loss_eval_), n_eval_jobs_, tmax_eval_, st);
+    launch_asset(as<LossJob>(j_loss_eval_), n_eval_jobs_, nmax_eval_, st);
+    launch_job_metrics(as<LossJob>(j_loss_eval_), n_eval_jobs_, st);
   }
-  void enqueue_epoch(int phase, float lr, int ignore_epoch, float sel) {
-    enqueue_train(phase, lr);
-    if (phase != 2) enqueue_eval();
+  void copy_train_scal(hipStream_t st) {
+    for (int g = 0; g < G_; ++g)
+      HIP_OK(hipMemcpyAsync(ws(g, 0).scal_prev.p, ws(g, 0).scal.p, SC_NSCAL * sizeof(float),
+                            hipMemcpyDeviceToDevice, st));
+  }
+  void enqueue_epoch_end(int phase, int ignore_epoch, float sel, hipStream_t st) {
     launch_epoch_end(as<EpochJob>(j_epoch_[phase]), G_, phase, ignore_epoch, sel, md_.residual_factor,
-                     md_.P, st_);
+                     md_.P, st);
+  }
+  // sequential epoch: train step, evaluation, bookkeeping
+  void enqueue_epoch(int phase, float lr, int ignore_epoch, float sel) {
+    enqueue_train_grads(phase);
+    copy_train_scal(st_);
+    launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);
+    if (phase != 2) enqueue_eval(st_);
+    enqueue_epoch_end(phase, ignore_epoch, sel, st_);
+  }
+  void enqueue_head(int phase, float lr) {
+    enqueue_train_grads(phase);
+    copy_train_scal(st_);
+    launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);
+  }
+  void enqueue_pipe(int phase, float lr, int ignore_epoch, float sel) {
+    HIP_OK(hipEventRecord(ev_fork_, st_));
+    HIP_OK(hipStreamWaitEvent(st2_, ev_fork_, 0));
+    enqueue_eval(st2_);                                   // previous epoch's evaluation
+    enqueue_epoch_end(phase, ignore_epoch, sel, st2_);    // ... and its bookkeeping
+    HIP_OK(hipEventRecord(ev_join_, st2_));
+    enqueue_train_grads(phase);                           // this epoch's forward/backward
+    HIP_OK(hipStreamWaitEvent(st_, ev_join_, 0));
+    copy_train_scal(st_);
+    launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);
+  }
+  void enqueue_tail(int phase, int ignore_epoch, float sel) {
+    enqueue_eval(st_);
+    enqueue_epoch_end(phase, ignore_epoch, sel, st_);
+  }
+  template <typename F>
+  hipGraphExec_t graph_for(const std::string& key, F&& enqueue) {
+    auto it = graphs_.find(key);
+    if (it != graphs_.end()) return it->second;
+    hipGraph_t graph;
+    HIP_OK(hipStreamBeginCapture(st_, hipStreamCaptureModeThreadLocal));
+    enqueue();
+    HIP_OK(hipStreamEndCapture(st_, &graph));
+    hipGraphExec_t exec;
+    HIP_OK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    HIP_OK(hipGraphDestroy(graph));
+    graphs_.emplace(key, exec);
+    return exec;
   }
   void fwd_only(int s, bool train_mode, bool do_mom) {
     const SplitDev& D = splits_[s];
@@ -736,6 +825,7 @@ PYBIND11_MODULE(_dlap_hip, m) {
       .def("epoch_count", &Engine::epoch_count)
       .def("history", &Engine::history)
       .def("run_epochs", &Engine::run_epochs, py::call_guard<py::gil_scoped_release>())
+      .def("set_pipeline", &Engine::set_pipeline)
       .def("forward_split", &Engine::forward_split)
       .def("train_step", &Engine::train_step)
       .def("backward_only", &Engine::backward_only)

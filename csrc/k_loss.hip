@@ -24,34 +24,34 @@ __global__ __launch_bounds__(256) void k_period_fwd(const LossJob* __restrict__ 
   if (t >= J.T) return;
   __shared__ float red[4];
   const int N = J.N;
-  const int r0 = J.row_ptr[t], r1 = J.row_ptr[t + 1];   // this period's compact rows
+  const int r0 = gp(J.row_ptr)[t], r1 = gp(J.row_ptr)[t + 1];   // this period's compact rows
   float sw = 0.f;
   if (J.normalize) {
-    for (int r = r0 + threadIdx.x; r < r1; r += 256) sw += J.w[r];
+    for (int r = r0 + threadIdx.x; r < r1; r += 256) sw += gp(J.w)[r];
     sw = block_sum<256>(sw, red);
   }
-  const float mu = J.normalize ? sw * J.invNt[t] : 0.f;
+  const float mu = J.normalize ? sw * gp(J.invNt)[t] : 0.f;
   float s_wr = 0.f, s_abs = 0.f, s_ww = 0.f;
-  float* wn = J.wn + (size_t)t * N;
+  float* wn = gp(J.wn) + (size_t)t * N;
   for (int r = r0 + threadIdx.x; r < r1; r += 256) {
-    const float v = J.w[r] - mu;
-    wn[J.rowti[r].y] = v;
-    s_wr += v * J.Rc[r];
+    const float v = gp(J.w)[r] - mu;
+    wn[gp(J.rowti)[r].y] = v;
+    s_wr += v * gp(J.Rc)[r];
     s_abs += fabsf(v);
     s_ww += v * v;
   }
-  if (threadIdx.x == 0) J.mu[t] = mu;
+  if (threadIdx.x == 0) gp(J.mu)[t] = mu;
   s_wr = block_sum<256>(s_wr, red);
   s_abs = block_sum<256>(s_abs, red);
-  if (J.rstat) s_ww = block_sum<256>(s_ww, red);
+  if (gp(J.rstat)) s_ww = block_sum<256>(s_ww, red);
   if (threadIdx.x == 0) {
-    const float p = J.weighted ? s_wr * J.invNt[t] * J.Nbar : s_wr;
-    J.P[t] = p;
-    J.sdfv[t] = 1.f + p;
-    if (J.port) J.port[t] = s_wr / fmaxf(s_abs, 1e-8f);
-    if (J.rstat) {
-      J.rstat[4 * t + 0] = s_ww;
-      J.rstat[4 * t + 1] = s_wr;
+    const float p = J.weighted ? s_wr * gp(J.invNt)[t] * J.Nbar : s_wr;
+    gp(J.P)[t] = p;
+    gp(J.sdfv)[t] = 1.f + p;
+    if (gp(J.port)) gp(J.port)[t] = s_wr / fmaxf(s_abs, 1e-8f);
+    if (gp(J.rstat)) {
+      gp(J.rstat)[4 * t + 0] = s_ww;
+      gp(J.rstat)[4 * t + 1] = s_wr;
     }
   }
 }
@@ -83,16 +83,16 @@ __global__ __launch_bounds__(256) void k_asset_part(const LossJob* __restrict__ 
 #pragma unroll 4
       for (int t = t0; t < t1; ++t) {
         const size_t d = (size_t)t * N + i;
-        const float q = J.Rm[d] * J.sdfv[t];
+        const float q = gp(J.Rm)[d] * gp(J.sdfv)[t];
         if (k0 == 0) eu += q;
         if (kn == 8 && (K & 3) == 0) {
-          const float* hp = J.h + d * K + k0;
+          const float* hp = gp(J.h) + d * K + k0;
           const f32x4 a = *reinterpret_cast<const f32x4*>(hp);
           const f32x4 b = *reinterpret_cast<const f32x4*>(hp + 4);
 #pragma unroll
           for (int k = 0; k < 4; ++k) { e[k] += a[k] * q; e[4 + k] += b[k] * q; }
         } else {
-          for (int k = 0; k < kn; ++k) e[k] += J.h[d * K + k0 + k] * q;
+          for (int k = 0; k < kn; ++k) e[k] += gp(J.h)[d * K + k0 + k] * q;
         }
       }
     }
@@ -102,10 +102,10 @@ __global__ __launch_bounds__(256) void k_asset_part(const LossJob* __restrict__ 
     red[wave][lane][8] = eu;
     __syncthreads();
     if (wave == 0 && ok) {
-      float* pe = J.pe + ((size_t)ch * N + i) * K;
+      float* pe = gp(J.pe) + ((size_t)ch * N + i) * K;
       for (int k = 0; k < kn; ++k)
         pe[k0 + k] = red[0][lane][k] + red[1][lane][k] + red[2][lane][k] + red[3][lane][k];
-      if (k0 == 0) J.pu[(size_t)ch * N + i] = red[0][lane][8] + red[1][lane][8] + red[2][lane][8] + red[3][lane][8];
+      if (k0 == 0) gp(J.pu)[(size_t)ch * N + i] = red[0][lane][8] + red[1][lane][8] + red[2][lane][8] + red[3][lane][8];
     }
   }
 }
@@ -121,20 +121,20 @@ __global__ __launch_bounds__(256) void k_asset_red(const LossJob* __restrict__ j
   const bool ok = i < N;
   float lc = 0.f, lu = 0.f;
   if (ok) {
-    const float invT = J.invT[i];
+    const float invT = gp(J.invT)[i];
     float u = 0.f;
-    for (int ch = 0; ch < DLAP_TCH; ++ch) u += J.pu[(size_t)ch * N + i];
+    for (int ch = 0; ch < DLAP_TCH; ++ch) u += gp(J.pu)[(size_t)ch * N + i];
     u *= invT;
-    J.Eu[i] = u;
-    if (J.dEu) J.dEu[i] = J.coef_u * u;
+    gp(J.Eu)[i] = u;
+    if (gp(J.dEu)) gp(J.dEu)[i] = J.coef_u * u;
     lu = u * u;
-    if (J.h) {
+    if (gp(J.h)) {
       for (int k = 0; k < K; ++k) {
         float v = 0.f;
-        for (int ch = 0; ch < DLAP_TCH; ++ch) v += J.pe[((size_t)ch * N + i) * K + k];
+        for (int ch = 0; ch < DLAP_TCH; ++ch) v += gp(J.pe)[((size_t)ch * N + i) * K + k];
         v *= invT;
-        J.E[(size_t)i * K + k] = v;
-        if (J.dE) J.dE[(size_t)i * K + k] = J.coef_c * v;
+        gp(J.E)[(size_t)i * K + k] = v;
+        if (gp(J.dE)) gp(J.dE)[(size_t)i * K + k] = J.coef_c * v;
         lc += v * v;
       }
     }
@@ -142,15 +142,15 @@ __global__ __launch_bounds__(256) void k_asset_red(const LossJob* __restrict__ j
   lc = block_sum<256>(lc, red);
   lu = block_sum<256>(lu, red);
   if (threadIdx.x == 0) {
-    J.part[2 * blockIdx.x + 0] = lc;
-    J.part[2 * blockIdx.x + 1] = lu;
+    gp(J.part)[2 * blockIdx.x + 0] = lc;
+    gp(J.part)[2 * blockIdx.x + 1] = lu;
   }
 }
 
 DLAP_DEV void final_losses(const LossJob& J, float& lc, float& lu) {
   const int nblk = (J.N + 255) >> 8;
   float a = 0.f, b = 0.f;
-  for (int k = 0; k < nblk; ++k) { a += J.part[2 * k]; b += J.part[2 * k + 1]; }
+  for (int k = 0; k < nblk; ++k) { a += gp(J.part)[2 * k]; b += gp(J.part)[2 * k + 1]; }
   lc = J.h ? a / ((float)J.K * (float)J.N) : 0.f;
   lu = b / (float)J.N;
 }
@@ -161,9 +161,9 @@ DLAP_DEV void final_losses(const LossJob& J, float& lc, float& lu) {
 DLAP_DEV void residual_stats(const LossJob& J, float& lres, float& inv_b, float& n1) {
   float a = 0.f, b = 0.f, c1 = 0.f, c2 = 0.f;
   for (int t = 0; t < J.T; ++t) {
-    const float n = J.Nt[t];
+    const float n = gp(J.Nt)[t];
     if (n < 2.f) continue;
-    const float ww = J.rstat[4 * t + 0], rw = J.rstat[4 * t + 1], rr = J.RR[t];
+    const float ww = gp(J.rstat)[4 * t + 0], rw = gp(J.rstat)[4 * t + 1], rr = gp(J.RR)[t];
     b += rr / n; c2 += 1.f;
     if (ww > 1e-8f) { a += (rr - rw * rw / ww) / n; c1 += 1.f; }
   }
@@ -182,50 +182,50 @@ __global__ __launch_bounds__(256) void k_period_bwd(const LossJob* __restrict__ 
   __shared__ float red[4];
   const int N = J.N, K = J.K;
   const size_t base = (size_t)t * N;
-  const int r0 = J.row_ptr[t], r1 = J.row_ptr[t + 1];
+  const int r0 = gp(J.row_ptr)[t], r1 = gp(J.row_ptr)[t + 1];
   float s = 0.f;
   for (int rr = r0 + threadIdx.x; rr < r1; rr += 256) {
-    const int i = J.rowti[rr].y;
-    const float r = J.Rc[rr];
+    const int i = gp(J.rowti)[rr].y;
+    const float r = gp(J.Rc)[rr];
     float g;
     if (J.phase == 1) {
-      g = J.dEu[i];
+      g = gp(J.dEu)[i];
     } else {
       g = 0.f;
-      const float* hp = J.h + (base + i) * K;
-      const float* de = J.dE + (size_t)i * K;
+      const float* hp = gp(J.h) + (base + i) * K;
+      const float* de = gp(J.dE) + (size_t)i * K;
       for (int k = 0; k < K; ++k) g += de[k] * hp[k];
     }
-    s += g * r * J.invT[i];
+    s += g * r * gp(J.invT)[i];
   }
   s = block_sum<256>(s, red);
-  const float c = J.weighted ? s * J.Nbar * J.invNt[t] : s;   // dL/dS_t with S_t = sum w' R m
+  const float c = J.weighted ? s * J.Nbar * gp(J.invNt)[t] : s;   // dL/dS_t with S_t = sum w' R m
   // optional residual-loss gradient wrt w' (valid stocks of period t)
   float rcoef = 0.f, beta = 0.f;
   if (J.res_factor > 0.f) {
     float lres, inv_b, n1;
     residual_stats(J, lres, inv_b, n1);
-    const float n = J.Nt[t], ww = J.rstat[4 * t + 0], rw = J.rstat[4 * t + 1];
+    const float n = gp(J.Nt)[t], ww = gp(J.rstat)[4 * t + 0], rw = gp(J.rstat)[4 * t + 1];
     if (n >= 2.f && ww > 1e-8f && n1 > 0.f) {
       beta = rw / ww;
       rcoef = J.res_factor * inv_b / n1 * (-2.f / n) * beta;   // d/dw'_i = rcoef * (R_i - beta w'_i)
     }
   }
   // mean over valid stocks of the residual gradient (for the normalisation Jacobian)
-  const float mu = J.mu[t];
+  const float mu = gp(J.mu)[t];
   float gres_mean = 0.f;
   if (rcoef != 0.f && J.normalize) {
     float sg = 0.f;
-    for (int rr = r0 + threadIdx.x; rr < r1; rr += 256) sg += J.Rc[rr] - beta * (J.w[rr] - mu);
+    for (int rr = r0 + threadIdx.x; rr < r1; rr += 256) sg += gp(J.Rc)[rr] - beta * (gp(J.w)[rr] - mu);
     sg = block_sum<256>(sg, red);
-    gres_mean = rcoef * sg * J.invNt[t];
+    gres_mean = rcoef * sg * gp(J.invNt)[t];
   }
-  const float mR = J.normalize ? J.meanR[t] : 0.f;
+  const float mR = J.normalize ? gp(J.meanR)[t] : 0.f;
   for (int rr = r0 + threadIdx.x; rr < r1; rr += 256) {
-    const float R = J.Rc[rr];
+    const float R = gp(J.Rc)[rr];
     float g = c * (R - mR);
-    if (rcoef != 0.f) g += rcoef * (R - beta * (J.w[rr] - mu)) - gres_mean;
-    J.dw[rr] = g;
+    if (rcoef != 0.f) g += rcoef * (R - beta * (gp(J.w)[rr] - mu)) - gres_mean;
+    gp(J.dw)[rr] = g;
   }
 }
 
@@ -241,13 +241,13 @@ __global__ __launch_bounds__(256) void k_job_metrics(const LossJob* __restrict__
     final_losses(J, lc, lu);
     float lres = 0.f, inv_b, n1;
     if (J.res_factor > 0.f) residual_stats(J, lres, inv_b, n1);
-    J.scal[SC_LCOND] = lc;
-    J.scal[SC_LUNC] = lu;
-    J.scal[SC_LRES] = lres;
+    gp(J.scal)[SC_LCOND] = lc;
+    gp(J.scal)[SC_LUNC] = lu;
+    gp(J.scal)[SC_LRES] = lres;
   }
   // Sharpe of the weighted training portfolio P (train monitor) and of the L1 portfolio.
   for (int pass = 0; pass < 2; ++pass) {
-    const float* src = pass == 0 ? J.P : J.port;
+    const float* src = pass == 0 ? gp(J.P) : gp(J.port);
     if (!src) continue;
     for (int t = threadIdx.x; t < T; t += 256) ret[t] = src[t];
     __syncthreads();
@@ -262,18 +262,18 @@ __global__ __launch_bounds__(256) void k_job_metrics(const LossJob* __restrict__
       const float sd_u = T > 1 ? sqrtf(v / (float)(T - 1)) : __builtin_nanf("");
       const float sharpe = (sd_u < 1e-8f) ? 0.f : mean / sd_u;
       if (pass == 0) {
-        J.scal[SC_TRAIN_SHARPE] = sharpe;
+        gp(J.scal)[SC_TRAIN_SHARPE] = sharpe;
       } else {
-        J.scal[SC_SHARPE] = sharpe;
-        J.scal[SC_MEAN] = mean;
-        J.scal[SC_STD] = sqrtf(v / (float)T);
+        gp(J.scal)[SC_SHARPE] = sharpe;
+        gp(J.scal)[SC_MEAN] = mean;
+        gp(J.scal)[SC_STD] = sqrtf(v / (float)T);
         float cum = 1.f, peak = 1.f, mdd = 0.f;
         for (int t = 0; t < T; ++t) {
           cum *= 1.f + ret[t];
           peak = t == 0 ? cum : fmaxf(peak, cum);
           mdd = fminf(mdd, (cum - peak) / peak);
         }
-        J.scal[SC_MDD] = mdd;
+        gp(J.scal)[SC_MDD] = mdd;
       }
     }
     __syncthreads();

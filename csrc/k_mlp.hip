@@ -77,11 +77,11 @@ DLAP_DEV void issue_tile(const MlpJob& J, int tile, TileIn<KS1>& in) {
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
     const int r = min(tile * 32 + 16 * b + (l & 15), J.R - 1);   // clamp: no divergent loads
-    in.ti[b] = J.rowti[r];
-    const bf16x8* row = J.X + (size_t)r * (4 * KS1);
+    in.ti[b] = gp(J.rowti)[r];
+    const auto row = gp(J.X) + (size_t)r * (4 * KS1);
 #pragma unroll
     for (int s = 0; s < KS1; ++s) in.x[b][s] = row[4 * s + q];
-    if (DW) in.dw[b] = J.dw[r];
+    if (DW) in.dw[b] = gp(J.dw)[r];
   }
 }
 
@@ -102,7 +102,7 @@ DLAP_DEV RowInfo finish_tile(const MlpJob& J, const MlpDims& D, int tile, TileIn
 #pragma unroll
     for (int s = 0; s < KS1; ++s) xf[b][s] = ok ? in.x[b][s] : zero8();
     if (D.Dm > 0) {
-      const float* pp = J.pp + ri.t[b] * D.Dm;
+      const auto pp = gp(J.pp) + ri.t[b] * D.Dm;
 #pragma unroll
       for (int s = 0; s < KS1; ++s) {
         if (s >= s_lo && s <= s_hi) {                          // wave-uniform
@@ -168,20 +168,20 @@ struct DropCtx {
 
 // bias + ReLU + dropout in place; gate bit (u*4+r) per row block. Branch-free: one hash
 // per unit pair gives both keep decisions (see dropout_pair).
-template <int UB>
-DLAP_DEV void relu_dropout(f32x4 (&a)[2][UB], const float* bias0, const float* bias1,
+template <int UB, typename BP>
+DLAP_DEV void relu_dropout(f32x4 (&a)[2][UB], BP bias0, BP bias1,
                            const DropCtx& dc, int layer_id, const RowInfo& ri, uint32_t (&gate)[2]) {
   const int q = lane_id() >> 4;
   const uint32_t key = dropout_key(dc.seed, dc.step, layer_id);
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
-    const float* bp = b ? bias1 : bias0;
+    const BP bp = b ? bias1 : bias0;
     const uint32_t row = (uint32_t)ri.dense[b];
     const uint32_t rowmix = row * 0xcc9e2d51u ^ (row >> 16);
     uint32_t g = 0;
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
-      const f32x4 bb = *reinterpret_cast<const f32x4*>(bp + 16 * u + 4 * q);
+      const f32x4 bb = ld4(bp + 16 * u + 4 * q);
       uint32_t keep = 0xFu;
       if (dc.on) {   // wave-uniform
         const uint32_t pair0 = (uint32_t)(8 * u + 2 * q);
@@ -202,6 +202,29 @@ DLAP_DEV void relu_dropout(f32x4 (&a)[2][UB], const float* bias0, const float* b
   }
 }
 
+// bias + ReLU + dropout from gate bits stored by the training forward (bit u*4+r per row
+// block): bitwise the same activations as relu_dropout, without re-hashing the mask.
+template <int UB, typename BP>
+DLAP_DEV void relu_gates(f32x4 (&a)[2][UB], BP bias0, BP bias1, float scale,
+                         const uint32_t (&gate)[2]) {
+  const int q = lane_id() >> 4;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const BP bp = b ? bias1 : bias0;
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const f32x4 bb = ld4(bp + 16 * u + 4 * q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float z = a[b][u][r] + bb[r];
+        a[b][u][r] = ((gate[b] >> (u * 4 + r)) & 1u) ? z * scale : 0.f;
+      }
+    }
+  }
+}
+
+DLAP_DEV uint32_t gate_word(const uint32_t (&g)[2]) { return g[0] | (g[1] << 16); }
+
 DLAP_DEV float reduce_q(float v) {  // sum over the 4 lane groups that share l & 15
   v += __shfl_xor(v, 16, 64);
   v += __shfl_xor(v, 32, 64);
@@ -214,13 +237,13 @@ DLAP_DEV DropCtx drop_ctx(const MlpJob& J, const MlpDims& D) {
   dc.thr16 = (uint32_t)(D.dropout * 65536.f + 0.5f);
   dc.scale = dc.on ? 1.f / (1.f - D.dropout) : 1.f;
   dc.seed = J.seed;
-  dc.step = J.step ? (uint32_t)*J.step : 0u;
+  dc.step = J.step ? (uint32_t)*gp(J.step) : 0u;
   return dc;
 }
 
 DLAP_DEV void stage_weights(const MlpJob& J, const MlpDims& D, bf16x8* lds, float* aux) {
-  for (int i = threadIdx.x; i < D.blob_frags * 64; i += blockDim.x) lds[i] = J.blob[i];
-  for (int i = threadIdx.x; i < D.aux_floats; i += blockDim.x) aux[i] = J.aux[i];
+  for (int i = threadIdx.x; i < D.blob_frags * 64; i += blockDim.x) lds[i] = gp(J.blob)[i];
+  for (int i = threadIdx.x; i < D.aux_floats; i += blockDim.x) aux[i] = gp(J.aux)[i];
   __syncthreads();
 }
 
@@ -228,16 +251,18 @@ DLAP_DEV void stage_weights(const MlpJob& J, const MlpDims& D, bf16x8* lds, floa
 template <int KS1>
 DLAP_DEV void sdf_forward_tile(const bf16x8* lds, const float* aux, const MlpDims& D,
                                const DropCtx& dc, const RowInfo& ri, const bf16x8 (&xf)[2][KS1],
-                               float (&w)[2]) {
+                               DLAP_GLOBAL uint32_t* gout, float (&w)[2]) {
   f32x4 a[2][4];
   bf16x8 pf[2][2];
   uint32_t gate[2];
   layer0<KS1, 4>(lds, D.s_fwd0, xf, a);
   relu_dropout<4>(a, aux + D.a_sb, aux + D.a_sb, dc, 0, ri, gate);
+  if (gout) gout[0] = gate_word(gate);
   for (int j = 1; j < D.nl_sdf; ++j) {
     pack_blocks<4>(a, pf);
     layer_chain<4, 2>(lds, D.s_fwd + (j - 1) * 8, pf, a);
     relu_dropout<4>(a, aux + D.a_sb + 64 * j, aux + D.a_sb + 64 * j, dc, j, ri, gate);
+    if (gout) gout[64 * j] = gate_word(gate);
   }
   const int q = lane_id() >> 4;
   const float* wo = aux + D.a_wo;
@@ -259,35 +284,39 @@ DLAP_DEV void sdf_forward_tile(const bf16x8* lds, const float* aux, const MlpDim
 template <int KS1, int WMB>
 DLAP_DEV void mom_forward_tile(const bf16x8* lds, const float* aux, const MlpDims& D,
                                const MlpJob& J, const DropCtx& dc, const RowInfo& ri,
-                               const bf16x8 (&xf)[2][KS1]) {
+                               const bf16x8 (&xf)[2][KS1], DLAP_GLOBAL uint32_t* gout) {
   constexpr int KSM = (WMB + 1) / 2;
   f32x4 a[2][WMB];
   bf16x8 pf[2][KSM];
   uint32_t gate[2];
   const int q = lane_id() >> 4;
   layer0<KS1, WMB>(lds, D.m_fwd0, xf, a);
-  const float* pb0 = J.abias + ri.t[0] * 64;
-  const float* pb1 = J.abias + ri.t[1] * 64;
+  // layer-0 bias is per period (global), later biases are staged (LDS)
+  const auto ab0 = gp(J.abias) + ri.t[0] * 64, ab1 = gp(J.abias) + ri.t[1] * 64;
   for (int j = 0; j + 1 < D.nl_mom; ++j) {
-    if (j > 0) pb0 = pb1 = aux + D.a_mb + 64 * j;
-    relu_dropout<WMB>(a, pb0, pb1, dc, 16 + j, ri, gate);
+    if (j == 0) relu_dropout<WMB>(a, ab0, ab1, dc, 16 + j, ri, gate);
+    else relu_dropout<WMB>(a, aux + D.a_mb + 64 * j, aux + D.a_mb + 64 * j, dc, 16 + j, ri, gate);
+    if (gout) gout[64 * j] = gate_word(gate);
     pack_blocks<WMB>(a, pf);
     layer_chain<WMB, KSM>(lds, D.m_fwd + j * WMB * KSM, pf, a);
   }
-  if (D.nl_mom > 1) pb0 = pb1 = aux + D.a_mb + 64 * (D.nl_mom - 1);
+  auto emit = [&](auto pb0, auto pb1) {
 #pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    if (ri.dense[b] < 0) continue;
-    const float* bp = b ? pb1 : pb0;
-    float* dst = J.h_out + (size_t)ri.dense[b] * D.K;
+    for (int b = 0; b < 2; ++b) {
+      if (ri.dense[b] < 0) continue;
+      const auto bp = b ? pb1 : pb0;
+      const auto dst = gp(J.h_out) + (size_t)ri.dense[b] * D.K;
 #pragma unroll
-    for (int u = 0; u < WMB; ++u)
+      for (int u = 0; u < WMB; ++u)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int k = 16 * u + 4 * q + r;
-        if (k < D.K) dst[k] = tanhf(a[b][u][r] + bp[k]);
-      }
-  }
+        for (int r = 0; r < 4; ++r) {
+          const int k = 16 * u + 4 * q + r;
+          if (k < D.K) dst[k] = tanhf(a[b][u][r] + bp[k]);
+        }
+    }
+  };
+  if (D.nl_mom > 1) emit(aux + D.a_mb + 64 * (D.nl_mom - 1), aux + D.a_mb + 64 * (D.nl_mom - 1));
+  else emit(ab0, ab1);
 }
 
 // ============================== forward ==================================================
@@ -312,14 +341,19 @@ __global__ __launch_bounds__(256, 2) void k_mlp_fwd(const MlpJob* __restrict__ j
     const RowInfo ri = finish_tile<KS1>(J, D, tile, cur, xf);
     if (J.do_sdf) {
       float w[2];
-      sdf_forward_tile<KS1>(lds, aux, D, dc, ri, xf, w);
+      DLAP_GLOBAL uint32_t* gout = J.gbits ? gp(J.gbits) + (size_t)tile * D.nl_sdf * 64 + lane : nullptr;
+      sdf_forward_tile<KS1>(lds, aux, D, dc, ri, xf, gout, w);
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         const int r = tile * 32 + 16 * b + (lane & 15);
-        if (q == 0 && r < J.R) J.w_out[r] = w[b];
+        if (q == 0 && r < J.R) gp(J.w_out)[r] = w[b];
       }
     }
-    if (J.do_mom) mom_forward_tile<KS1, WMB>(lds, aux, D, J, dc, ri, xf);
+    if (J.do_mom) {
+      DLAP_GLOBAL uint32_t* gout = (J.mgbits && D.nl_mom > 1)
+                           ? gp(J.mgbits) + (size_t)tile * (D.nl_mom - 1) * 64 + lane : nullptr;
+      mom_forward_tile<KS1, WMB>(lds, aux, D, J, dc, ri, xf, gout);
+    }
     cur = nxt;
   }
 }
@@ -348,7 +382,7 @@ DLAP_DEV float* wg_slab_begin(char* smem, int slab_stride) {
   return red;
 }
 DLAP_DEV void wg_slab_store(const MlpJob& J, const float* red, int slab_stride) {
-  float* slab = J.slab + (size_t)(J.slab_base + blockIdx.z * gridDim.x + blockIdx.x) * slab_stride;
+  const auto slab = gp(J.slab) + (size_t)(J.slab_base + blockIdx.z * gridDim.x + blockIdx.x) * slab_stride;
   for (int i = threadIdx.x; i < slab_stride; i += blockDim.x) slab[i] = red[i];
 }
 
@@ -391,12 +425,21 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
   const int stride = gridDim.x * nwaves;
   int tile = blockIdx.x * nwaves + wave;
   TileIn<KS1> cur, nxt;
-  if (tile < ntiles) issue_tile<KS1, true>(J, tile, cur);
+  uint32_t gw_cur[NL], gw_nxt[NL];   // gate words of the forward pass, prefetched with the tile
+  if (tile < ntiles) {
+    issue_tile<KS1, true>(J, tile, cur);
+#pragma unroll
+    for (int j = 0; j < NL; ++j) gw_cur[j] = gp(J.gbits)[((size_t)tile * NL + j) * 64 + lane];
+  }
   for (; tile < ntiles; tile += stride) {
-    if (tile + stride < ntiles) issue_tile<KS1, true>(J, tile + stride, nxt);
+    if (tile + stride < ntiles) {
+      issue_tile<KS1, true>(J, tile + stride, nxt);
+#pragma unroll
+      for (int j = 0; j < NL; ++j) gw_nxt[j] = gp(J.gbits)[((size_t)(tile + stride) * NL + j) * 64 + lane];
+    }
     bf16x8 xf[2][KS1];
     const RowInfo ri = finish_tile<KS1>(J, D, tile, cur, xf);
-    // ---- forward recompute, keep packed activations + gates ----
+    // ---- forward recompute from the stored gates, keep packed activations ----
     bf16x8 act[NL][2][2];
     uint32_t gates[NL][2];
     f32x4 a[2][4];
@@ -404,7 +447,9 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       if (j > 0) layer_chain<4, 2>(lds, D.s_fwd + (j - 1) * 8, act[j - 1], a);
-      relu_dropout<4>(a, aux + D.a_sb + 64 * j, aux + D.a_sb + 64 * j, dc, j, ri, gates[j]);
+      gates[j][0] = gw_cur[j] & 0xFFFFu;
+      gates[j][1] = gw_cur[j] >> 16;
+      relu_gates<4>(a, aux + D.a_sb + 64 * j, aux + D.a_sb + 64 * j, dc.scale, gates[j]);
       pack_blocks<4>(a, act[j]);
     }
     // ---- output layer: w = wo . a_last + bo ----
@@ -472,26 +517,32 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
               dz[b][u][r] = on ? da[b][u][r] * dc.scale : 0.f;
             }
       } else if (D.nrnn > 0 && slice == 0) {
-        // dL/d(per-period input d) per row = sum_out W0[out][F + d] * dz0[out][row]
-        const float* wpp = aux + D.a_pp;
-        for (int d = 0; d < D.Dm; ++d) {
+        // dL/d(per-period input d) per row = sum_out W0[out][F + d] * dz0[out][row]: one MFMA
+        // chain per 16 inputs with the packed W0[:, F:F+Dm]^T fragments
+        for (int ub = 0; ub < D.ubpp; ++ub) {
+          f32x4 c0 = zero4(), c1 = zero4();
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const bf16x8 w = ldsf(lds, D.s_upp + 2 * ub + s);
+            c0 = mfma16(w, dzf[0][s], c0);
+            c1 = mfma16(w, dzf[1][s], c1);
+          }
 #pragma unroll
           for (int b = 0; b < 2; ++b) {
-            float s = 0.f;
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              const f32x4 ww = *reinterpret_cast<const f32x4*>(wpp + d * 64 + 16 * u + 4 * q);
-#pragma unroll
-              for (int r = 0; r < 4; ++r) s += dz[b][u][r] * ww[r];
-            }
-            s = reduce_q(s);
             const int row = tile * 32 + 16 * b + (lane & 15);
-            if (q == 0 && row < J.R) J.u_out[(size_t)row * D.Dm + d] = s;
+            const f32x4 c = b ? c1 : c0;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int d = 16 * ub + 4 * q + r;
+              if (d < D.Dm && row < J.R) gp(J.u_out)[(size_t)row * D.Dm + d] = c[r];
+            }
           }
         }
       }
     }
     cur = nxt;
+#pragma unroll
+    for (int j = 0; j < NL; ++j) gw_cur[j] = gw_nxt[j];
   }
   // ---- workgroup slab: waves add their partials into LDS in a fixed order ----
   float* red = wg_slab_begin(smem, slab_stride);
@@ -565,10 +616,21 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
 
   const int stride = gridDim.x * nwaves;
   int tile = blockIdx.x * nwaves + wave;
+  constexpr int NH = NLM > 1 ? NLM - 1 : 1;   // hidden layers with stored gate words
   TileIn<KS1> cur, nxt;
-  if (tile < ntiles) issue_tile<KS1, false>(J, tile, cur);
+  uint32_t gw_cur[NH], gw_nxt[NH];
+  if (tile < ntiles) {
+    issue_tile<KS1, false>(J, tile, cur);
+#pragma unroll
+    for (int j = 0; j + 1 < NLM; ++j) gw_cur[j] = gp(J.mgbits)[((size_t)tile * (NLM - 1) + j) * 64 + lane];
+  }
   for (; tile < ntiles; tile += stride) {
-    if (tile + stride < ntiles) issue_tile<KS1, false>(J, tile + stride, nxt);
+    if (tile + stride < ntiles) {
+      issue_tile<KS1, false>(J, tile + stride, nxt);
+#pragma unroll
+      for (int j = 0; j + 1 < NLM; ++j)
+        gw_nxt[j] = gp(J.mgbits)[((size_t)(tile + stride) * (NLM - 1) + j) * 64 + lane];
+    }
     bf16x8 xf[2][KS1];
     const RowInfo ri = finish_tile<KS1>(J, D, tile, cur, xf);
     bf16x8 act[NLM][2][KSM];
@@ -578,30 +640,35 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
 #pragma unroll
     for (int j = 0; j < NLM; ++j) {
       if (j > 0) layer_chain<WMB, KSM>(lds, D.m_fwd + (j - 1) * WMB * KSM, act[j - 1], a);
-      const float* b0 = j ? aux + D.a_mb + 64 * j : J.abias + ri.t[0] * 64;
-      const float* b1 = j ? aux + D.a_mb + 64 * j : J.abias + ri.t[1] * 64;
-      if (j + 1 < NLM) {
-        relu_dropout<WMB>(a, b0, b1, dc, 16 + j, ri, gates[j]);
-        pack_blocks<WMB>(a, act[j]);
-      } else {
-        // h = tanh(z); dz = dh (1 - h^2), dh = dE[i][k] R SDF_t / T_i
+      auto body = [&](auto b0, auto b1) {
+        if (j + 1 < NLM) {
+          gates[j][0] = gw_cur[j < NH ? j : 0] & 0xFFFFu;
+          gates[j][1] = gw_cur[j < NH ? j : 0] >> 16;
+          relu_gates<WMB>(a, b0, b1, dc.scale, gates[j]);
+          pack_blocks<WMB>(a, act[j]);
+        } else {
+          // h = tanh(z); dz = dh (1 - h^2), dh = dE[i][k] R SDF_t / T_i
 #pragma unroll
-        for (int b = 0; b < 2; ++b) {
-          const float* bp = b ? b1 : b0;
-          const int d = ri.dense[b];
-          const float cst = d >= 0 ? J.Rm[d] * J.sdfv[ri.t[b]] * J.invT[ri.i[b]] : 0.f;
-          const float* de = J.dE + (size_t)ri.i[b] * D.K;
+          for (int b = 0; b < 2; ++b) {
+            const auto bp = b ? b1 : b0;
+            const int d = ri.dense[b];
+            const float cst = d >= 0 ? gp(J.Rm)[d] * gp(J.sdfv)[ri.t[b]] * gp(J.invT)[ri.i[b]] : 0.f;
+            const auto de = gp(J.dE) + (size_t)ri.i[b] * D.K;
 #pragma unroll
-          for (int u = 0; u < WMB; ++u)
+            for (int u = 0; u < WMB; ++u)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int k = 16 * u + 4 * q + r;
-              const float h = tanhf(a[b][u][r] + bp[k]);
-              const float g = (d >= 0 && k < D.K) ? de[k] * cst : 0.f;
-              a[b][u][r] = g * (1.f - h * h);
-            }
+              for (int r = 0; r < 4; ++r) {
+                const int k = 16 * u + 4 * q + r;
+                const float h = tanhf(a[b][u][r] + bp[k]);
+                const float g = (d >= 0 && k < D.K) ? de[k] * cst : 0.f;
+                a[b][u][r] = g * (1.f - h * h);
+              }
+          }
         }
-      }
+      };
+      // layer-0 bias is per period (global), later biases are staged (LDS)
+      if (j == 0) body(gp(J.abias) + ri.t[0] * 64, gp(J.abias) + ri.t[1] * 64);
+      else body(aux + D.a_mb + 64 * j, aux + D.a_mb + 64 * j);
     }
     f32x4 dz[2][WMB];
 #pragma unroll
@@ -661,12 +728,14 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
           if (row < J.R) {
 #pragma unroll
             for (int u = 0; u < WMB; ++u)
-              *reinterpret_cast<f32x4*>(J.v_out + (size_t)row * 64 + 16 * u + 4 * q) = dz[b][u];
+              *reinterpret_cast<f32x4*>(gp(J.v_out) + (size_t)row * 64 + 16 * u + 4 * q) = dz[b][u];
           }
         }
       }
     }
     cur = nxt;
+#pragma unroll
+    for (int j = 0; j < NH; ++j) gw_cur[j] = gw_nxt[j];
   }
   float* red = wg_slab_begin(smem, slab_stride);
   for (int w = 0; w < nwaves; ++w) {

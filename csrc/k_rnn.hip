@@ -19,6 +19,7 @@
 //               with v_readlane), then every thread reduces the weight gradients over t
 //               from LDS-staged dgates (thread per macro column: 4H FMAs per load).
 //               Phase 2 instead builds the moment layer-0 macro-column / bias gradients.
+#include <cstdlib>
 #include "common.h"
 #include "layout.h"
 #include "rnn.h"
@@ -50,15 +51,16 @@ __global__ __launch_bounds__(256) void k_proj(const RnnJob* __restrict__ jobs,
   const int nt = min(4, T - t0);
   for (int i = threadIdx.x; i < 4 * M; i += 256) {
     const int tl = i / M;
-    x[i] = tl < nt ? J.macro[(size_t)(t0 + tl) * M + (i - tl * M)] : 0.f;
+    x[i] = tl < nt ? gp(J.macro)[(size_t)(t0 + tl) * M + (i - tl * M)] : 0.f;
   }
-  const float* Wih = J.params + md->lstm_w_ih[0];
+  const auto params = gp(J.params);
+  const auto Wih = params + md->lstm_w_ih[0];
   const PackLayer& L0 = md->m[0];
   for (int i = threadIdx.x; i < nout * M; i += 256) {
     const int o = i / M, m = i - o * M;
     float v = 0.f;
     if (o < G4) v = Wih[(size_t)o * M + m];
-    else if (o - G4 < cm1) v = J.params[L0.w_off + (size_t)(o - G4) * L0.ld + m];
+    else if (o - G4 < cm1) v = params[L0.w_off + (size_t)(o - G4) * L0.ld + m];
     w[i] = v;
   }
   __syncthreads();
@@ -72,19 +74,37 @@ __global__ __launch_bounds__(256) void k_proj(const RnnJob* __restrict__ jobs,
     s0 += wv * x[m]; s1 += wv * x[M + m]; s2 += wv * x[2 * M + m]; s3 += wv * x[3 * M + m];
   }
   float b = 0.f;
-  if (o < G4) b = J.params[md->lstm_b_ih[0] + o] + J.params[md->lstm_b_hh[0] + o];
-  else if (o - G4 < cm1) b = J.params[L0.b_off + o - G4];
+  if (o < G4) b = params[md->lstm_b_ih[0] + o] + params[md->lstm_b_hh[0] + o];
+  else if (o - G4 < cm1) b = params[L0.b_off + o - G4];
   else b = 0.f;
   const float s[4] = {s0, s1, s2, s3};
   for (int tl = 0; tl < nt; ++tl) {
     const int t = t0 + tl;
-    if (o < G4) J.xg[(size_t)t * G4 + o] = s[tl] + b;
-    else J.abias[t * 64 + (o - G4)] = (o - G4 < cm1) ? s[tl] + b : 0.f;
+    if (o < G4) gp(J.xg)[(size_t)t * G4 + o] = s[tl] + b;
+    else gp(J.abias)[t * 64 + (o - G4)] = (o - G4 < cm1) ? s[tl] + b : 0.f;
   }
 }
 
 // ------------------------------------------------------------------------ k_lstm -------
+// STAGE: layer-0 input projections staged in LDS (T*4H <= 12288). The layer-0 and deeper
+// layer loops are separate and fully unrolled over HM (>= H; padded units have zero weights,
+// so they stay at h = c = 0 and contribute nothing): the time loop has no branches, no
+// memory loads outside LDS, and only fire-and-forget global stores, so nothing on the serial
+// chain waits on HBM.
 template <int HM>
+DLAP_DEV float bcast_dot(const float (&w)[HM], float v) {
+  // sum_j w[j] * v(lane j) as a balanced tree (dependency depth log2 HM + 1)
+  float p[HM];
+#pragma unroll
+  for (int j = 0; j < HM; ++j) p[j] = w[j] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+#pragma unroll
+  for (int w2 = 1; w2 < HM; w2 *= 2)
+#pragma unroll
+    for (int j = 0; j + w2 < HM; j += 2 * w2) p[j] += p[j + w2];
+  return p[0];
+}
+
+template <int HM, bool STAGE>
 __global__ __launch_bounds__(64) void k_lstm(const RnnJob* __restrict__ jobs,
                                              const ModelDesc* __restrict__ md) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
@@ -93,88 +113,208 @@ __global__ __launch_bounds__(64) void k_lstm(const RnnJob* __restrict__ jobs,
   if (nrnn == 0) return;
   const int T = J.T, H = md->H, G4 = 4 * H;
   const int lane = threadIdx.x;
-  const int k = lane < H ? lane : 0;
   const bool act = lane < H;
+  const int k = act ? lane : 0;
   const bool drop = J.train && md->dropout > 0.f;
   const uint32_t thr = (uint32_t)(md->dropout * 16777216.f + 0.5f);
   const float scale = drop ? 1.f / (1.f - md->dropout) : 1.f;
-  const uint32_t step = J.step ? (uint32_t)*J.step : 0u;
-  const bool stage = T * G4 <= 12288;          // 48 KiB of LDS
+  const uint32_t step = J.step ? (uint32_t)*gp(J.step) : 0u;
+  const auto params = gp(J.params);
+  const auto xg = gp(J.xg);
+  const bool save = J.sc != nullptr;
   for (int l = 0; l < nrnn; ++l) {
-    const float* Whh = J.params + md->lstm_w_hh[l];
+    const auto Whh = params + md->lstm_w_hh[l];
     float whh[4][HM], wih[4][HM], bias[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
 #pragma unroll
       for (int j = 0; j < HM; ++j) {
-        whh[q][j] = j < H ? Whh[(q * H + k) * H + j] : 0.f;
-        wih[q][j] = (l > 0 && j < H) ? J.params[md->lstm_w_ih[l] + (q * H + k) * H + j] : 0.f;
+        const bool ok = act && j < H;
+        const int jj = j < H ? j : 0;
+        const float a = Whh[(q * H + k) * H + jj];
+        const float b = l > 0 ? params[md->lstm_w_ih[l] + (q * H + k) * H + jj] : 0.f;
+        whh[q][j] = ok ? a : 0.f;
+        wih[q][j] = ok ? b : 0.f;
       }
-      bias[q] = l > 0 ? J.params[md->lstm_b_ih[l] + q * H + k] + J.params[md->lstm_b_hh[l] + q * H + k] : 0.f;
+      const float bb = l > 0 ? params[md->lstm_b_ih[l] + q * H + k] + params[md->lstm_b_hh[l] + q * H + k] : 0.f;
+      bias[q] = act ? bb : 0.f;
     }
-    if (l == 0 && stage) {
-      for (int i = lane; i < T * G4; i += 64) sm[i] = J.xg[i];
+    if (STAGE && l == 0) {
+      for (int i = lane; i < T * G4; i += 64) sm[i] = xg[i];
       __syncthreads();
     }
-    float* hout = J.sh ? J.sh + (size_t)l * T * H : J.out;
-    const float* xin = J.xin;                      // layer l-1 output after dropout
-    const uint32_t key_in = l > 0 ? dropout_key(J.seed, step, 32 + (l - 1)) : 0u;
+    const auto hout = save ? gp(J.sh) + (size_t)l * T * H : gp(J.out);
+    const auto sc = gp(J.sc) + (size_t)l * T * H;
+    const auto sg = gp(J.sg) + (size_t)l * T * G4;
     float h = 0.f, c = 0.f;
-    float nx[4];
-    if (l == 0) {
-      const float* xr = stage ? sm : J.xg;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) nx[q] = xr[q * H + k];
-    }
-    for (int t = 0; t < T; ++t) {
-      float p[4];
-      if (l == 0) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) p[q] = nx[q];
-        const int tn = t + 1 < T ? t + 1 : t;           // prefetch the next step's inputs
-        const float* xr = stage ? sm + tn * G4 : J.xg + (size_t)tn * G4;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) nx[q] = xr[q * H + k];
-      } else {
-        float xv = act ? xin[(size_t)t * H + k] : 0.f;
-        if (drop) xv = dropout_keep(key_in, (uint32_t)t, (uint32_t)k, thr) ? xv * scale : 0.f;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) p[q] = bias[q];
-#pragma unroll
-        for (int j = 0; j < HM; ++j) {
-          if (j < H) {
-            const float xj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), j));
-#pragma unroll
-            for (int q = 0; q < 4; ++q) p[q] += wih[q][j] * xj;
-          }
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < HM; ++j) {
-        if (j < H) {
-          const float hj = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(h), j));
-#pragma unroll
-          for (int q = 0; q < 4; ++q) p[q] += whh[q][j] * hj;
-        }
-      }
+    auto cell = [&](int t, const float (&p)[4]) {
       const float gi = sigm(p[0]), gf = sigm(p[1]), gg = ftanh(p[2]), go = sigm(p[3]);
       c = gf * c + gi * gg;
       h = go * ftanh(c);
       if (act) {
         hout[(size_t)t * H + k] = h;
-        if (J.sc) {
-          J.sc[((size_t)l * T + t) * H + k] = c;
-          float* sg = J.sg + ((size_t)l * T + t) * G4;
-          sg[k] = gi; sg[H + k] = gf; sg[2 * H + k] = gg; sg[3 * H + k] = go;
+        if (save) {
+          sc[(size_t)t * H + k] = c;
+          const auto g = sg + (size_t)t * G4;
+          g[k] = gi; g[H + k] = gf; g[2 * H + k] = gg; g[3 * H + k] = go;
         }
+      }
+    };
+    if (l == 0) {
+      auto ldx = [&](int t, float (&v)[4]) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float x = STAGE ? sm[t * G4 + q * H + k] : xg[(size_t)t * G4 + q * H + k];
+          v[q] = act ? x : 0.f;
+        }
+      };
+      float nx[4];
+      ldx(0, nx);
+      for (int t = 0; t < T; ++t) {
+        float p[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) p[q] = nx[q];
+        ldx(t + 1 < T ? t + 1 : t, nx);                // prefetch the next step's inputs
+#pragma unroll
+        for (int q = 0; q < 4; ++q) p[q] += bcast_dot<HM>(whh[q], h);
+        cell(t, p);
+      }
+    } else {
+      const auto xin = gp(J.xin);                   // layer l-1 output (dropout on read)
+      const uint32_t key_in = dropout_key(J.seed, step, 32 + (l - 1));
+      float nxv = act ? xin[k] : 0.f;
+      for (int t = 0; t < T; ++t) {
+        float xv = nxv;
+        nxv = act ? xin[(size_t)(t + 1 < T ? t + 1 : t) * H + k] : 0.f;
+        if (drop) xv = dropout_keep(key_in, (uint32_t)t, (uint32_t)k, thr) ? xv * scale : 0.f;
+        float p[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) p[q] = bias[q] + bcast_dot<HM>(wih[q], xv) + bcast_dot<HM>(whh[q], h);
+        cell(t, p);
       }
     }
     __threadfence_block();
     if (l + 1 < nrnn) {
-      for (int i = lane; i < T * H; i += 64) J.xin[i] = hout[i];   // dropout applied on read
+      const auto xin = gp(J.xin);
+      for (int i = lane; i < T * H; i += 64) xin[i] = hout[i];
       __threadfence_block();
-    } else if (J.sh) {
-      for (int i = lane; i < T * H; i += 64) J.out[i] = hout[i];
+    } else if (save) {
+      const auto out = gp(J.out);
+      for (int i = lane; i < T * H; i += 64) out[i] = hout[i];
+    }
+  }
+}
+
+// ----------------------------------------------------------------------- k_lstm_gl -----
+// Gate-per-lane recurrence for 4H <= 64: lane L owns gate row L (q = L / H, unit L % H), so a
+// step is HM broadcast FMAs + ONE activation per lane (sigmoid, or tanh = 2 sigm(2x) - 1 on
+// the g rows) instead of four per unit lane; the f/g/o values are then gathered onto the unit
+// lanes (DPP row rotates when 4H <= 16, ds_bpermute otherwise). ~3x fewer instructions on
+// the serial chain than the unit-per-lane form. EXACT = HM is H itself (DPP offsets need it).
+template <int HM, bool DPPG>
+DLAP_DEV float gl_gather(float y, int off_units, int q) {
+  if constexpr (DPPG) {
+    // lane l receives lane (l - n) mod 16 for row_ror:n  ->  n = 16 - q*H reads lane l + q*H
+    if (q == 1) return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(y), 0x120 + (16 - HM), 0xF, 0xF, false));
+    if (q == 2) return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(y), 0x120 + (16 - 2 * HM), 0xF, 0xF, false));
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(y), 0x120 + (16 - 3 * HM), 0xF, 0xF, false));
+  } else {
+    return __shfl(y, (int)(threadIdx.x & 63) + off_units, 64);
+  }
+}
+
+template <int HM, bool DPPG, bool STAGE>
+__global__ __launch_bounds__(64) void k_lstm_gl(const RnnJob* __restrict__ jobs,
+                                                const ModelDesc* __restrict__ md) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const RnnJob& J = jobs[blockIdx.x];
+  const int nrnn = md->nrnn;
+  if (nrnn == 0) return;
+  const int T = J.T, H = DPPG ? HM : md->H, G4 = 4 * H;
+  const int L = threadIdx.x;
+  const bool gl = L < G4;                 // lane owns gate row L
+  const bool ul = L < H;                  // lane owns unit L (cell state, output)
+  const int row = gl ? L : 0;
+  const bool is_g = gl && L >= 2 * H && L < 3 * H;
+  const float ka = is_g ? 2.f : 1.f;      // act(x) = kb * sigm(ka x) + kc
+  const float kb = is_g ? 2.f : 1.f, kc = is_g ? -1.f : 0.f;
+  const bool drop = J.train && md->dropout > 0.f;
+  const uint32_t thr = (uint32_t)(md->dropout * 16777216.f + 0.5f);
+  const float scale = drop ? 1.f / (1.f - md->dropout) : 1.f;
+  const uint32_t step = J.step ? (uint32_t)*gp(J.step) : 0u;
+  const auto params = gp(J.params);
+  const auto xg = gp(J.xg);
+  const bool save = J.sc != nullptr;
+  for (int l = 0; l < nrnn; ++l) {
+    float whh[HM], wih[HM];
+#pragma unroll
+    for (int j = 0; j < HM; ++j) {
+      const bool ok = gl && j < H;
+      const int jj = j < H ? j : 0;
+      const float a = params[md->lstm_w_hh[l] + row * H + jj];
+      const float b = l > 0 ? params[md->lstm_w_ih[l] + row * H + jj] : 0.f;
+      whh[j] = ok ? a : 0.f;
+      wih[j] = ok ? b : 0.f;
+    }
+    const float bb = l > 0 ? params[md->lstm_b_ih[l] + row] + params[md->lstm_b_hh[l] + row] : 0.f;
+    const float bias = gl ? bb : 0.f;
+    if (STAGE && l == 0) {
+      for (int i = L; i < T * G4; i += 64) sm[i] = xg[i];
+      __syncthreads();
+    }
+    const auto hout = save ? gp(J.sh) + (size_t)l * T * H : gp(J.out);
+    const auto sc = gp(J.sc) + (size_t)l * T * H;
+    const auto sg = gp(J.sg) + (size_t)l * T * G4;
+    float h = 0.f, c = 0.f;
+    auto cell = [&](int t, float pre) {
+      pre += bcast_dot<HM>(whh, h);
+      float y = kb * sigm(ka * pre) + kc;
+      if (is_g && fabsf(pre) < 0.0125f) y = pre * (1.f - pre * pre * (1.f / 3.f));
+      const float gf = gl_gather<HM, DPPG>(y, H, 1);
+      const float gg = gl_gather<HM, DPPG>(y, 2 * H, 2);
+      const float go = gl_gather<HM, DPPG>(y, 3 * H, 3);
+      c = gf * c + y * gg;                 // y = i on the unit lanes
+      const float hn = go * ftanh(c);
+      h = ul ? hn : 0.f;
+      if (save && gl) sg[(size_t)t * G4 + L] = y;
+      if (ul) {
+        hout[(size_t)t * H + L] = h;
+        if (save) sc[(size_t)t * H + L] = c;
+      }
+    };
+    if (l == 0) {
+      float nx = gl ? (STAGE ? sm[L] : xg[L]) : 0.f;
+      for (int t = 0; t < T; ++t) {
+        const float pre = nx;
+        const int tn = t + 1 < T ? t + 1 : t;            // prefetch the next step's input
+        const float v = STAGE ? sm[tn * G4 + row] : xg[(size_t)tn * G4 + row];
+        nx = gl ? v : 0.f;
+        cell(t, pre);
+      }
+    } else {
+      const auto xin = gp(J.xin);                        // layer l-1 output (dropout on read)
+      const uint32_t key_in = dropout_key(J.seed, step, 32 + (l - 1));
+      float nxv = ul ? xin[L] : 0.f;
+      for (int t = 0; t < T; ++t) {
+        float xv = nxv;
+        const float v = xin[(size_t)(t + 1 < T ? t + 1 : t) * H + (ul ? L : 0)];
+        nxv = ul ? v : 0.f;
+        if (drop) xv = dropout_keep(key_in, (uint32_t)t, (uint32_t)(ul ? L : 0), thr) ? xv * scale : 0.f;
+        float pre = bias;
+#pragma unroll
+        for (int j = 0; j < HM; ++j)
+          pre += wih[j] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), j));
+        cell(t, pre);
+      }
+    }
+    __threadfence_block();
+    if (l + 1 < nrnn) {
+      const auto xin = gp(J.xin);
+      for (int i = L; i < T * H; i += 64) xin[i] = hout[i];
+      __threadfence_block();
+    } else if (save) {
+      const auto out = gp(J.out);
+      for (int i = L; i < T * H; i += 64) out[i] = hout[i];
     }
   }
 }
@@ -189,11 +329,23 @@ void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* m
     HIP_OK(hipGetLastError());
   }
   if (mh.nrnn > 0) {
-    const size_t sh = 12288 * sizeof(float);
-    if (mh.H <= 4) hipLaunchKernelGGL((k_lstm<4>), dim3(njobs), dim3(64), sh, st, jobs, md);
-    else if (mh.H <= 8) hipLaunchKernelGGL((k_lstm<8>), dim3(njobs), dim3(64), sh, st, jobs, md);
-    else if (mh.H <= 16) hipLaunchKernelGGL((k_lstm<16>), dim3(njobs), dim3(64), sh, st, jobs, md);
-    else hipLaunchKernelGGL((k_lstm<32>), dim3(njobs), dim3(64), sh, st, jobs, md);
+    const bool stage = tmax * 4 * mh.H <= 12288;     // 48 KiB of LDS
+    const size_t sh = stage ? (size_t)tmax * 4 * mh.H * sizeof(float) : 0;
+#define L_CASE(HM) \
+    if (stage) hipLaunchKernelGGL((k_lstm<HM, true>), dim3(njobs), dim3(64), sh, st, jobs, md); \
+    else hipLaunchKernelGGL((k_lstm<HM, false>), dim3(njobs), dim3(64), sh, st, jobs, md);
+#define G_CASE(HM, DP) \
+    if (stage) hipLaunchKernelGGL((k_lstm_gl<HM, DP, true>), dim3(njobs), dim3(64), sh, st, jobs, md); \
+    else hipLaunchKernelGGL((k_lstm_gl<HM, DP, false>), dim3(njobs), dim3(64), sh, st, jobs, md);
+    const char* ul_env = std::getenv("DLAP_LSTM_UNIT_LANES");
+    if (ul_env && std::atoi(ul_env) == 1) {       // unit-per-lane form (reference for tests)
+      if (mh.H <= 4) { L_CASE(4) } else if (mh.H <= 8) { L_CASE(8) } else if (mh.H <= 16) { L_CASE(16) } else { L_CASE(32) }
+    } else if (mh.H == 1) { G_CASE(1, true) } else if (mh.H == 2) { G_CASE(2, true) }
+    else if (mh.H == 3) { G_CASE(3, true) } else if (mh.H == 4) { G_CASE(4, true) }
+    else if (mh.H <= 8) { G_CASE(8, false) } else if (mh.H <= 16) { G_CASE(16, false) }
+    else { L_CASE(32) }
+#undef L_CASE
+#undef G_CASE
     HIP_OK(hipGetLastError());
   }
 }
@@ -215,38 +367,54 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
   const bool drop = md->dropout > 0.f;
   const uint32_t thr = (uint32_t)(md->dropout * 16777216.f + 0.5f);
   const float scale = drop ? 1.f / (1.f - md->dropout) : 1.f;
-  const uint32_t step = (uint32_t)*J.drop_step;
+  const uint32_t step = (uint32_t)*gp(J.drop_step);
+  const auto params = gp(J.params);
+  const auto grads = gp(J.grads);
   float* s_g = sm;                    // [T][4H] saved gates
   float* s_c = s_g + T * G4;          // [T][H]  cells
   float* s_h = s_c + T * H;           // [T][H]  layer outputs
   float* s_d = s_h + T * H;           // [T][H]  incoming gradient
   float* dgs = s_d + T * H;           // [T][4H] gate pre-activation gradients
   for (int l = md->nrnn - 1; l >= 0; --l) {
-    const float* dout = l == md->nrnn - 1 ? J.dpp : J.dx;
+    const auto dout = l == md->nrnn - 1 ? gp(J.dpp) : gp(J.dx);
+    const auto sg = gp(J.sg) + (size_t)l * T * G4;
+    const auto scg = gp(J.sc) + (size_t)l * T * H;
+    const auto shg = gp(J.sh) + (size_t)l * T * H;
     __syncthreads();
-    for (int i = threadIdx.x; i < T * G4; i += 256) s_g[i] = J.sg[(size_t)l * T * G4 + i];
+    for (int i = threadIdx.x; i < T * G4; i += 256) s_g[i] = sg[i];
     for (int i = threadIdx.x; i < T * H; i += 256) {
-      s_c[i] = J.sc[(size_t)l * T * H + i];
-      s_h[i] = J.sh[(size_t)l * T * H + i];
+      s_c[i] = scg[i];
+      s_h[i] = shg[i];
       s_d[i] = dout[i];
     }
     __syncthreads();
     if (wave == 0) {
       const int k = lane < H ? lane : 0;
       const bool act = lane < H;
-      const float* Whh = J.params + md->lstm_w_hh[l];
-      float wt[4][HM];            // wt[q][j] = W_hh[q*H + j][k]
+      const auto Whh = params + md->lstm_w_hh[l];
+      float wt[4][HM];            // wt[q][j] = W_hh[q*H + j][k] (0 for padded j)
 #pragma unroll
       for (int q = 0; q < 4; ++q)
 #pragma unroll
-        for (int j = 0; j < HM; ++j) wt[q][j] = j < H ? Whh[(q * H + j) * H + k] : 0.f;
+        for (int j = 0; j < HM; ++j) {
+          const float w = Whh[(q * H + (j < H ? j : 0)) * H + k];
+          wt[q][j] = j < H ? w : 0.f;
+        }
       float dh_next = 0.f, dc_next = 0.f;
-      for (int t = T - 1; t >= 0; --t) {
+      // step inputs of t (prefetched one step ahead: LDS latency off the serial chain)
+      auto fetch = [&](int t, float (&v)[7]) {
         const float* g = s_g + t * G4;
-        const float gi = g[k], gf = g[H + k], gg = g[2 * H + k], go = g[3 * H + k];
-        const float c = s_c[t * H + k];
-        const float cp = t > 0 ? s_c[(t - 1) * H + k] : 0.f;
-        const float dh = (act ? s_d[t * H + k] : 0.f) + dh_next;
+        v[0] = g[k]; v[1] = g[H + k]; v[2] = g[2 * H + k]; v[3] = g[3 * H + k];
+        v[4] = s_c[t * H + k];
+        v[5] = t > 0 ? s_c[(t - 1) * H + k] : 0.f;
+        v[6] = act ? s_d[t * H + k] : 0.f;
+      };
+      float cur[7], nxt[7];
+      fetch(T - 1, cur);
+      for (int t = T - 1; t >= 0; --t) {
+        fetch(t > 0 ? t - 1 : 0, nxt);
+        const float gi = cur[0], gf = cur[1], gg = cur[2], go = cur[3], c = cur[4], cp = cur[5];
+        const float dh = cur[6] + dh_next;
         const float tc = ftanh(c);
         const float dc = dh * go * (1.f - tc * tc) + dc_next;
         float d[4];
@@ -259,36 +427,33 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
 #pragma unroll
           for (int q = 0; q < 4; ++q) dgs[t * G4 + q * H + k] = d[q];
         }
-        float s = 0.f;
-#pragma unroll
-        for (int j = 0; j < HM; ++j) {
-          if (j < H) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-              s += wt[q][j] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(d[q]), j));
-          }
-        }
+        const float s = (bcast_dot<HM>(wt[0], d[0]) + bcast_dot<HM>(wt[1], d[1])) +
+                        (bcast_dot<HM>(wt[2], d[2]) + bcast_dot<HM>(wt[3], d[3]));
         dh_next = act ? s : 0.f;
+#pragma unroll
+        for (int e = 0; e < 7; ++e) cur[e] = nxt[e];
       }
     }
     __syncthreads();
-    if (l == 0)
-      for (int i = threadIdx.x; i < T * G4; i += 256) J.dg[i] = dgs[i];   // for k_wgrad
+    if (l == 0) {
+      const auto dg = gp(J.dg);
+      for (int i = threadIdx.x; i < T * G4; i += 256) dg[i] = dgs[i];   // for k_wgrad
+    }
     // W_hh [4H][H] and the biases: thread per (gate, column)
     const int in_dim = l == 0 ? M : H;
     const uint32_t key_below = l > 0 ? dropout_key(J.seed, step, 32 + (l - 1)) : 0u;
-    const float* hb = l > 0 ? J.sh + (size_t)(l - 1) * T * H : nullptr;
+    const auto hb = gp(J.sh) + (size_t)(l > 0 ? l - 1 : 0) * T * H;
     const int ncol = H + 1 + (l > 0 ? H : 0);
     for (int idx = threadIdx.x; idx < G4 * ncol; idx += 256) {
       const int g = idx % G4, col = idx / G4;
       float acc = 0.f;
       if (col < H) {
         for (int t = 1; t < T; ++t) acc += dgs[t * G4 + g] * s_h[(t - 1) * H + col];
-        J.grads[md->lstm_w_hh[l] + g * H + col] = acc;
+        grads[md->lstm_w_hh[l] + g * H + col] = acc;
       } else if (col == H) {
         for (int t = 0; t < T; ++t) acc += dgs[t * G4 + g];
-        J.grads[md->lstm_b_ih[l] + g] = acc;
-        J.grads[md->lstm_b_hh[l] + g] = acc;
+        grads[md->lstm_b_ih[l] + g] = acc;
+        grads[md->lstm_b_hh[l] + g] = acc;
       } else {
         const int m = col - H - 1;     // W_ih of layer l > 0 (input = dropout(h_{l-1}))
         for (int t = 0; t < T; ++t) {
@@ -296,17 +461,18 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
           if (drop) x = dropout_keep(key_below, (uint32_t)t, (uint32_t)m, thr) ? x * scale : 0.f;
           acc += dgs[t * G4 + g] * x;
         }
-        J.grads[md->lstm_w_ih[l] + g * in_dim + m] = acc;
+        grads[md->lstm_w_ih[l] + g * in_dim + m] = acc;
       }
     }
     if (l > 0) {
-      const float* Wih = J.params + md->lstm_w_ih[l];
+      const auto Wih = params + md->lstm_w_ih[l];
+      const auto dx = gp(J.dx);
       for (int idx = threadIdx.x; idx < T * H; idx += 256) {
         const int t = idx / H, m = idx - t * H;
         float s = 0.f;
         for (int g = 0; g < G4; ++g) s += Wih[g * H + m] * dgs[t * G4 + g];
         if (drop) s = dropout_keep(key_below, (uint32_t)t, (uint32_t)m, thr) ? s * scale : 0.f;
-        J.dx[idx] = s;
+        dx[idx] = s;
       }
       __threadfence_block();
     }
@@ -327,7 +493,7 @@ __global__ __launch_bounds__(256) void k_wgrad(const UpdJob* __restrict__ jobs,
   const bool mom = phase == 2;
   const int G = mom ? md->m[0].out : 4 * md->H;
   const int ldG = mom ? 64 : G;
-  const float* dG = mom ? J.dab : J.dg;
+  const auto dG = gp(mom ? J.dab : J.dg);
   const int cl = threadIdx.x & 15, tg = threadIdx.x >> 4;
   const int col = blockIdx.x * 16 + cl;
   float acc[GM];
@@ -336,8 +502,8 @@ __global__ __launch_bounds__(256) void k_wgrad(const UpdJob* __restrict__ jobs,
   if (col <= M) {
 #pragma unroll 2
     for (int t = tg; t < T; t += 16) {
-      const float x = col < M ? J.macro[(size_t)t * M + col] : 1.f;
-      const float* dr = dG + (size_t)t * ldG;
+      const float x = col < M ? gp(J.macro)[(size_t)t * M + col] : 1.f;
+      const auto dr = dG + (size_t)t * ldG;
 #pragma unroll
       for (int g = 0; g < GM; ++g) acc[g] += dr[g] * x;
     }
@@ -354,10 +520,10 @@ __global__ __launch_bounds__(256) void k_wgrad(const UpdJob* __restrict__ jobs,
     for (int q = 0; q < 16; ++q) s += red[q][c][g];
     if (mom) {
       const PackLayer& L0 = md->m[0];
-      if (cc < M) J.grads[L0.w_off + (size_t)g * L0.ld + cc] = s;
-      else J.grads[L0.b_off + g] = s;
+      if (cc < M) gp(J.grads)[L0.w_off + (size_t)g * L0.ld + cc] = s;
+      else gp(J.grads)[L0.b_off + g] = s;
     } else if (cc < M) {
-      J.grads[md->lstm_w_ih[0] + (size_t)g * M + cc] = s;
+      gp(J.grads)[md->lstm_w_ih[0] + (size_t)g * M + cc] = s;
     }
   }
 }

@@ -31,13 +31,13 @@ __global__ __launch_bounds__(256) void k_finalize(const FinJob* __restrict__ job
     const int o = e >> 6, i = (e & 63) + 64 * G.chunk;
     if (o >= G.out || i >= G.in) return;
     // position of this tile inside its slice's slab
-    const int tps = 1;
+    const int tps = mom ? md->tps_m : md->tps_s;
     const int tpos = ti - G.slice * tps;
-    const float* src = J.slab + (size_t)G.slice * J.nslab * slab_stride + tpos * 4096 + e;
+    const float* src = gp(J.slab) + (size_t)G.slice * J.nslab * slab_stride + tpos * 4096 + e;
     float s = 0.f;
 #pragma unroll 16
     for (int k = 0; k < J.nslab; ++k) s += src[(size_t)k * slab_stride];
-    J.grads[G.w_off + o * G.ld + G.col0 + i] = s;
+    gp(J.grads)[G.w_off + o * G.ld + G.col0 + i] = s;
     return;
   }
   b -= nb_tiles;
@@ -46,11 +46,11 @@ __global__ __launch_bounds__(256) void k_finalize(const FinJob* __restrict__ job
     if (e >= SLAB_EXTRA) return;
     const int dst = mom ? md->extra_m[e] : md->extra_s[e];
     if (dst < 0) return;
-    const float* src = J.slab + 1 * 4096 + e;   // slice-0 slabs (tps = 1)
+    const float* src = gp(J.slab) + (mom ? md->tps_m : md->tps_s) * 4096 + e;   // slice-0 slabs
     float s = 0.f;
 #pragma unroll 16
     for (int k = 0; k < J.nslab; ++k) s += src[(size_t)k * slab_stride];
-    J.grads[dst] = s;
+    gp(J.grads)[dst] = s;
     return;
   }
   b -= nb_extra;
@@ -62,8 +62,8 @@ __global__ __launch_bounds__(256) void k_finalize(const FinJob* __restrict__ job
   int Dp = 1;
   while (Dp < D) Dp <<= 1;
   const int nrg = 256 / Dp, d = threadIdx.x % Dp, rg = threadIdx.x / Dp;
-  const float* src = mom ? J.v : J.u;
-  const int r0 = J.row_ptr[t], r1 = J.row_ptr[t + 1];
+  const float* src = mom ? gp(J.v) : gp(J.u);
+  const int r0 = gp(J.row_ptr)[t], r1 = gp(J.row_ptr)[t + 1];
   float s = 0.f;
   if (d < D)
     for (int r = r0 + rg; r < r1; r += nrg) s += src[(size_t)r * D + d];
@@ -72,8 +72,8 @@ __global__ __launch_bounds__(256) void k_finalize(const FinJob* __restrict__ job
   if (rg == 0 && d < D) {
     float tot = 0.f;
     for (int g = 0; g < nrg; ++g) tot += red[g * Dp + d];
-    if (mom) J.dab[t * 64 + d] = tot;
-    else J.dpp[t * D + d] = tot;
+    if (mom) gp(J.dab)[t * 64 + d] = tot;
+    else gp(J.dpp)[t * D + d] = tot;
   }
 }
 
@@ -90,128 +90,175 @@ void launch_finalize(const FinJob* jobs, int njobs, const ModelDesc* md, const M
 // ============================================================ packing ===================
 DLAP_DEV int perm_u(int q, int j) { return j < 4 ? 4 * q + j : 16 + 4 * q + (j - 4); }
 
-// Pack blob + aux of one model (all threads of the block participate).
-DLAP_DEV void pack_model(const ModelDesc* __restrict__ md, const float* __restrict__ P,
-                         bf16x8* blob, float* aux) {
+// Pack one blob element / aux float of a model from its flat parameter vector.
+template <typename PP>
+DLAP_DEV float pack_blob_elem(const ModelDesc* __restrict__ md, PP P, int e) {
   const MlpDims& D = md->md;
   const int KS1 = md->KS1, WMB = md->WMB, KSM = (WMB + 1) / 2;
-  __bf16* out = reinterpret_cast<__bf16*>(blob);
-  const int nel = D.blob_frags * 512;
-  for (int e = threadIdx.x; e < nel; e += blockDim.x) {
-    const int frag = e >> 9, lane = (e >> 3) & 63, j = e & 7;
-    const int q = lane >> 4, n = lane & 15;
-    float val = 0.f;
-    if (frag < D.s_fwd) {                         // SDF layer 0, natural k
-      const int u = frag / KS1, s = frag - u * KS1;
-      const PackLayer& L = md->s[0];
-      const int o = 16 * u + n, k = 32 * s + 8 * q + j;
-      if (o < L.out && k < L.in) val = P[L.w_off + o * L.ld + k];
-    } else if (frag < D.s_bwd) {                  // SDF chain forward
-      const int loc = frag - D.s_fwd, jl = loc / 8 + 1, r = loc % 8, u = r >> 1, s = r & 1;
-      const PackLayer& L = md->s[jl];
-      const int o = 16 * u + n, i = 32 * s + perm_u(q, j);
-      if (o < L.out && i < L.in) val = P[L.w_off + o * L.ld + i];
-    } else if (frag < D.m_fwd0) {                 // SDF chain backward (W^T)
-      const int loc = frag - D.s_bwd, jl = loc / 8 + 1, r = loc % 8, u = r >> 1, s = r & 1;
-      const PackLayer& L = md->s[jl];
-      const int i = 16 * u + n, o = 32 * s + perm_u(q, j);
-      if (o < L.out && i < L.in) val = P[L.w_off + o * L.ld + i];
-    } else if (frag < D.m_fwd) {                  // moment layer 0 (x columns only)
-      const int loc = frag - D.m_fwd0, u = loc / KS1, s = loc - u * KS1;
-      const PackLayer& L = md->m[0];
-      const int o = 16 * u + n, k = 32 * s + 8 * q + j;
-      if (o < L.out && k < L.in) val = P[L.w_off + o * L.ld + L.col0 + k];
-    } else if (frag < D.m_bwd) {                  // moment chain forward
-      const int per = WMB * KSM;
-      const int loc = frag - D.m_fwd, jl = loc / per + 1, r = loc % per, u = r / KSM, s = r % KSM;
-      const PackLayer& L = md->m[jl];
-      const int o = 16 * u + n, i = 32 * s + perm_u(q, j);
-      if (o < L.out && i < L.in) val = P[L.w_off + o * L.ld + i];
-    } else {                                      // moment chain backward
-      const int per = WMB * KSM;
-      const int loc = frag - D.m_bwd, jl = loc / per + 1, r = loc % per, u = r / KSM, s = r % KSM;
-      const PackLayer& L = md->m[jl];
-      const int i = 16 * u + n, o = 32 * s + perm_u(q, j);
-      if (o < L.out && i < L.in) val = P[L.w_off + o * L.ld + i];
-    }
-    out[e] = (__bf16)val;
+  const int frag = e >> 9, lane = (e >> 3) & 63, j = e & 7;
+  const int q = lane >> 4, n = lane & 15;
+  float val = 0.f;
+  if (frag < D.s_fwd) {                         // SDF layer 0, natural k
+    const int u = frag / KS1, s = frag - u * KS1;
+    const PackLayer& L = md->s[0];
+    const int o = 16 * u + n, k = 32 * s + 8 * q + j;
+    if (o < L.out && k < L.in) val = P[L.w_off + o * L.ld + k];
+  } else if (frag < D.s_bwd) {                  // SDF chain forward
+    const int loc = frag - D.s_fwd, jl = loc / 8 + 1, r = loc % 8, u = r >> 1, s = r & 1;
+    const PackLayer& L = md->s[jl];
+    const int o = 16 * u + n, i = 32 * s + perm_u(q, j);
+    if (o < L.out && i < L.in) val = P[L.w_off + o * L.ld + i];
+  } else if (frag < D.m_fwd0) {                 // SDF chain backward (W^T)
+    const int loc = frag - D.s_bwd, jl = loc / 8 + 1, r = loc % 8, u = r >> 1, s = r & 1;
+    const PackLayer& L = md->s[jl];
+    const int i = 16 * u + n, o = 32 * s + perm_u(q, j);
+    if (o < L.out && i < L.in) val = P[L.w_off + o * L.ld + i];
+  } else if (frag < D.m_fwd) {                  // moment layer 0 (x columns only)
+    const int loc = frag - D.m_fwd0, u = loc / KS1, s = loc - u * KS1;
+    const PackLayer& L = md->m[0];
+    const int o = 16 * u + n, k = 32 * s + 8 * q + j;
+    if (o < L.out && k < L.in) val = P[L.w_off + o * L.ld + L.col0 + k];
+  } else if (frag < D.m_bwd) {                  // moment chain forward
+    const int per = WMB * KSM;
+    const int loc = frag - D.m_fwd, jl = loc / per + 1, r = loc % per, u = r / KSM, s = r % KSM;
+    const PackLayer& L = md->m[jl];
+    const int o = 16 * u + n, i = 32 * s + perm_u(q, j);
+    if (o < L.out && i < L.in) val = P[L.w_off + o * L.ld + i];
+  } else if (frag < D.s_upp) {                  // moment chain backward
+    const int per = WMB * KSM;
+    const int loc = frag - D.m_bwd, jl = loc / per + 1, r = loc % per, u = r / KSM, s = r % KSM;
+    const PackLayer& L = md->m[jl];
+    const int i = 16 * u + n, o = 32 * s + perm_u(q, j);
+    if (o < L.out && i < L.in) val = P[L.w_off + o * L.ld + i];
+  } else {                                      // SDF layer 0, per-period columns (W^T)
+    const int loc = frag - D.s_upp, u = loc >> 1, s = loc & 1;
+    const PackLayer& L = md->s[0];
+    const int d = 16 * u + n, o = 32 * s + perm_u(q, j);
+    if (o < L.out && d < md->Dm) val = P[L.w_off + o * L.ld + md->F + d];
   }
-  for (int e = threadIdx.x; e < D.aux_floats; e += blockDim.x) {
-    float val = 0.f;
-    if (e < D.a_wo) {
-      const int jl = e >> 6, o = e & 63;
-      if (jl < md->nl_s && o < md->s[jl].out) val = P[md->s[jl].b_off + o];
-    } else if (e < D.a_bo) {
-      const int o = e - D.a_wo;
-      if (o < md->s[md->nl_s - 1].out) val = P[md->so_w + o];
-    } else if (e < D.a_pp) {
-      if (e == D.a_bo) val = P[md->so_b];
-    } else if (e < D.a_mb) {
-      const int d = (e - D.a_pp) >> 6, o = (e - D.a_pp) & 63;
-      const PackLayer& L = md->s[0];
-      if (o < L.out && d < md->Dm) val = P[L.w_off + o * L.ld + md->F + d];
-    } else {
-      const int jl = (e - D.a_mb) >> 6, o = (e - D.a_mb) & 63;
-      if (jl >= 1 && jl < md->nl_m && o < md->m[jl].out) val = P[md->m[jl].b_off + o];
+  return val;
+}
+
+template <typename PP>
+DLAP_DEV float pack_aux_elem(const ModelDesc* __restrict__ md, PP P, int e) {
+  const MlpDims& D = md->md;
+  float val = 0.f;
+  if (e < D.a_wo) {
+    const int jl = e >> 6, o = e & 63;
+    if (jl < md->nl_s && o < md->s[jl].out) val = P[md->s[jl].b_off + o];
+  } else if (e < D.a_bo) {
+    const int o = e - D.a_wo;
+    if (o < md->s[md->nl_s - 1].out) val = P[md->so_w + o];
+  } else if (e < D.a_pp) {
+    if (e == D.a_bo) val = P[md->so_b];
+  } else if (e < D.a_mb) {
+    const int d = (e - D.a_pp) >> 6, o = (e - D.a_pp) & 63;
+    const PackLayer& L = md->s[0];
+    if (o < L.out && d < md->Dm) val = P[L.w_off + o * L.ld + md->F + d];
+  } else {
+    const int jl = (e - D.a_mb) >> 6, o = (e - D.a_mb) & 63;
+    if (jl >= 1 && jl < md->nl_m && o < md->m[jl].out) val = P[md->m[jl].b_off + o];
+  }
+  return val;
+}
+
+// Re-pack the bf16 MFMA weight fragments + fp32 aux of every model after an update.
+// grid (blocks, models); each block stages the parameter vector in LDS once (the packing
+// gathers are scattered) and writes a contiguous range of packed elements.
+// Block 0 also advances the step counters (after every Adam block has read them).
+#define PACK_EPB 4096
+#define PACK_LDS_FLOATS 16384
+__global__ __launch_bounds__(256) void k_pack(const UpdJob* __restrict__ jobs,
+                                              const ModelDesc* __restrict__ md, int bump) {
+  const UpdJob& J = jobs[blockIdx.y];
+  extern __shared__ float sp[];
+  const int P = md->P;
+  const bool stage = P <= PACK_LDS_FLOATS;   // wave-uniform
+  if (stage) {
+    for (int i = threadIdx.x; i < P; i += 256) sp[i] = gp(J.params)[i];
+    __syncthreads();
+  }
+  const int nel = md->md.blob_frags * 512, total = nel + md->md.aux_floats;
+  const int e0 = blockIdx.x * PACK_EPB, e1 = min(e0 + PACK_EPB, total);
+  const auto out = (DLAP_GLOBAL __bf16*)(J.blob);
+  auto run = [&](auto src) {   // LDS or global source: one code path per address space
+    for (int e = e0 + threadIdx.x; e < e1; e += 256) {
+      if (e < nel) out[e] = (__bf16)pack_blob_elem(md, src, e);
+      else gp(J.aux)[e - nel] = pack_aux_elem(md, src, e - nel);
     }
-    aux[e] = val;
+  };
+  if (stage) run(static_cast<const float*>(sp));
+  else run(gp(static_cast<const float*>(J.params)));
+  if (bump && blockIdx.x == 0 && threadIdx.x == 0) {
+    gp(J.adam_step)[bump - 1] = gp(J.adam_step)[bump - 1] + 1;
+    gp(J.drop_step)[0] = gp(J.drop_step)[0] + 1;
   }
 }
 
-__global__ __launch_bounds__(256) void k_pack(const UpdJob* __restrict__ jobs, const ModelDesc* __restrict__ md) {
-  const UpdJob& J = jobs[blockIdx.x];
-  pack_model(md, J.params, J.blob, J.aux);
+static size_t pack_lds(const ModelDesc& mh) { return mh.P <= PACK_LDS_FLOATS ? (size_t)mh.P * 4 : 0; }
+static int pack_blocks_of(const ModelDesc& mh) {
+  return (mh.md.blob_frags * 512 + mh.md.aux_floats + PACK_EPB - 1) / PACK_EPB;
 }
 
-void launch_pack(float* const*, const UpdJob* jobs, int njobs, const ModelDesc* md, hipStream_t st) {
-  hipLaunchKernelGGL(k_pack, dim3(njobs), dim3(256), 0, st, jobs, md);
+void launch_pack(float* const*, const UpdJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
+                 hipStream_t st) {
+  hipLaunchKernelGGL(k_pack, dim3(pack_blocks_of(mh), njobs), dim3(256), pack_lds(mh), st, jobs,
+                     md, 0);
   HIP_OK(hipGetLastError());
 }
 
 // ============================================================ update ====================
-__global__ __launch_bounds__(256) void k_update(const UpdJob* __restrict__ jobs,
-                                                const ModelDesc* __restrict__ md, int phase, float lr,
-                                                int apply) {
-  const UpdJob& J = jobs[blockIdx.x];
+// Clip-by-global-norm + Adam over the phase's scope. grid (blocks, models): every block
+// reduces the full scope norm itself (fixed order -> identical in all blocks, no grid
+// barrier) and updates its own ADAM_PB-parameter range.
+#define ADAM_PB 1024
+__global__ __launch_bounds__(256) void k_adam(const UpdJob* __restrict__ jobs,
+                                              const ModelDesc* __restrict__ md, int phase, float lr) {
+  const UpdJob& J = jobs[blockIdx.y];
   __shared__ float red[4];
   const bool mom = phase == 2;
-  (void)apply;
   const int p0 = mom ? md->P_sdf : 0, p1 = mom ? md->P : md->P_sdf;
+  const float* __restrict__ grads = gp(J.grads);
   float ss = 0.f;
-  for (int i = p0 + threadIdx.x; i < p1; i += 256) { const float g = J.grads[i]; ss += g * g; }
+#pragma unroll 4
+  for (int i = p0 + threadIdx.x; i < p1; i += 256) { const float g = grads[i]; ss += g * g; }
   ss = block_sum<256>(ss, red);
   const float norm = sqrtf(ss);
   const float coef = fminf(1.f / (norm + 1e-6f), 1.f);
-  const int step = J.adam_step[mom ? 1 : 0] + 1;
+  const int step = gp(J.adam_step)[mom ? 1 : 0] + 1;
   const double bc1 = 1.0 - pow(0.9, (double)step);
   const double bc2 = 1.0 - pow(0.999, (double)step);
   const float step_size = (float)(lr / bc1);
   const float bc2s = (float)sqrt(bc2);
-  for (int i = p0 + threadIdx.x; i < p1; i += 256) {
-    const float g = J.grads[i] * coef;
-    float m = J.m[i];
-    m = m + 0.1f * (g - m);
-    float v = 0.999f * J.v[i] + 0.001f * g * g;
-    J.m[i] = m;
-    J.v[i] = v;
-    const float denom = sqrtf(v) / bc2s + 1e-8f;
-    J.params[i] = J.params[i] - step_size * (m / denom);
+  const int i = p0 + blockIdx.x * ADAM_PB;
+  float* __restrict__ pm = gp(J.m);
+  float* __restrict__ pv = gp(J.v);
+  float* __restrict__ pp = gp(J.params);
+#pragma unroll
+  for (int k = 0; k < ADAM_PB / 256; ++k) {
+    const int e = i + k * 256 + threadIdx.x;
+    if (e < p1) {
+      const float g = grads[e] * coef;
+      float m = pm[e];
+      m = m + 0.1f * (g - m);
+      const float v = 0.999f * pv[e] + 0.001f * g * g;
+      pm[e] = m;
+      pv[e] = v;
+      const float denom = sqrtf(v) / bc2s + 1e-8f;
+      pp[e] = pp[e] - step_size * (m / denom);
+    }
   }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    J.adam_step[mom ? 1 : 0] = step;
-    J.gnorm[0] = norm;
-  }
-  __threadfence_block();
-  __syncthreads();
-  pack_model(md, J.params, J.blob, J.aux);
-  __syncthreads();
-  if (threadIdx.x == 0) J.drop_step[0] = J.drop_step[0] + 1;
+  if (blockIdx.x == 0 && threadIdx.x == 0) gp(J.gnorm)[0] = norm;
 }
 
-void launch_update(const UpdJob* jobs, int njobs, const ModelDesc* md, int phase, float lr,
-                   hipStream_t st, int apply) {
-  hipLaunchKernelGGL(k_update, dim3(njobs), dim3(256), 0, st, jobs, md, phase, lr, apply);
+void launch_update(const UpdJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh, int phase,
+                   float lr, hipStream_t st) {
+  const int n = phase == 2 ? mh.P - mh.P_sdf : mh.P_sdf;
+  hipLaunchKernelGGL(k_adam, dim3((n + ADAM_PB - 1) / ADAM_PB, njobs), dim3(256), 0, st, jobs, md, phase,
+                     lr);
+  HIP_OK(hipGetLastError());
+  hipLaunchKernelGGL(k_pack, dim3(pack_blocks_of(mh), njobs), dim3(256), pack_lds(mh), st, jobs, md,
+                     phase == 2 ? 2 : 1);
   HIP_OK(hipGetLastError());
 }
 
@@ -221,9 +268,9 @@ __global__ __launch_bounds__(256) void k_epoch_end(const EpochJob* __restrict__ 
   const EpochJob& J = jobs[blockIdx.x];
   __shared__ int dec[2];
   if (threadIdx.x == 0) {
-    const int ep = J.ep[0], ep_ph = J.ep[1];
-    float* row = J.hist + (size_t)ep * HIST_W;
-    const float* tr = J.sc_train;
+    const int ep = gp(J.ep)[0], ep_ph = gp(J.ep)[1];
+    float* row = gp(J.hist) + (size_t)ep * HIST_W;
+    const float* tr = gp(J.sc_train);
     const float lres = tr[SC_LRES] * res_factor;
     float tloss;
     if (phase == 1) tloss = tr[SC_LUNC] + lres;
@@ -236,10 +283,10 @@ __global__ __launch_bounds__(256) void k_epoch_end(const EpochJob* __restrict__ 
     row[H_TRAIN_LUNC] = phase == 2 ? 0.f : tr[SC_LUNC];
     row[H_TRAIN_LCOND] = phase == 1 ? 0.f : tr[SC_LCOND];
     row[H_TRAIN_LRES] = tr[SC_LRES];
-    row[H_GNORM] = J.gnorm[0];
+    row[H_GNORM] = gp(J.gnorm)[0];
     int up_loss = 0, up_sr = 0;
     if (phase != 2) {
-      const float* va = J.sc_valid;
+      const float* va = gp(J.sc_valid);
       const float vloss = phase == 1 ? va[SC_LUNC] : va[SC_LCOND];
       row[H_VALID_LOSS] = vloss;
       row[H_VALID_SHARPE] = va[SC_SHARPE];
@@ -248,8 +295,8 @@ __global__ __launch_bounds__(256) void k_epoch_end(const EpochJob* __restrict__ 
       row[H_VALID_MDD] = va[SC_MDD];
       row[H_VALID_MEAN] = va[SC_MEAN];
       row[H_VALID_STD] = va[SC_STD];
-      if (J.sc_test) {
-        const float* te = J.sc_test;
+      if (gp(J.sc_test)) {
+        const float* te = gp(J.sc_test);
         row[H_TEST_LOSS] = phase == 1 ? te[SC_LUNC] : te[SC_LCOND];
         row[H_TEST_SHARPE] = te[SC_SHARPE];
         row[H_TEST_LUNC] = te[SC_LUNC];
@@ -259,28 +306,28 @@ __global__ __launch_bounds__(256) void k_epoch_end(const EpochJob* __restrict__ 
         row[H_TEST_STD] = te[SC_STD];
       }
       if (ep_ph > ignore_epoch) {
-        if (vloss < J.best[0]) { J.best[0] = vloss; up_loss = 1; }
+        if (vloss < gp(J.best)[0]) { gp(J.best)[0] = vloss; up_loss = 1; }
         const float s = sel * va[SC_SHARPE];
-        if (s > J.best[1]) { J.best[1] = s; up_sr = 1; }
+        if (s > gp(J.best)[1]) { gp(J.best)[1] = s; up_sr = 1; }
       }
     } else {
       const float lc = tr[SC_LCOND];
-      if (lc > J.best[2]) { J.best[2] = lc; up_loss = 1; }
+      if (lc > gp(J.best)[2]) { gp(J.best)[2] = lc; up_loss = 1; }
     }
     row[H_BEST_LOSS] = (float)up_loss;
     row[H_BEST_SR] = (float)up_sr;
-    if (up_loss) J.snap_flags[0] = 1;
-    if (up_sr) J.snap_flags[1] = 1;
-    J.ep[0] = ep + 1;
-    J.ep[1] = ep_ph + 1;
+    if (up_loss) gp(J.snap_flags)[0] = 1;
+    if (up_sr) gp(J.snap_flags)[1] = 1;
+    gp(J.ep)[0] = ep + 1;
+    gp(J.ep)[1] = ep_ph + 1;
     dec[0] = up_loss;
     dec[1] = up_sr;
   }
   __syncthreads();
   if (dec[0])
-    for (int i = threadIdx.x; i < P; i += 256) J.snap_loss[i] = J.params[i];
+    for (int i = threadIdx.x; i < P; i += 256) gp(J.snap_loss)[i] = gp(J.params)[i];
   if (dec[1])
-    for (int i = threadIdx.x; i < P; i += 256) J.snap_sharpe[i] = J.params[i];
+    for (int i = threadIdx.x; i < P; i += 256) gp(J.snap_sharpe)[i] = gp(J.params)[i];
 }
 
 void launch_epoch_end(const EpochJob* jobs, int njobs, int phase, int ignore_epoch, float sel,

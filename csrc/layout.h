@@ -50,6 +50,7 @@ struct ModelDesc {
   MlpDims md;
   // gradient reduction tables (phase-specific tower)
   int ntile_s, ntile_m, nslice_s, nslice_m;
+  int tps_s, tps_m;        // gradient tiles accumulated per backward slice
   GradTile tile_s[DLAP_MAX_TILES], tile_m[DLAP_MAX_TILES];
   int extra_s[SLAB_EXTRA], extra_m[SLAB_EXTRA];   // slab extra slot -> flat index (-1 unused)
 };

@@ -4,14 +4,14 @@
 
 struct MlpJob {
   const bf16x8* X;        // [R][KP/8] bf16 panel rows (cols [F, F+Dm) reserved, zero)
-  const int* row_dense;   // [R] dense index t*N + i
+  const int2* rowti;      // [R] (t, i) of each compact row
   const float* pp;        // [T][Dm] per-period SDF inputs (LSTM output or raw macro)
   const float* abias;     // [T][64] moment layer-0 per-period bias (W_macro . m_t + b)
   const bf16x8* blob;     // packed weight fragments of this job's model
   const float* aux;       // fp32 biases / output row of this job's model
-  float* w_out;           // fwd: dense [T*N] raw SDF weights (valid rows written)
+  float* w_out;           // fwd: compact [R] raw SDF weights
   float* h_out;           // fwd: dense [T*N][K] moments (valid rows written)
-  const float* dw;        // bwd sdf: dense [T*N] dL/dw_raw
+  const float* dw;        // bwd sdf: compact [R] dL/dw_raw
   const float* dE;        // bwd mom: [N][K] dL/dE
   const float* Rm;        // dense [T*N] returns (zero-filled)
   const float* sdfv;      // [T] SDF_t = 1 + P_t
@@ -19,6 +19,9 @@ struct MlpJob {
   float* slab;            // bwd: per-wave gradient partials
   float* u_out;           // bwd sdf: [R][Dm] dL/d(per-period inputs) per row
   float* v_out;           // bwd mom: [R][64] dL/d(moment layer-0 pre-activation) per row
+  uint32_t* gbits;        // train fwd writes / bwd reads the SDF ReLU*keep gate bits:
+                          //   [tile][layer][lane] = gate(b=0) | gate(b=1) << 16
+  uint32_t* mgbits;       // same for the moment tower's hidden layers (phase 2)
   const int* step;        // device step counter (dropout stream)
   int R, N;
   unsigned seed;
@@ -35,6 +38,7 @@ struct MlpDims {
   float dropout;
   int s_fwd0, s_fwd, s_bwd;      // blob frag offsets: SDF layer 0, chain fwd base, chain bwd base
   int m_fwd0, m_fwd, m_bwd;      // moment tower
+  int s_upp, ubpp;               // W0[:, F:F+Dm]^T fragments (ubpp blocks of 16 inputs, 2 k-steps)
   int a_sb, a_wo, a_bo, a_pp, a_mb;   // aux offsets: SDF biases [nl][64], out row [64], out
                                       // bias, W0 per-period cols [Dm][64], moment biases [nl][64]
   int blob_frags, aux_floats;

@@ -62,11 +62,11 @@ struct EpochJob {          // one model
 
 void launch_finalize(const FinJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
                      int phase, int slab_stride, int tmax, hipStream_t st);
-void launch_update(const UpdJob* jobs, int njobs, const ModelDesc* md, int phase, float lr,
-                   hipStream_t st, int apply = 1);
+void launch_update(const UpdJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh, int phase,
+                   float lr, hipStream_t st);
 void launch_lstm_bwd(const UpdJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
                      int T, int phase, hipStream_t st);
 void launch_pack(float* const* params_unused, const UpdJob* jobs, int njobs, const ModelDesc* md,
-                 hipStream_t st);
+                 const ModelDesc& mh, hipStream_t st);
 void launch_epoch_end(const EpochJob* jobs, int njobs, int phase, int ignore_epoch, float sel,
                       float res_factor, int P, hipStream_t st);
