@@ -81,6 +81,7 @@ struct ModelState {
   DevBuf<int> adam_step, drop_step, snap_flags, ep;
   DevBuf<uint16_t> blob;
   unsigned seed = 0;
+  float lr = 0.f;         // per-model learning rate override (0: use the run's lr)
 };
 
 }  // namespace
@@ -213,6 +214,7 @@ class Engine {
     sync();
   }
   void set_seed(int g, unsigned seed) { models_[check_g(g)].seed = seed; graphs_dirty_ = true; }
+  void set_lr(int g, float lr) { models_[check_g(g)].lr = lr; graphs_dirty_ = true; }
   py::dict get_opt_state(int g) {
     ModelState& S = models_[check_g(g)];
     py::dict d;
@@ -644,7 +646,7 @@ class Engine {
       U.adam_step = S.adam_step.p; U.drop_step = S.drop_step.p; U.gnorm = S.gnorm.p;
       U.blob = reinterpret_cast<bf16x8*>(S.blob.p); U.aux = S.aux.p;
       U.dpp = W.dpp.p; U.macro = splits_[0].macro.p; U.sg = W.sg.p; U.sc = W.sc.p; U.sh = W.sh.p;
-      U.dg = W.dg.p; U.dx = W.dx.p; U.dab = W.dab.p; U.T = splits_[0].T; U.seed = S.seed;
+      U.dg = W.dg.p; U.dx = W.dx.p; U.dab = W.dab.p; U.T = splits_[0].T; U.seed = S.seed; U.lr = S.lr;
       uj.push_back(U);
     }
     n_eval_jobs_ = (int)le.size();
@@ -826,6 +828,7 @@ PYBIND11_MODULE(_dlap_hip, m) {
       .def("history", &Engine::history)
       .def("run_epochs", &Engine::run_epochs, py::call_guard<py::gil_scoped_release>())
       .def("set_pipeline", &Engine::set_pipeline)
+      .def("set_lr", &Engine::set_lr)
       .def("forward_split", &Engine::forward_split)
       .def("train_step", &Engine::train_step)
       .def("backward_only", &Engine::backward_only)

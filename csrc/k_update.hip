@@ -228,7 +228,8 @@ __global__ __launch_bounds__(256) void k_adam(const UpdJob* __restrict__ jobs,
   const int step = gp(J.adam_step)[mom ? 1 : 0] + 1;
   const double bc1 = 1.0 - pow(0.9, (double)step);
   const double bc2 = 1.0 - pow(0.999, (double)step);
-  const float step_size = (float)(lr / bc1);
+  const float lr_g = J.lr > 0.f ? J.lr : lr;
+  const float step_size = (float)(lr_g / bc1);
   const float bc2s = (float)sqrt(bc2);
   const int i = p0 + blockIdx.x * ADAM_PB;
   float* __restrict__ pm = gp(J.m);

@@ -36,6 +36,8 @@ struct UpdJob {            // one model
   const float* dab;        // [T][64]
   int T;
   unsigned seed;
+  float lr;                // > 0: this model's learning rate (sweeps batch configs that
+                           // differ only in lr); 0: the launch-wide lr
 };
 
 // History row written per epoch by k_epoch_end (HIST_W floats).

@@ -139,6 +139,54 @@ def _draw_all(T: int, N: int, F: int, M: int, K: int = 5):
     return r, ch, mac, mask
 
 
+# ---- public building blocks under the reference's names / signatures ---------------------
+def generate_factor_returns(n_periods: int, n_factors: int = 5, monthly_vol: float = 0.02,
+                            factor_autocorr: float = 0.1) -> np.ndarray:
+    return _factor_returns(n_periods, n_factors, monthly_vol, factor_autocorr)
+
+
+def generate_factor_loadings(n_stocks: int, n_factors: int = 5, loading_vol: float = 1.0) -> np.ndarray:
+    b = np.random.randn(n_stocks, n_factors) * loading_vol
+    b[:, 0] = np.abs(b[:, 0]) + 0.5
+    return b
+
+
+def generate_characteristics(n_periods: int, n_stocks: int, n_features: int,
+                             factor_loadings: np.ndarray, noise_level: float = 0.5) -> np.ndarray:
+    return _characteristics(n_periods, n_stocks, n_features, factor_loadings, noise_level)
+
+
+def generate_returns(factor_returns: np.ndarray, factor_loadings: np.ndarray,
+                     idio_vol: float = 0.08) -> np.ndarray:
+    return _returns(factor_returns, factor_loadings, idio_vol)
+
+
+def generate_macro_features(n_periods: int, n_macro: int = 8,
+                            factor_returns: Optional[np.ndarray] = None) -> np.ndarray:
+    return _macro(n_periods, n_macro, factor_returns)
+
+
+def generate_missing_pattern(n_periods: int, n_stocks: int, avg_coverage: float = 0.7,
+                             min_history: int = 12) -> np.ndarray:
+    return _missing(n_periods, n_stocks, avg_coverage, min_history)
+
+
+def apply_missing_values(data: np.ndarray, mask: np.ndarray, missing_value: float = -99.99) -> np.ndarray:
+    """Sentinel at invalid (t, i) entries of a [T, N] or [T, N, F] array (copy)."""
+    out = np.array(data, copy=True)
+    out[~np.asarray(mask, dtype=bool)] = missing_value
+    return out
+
+
+def create_individual_npz(returns: np.ndarray, characteristics: np.ndarray, mask: np.ndarray,
+                          n_features: int, start_date: int = 196703) -> Dict[str, np.ndarray]:
+    return _char_npz(returns, characteristics, mask, n_features, start_date)
+
+
+def create_macro_npz(macro_features: np.ndarray, start_date: int = 196703) -> Dict[str, np.ndarray]:
+    return _macro_npz(macro_features, start_date)
+
+
 def generate_dataset(n_periods: int, n_stocks: int, n_features: int = 46, n_macro: int = 8,
                      n_factors: int = 5, seed: Optional[int] = None, start_date: int = 196703):
     """One split as (individual npz dict, macro npz dict)."""

@@ -142,11 +142,12 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
                      num_epochs_unc=256, num_epochs_moment=64, num_epochs=1024, lr=1e-3,
                      print_freq=128, save_dir=None, ignore_epoch=64, seed=None,
                      precision="bf16", selection_sign=1.0, verbose=True, n_models=1,
-                     models=None, seeds=None, save_dirs=None):
+                     models=None, seeds=None, save_dirs=None, lrs=None):
     """GPU executor of the 3-phase schedule; with ``n_models > 1`` trains an ensemble batch.
 
     Returns ``(model, history)`` for a single model, or ``(models, histories)`` when
-    ``n_models > 1`` (``models``/``seeds``/``save_dirs`` give per-member inputs).
+    ``n_models > 1`` (``models``/``seeds``/``save_dirs`` give per-member inputs; ``lrs`` gives
+    per-member learning rates, e.g. the lr axis of a hyperparameter sweep).
     """
     from ..models.gan import AssetPricingGAN
     if precision != "bf16":
@@ -174,6 +175,8 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
     eng.set_data(train_data, valid_data, test_data)
     for g, m in enumerate(models):
         eng.set_model(g, m, seeds[g])
+        if lrs is not None:
+            eng.eng.set_lr(g, float(lrs[g]))
     template = AssetPricingGAN(config)
     t_start = time.time()
     best_state = [False] * n_models

@@ -1,0 +1,130 @@
+"""Process-group plumbing for the multi-GPU drivers (one process per GPU).
+
+``torch.distributed`` with backend ``"nccl"`` is RCCL on ROCm: collectives run over xGMI between
+the GPUs of a node. Every message of this workload is small (KB-MB: weights [T, N] per model,
+metric tables), so the drivers issue ONE collective per payload (a padded all-gather of a
+stacked tensor), never one per model. Without a GPU (tests, CPU plumbing) the same code runs
+on ``gloo``.
+
+Launch: ``torchrun --nproc-per-node N --master-addr 127.0.0.1 -m <driver> ...``; a driver
+calls ``init()`` and gets a ``Dist`` context (single-process when WORLD_SIZE is unset).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+import torch.distributed as tdist
+
+
+@dataclass
+class Dist:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+    device: torch.device = torch.device("cpu")
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+    @property
+    def active(self) -> bool:
+        return self.world > 1 and tdist.is_available() and tdist.is_initialized()
+
+    def comm_device(self) -> torch.device:
+        """Where collective buffers must live (RCCL: the rank's GPU; gloo: host)."""
+        return self.device if self.backend == "nccl" else torch.device("cpu")
+
+
+def init(backend: Optional[str] = None, timeout_s: float = 600.0, use_gpu: Optional[bool] = None) -> Dist:
+    """Initialise from torchrun-style env vars. ``timeout_s`` bounds every collective, so a
+    rank that died turns into an error on its peers instead of a hang."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    if use_gpu is None:
+        use_gpu = torch.cuda.is_available()
+    dev = torch.device("cuda", local) if use_gpu else torch.device("cpu")
+    if use_gpu:
+        torch.cuda.set_device(dev)
+    if world <= 1:
+        return Dist(0, 1, 0, "none", dev)
+    backend = backend or ("nccl" if use_gpu else "gloo")
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if not tdist.is_initialized():
+        kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))
+        if backend == "nccl":
+            kw["device_id"] = dev
+        tdist.init_process_group(**kw)
+    return Dist(rank, world, local, backend, dev)
+
+
+def shutdown(d: Dist):
+    if d.active:
+        tdist.barrier()
+        tdist.destroy_process_group()
+
+
+def shard(n: int, rank: int, world: int) -> List[int]:
+    """Round-robin item indices of ``rank`` (9 seeds over 8 ranks: rank 0 gets 2)."""
+    return list(range(rank, n, world))
+
+
+def barrier(d: Dist):
+    if d.active:
+        tdist.barrier()
+
+
+def all_gather_rows(d: Dist, local: np.ndarray, n_total: int, owner_index: Sequence[int]) -> np.ndarray:
+    """Gather per-item rows from all ranks into item order.
+
+    ``local`` is [n_local, ...] for the items ``owner_index`` of this rank (the ``shard``
+    assignment); returns [n_total, ...] on every rank. One padded all-gather of a single
+    stacked tensor (plus nothing else: counts follow from ``shard``).
+    """
+    local = np.ascontiguousarray(local)
+    if not d.active:
+        out = np.empty((n_total,) + local.shape[1:], local.dtype)
+        out[list(owner_index)] = local
+        return out
+    per = [len(shard(n_total, r, d.world)) for r in range(d.world)]
+    cap = max(per)
+    pad = np.zeros((cap,) + local.shape[1:], local.dtype)
+    pad[:len(local)] = local
+    dev = d.comm_device()
+    t = torch.from_numpy(pad).to(dev)
+    bufs = torch.empty((d.world * cap,) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+    tdist.all_gather_into_tensor(bufs, t)          # concatenated along dim 0 (RCCL and gloo)
+    g = bufs.cpu().numpy().reshape((d.world, cap) + local.shape[1:])
+    out = np.empty((n_total,) + local.shape[1:], local.dtype)
+    for r in range(d.world):
+        idx = shard(n_total, r, d.world)
+        out[idx] = g[r, :len(idx)]
+    return out
+
+
+def broadcast_arrays(d: Dist, arrays: Optional[dict], src: int = 0) -> dict:
+    """Broadcast a dict of numpy arrays from ``src`` (e.g. a panel read once from disk): one
+    metadata object broadcast, then one tensor broadcast per array."""
+    if not d.active:
+        return arrays
+    meta = [None]
+    if d.rank == src:
+        meta = [{k: (v.shape, str(v.dtype)) for k, v in arrays.items()}]
+    tdist.broadcast_object_list(meta, src=src)
+    dev = d.comm_device()
+    out = {}
+    for k, (shape, dt) in meta[0].items():
+        if d.rank == src:
+            t = torch.from_numpy(np.ascontiguousarray(arrays[k])).to(dev)
+        else:
+            t = torch.empty(shape, dtype=torch.from_numpy(np.empty(0, np.dtype(dt))).dtype, device=dev)
+        tdist.broadcast(t, src=src)
+        out[k] = t.cpu().numpy()
+    return out

@@ -1,0 +1,175 @@
+"""Hyperparameter sweep over the paper's 384-configuration grid, sharded over the GPUs of a node
+(BASELINE config 4).
+
+Grid (paper Table A.VIII):
+    HL  {2,3,4}        SDF hidden layers of 64 units        -> hidden_dim = [64] * HL
+    SMV {4,8}          macro LSTM states                    -> num_units_rnn = [SMV]
+    CSMV {16,32}       conditional-network macro states     -> num_units_rnn_moment = [CSMV]
+                       (accepted and ignored by the model, exactly as in the reference)
+    CHL {0,1}          conditional hidden layers            -> hidden_dim_moment = [] | [CHU]
+    CHU {4,8,16,32}    conditional units (moment count)     -> num_condition_moment = CHU
+    LR  {1e-3,5e-4,2e-4,1e-4}
+3 * 2 * 2 * 2 * 4 * 4 = 384 configurations.
+
+Execution: configurations that share an architecture (everything but LR) form a *bucket*; a
+bucket is trained as ONE batched native-engine run with one member per LR (per-member learning
+rates, ``Engine.set_lr``), so the 384 configs are 96 engine runs. Buckets are dealt round-robin
+over ranks. A bucket that raises marks its configs failed (metrics NaN) without stopping the
+sweep; the per-config metric table is exchanged with one all-gather and every rank ranks the
+configs identically (best = highest validation Sharpe of the paper-sign SDF factor by default).
+"""
+from __future__ import annotations
+
+import argparse
+import itertools
+import json
+import time
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from ..config import default_cli_config
+from . import comm
+from .ensemble import SPLITS, _init_models, _load_batches
+
+GRID = {"HL": (2, 3, 4), "SMV": (4, 8), "CSMV": (16, 32), "CHL": (0, 1), "CHU": (4, 8, 16, 32),
+        "LR": (1e-3, 5e-4, 2e-4, 1e-4)}
+METRICS = ("ok", "valid_sharpe", "test_sharpe", "train_sharpe", "valid_loss", "test_loss", "wall_s")
+
+
+def paper_grid(M: int, F: int, grid: Dict = GRID, dropout: float = 0.05) -> List[Tuple[Dict, float, Dict]]:
+    """[(model config, lr, grid point)] in a fixed order (384 entries for the paper grid)."""
+    keys = list(grid)
+    out = []
+    for vals in itertools.product(*(grid[k] for k in keys)):
+        pt = dict(zip(keys, vals))
+        cfg = default_cli_config(M, F, hidden_dim=[64] * pt["HL"], rnn_dim=[pt["SMV"]],
+                                 num_moments=pt["CHU"], dropout=dropout,
+                                 hidden_dim_moment=[pt["CHU"]] * pt["CHL"], rnn_dim_moment=[pt["CSMV"]])
+        out.append((cfg, float(pt["LR"]), pt))
+    return out
+
+
+def buckets(entries: Sequence[Tuple[Dict, float, Dict]]) -> List[List[int]]:
+    """Group config indices that differ only in lr (same architecture -> one batched run)."""
+    groups: Dict[str, List[int]] = {}
+    for i, (cfg, _, _) in enumerate(entries):
+        groups.setdefault(json.dumps(cfg, sort_keys=True), []).append(i)
+    return list(groups.values())
+
+
+def _sharpe_unbiased(p: np.ndarray) -> float:
+    sd = float(np.std(p, ddof=1)) if len(p) > 1 else 0.0
+    return 0.0 if sd < 1e-8 else float(np.mean(p) / sd)
+
+
+def run_bucket(entries, idx: List[int], batches: Dict[str, Dict], device: torch.device, epochs, ignore_epoch,
+               seed: int, selection_sign: float) -> np.ndarray:
+    """Train one architecture bucket; returns [len(idx), len(METRICS)]."""
+    out = np.full((len(idx), len(METRICS)), np.nan)
+    out[:, 0] = 0.0
+    cfg = entries[idx[0]][0]
+    lrs = [entries[i][1] for i in idx]
+    t0 = time.time()
+    n1, n2, n3 = epochs
+    tr, va, te = (batches[s] for s in SPLITS)
+    if device.type == "cuda":
+        from ..engine.runner import train_3phase_gpu
+        models = _init_models(cfg, [seed] * len(idx))
+        ms, hs = train_3phase_gpu(cfg, tr, va, te, device=device, num_epochs_unc=n1, num_epochs_moment=n2,
+                                  num_epochs=n3, lr=lrs[0], print_freq=10 ** 9, ignore_epoch=ignore_epoch,
+                                  selection_sign=selection_sign, verbose=False, models=models,
+                                  seeds=[seed + 17 * k for k in range(len(idx))], lrs=lrs)
+        if len(idx) == 1:
+            ms = [ms]
+        finals = [m.engine_final_eval for m in ms]
+        for k, fe in enumerate(finals):
+            out[k, 1:6] = [fe[1]["sharpe"], fe[2]["sharpe"], fe[0]["sharpe"], fe[1]["loss"], fe[2]["loss"]]
+    else:
+        from ..train.trainer import evaluate, train_3phase
+        for k, lr in enumerate(lrs):
+            torch.manual_seed(seed)
+            model, _ = train_3phase(cfg, tr, va, te, device=torch.device("cpu"), num_epochs_unc=n1,
+                                    num_epochs_moment=n2, num_epochs=n3, lr=lr, print_freq=10 ** 9,
+                                    ignore_epoch=ignore_epoch, selection_sign=selection_sign, verbose=False)
+            ev = [evaluate(model, b, "cpu") for b in (tr, va, te)]
+            out[k, 1:6] = [ev[1]["sharpe"], ev[2]["sharpe"], ev[0]["sharpe"], ev[1]["loss"], ev[2]["loss"]]
+    out[:, 0] = 1.0
+    out[:, 6] = time.time() - t0
+    return out
+
+
+def run_sweep(batches: Dict[str, Dict], entries, dist: Optional[comm.Dist] = None, epochs=(256, 64, 1024),
+              ignore_epoch: int = 64, seed: int = 42, selection_sign: float = 1.0,
+              rank_sign: float = -1.0, fail_buckets: Sequence[int] = ()) -> Dict:
+    d = dist or comm.Dist()
+    bks = buckets(entries)
+    mine = comm.shard(len(bks), d.rank, d.world)
+    local = {}
+    errors = {}
+    for b in mine:
+        try:
+            if b in set(fail_buckets):
+                raise RuntimeError("injected failure")
+            local[b] = run_bucket(entries, bks[b], batches, d.device, epochs, ignore_epoch, seed, selection_sign)
+        except Exception as e:  # isolate: this bucket's configs report NaN
+            errors[b] = f"{type(e).__name__}: {e}"
+            z = np.full((len(bks[b]), len(METRICS)), np.nan)
+            z[:, 0] = 0.0
+            local[b] = z
+    # one all-gather of a fixed-size table per rank: rows = configs in bucket order
+    width = max(len(x) for x in bks)
+    tab = np.full((len(mine), width, len(METRICS)), np.nan)
+    for k, b in enumerate(mine):
+        tab[k, :len(bks[b])] = local[b]
+    allb = comm.all_gather_rows(d, tab, len(bks), mine)
+    table = np.full((len(entries), len(METRICS)), np.nan)
+    for b, ids in enumerate(bks):
+        table[ids] = allb[b, :len(ids)]
+    ok = table[:, 0] > 0.5
+    score = np.where(ok, rank_sign * table[:, 1], -np.inf)
+    best = int(np.argmax(score)) if ok.any() else -1
+    return {"n_configs": len(entries), "n_buckets": len(bks), "n_ok": int(ok.sum()),
+            "failed": [int(i) for i in np.where(~ok)[0]], "best_index": best,
+            "best_point": entries[best][2] if best >= 0 else None,
+            "best_valid_sharpe": float(table[best, 1]) if best >= 0 else None,
+            "best_test_sharpe": float(table[best, 2]) if best >= 0 else None,
+            "table": table, "metrics": METRICS, "errors_local": errors}
+
+
+def main(argv=None):
+    p = argparse.ArgumentParser(description="384-config hyperparameter sweep over the GPUs of one node")
+    p.add_argument("--data_dir", type=str, default=None)
+    p.add_argument("--synthetic", type=int, nargs=6, default=None,
+                   metavar=("T_TRAIN", "T_VALID", "T_TEST", "N", "F", "M"))
+    p.add_argument("--data_seed", type=int, default=0)
+    p.add_argument("--epochs_unc", type=int, default=256)
+    p.add_argument("--epochs_moment", type=int, default=64)
+    p.add_argument("--epochs", type=int, default=1024)
+    p.add_argument("--ignore_epoch", type=int, default=64)
+    p.add_argument("--seed", type=int, default=42)
+    p.add_argument("--limit", type=int, default=None, help="only the first K grid points")
+    p.add_argument("--out", type=str, default=None, help="write the metric table (.npz) here")
+    p.add_argument("--cpu", action="store_true")
+    a = p.parse_args(argv)
+    if not a.synthetic and not a.data_dir:
+        p.error("--data_dir or --synthetic is required")
+    d = comm.init(use_gpu=not a.cpu and torch.cuda.is_available())
+    batches = _load_batches(a)
+    M = batches["train"]["macro_features"].shape[-1] if "macro_features" in batches["train"] else 0
+    F = batches["train"]["individual_features"].shape[-1]
+    entries = paper_grid(M, F)
+    if a.limit:
+        entries = entries[:a.limit]
+    res = run_sweep(batches, entries, d, (a.epochs_unc, a.epochs_moment, a.epochs), a.ignore_epoch, a.seed)
+    if d.is_main:
+        if a.out:
+            np.savez(a.out, table=res["table"], metrics=np.array(METRICS))
+        print(json.dumps({k: v for k, v in res.items() if k not in ("table",)}, default=str))
+    comm.shutdown(d)
+    return res
+
+
+if __name__ == "__main__":
+    main()

@@ -1,3 +1,4 @@
+import importlib.util
 import os
 import sys
 
@@ -8,6 +9,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 REFERENCE = "/root/reference"
+SHIPPED_DATA = os.path.join(REFERENCE, "data", "synthetic_data")
 
 
 def pytest_configure(config):
@@ -15,12 +17,32 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running")
 
 
+def _load_reference_package():
+    """Import the read-only reference ``src`` package under the name ``ref_src`` (this repo has
+    its own top-level ``src`` compatibility package, so the name must not collide)."""
+    if "ref_src" in sys.modules:
+        return sys.modules["ref_src"]
+    sys.dont_write_bytecode = True       # never write .pyc files into the read-only checkout
+    init = os.path.join(REFERENCE, "src", "__init__.py")
+    spec = importlib.util.spec_from_file_location("ref_src", init,
+                                                  submodule_search_locations=[os.path.dirname(init)])
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules["ref_src"] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
 @pytest.fixture(scope="session")
 def reference_src():
-    """The read-only reference package, used only as a test oracle (skips if absent)."""
-    if not os.path.isdir(os.path.join(REFERENCE, "src")):
+    """The reference package as a test oracle (skips where the checkout is absent, e.g. on the
+    GPU box). Only its Python sources are imported; nothing prebuilt is loaded."""
+    if not os.path.isfile(os.path.join(REFERENCE, "src", "__init__.py")):
         pytest.skip("reference checkout not available on this machine")
-    if REFERENCE not in sys.path:
-        sys.path.append(REFERENCE)
-    import importlib
-    return importlib.import_module("src")
+    return _load_reference_package()
+
+
+@pytest.fixture(scope="session")
+def shipped_data():
+    if not os.path.isdir(os.path.join(SHIPPED_DATA, "char")):
+        pytest.skip("reference synthetic data not available")
+    return SHIPPED_DATA

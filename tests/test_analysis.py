@@ -1,0 +1,93 @@
+"""Ensemble evaluator / plots / downloader vs the reference tools."""
+import importlib
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from deeplearninginassetpricing_paperreplication_amd.analysis import ensemble as ens
+from deeplearninginassetpricing_paperreplication_amd.analysis import plots
+from deeplearninginassetpricing_paperreplication_amd.analysis import portfolio as pf
+from deeplearninginassetpricing_paperreplication_amd.data import download
+from deeplearninginassetpricing_paperreplication_amd.train import cli
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def two_checkpoints(shipped_data, tmp_path_factory):
+    root = tmp_path_factory.mktemp("ens")
+    dirs = []
+    for seed in (1, 2):
+        d = root / f"m{seed}"
+        cli.main(["--data_dir", shipped_data, "--epochs_unc", "3", "--epochs_moment", "1", "--epochs", "3",
+                  "--ignore_epoch", "0", "--print_freq", "100", "--seed", str(seed), "--device", "cpu",
+                  "--save_dir", str(d)])
+        dirs.append(str(d))
+    return dirs
+
+
+def test_renormalize_matches_loop():
+    rng = np.random.RandomState(0)
+    w = rng.randn(7, 11).astype(np.float32)
+    m = rng.rand(7, 11) > 0.3
+    w[2] = 0
+    ref = w.copy()
+    for t in range(7):
+        s = np.abs(ref[t] * m[t].astype(float)).sum()
+        if s > 1e-8:
+            ref[t] = ref[t] / s
+    np.testing.assert_allclose(pf.renormalize(w, m), ref, rtol=1e-6)
+
+
+def test_evaluate_ensemble_matches_reference(reference_src, shipped_data, two_checkpoints, capsys):
+    ref = importlib.import_module("ref_src.evaluate_ensemble")
+    a = ref.evaluate_ensemble(two_checkpoints, shipped_data)
+    b = ens.evaluate_ensemble(two_checkpoints, shipped_data, verbose=False)
+    capsys.readouterr()
+    for k in ("train_sharpe", "valid_sharpe", "test_sharpe"):
+        assert b[k] == pytest.approx(a[k], rel=1e-5, abs=1e-7), k
+    np.testing.assert_allclose(b["individual_sharpes"], a["individual_sharpes"], rtol=1e-5)
+
+
+def test_summary_statistics_match_reference_table(reference_src, shipped_data, two_checkpoints):
+    p = plots._Panel(two_checkpoints, shipped_data)
+    f = p.ensemble_factor("test").astype(np.float64)
+    s = pf.sdf_statistics(f)
+    mu, sd = f.mean(), f.std()
+    assert s["sharpe"] == pytest.approx(mu / sd, rel=1e-6)
+    assert s["kurtosis"] == pytest.approx(((f - mu) ** 4).mean() / sd ** 4 - 3, rel=1e-6)
+    growth = np.cumprod(1 + f)
+    assert s["max_drawdown"] == pytest.approx(((growth - np.maximum.accumulate(growth)) /
+                                               np.maximum.accumulate(growth)).min(), rel=1e-6)
+
+
+def test_generate_all_plots(shipped_data, two_checkpoints, tmp_path, capsys):
+    plots.generate_all_plots(two_checkpoints, shipped_data, str(tmp_path))
+    capsys.readouterr()
+    for f in ("cumulative_sdf.png", "training_curves.png", "sharpe_comparison.png", "monthly_returns.png",
+              "summary_statistics.png"):
+        assert (tmp_path / f).stat().st_size > 1000, f
+
+
+def test_month_range():
+    d = plots.month_range(1967, 14)
+    assert (d[0].year, d[0].month) == (1967, 3) and (d[10].year, d[10].month) == (1968, 1)
+
+
+def test_download_check_and_graceful_failure(shipped_data, tmp_path, capsys):
+    assert download.check_data_exists(shipped_data)["complete"]
+    st = download.check_data_exists(str(tmp_path))
+    assert not st["complete"] and len(st["missing"]) == 6
+    ok = download.download_all_data(str(tmp_path), quiet=True)      # no gdown / network here
+    assert ok is False
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1")
+    r = subprocess.run([sys.executable, "-m", "src.download_data", "--check", "-o", str(tmp_path)], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 1 and "Missing" in r.stdout
+    r = subprocess.run([sys.executable, "-m", "src.download_data", "--check", "-o", shipped_data], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0

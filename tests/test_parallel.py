@@ -1,0 +1,125 @@
+"""Multi-process drivers on the CPU (gloo, 2 ranks): collectives, the seed ensemble and the
+hyperparameter sweep, including uneven sharding and failure isolation. The same code paths use
+RCCL ("nccl") with one process per GPU on an MI355X node."""
+import json
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from deeplearninginassetpricing_paperreplication_amd.data.synthetic import generate_panel_fast
+from deeplearninginassetpricing_paperreplication_amd.parallel import comm
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _batches(seed=0, T=(10, 4, 5), N=30, F=6, M=3):
+    ret, feats, mask, mac = generate_panel_fast(sum(T), N, F, M, seed=seed)
+    mac = (mac - mac[:T[0]].mean(0)) / (mac[:T[0]].std(0, unbiased=False) + 1e-8)
+    cuts = {"train": (0, T[0]), "valid": (T[0], T[0] + T[1]), "test": (T[0] + T[1], sum(T))}
+    return {k: {"returns": ret[a:b].contiguous(), "individual_features": feats[a:b].contiguous(),
+                "mask": mask[a:b].contiguous(), "macro_features": mac[a:b].contiguous()}
+            for k, (a, b) in cuts.items()}
+
+
+def _cfg(b):
+    from deeplearninginassetpricing_paperreplication_amd.config import default_cli_config
+    return default_cli_config(b["train"]["macro_features"].shape[1], b["train"]["individual_features"].shape[2],
+                              hidden_dim=[8], rnn_dim=[2])
+
+
+def _worker(rank, world, port, outdir, job):
+    os.environ.update(WORLD_SIZE=str(world), RANK=str(rank), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(1)
+    d = comm.init(backend="gloo", use_gpu=False, timeout_s=120)
+    out = {}
+    if job == "collectives":
+        n = 5
+        mine = comm.shard(n, d.rank, d.world)
+        loc = np.stack([np.full((2, 3), i, np.float32) for i in mine])
+        g = comm.all_gather_rows(d, loc, n, mine)
+        out["gathered"] = g[:, 0, 0].tolist()
+        arr = {"x": np.arange(6, dtype=np.int32).reshape(2, 3), "m": np.array([True, False])} if d.rank == 0 else None
+        got = comm.broadcast_arrays(d, arr)
+        out["bcast"] = [got["x"].tolist(), got["m"].tolist()]
+    elif job in ("ensemble", "ensemble_fail"):
+        from deeplearninginassetpricing_paperreplication_amd.parallel.ensemble import run_ensemble
+        b = _batches()
+        res = run_ensemble(_cfg(b), b, seeds=(3, 4, 5), dist=d, epochs=(2, 1, 2), ignore_epoch=0,
+                           print_freq=100, fail_seeds=(4,) if job == "ensemble_fail" else ())
+        out = {k: v for k, v in res.items() if k != "errors"}
+    elif job == "sweep":
+        from deeplearninginassetpricing_paperreplication_amd.parallel.sweep import paper_grid, run_sweep
+        b = _batches()
+        grid = {"HL": (1,), "SMV": (2,), "CSMV": (16,), "CHL": (0, 1), "CHU": (4,), "LR": (1e-3, 1e-4)}
+        entries = paper_grid(3, 6, grid)
+        res = run_sweep(b, entries, d, epochs=(2, 1, 2), ignore_epoch=0, fail_buckets=(1,))
+        out = {"table": np.nan_to_num(res["table"], nan=-999).tolist(), "best": res["best_index"],
+               "failed": res["failed"], "n_buckets": res["n_buckets"]}
+    with open(os.path.join(outdir, f"r{rank}.json"), "w") as fh:
+        json.dump(out, fh)
+    comm.shutdown(d)
+
+
+def _run(job, tmp_path, world=2):
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), job), nprocs=world, join=True)
+    return [json.load(open(tmp_path / f"r{r}.json")) for r in range(world)]
+
+
+def test_shard_round_robin():
+    assert comm.shard(9, 0, 8) == [0, 8] and comm.shard(9, 7, 8) == [7]
+    assert sorted(sum((comm.shard(9, r, 4) for r in range(4)), [])) == list(range(9))
+
+
+def test_collectives_gloo(tmp_path):
+    r = _run("collectives", tmp_path)
+    for x in r:
+        assert x["gathered"] == [0, 1, 2, 3, 4]
+        assert x["bcast"] == [[[0, 1, 2], [3, 4, 5]], [True, False]]
+
+
+def test_distributed_ensemble_equals_serial(tmp_path):
+    from deeplearninginassetpricing_paperreplication_amd.parallel.ensemble import run_ensemble
+    dist = _run("ensemble", tmp_path)
+    assert dist[0] == {**dist[0], **{k: dist[1][k] for k in ("test_sharpe", "individual_sharpes")}}
+    torch.set_num_threads(1)
+    b = _batches()
+    serial = run_ensemble(_cfg(b), b, seeds=(3, 4, 5), epochs=(2, 1, 2), ignore_epoch=0, print_freq=100)
+    for k in ("train_sharpe", "valid_sharpe", "test_sharpe"):
+        assert dist[0][k] == pytest.approx(serial[k], rel=1e-6, abs=1e-9), k
+    np.testing.assert_allclose(dist[0]["individual_sharpes"], serial["individual_sharpes"], rtol=1e-6)
+    assert dist[0]["world_size"] == 2 and serial["failed"] == []
+
+
+def test_ensemble_failure_isolation(tmp_path):
+    r = _run("ensemble_fail", tmp_path)
+    for x in r:
+        assert x["failed"] == [4] and x["ok"] == [True, False, True]
+        assert np.isnan(x["individual_sharpes"][1]) and np.isfinite(x["test_sharpe"])
+
+
+def test_sweep_sharding_and_failure_isolation(tmp_path):
+    r = _run("sweep", tmp_path)
+    assert r[0]["table"] == r[1]["table"] and r[0]["best"] == r[1]["best"]
+    t = np.array(r[0]["table"])
+    assert r[0]["n_buckets"] == 2 and t.shape == (4, 7)
+    ok = t[:, 0] > 0.5
+    assert ok.sum() == 2 and len(r[0]["failed"]) == 2       # bucket 1 (2 lr configs) failed
+    assert np.all(np.isfinite(t[ok, 1]))
+
+
+def test_paper_grid_is_384_configs_in_96_buckets():
+    from deeplearninginassetpricing_paperreplication_amd.parallel.sweep import buckets, paper_grid
+    e = paper_grid(178, 46)
+    assert len(e) == 384 and len(buckets(e)) == 96
+    cfg, lr, pt = e[0]
+    assert cfg["hidden_dim"] == [64, 64] and cfg["num_units_rnn"] == [4] and lr == 1e-3
+    assert {len(b) for b in buckets(e)} == {4}
