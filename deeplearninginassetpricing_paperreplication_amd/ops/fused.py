@@ -20,6 +20,7 @@ Gradient scopes per phase (what ``loss.backward()`` produces, as in autograd):
 """
 from __future__ import annotations
 
+import dataclasses
 from collections import OrderedDict
 from typing import Dict, Optional
 
@@ -42,7 +43,7 @@ class _Slot:
 
 
 def _slot(spec) -> _Slot:
-    key = spec.key() if hasattr(spec, "key") else repr(spec)
+    key = repr(spec)
     s = _CACHE.get(key)
     if s is None:
         s = _Slot(spec)
@@ -62,7 +63,10 @@ def _tkey(t: Optional[torch.Tensor]):
 
 def _prepare(model, macro, individual, returns, mask) -> _Slot:
     from ..engine.runner import flatten_state
-    s = _slot(model.spec)
+    # eval mode: an engine built without dropout, so the analytic backward of a no-grad-free
+    # eval forward (rare, but legal in autograd) sees exactly the forward's activations
+    spec = model.spec if model.training else dataclasses.replace(model.spec, dropout=0.0)
+    s = _slot(spec)
     key = (_tkey(macro), _tkey(individual), _tkey(returns), _tkey(mask))
     if key != s.data_key:
         batch = {"individual_features": individual.detach(), "returns": returns.detach(),
@@ -161,8 +165,16 @@ def gan_forward(model, macro, individual, returns, mask, phase: str = "condition
     }
 
 
+_ZEROS: Dict[tuple, torch.Tensor] = {}
+
+
 def gan_weights(model, macro, individual, mask, normalized: bool = False) -> torch.Tensor:
-    zeros = torch.zeros(mask.shape, dtype=torch.float32, device=mask.device)
+    # get_weights has no returns argument: a cached zero panel keeps the upload cache valid
+    zk = _tkey(mask)
+    zeros = _ZEROS.get(zk)
+    if zeros is None:
+        _ZEROS.clear()
+        zeros = _ZEROS[zk] = torch.zeros(mask.shape, dtype=torch.float32, device=mask.device)
     s = _prepare(model, macro, individual, zeros, mask)
     s.eng.eng.forward_split(0, bool(model.training), False)
     w = torch.from_numpy(s.eng.eng.read_ws(0, 0, "wn").reshape(s.T, s.N)).to(individual.device)
