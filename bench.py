@@ -88,6 +88,8 @@ def main():
     w1, w2, w3 = schedule_split(max(a.warmup, 3))
     eng = GANEngine(AssetPricingGAN(cfg).spec, n_models=G, max_epochs=n1 + n2 + n3 + w1 + w2 + w3 + 8)
     eng.set_data(tr, va, te)
+    if os.environ.get("DLAP_PIPELINE", "1") == "0":      # profiling: sequential epoch graph
+        eng.eng.set_pipeline(False)
     for g in range(G):
         seed = 1000 * rank + g
         torch.manual_seed(seed)

@@ -77,7 +77,7 @@ struct ModelSplitWS {   // per (model, split)
 };
 
 struct ModelState {
-  DevBuf<float> params, grads, m, v, snap_loss, snap_sharpe, gnorm, best, aux, hist;
+  DevBuf<float> params, grads, m, v, snap_loss, snap_sharpe, gnorm, best, aux, hist, wproj;
   DevBuf<int> adam_step, drop_step, snap_flags, ep;
   DevBuf<uint16_t> blob;
   unsigned seed = 0;
@@ -85,6 +85,11 @@ struct ModelState {
 };
 
 }  // namespace
+
+static int env_int(const char* name, int dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoi(v) : dflt;
+}
 
 class Engine {
  public:
@@ -109,6 +114,7 @@ class Engine {
       S.hist.alloc((size_t)max_epochs_ * HIST_W);
       S.adam_step.alloc(2); S.drop_step.alloc(1); S.snap_flags.alloc(2); S.ep.alloc(2);
       S.blob.alloc((size_t)md_.md.blob_frags * 512);
+      S.wproj.alloc((size_t)(md_.proj_mp + 1) * md_.proj_np);
     }
     ws_.resize((size_t)G * 3);
   }
@@ -399,6 +405,7 @@ class Engine {
     J.params = models_[g].params.p;
     J.blob = reinterpret_cast<bf16x8*>(models_[g].blob.p);
     J.aux = models_[g].aux.p;
+    J.wproj = models_[g].wproj.p;
     DevBuf<char> tmp;
     std::vector<UpdJob> v{J};
     upload(tmp, v);
@@ -494,6 +501,8 @@ class Engine {
       d.tile_m[t] = GradTile{d.m[j].w_off, d.m[j].ld, 0, d.m[j].out, d.m[j].in, 0, t};
     d.ntile_m = d.nslice_m = t;
     d.tps_m = 1;
+    d.proj_mp = std::max(4, (M + 3) / 4 * 4);
+    d.proj_np = ((nrnn > 0 ? 4 * H : 0) + 64 + 15) / 16 * 16;   // whole 16-wide MFMA tiles
     for (int e = 0; e < SLAB_EXTRA; ++e) { d.extra_s[e] = -1; d.extra_m[e] = -1; }
     for (int j = 0; j < d.nl_s; ++j)
       for (int o = 0; o < d.s[j].out; ++o) d.extra_s[j * 64 + o] = d.s[j].b_off + o;
@@ -542,11 +551,17 @@ class Engine {
     }
     if (s == 0) {
       const int ntiles = (R + 31) / 32;
-      gx_bwd_ = std::max(1, std::min((ntiles + 3) / 4, 256));
+      gx_bwd_ = std::max(1, std::min((ntiles + 3) / 4, env_int("DLAP_GX_BWD", 256)));
       const int nsl = std::max(md_.nslice_s, md_.nslice_m);
       slab_.alloc((size_t)G_ * nsl * gx_bwd_ * slab_stride());
     }
-    gx_fwd_[s] = std::max(1, std::min(((R + 31) / 32 + 3) / 4, 1024));
+    gx_fwd_[s] = std::max(1, std::min(((R + 31) / 32 + 3) / 4, env_int("DLAP_GX_FWD", 1024)));
+    // per-period SDF inputs [T][Dm] are staged in LDS by the tower kernels when small
+    int tmax = 0;
+    for (int k = 0; k < 3; ++k)
+      if (splits_[k].set || k == s) tmax = std::max(tmax, splits_[k].T);
+    const int ppf = tmax * md_.Dm;
+    md_.md.pp_lds_floats = (md_.Dm > 0 && ppf <= 8192 && !env_int("DLAP_PP_GLOBAL", 0)) ? ppf : 0;
   }
 
   // ------------------------------------------------------------ job tables ------------
@@ -555,6 +570,7 @@ class Engine {
     SplitDev& D = splits_[s];
     RnnJob J{};
     J.params = models_[g].params.p;
+    J.wproj = models_[g].wproj.p;
     J.macro = D.macro.p;
     J.T = D.T;
     J.out = W.pp.p;
@@ -586,7 +602,7 @@ class Engine {
     J.slab = slab_.p;
     J.u_out = W.u.p; J.v_out = W.v.p;
     J.step = models_[g].drop_step.p;
-    J.R = D.R; J.N = D.N;
+    J.R = D.R; J.N = D.N; J.T = D.T;
     J.seed = models_[g].seed;
     J.train = train; J.do_sdf = do_sdf; J.do_mom = do_mom;
     const int nsl = std::max(md_.nslice_s, md_.nslice_m);
@@ -644,7 +660,7 @@ class Engine {
       UpdJob U{};
       U.params = S.params.p; U.grads = S.grads.p; U.m = S.m.p; U.v = S.v.p;
       U.adam_step = S.adam_step.p; U.drop_step = S.drop_step.p; U.gnorm = S.gnorm.p;
-      U.blob = reinterpret_cast<bf16x8*>(S.blob.p); U.aux = S.aux.p;
+      U.blob = reinterpret_cast<bf16x8*>(S.blob.p); U.aux = S.aux.p; U.wproj = S.wproj.p;
       U.dpp = W.dpp.p; U.macro = splits_[0].macro.p; U.sg = W.sg.p; U.sc = W.sc.p; U.sh = W.sh.p;
       U.dg = W.dg.p; U.dx = W.dx.p; U.dab = W.dab.p; U.T = splits_[0].T; U.seed = S.seed; U.lr = S.lr;
       uj.push_back(U);
@@ -829,6 +845,7 @@ PYBIND11_MODULE(_dlap_hip, m) {
       .def("run_epochs", &Engine::run_epochs, py::call_guard<py::gil_scoped_release>())
       .def("set_pipeline", &Engine::set_pipeline)
       .def("set_lr", &Engine::set_lr)
+      .def_static("rnn_timestamps", []() { return rnn_timestamps(); })
       .def("forward_split", &Engine::forward_split)
       .def("train_step", &Engine::train_step)
       .def("backward_only", &Engine::backward_only)

@@ -85,10 +85,11 @@ DLAP_DEV void issue_tile(const MlpJob& J, int tile, TileIn<KS1>& in) {
   }
 }
 
-// Finish a prefetched tile: row info, zero rows beyond R, insert the per-period columns.
-template <int KS1>
+// Finish a prefetched tile: row info, zero rows beyond R, insert the per-period columns
+// (INS; from the LDS copy staged with the weights when it fits, else from global memory).
+template <int KS1, bool INS = true>
 DLAP_DEV RowInfo finish_tile(const MlpJob& J, const MlpDims& D, int tile, TileIn<KS1>& in,
-                             bf16x8 (&xf)[2][KS1]) {
+                             bf16x8 (&xf)[2][KS1], const float* spp = nullptr) {
   RowInfo ri;
   const int l = lane_id(), q = l >> 4;
   const int s_lo = D.F >> 5, s_hi = (D.F + D.Dm - 1) >> 5;
@@ -101,20 +102,23 @@ DLAP_DEV RowInfo finish_tile(const MlpJob& J, const MlpDims& D, int tile, TileIn
     ri.dense[b] = ok ? in.ti[b].x * J.N + in.ti[b].y : -1;
 #pragma unroll
     for (int s = 0; s < KS1; ++s) xf[b][s] = ok ? in.x[b][s] : zero8();
-    if (D.Dm > 0) {
-      const auto pp = gp(J.pp) + ri.t[b] * D.Dm;
+    if (INS && D.Dm > 0) {
+      auto insert = [&](auto pp) {
 #pragma unroll
-      for (int s = 0; s < KS1; ++s) {
-        if (s >= s_lo && s <= s_hi) {                          // wave-uniform
+        for (int s = 0; s < KS1; ++s) {
+          if (s >= s_lo && s <= s_hi) {                          // wave-uniform
 #pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const int col = 32 * s + 8 * q + j - D.F;
-            const bool in_rng = (unsigned)col < (unsigned)D.Dm;
-            const float v = pp[min(max(col, 0), D.Dm - 1)];
-            if (in_rng && ok) xf[b][s][j] = (__bf16)v;
+            for (int j = 0; j < 8; ++j) {
+              const int col = 32 * s + 8 * q + j - D.F;
+              const bool in_rng = (unsigned)col < (unsigned)D.Dm;
+              const float v = pp[min(max(col, 0), D.Dm - 1)];
+              if (in_rng && ok) xf[b][s][j] = (__bf16)v;
+            }
           }
         }
-      }
+      };
+      if (D.pp_lds_floats > 0) insert(spp + ri.t[b] * D.Dm);      // LDS: ~100-cycle lookups
+      else insert(gp(J.pp) + ri.t[b] * D.Dm);
     }
     if (!ok) in.dw[b] = 0.f;
   }
@@ -241,9 +245,14 @@ DLAP_DEV DropCtx drop_ctx(const MlpJob& J, const MlpDims& D) {
   return dc;
 }
 
-DLAP_DEV void stage_weights(const MlpJob& J, const MlpDims& D, bf16x8* lds, float* aux) {
+DLAP_DEV float* pp_lds_ptr(char* smem, const MlpDims& D) {
+  return reinterpret_cast<float*>(smem + (size_t)D.blob_frags * 1024 + (size_t)((D.aux_floats + 3) & ~3) * 4);
+}
+DLAP_DEV void stage_weights(const MlpJob& J, const MlpDims& D, bf16x8* lds, float* aux, float* spp = nullptr) {
   for (int i = threadIdx.x; i < D.blob_frags * 64; i += blockDim.x) lds[i] = gp(J.blob)[i];
   for (int i = threadIdx.x; i < D.aux_floats; i += blockDim.x) aux[i] = gp(J.aux)[i];
+  if (spp && D.pp_lds_floats > 0 && D.Dm > 0)
+    for (int i = threadIdx.x; i < J.T * D.Dm; i += blockDim.x) spp[i] = gp(J.pp)[i];
   __syncthreads();
 }
 
@@ -326,19 +335,20 @@ __global__ __launch_bounds__(256, 2) void k_mlp_fwd(const MlpJob* __restrict__ j
   const MlpJob& J = jobs[blockIdx.y];
   bf16x8* lds = reinterpret_cast<bf16x8*>(smem);
   float* aux = reinterpret_cast<float*>(smem + (size_t)D.blob_frags * 1024);
-  stage_weights(J, D, lds, aux);
-  const DropCtx dc = drop_ctx(J, D);
+  float* spp = pp_lds_ptr(smem, D);
   const int wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   const int ntiles = (J.R + 31) >> 5;
   const int q = lane_id() >> 4, lane = lane_id();
   const int stride = gridDim.x * nwaves;
   int tile = blockIdx.x * nwaves + wave;
   TileIn<KS1> cur, nxt;
-  if (tile < ntiles) issue_tile<KS1, false>(J, tile, cur);
+  if (tile < ntiles) issue_tile<KS1, false>(J, tile, cur);   // in flight during the staging
+  stage_weights(J, D, lds, aux, spp);
+  const DropCtx dc = drop_ctx(J, D);
   for (; tile < ntiles; tile += stride) {
     if (tile + stride < ntiles) issue_tile<KS1, false>(J, tile + stride, nxt);
     bf16x8 xf[2][KS1];
-    const RowInfo ri = finish_tile<KS1>(J, D, tile, cur, xf);
+    const RowInfo ri = finish_tile<KS1>(J, D, tile, cur, xf, spp);
     if (J.do_sdf) {
       float w[2];
       DLAP_GLOBAL uint32_t* gout = J.gbits ? gp(J.gbits) + (size_t)tile * D.nl_sdf * 64 + lane : nullptr;
@@ -394,8 +404,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
   const MlpJob& J = jobs[blockIdx.y];
   bf16x8* lds = reinterpret_cast<bf16x8*>(smem);
   float* aux = reinterpret_cast<float*>(smem + (size_t)D.blob_frags * 1024);
-  stage_weights(J, D, lds, aux);
-  const DropCtx dc = drop_ctx(J, D);
+  float* spp = pp_lds_ptr(smem, D);
   const int lane = lane_id(), q = lane >> 4, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   const int ntiles = (J.R + 31) >> 5;
   const int slice = blockIdx.z;
@@ -431,6 +440,8 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
 #pragma unroll
     for (int j = 0; j < NL; ++j) gw_cur[j] = gp(J.gbits)[((size_t)tile * NL + j) * 64 + lane];
   }
+  stage_weights(J, D, lds, aux, spp);          // first tile's loads are already in flight
+  const DropCtx dc = drop_ctx(J, D);
   for (; tile < ntiles; tile += stride) {
     if (tile + stride < ntiles) {
       issue_tile<KS1, true>(J, tile + stride, nxt);
@@ -438,7 +449,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
       for (int j = 0; j < NL; ++j) gw_nxt[j] = gp(J.gbits)[((size_t)(tile + stride) * NL + j) * 64 + lane];
     }
     bf16x8 xf[2][KS1];
-    const RowInfo ri = finish_tile<KS1>(J, D, tile, cur, xf);
+    const RowInfo ri = finish_tile<KS1>(J, D, tile, cur, xf, spp);
     // ---- forward recompute from the stored gates, keep packed activations ----
     bf16x8 act[NL][2][2];
     uint32_t gates[NL][2];
@@ -587,8 +598,6 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
   const MlpJob& J = jobs[blockIdx.y];
   bf16x8* lds = reinterpret_cast<bf16x8*>(smem);
   float* aux = reinterpret_cast<float*>(smem + (size_t)D.blob_frags * 1024);
-  stage_weights(J, D, lds, aux);
-  const DropCtx dc = drop_ctx(J, D);
   const int lane = lane_id(), q = lane >> 4, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   const int ntiles = (J.R + 31) >> 5;
   const int slice = blockIdx.z;
@@ -624,6 +633,8 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
 #pragma unroll
     for (int j = 0; j + 1 < NLM; ++j) gw_cur[j] = gp(J.mgbits)[((size_t)tile * (NLM - 1) + j) * 64 + lane];
   }
+  stage_weights(J, D, lds, aux);
+  const DropCtx dc = drop_ctx(J, D);
   for (; tile < ntiles; tile += stride) {
     if (tile + stride < ntiles) {
       issue_tile<KS1, false>(J, tile + stride, nxt);
@@ -632,7 +643,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
         gw_nxt[j] = gp(J.mgbits)[((size_t)(tile + stride) * (NLM - 1) + j) * 64 + lane];
     }
     bf16x8 xf[2][KS1];
-    const RowInfo ri = finish_tile<KS1>(J, D, tile, cur, xf);
+    const RowInfo ri = finish_tile<KS1, false>(J, D, tile, cur, xf);   // moment tower: no per-period cols
     bf16x8 act[NLM][2][KSM];
     uint32_t gates[NLM][2];
     f32x4 a[2][WMB];
@@ -764,7 +775,9 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
 }
 
 // ---- host launchers -------------------------------------------------------------------
-size_t mlp_lds_bytes(const MlpDims& D) { return (size_t)D.blob_frags * 1024 + (size_t)D.aux_floats * 4; }
+size_t mlp_lds_bytes(const MlpDims& D) {
+  return (size_t)D.blob_frags * 1024 + (size_t)((D.aux_floats + 3) & ~3) * 4 + (size_t)D.pp_lds_floats * 4;
+}
 static size_t bwd_lds_bytes(const MlpDims& D, int slab_stride) {
   size_t a = mlp_lds_bytes(D), b = (size_t)slab_stride * 4;
   return a > b ? a : b;

@@ -8,7 +8,7 @@
 //   * inter-layer dropout on every layer output but the last (torch semantics), train only.
 //
 // Kernels
-//   k_proj      grid (ceil(T/4), jobs): the layer-0 input projection of every step
+//   k_proj      grid (ceil(T/16), jobs): the layer-0 input projection of every step
 //               xg[t] = W_ih x_t + b_ih + b_hh and the moment table
 //               abias[t][c] = W_m0[c, :M] . m_t + b_m0[c]  (zero-padded to 64 columns);
 //               the weights are staged in LDS, each thread owns one output for 4 periods.
@@ -19,6 +19,7 @@
 //               with v_readlane), then every thread reduces the weight gradients over t
 //               from LDS-staged dgates (thread per macro column: 4H FMAs per load).
 //               Phase 2 instead builds the moment layer-0 macro-column / bias gradients.
+#include <algorithm>
 #include <cstdlib>
 #include "common.h"
 #include "layout.h"
@@ -26,6 +27,12 @@
 #include "update.h"
 
 #define DLAP_MAX_M 1024
+
+// In-kernel phase timestamps (wall clock, 100 MHz) for profiling the serial kernels, read by
+// Engine.rnn_timestamps(). Slots: [0..3] k_lstm_gl train launch, [4..7] its eval launch (last
+// block = longest split), [8..12] k_lstm_bwd.
+__device__ long long g_rnn_ts[16];
+#define RNN_TS(slot, cond) do { if ((cond) && threadIdx.x == 0) g_rnn_ts[slot] = wall_clock64(); } while (0)
 
 // Fast activations (v_exp + v_rcp): |err| < 1e-6 relative in the ranges that matter; tanh
 // switches to its cubic Taylor form near 0 where 2*sigm(2x)-1 would cancel.
@@ -36,54 +43,66 @@ DLAP_DEV float ftanh(float x) {
 }
 
 // ------------------------------------------------------------------------ k_proj -------
-__global__ __launch_bounds__(256) void k_proj(const RnnJob* __restrict__ jobs,
-                                              const ModelDesc* __restrict__ md) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const RnnJob& J = jobs[blockIdx.y];
-  const int T = J.T, M = md->M;
-  const int t0 = blockIdx.x * 4;
-  if (t0 >= T) return;
+// xg[t] = W_ih x_t + b_ih + b_hh (layer-0 LSTM gates) and abias[t] = W_m0[:, :M] x_t + b_m0
+// (moment layer-0 per-period bias, zero-padded to 64): a [T x MP] . [MP x NP] fp32 GEMM on
+// the matrix cores. grid (ceil(T/16), NP/16, jobs), one wave per 16x16 output tile, K = 4 per
+// v_mfma_f32_16x16x4f32 (full fp32 products / accumulation). Operands come straight from
+// global memory (macro rows, and the k_pack-produced wproj [MP+1][NP] whose last row holds
+// the biases): all loads of a tile are independent, so the tile costs ~one memory round trip.
+//   A (16x4): lane l -> A[t = l&15][k = l>>4];  B (4x16): lane l -> B[k = l>>4][o = l&15]
+//   C (16x16): lane l -> C[t = 4*(l>>4) + r][o = l&15]
+__global__ __launch_bounds__(64) void k_proj(const RnnJob* __restrict__ jobs,
+                                             const ModelDesc* __restrict__ md) {
+  const RnnJob& J = jobs[blockIdx.z];
+  const int T = J.T, M = md->M, MP = md->proj_mp, NP = md->proj_np;
+  const int t0 = blockIdx.x * 16, o0 = blockIdx.y * 16;
   const int G4 = md->nrnn > 0 ? 4 * md->H : 0;
-  const int cm1 = J.abias ? md->m[0].out : 0;
-  const int nout = G4 + (J.abias ? 64 : 0);
-  float* x = sm;                 // [4][M]
-  float* w = sm + 4 * M;         // [nout][M]
-  const int nt = min(4, T - t0);
-  for (int i = threadIdx.x; i < 4 * M; i += 256) {
-    const int tl = i / M;
-    x[i] = tl < nt ? gp(J.macro)[(size_t)(t0 + tl) * M + (i - tl * M)] : 0.f;
+  if (t0 >= T) return;
+  if (o0 >= G4 && !J.abias) return;
+  const bool tsm = blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0;
+  RNN_TS(12, tsm);
+  const int l = threadIdx.x, n = l & 15, kq = l >> 4;
+  const int ta = min(t0 + n, T - 1);
+  const auto xrow = gp(J.macro) + (size_t)ta * M;
+  const auto wcol = gp(J.wproj) + o0 + n;
+  f32x4 acc = zero4();
+  // all operand loads of a K chunk are issued before the first MFMA consumes them: one
+  // memory round trip per PROJ_KC * 4 columns instead of one per unrolled group
+  constexpr int PROJ_KC = 48;
+  for (int kb = 0; kb < MP; kb += 4 * PROJ_KC) {
+    float a[PROJ_KC], b[PROJ_KC];
+#pragma unroll
+    for (int s = 0; s < PROJ_KC; ++s) {
+      const int m = kb + 4 * s + kq;
+      const float x = xrow[m < M ? m : M - 1];
+      const float w = wcol[(size_t)(m < MP ? m : MP - 1) * NP];
+      a[s] = m < M ? x : 0.f;
+      b[s] = m < MP ? w : 0.f;
+    }
+#pragma unroll
+    for (int s = 0; s < PROJ_KC; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
   }
-  const auto params = gp(J.params);
-  const auto Wih = params + md->lstm_w_ih[0];
-  const PackLayer& L0 = md->m[0];
-  for (int i = threadIdx.x; i < nout * M; i += 256) {
-    const int o = i / M, m = i - o * M;
-    float v = 0.f;
-    if (o < G4) v = Wih[(size_t)o * M + m];
-    else if (o - G4 < cm1) v = params[L0.w_off + (size_t)(o - G4) * L0.ld + m];
-    w[i] = v;
+  const float bias = wcol[(size_t)MP * NP];
+  const int o = o0 + n;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const int t = t0 + 4 * kq + r;
+    if (t >= T) break;
+    const float v = acc[r] + bias;
+    if (o < G4) gp(J.xg)[(size_t)t * G4 + o] = v;
+    else if (o - G4 < 64) gp(J.abias)[t * 64 + (o - G4)] = v;
   }
-  __syncthreads();
-  const int o = threadIdx.x;
-  if (o >= nout) return;
-  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
-  const float* wr = w + (size_t)o * M;
-#pragma unroll 4
-  for (int m = 0; m < M; ++m) {
-    const float wv = wr[m];
-    s0 += wv * x[m]; s1 += wv * x[M + m]; s2 += wv * x[2 * M + m]; s3 += wv * x[3 * M + m];
-  }
-  float b = 0.f;
-  if (o < G4) b = params[md->lstm_b_ih[0] + o] + params[md->lstm_b_hh[0] + o];
-  else if (o - G4 < cm1) b = params[L0.b_off + o - G4];
-  else b = 0.f;
-  const float s[4] = {s0, s1, s2, s3};
-  for (int tl = 0; tl < nt; ++tl) {
-    const int t = t0 + tl;
-    if (o < G4) gp(J.xg)[(size_t)t * G4 + o] = s[tl] + b;
-    else gp(J.abias)[t * 64 + (o - G4)] = (o - G4 < cm1) ? s[tl] + b : 0.f;
-  }
+  RNN_TS(14, tsm);
 }
+
+
+// BPTT coefficients of one (t, unit), computed by k_lstm_bwd in a parallel pre-pass from the
+// saved gates / cells, so that the serial backward recurrence is only
+//   dh = dout + dh_next; dc = dh*A + dc_next; d_q = dc*B_q (d_o = dh*B_o); dc_next = dc*F;
+//   dh_next = W_hh^T d.
+// Layout [t][6][H]: A = o (1 - tanh(c)^2), Bi = g i (1 - i), Bf = c_prev f (1 - f),
+// Bg = i (1 - g^2), Bo = tanh(c) o (1 - o), F = f.
+#define LSTM_NCOEF 6
 
 // ------------------------------------------------------------------------ k_lstm -------
 // STAGE: layer-0 input projections staged in LDS (T*4H <= 12288). The layer-0 and deeper
@@ -144,8 +163,8 @@ __global__ __launch_bounds__(64) void k_lstm(const RnnJob* __restrict__ jobs,
       __syncthreads();
     }
     const auto hout = save ? gp(J.sh) + (size_t)l * T * H : gp(J.out);
-    const auto sc = gp(J.sc) + (size_t)l * T * H;
     const auto sg = gp(J.sg) + (size_t)l * T * G4;
+    const auto sc = gp(J.sc) + (size_t)l * T * H;
     float h = 0.f, c = 0.f;
     auto cell = [&](int t, const float (&p)[4]) {
       const float gi = sigm(p[0]), gf = sigm(p[1]), gg = ftanh(p[2]), go = sigm(p[3]);
@@ -245,6 +264,9 @@ __global__ __launch_bounds__(64) void k_lstm_gl(const RnnJob* __restrict__ jobs,
   const auto params = gp(J.params);
   const auto xg = gp(J.xg);
   const bool save = J.sc != nullptr;
+  const int tsb = save ? 0 : 4;
+  const bool tsm = save || blockIdx.x == gridDim.x - 1;
+  RNN_TS(tsb + 0, tsm);
   for (int l = 0; l < nrnn; ++l) {
     float whh[HM], wih[HM];
 #pragma unroll
@@ -262,9 +284,12 @@ __global__ __launch_bounds__(64) void k_lstm_gl(const RnnJob* __restrict__ jobs,
       for (int i = L; i < T * G4; i += 64) sm[i] = xg[i];
       __syncthreads();
     }
+    if (l == 0) RNN_TS(tsb + 1, tsm);
     const auto hout = save ? gp(J.sh) + (size_t)l * T * H : gp(J.out);
-    const auto sc = gp(J.sc) + (size_t)l * T * H;
     const auto sg = gp(J.sg) + (size_t)l * T * G4;
+    const auto sc = gp(J.sc) + (size_t)l * T * H;
+    const auto out = gp(J.out);
+    const bool last = l + 1 == nrnn;
     float h = 0.f, c = 0.f;
     auto cell = [&](int t, float pre) {
       pre += bcast_dot<HM>(whh, h);
@@ -274,12 +299,14 @@ __global__ __launch_bounds__(64) void k_lstm_gl(const RnnJob* __restrict__ jobs,
       const float gg = gl_gather<HM, DPPG>(y, 2 * H, 2);
       const float go = gl_gather<HM, DPPG>(y, 3 * H, 3);
       c = gf * c + y * gg;                 // y = i on the unit lanes
-      const float hn = go * ftanh(c);
-      h = ul ? hn : 0.f;
+      h = ul ? go * ftanh(c) : 0.f;
       if (save && gl) sg[(size_t)t * G4 + L] = y;
       if (ul) {
         hout[(size_t)t * H + L] = h;
-        if (save) sc[(size_t)t * H + L] = c;
+        if (save) {
+          sc[(size_t)t * H + L] = c;
+          if (last) out[(size_t)t * H + L] = h;      // the tower input, no copy pass
+        }
       }
     };
     if (l == 0) {
@@ -307,25 +334,21 @@ __global__ __launch_bounds__(64) void k_lstm_gl(const RnnJob* __restrict__ jobs,
         cell(t, pre);
       }
     }
+    if (l == 0) RNN_TS(tsb + 2, tsm);
     __threadfence_block();
     if (l + 1 < nrnn) {
       const auto xin = gp(J.xin);
       for (int i = L; i < T * H; i += 64) xin[i] = hout[i];
       __threadfence_block();
-    } else if (save) {
-      const auto out = gp(J.out);
-      for (int i = L; i < T * H; i += 64) out[i] = hout[i];
     }
   }
+  RNN_TS(tsb + 3, tsm);
 }
 
 void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* md, const ModelDesc& mh,
                      hipStream_t st) {
   {
-    const int nout = (mh.nrnn > 0 ? 4 * mh.H : 0) + 64;
-    const size_t sh = (size_t)(4 * mh.M + nout * mh.M + 4) * sizeof(float);
-    if (sh > 160 * 1024) dlap_throw_hip(hipErrorInvalidValue, "k_proj: macro dim too large", __FILE__, __LINE__);
-    hipLaunchKernelGGL(k_proj, dim3((tmax + 3) / 4, njobs), dim3(256), sh, st, jobs, md);
+    hipLaunchKernelGGL(k_proj, dim3((tmax + 15) / 16, mh.proj_np / 16, njobs), dim3(64), 0, st, jobs, md);
     HIP_OK(hipGetLastError());
   }
   if (mh.nrnn > 0) {
@@ -370,24 +393,37 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
   const uint32_t step = (uint32_t)*gp(J.drop_step);
   const auto params = gp(J.params);
   const auto grads = gp(J.grads);
-  float* s_g = sm;                    // [T][4H] saved gates
-  float* s_c = s_g + T * G4;          // [T][H]  cells
-  float* s_h = s_c + T * H;           // [T][H]  layer outputs
-  float* s_d = s_h + T * H;           // [T][H]  incoming gradient
-  float* dgs = s_d + T * H;           // [T][4H] gate pre-activation gradients
+  const bool tsm = blockIdx.x == 0;
+  RNN_TS(8, tsm);
+  float* s_cf = sm;                           // [T][6][H] BPTT coefficients (pre-pass)
+  float* s_h = s_cf + T * LSTM_NCOEF * H;      // [T][H]  layer outputs
+  float* s_d = s_h + T * H;                    // [T][H]  incoming gradient
+  float* dgs = s_d + T * H;                    // [T][4H] gate pre-activation gradients
   for (int l = md->nrnn - 1; l >= 0; --l) {
     const auto dout = l == md->nrnn - 1 ? gp(J.dpp) : gp(J.dx);
-    const auto sg = gp(J.sg) + (size_t)l * T * G4;
+    const auto sgg = gp(J.sg) + (size_t)l * T * G4;
     const auto scg = gp(J.sc) + (size_t)l * T * H;
     const auto shg = gp(J.sh) + (size_t)l * T * H;
     __syncthreads();
-    for (int i = threadIdx.x; i < T * G4; i += 256) s_g[i] = sg[i];
+    // parallel pre-pass: everything of the backward step that does not depend on dh_next
     for (int i = threadIdx.x; i < T * H; i += 256) {
-      s_c[i] = scg[i];
+      const int t = i / H, k = i - t * H;
+      const float gi = sgg[(size_t)t * G4 + k], gf = sgg[(size_t)t * G4 + H + k];
+      const float gg = sgg[(size_t)t * G4 + 2 * H + k], go = sgg[(size_t)t * G4 + 3 * H + k];
+      const float c = scg[i], cp = t > 0 ? scg[i - H] : 0.f;
+      const float tc = ftanh(c);
+      float* q = s_cf + t * LSTM_NCOEF * H + k;
+      q[0 * H] = go * (1.f - tc * tc);
+      q[1 * H] = gg * gi * (1.f - gi);
+      q[2 * H] = cp * gf * (1.f - gf);
+      q[3 * H] = gi * (1.f - gg * gg);
+      q[4 * H] = tc * go * (1.f - go);
+      q[5 * H] = gf;
       s_h[i] = shg[i];
       s_d[i] = dout[i];
     }
     __syncthreads();
+    if (l == 0) RNN_TS(9, tsm);
     if (wave == 0) {
       const int k = lane < H ? lane : 0;
       const bool act = lane < H;
@@ -401,28 +437,21 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
           wt[q][j] = j < H ? w : 0.f;
         }
       float dh_next = 0.f, dc_next = 0.f;
-      // step inputs of t (prefetched one step ahead: LDS latency off the serial chain)
       auto fetch = [&](int t, float (&v)[7]) {
-        const float* g = s_g + t * G4;
-        v[0] = g[k]; v[1] = g[H + k]; v[2] = g[2 * H + k]; v[3] = g[3 * H + k];
-        v[4] = s_c[t * H + k];
-        v[5] = t > 0 ? s_c[(t - 1) * H + k] : 0.f;
+        const float* q = s_cf + t * LSTM_NCOEF * H + k;
+#pragma unroll
+        for (int e = 0; e < LSTM_NCOEF; ++e) v[e] = q[e * H];
         v[6] = act ? s_d[t * H + k] : 0.f;
       };
-      float cur[7], nxt[7];
-      fetch(T - 1, cur);
-      for (int t = T - 1; t >= 0; --t) {
-        fetch(t > 0 ? t - 1 : 0, nxt);
-        const float gi = cur[0], gf = cur[1], gg = cur[2], go = cur[3], c = cur[4], cp = cur[5];
-        const float dh = cur[6] + dh_next;
-        const float tc = ftanh(c);
-        const float dc = dh * go * (1.f - tc * tc) + dc_next;
+      auto step = [&](int t, const float (&v)[7]) {
+        const float dh = v[6] + dh_next;
+        const float dc = dh * v[0] + dc_next;
         float d[4];
-        d[0] = dc * gg * gi * (1.f - gi);
-        d[1] = dc * cp * gf * (1.f - gf);
-        d[2] = dc * gi * (1.f - gg * gg);
-        d[3] = dh * tc * go * (1.f - go);
-        dc_next = dc * gf;
+        d[0] = dc * v[1];
+        d[1] = dc * v[2];
+        d[2] = dc * v[3];
+        d[3] = dh * v[4];
+        dc_next = dc * v[5];
         if (act) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) dgs[t * G4 + q * H + k] = d[q];
@@ -430,11 +459,37 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
         const float s = (bcast_dot<HM>(wt[0], d[0]) + bcast_dot<HM>(wt[1], d[1])) +
                         (bcast_dot<HM>(wt[2], d[2]) + bcast_dot<HM>(wt[3], d[3]));
         dh_next = act ? s : 0.f;
+      };
+      // blocks of U steps; the next block's LDS operands are loaded a whole block ahead
+      constexpr int U = 8;
+      const int nfull = T / U;
+      int t = T - 1;
+      for (; t >= nfull * U; --t) {              // top remainder, one at a time
+        float v[7];
+        fetch(t, v);
+        step(t, v);
+      }
+      float A[U][7], B[U][7];
+      auto load_block = [&](int t0, float (&buf)[U][7]) {
 #pragma unroll
-        for (int e = 0; e < 7; ++e) cur[e] = nxt[e];
+        for (int u = 0; u < U; ++u) fetch(t0 - u, buf[u]);
+      };
+      if (nfull > 0) load_block(t, A);
+      for (int b = 0; b < nfull; b += 2) {
+        if (b + 1 < nfull) load_block(t - U, B);
+#pragma unroll
+        for (int u = 0; u < U; ++u) step(t - u, A[u]);
+        t -= U;
+        if (b + 1 < nfull) {
+          if (b + 2 < nfull) load_block(t - U, A);
+#pragma unroll
+          for (int u = 0; u < U; ++u) step(t - u, B[u]);
+          t -= U;
+        }
       }
     }
     __syncthreads();
+    if (l == 0) RNN_TS(10, tsm);
     if (l == 0) {
       const auto dg = gp(J.dg);
       for (int i = threadIdx.x; i < T * G4; i += 256) dg[i] = dgs[i];   // for k_wgrad
@@ -477,6 +532,8 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
       __threadfence_block();
     }
   }
+  __syncthreads();
+  RNN_TS(11, tsm);
 }
 
 // --------------------------------------------------------------------------- k_wgrad ---
@@ -531,7 +588,7 @@ __global__ __launch_bounds__(256) void k_wgrad(const UpdJob* __restrict__ jobs,
 void launch_lstm_bwd(const UpdJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
                      int T, int phase, hipStream_t st) {
   if (phase != 2 && mh.nrnn > 0) {
-    const size_t sh = (size_t)T * (8 * mh.H + 3 * mh.H) * sizeof(float);
+    const size_t sh = (size_t)T * (LSTM_NCOEF + 2 + 4) * mh.H * sizeof(float);   // coef, h, d, dgates
     if (sh > 160 * 1024) dlap_throw_hip(hipErrorInvalidValue, "lstm_bwd: T*H too large for LDS", __FILE__, __LINE__);
     if (mh.H <= 4) hipLaunchKernelGGL((k_lstm_bwd<4>), dim3(njobs), dim3(256), sh, st, jobs, md);
     else if (mh.H <= 8) hipLaunchKernelGGL((k_lstm_bwd<8>), dim3(njobs), dim3(256), sh, st, jobs, md);
@@ -547,4 +604,10 @@ void launch_lstm_bwd(const UpdJob* jobs, int njobs, const ModelDesc* md, const M
   else if (G <= 32) hipLaunchKernelGGL((k_wgrad<32>), grid, dim3(256), 0, st, jobs, md, phase);
   else hipLaunchKernelGGL((k_wgrad<64>), grid, dim3(256), 0, st, jobs, md, phase);
   HIP_OK(hipGetLastError());
+}
+
+std::vector<long long> rnn_timestamps() {
+  std::vector<long long> v(16);
+  HIP_OK(hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(g_rnn_ts), sizeof(long long) * 16));
+  return v;
 }

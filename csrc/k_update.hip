@@ -22,35 +22,39 @@ __global__ __launch_bounds__(256) void k_finalize(const FinJob* __restrict__ job
   const FinJob& J = jobs[blockIdx.y];
   const bool mom = phase == 2;
   const int ntile = mom ? md->ntile_m : md->ntile_s;
-  const int nb_tiles = ntile * 16;
-  const int nb_extra = (SLAB_EXTRA + 255) / 256;
+  const int tps = mom ? md->tps_m : md->tps_s;
+  const int nb_tiles = ntile * 64;                    // 64 elements per block
+  const int nb_extra = (SLAB_EXTRA + 63) / 64;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   int b = blockIdx.x;
+  // slab sums: lane = element, the 4 waves split the slabs (each sums its quarter in order,
+  // 16 independent loads in flight), then a fixed-order LDS combine
+  auto slab_sum = [&](const float* src) {
+    const auto s0 = gp(src);
+    float acc = 0.f;
+#pragma unroll 16
+    for (int k = wave; k < J.nslab; k += 4) acc += s0[(size_t)k * slab_stride];
+    red[wave][lane] = acc;
+    __syncthreads();
+    return red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+  };
   if (b < nb_tiles) {
-    const int ti = b >> 4, e = ((b & 15) << 8) + threadIdx.x;
+    const int ti = b >> 6, e = ((b & 63) << 6) + lane;
     const GradTile& G = mom ? md->tile_m[ti] : md->tile_s[ti];
     const int o = e >> 6, i = (e & 63) + 64 * G.chunk;
-    if (o >= G.out || i >= G.in) return;
-    // position of this tile inside its slice's slab
-    const int tps = mom ? md->tps_m : md->tps_s;
     const int tpos = ti - G.slice * tps;
-    const float* src = gp(J.slab) + (size_t)G.slice * J.nslab * slab_stride + tpos * 4096 + e;
-    float s = 0.f;
-#pragma unroll 16
-    for (int k = 0; k < J.nslab; ++k) s += src[(size_t)k * slab_stride];
-    gp(J.grads)[G.w_off + o * G.ld + G.col0 + i] = s;
+    const float v = slab_sum(J.slab + (size_t)G.slice * J.nslab * slab_stride + tpos * 4096 + e);
+    if (wave == 0 && o < G.out && i < G.in) gp(J.grads)[G.w_off + o * G.ld + G.col0 + i] = v;
     return;
   }
   b -= nb_tiles;
   if (b < nb_extra) {
-    const int e = b * 256 + threadIdx.x;
-    if (e >= SLAB_EXTRA) return;
-    const int dst = mom ? md->extra_m[e] : md->extra_s[e];
-    if (dst < 0) return;
-    const float* src = gp(J.slab) + (mom ? md->tps_m : md->tps_s) * 4096 + e;   // slice-0 slabs
-    float s = 0.f;
-#pragma unroll 16
-    for (int k = 0; k < J.nslab; ++k) s += src[(size_t)k * slab_stride];
-    gp(J.grads)[dst] = s;
+    const int e = b * 64 + lane;
+    const int ec = e < SLAB_EXTRA ? e : SLAB_EXTRA - 1;
+    const float v = slab_sum(J.slab + tps * 4096 + ec);     // slice-0 slabs
+    const int dst = e < SLAB_EXTRA ? (mom ? md->extra_m[e] : md->extra_s[e]) : -1;
+    if (wave == 0 && dst >= 0) gp(J.grads)[dst] = v;
     return;
   }
   b -= nb_extra;
@@ -58,20 +62,22 @@ __global__ __launch_bounds__(256) void k_finalize(const FinJob* __restrict__ job
   const int D = mom ? 64 : (md->nrnn > 0 ? md->Dm : 0);
   const int t = b;
   if (D == 0 || t >= J.T) return;
-  __shared__ float red[256];
+  __shared__ float seg[256];
   int Dp = 1;
   while (Dp < D) Dp <<= 1;
   const int nrg = 256 / Dp, d = threadIdx.x % Dp, rg = threadIdx.x / Dp;
-  const float* src = mom ? gp(J.v) : gp(J.u);
+  const auto src = gp(mom ? J.v : J.u);
   const int r0 = gp(J.row_ptr)[t], r1 = gp(J.row_ptr)[t + 1];
   float s = 0.f;
-  if (d < D)
+  if (d < D) {
+#pragma unroll 8
     for (int r = r0 + rg; r < r1; r += nrg) s += src[(size_t)r * D + d];
-  red[threadIdx.x] = s;
+  }
+  seg[threadIdx.x] = s;
   __syncthreads();
   if (rg == 0 && d < D) {
     float tot = 0.f;
-    for (int g = 0; g < nrg; ++g) tot += red[g * Dp + d];
+    for (int g = 0; g < nrg; ++g) tot += seg[g * Dp + d];
     if (mom) gp(J.dab)[t * 64 + d] = tot;
     else gp(J.dpp)[t * D + d] = tot;
   }
@@ -82,7 +88,7 @@ void launch_finalize(const FinJob* jobs, int njobs, const ModelDesc* md, const M
   const bool mom = phase == 2;
   const int ntile = mom ? mh.ntile_m : mh.ntile_s;
   const int D = mom ? 64 : (mh.nrnn > 0 ? mh.Dm : 0);
-  const int nb = ntile * 16 + (SLAB_EXTRA + 255) / 256 + (D > 0 ? tmax : 0);
+  const int nb = ntile * 64 + (SLAB_EXTRA + 63) / 64 + (D > 0 ? tmax : 0);
   hipLaunchKernelGGL(k_finalize, dim3(nb, njobs), dim3(256), 0, st, jobs, md, phase, slab_stride);
   HIP_OK(hipGetLastError());
 }
@@ -162,48 +168,52 @@ DLAP_DEV float pack_aux_elem(const ModelDesc* __restrict__ md, PP P, int e) {
   return val;
 }
 
+// Input-projection matrix for k_proj (ModelDesc::proj_mp): transposed, zero padded, biases in
+// the last row, so k_proj can stage it with plain coalesced 16-byte loads.
+template <typename PP>
+DLAP_DEV float pack_proj_elem(const ModelDesc* __restrict__ md, PP P, int f) {
+  const int NP = md->proj_np, M = md->M;
+  const int m = f / NP, o = f - m * NP;
+  const int G4 = md->nrnn > 0 ? 4 * md->H : 0;
+  const PackLayer& L0 = md->m[0];
+  const int om = o - G4;
+  if (m == md->proj_mp) {                       // bias row
+    if (o < G4) return P[md->lstm_b_ih[0] + o] + P[md->lstm_b_hh[0] + o];
+    return om < md->cm1 ? P[L0.b_off + om] : 0.f;
+  }
+  if (m >= M) return 0.f;
+  if (o < G4) return P[md->lstm_w_ih[0] + o * M + m];
+  return om < md->cm1 ? P[L0.w_off + om * L0.ld + m] : 0.f;
+}
+
 // Re-pack the bf16 MFMA weight fragments + fp32 aux of every model after an update.
-// grid (blocks, models); each block stages the parameter vector in LDS once (the packing
-// gathers are scattered) and writes a contiguous range of packed elements.
+// grid (ceil(elements / 256), models): one packed element per thread, gathered straight from
+// the (L2-resident) parameter vector -- a single memory round trip per launch.
 // Block 0 also advances the step counters (after every Adam block has read them).
-#define PACK_EPB 4096
-#define PACK_LDS_FLOATS 16384
 __global__ __launch_bounds__(256) void k_pack(const UpdJob* __restrict__ jobs,
                                               const ModelDesc* __restrict__ md, int bump) {
   const UpdJob& J = jobs[blockIdx.y];
-  extern __shared__ float sp[];
-  const int P = md->P;
-  const bool stage = P <= PACK_LDS_FLOATS;   // wave-uniform
-  if (stage) {
-    for (int i = threadIdx.x; i < P; i += 256) sp[i] = gp(J.params)[i];
-    __syncthreads();
-  }
-  const int nel = md->md.blob_frags * 512, total = nel + md->md.aux_floats;
-  const int e0 = blockIdx.x * PACK_EPB, e1 = min(e0 + PACK_EPB, total);
-  const auto out = (DLAP_GLOBAL __bf16*)(J.blob);
-  auto run = [&](auto src) {   // LDS or global source: one code path per address space
-    for (int e = e0 + threadIdx.x; e < e1; e += 256) {
-      if (e < nel) out[e] = (__bf16)pack_blob_elem(md, src, e);
-      else gp(J.aux)[e - nel] = pack_aux_elem(md, src, e - nel);
-    }
-  };
-  if (stage) run(static_cast<const float*>(sp));
-  else run(gp(static_cast<const float*>(J.params)));
+  const int nel = md->md.blob_frags * 512, naux = nel + md->md.aux_floats;
+  const int NP = md->proj_np, MP = md->proj_mp;
+  const int total = naux + (MP + 1) * NP;
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const auto src = gp(static_cast<const float*>(J.params));
+  if (e < nel) ((DLAP_GLOBAL __bf16*)(J.blob))[e] = (__bf16)pack_blob_elem(md, src, e);
+  else if (e < naux) gp(J.aux)[e - nel] = pack_aux_elem(md, src, e - nel);
+  else if (e < total) gp(J.wproj)[e - naux] = pack_proj_elem(md, src, e - naux);
   if (bump && blockIdx.x == 0 && threadIdx.x == 0) {
     gp(J.adam_step)[bump - 1] = gp(J.adam_step)[bump - 1] + 1;
     gp(J.drop_step)[0] = gp(J.drop_step)[0] + 1;
   }
 }
 
-static size_t pack_lds(const ModelDesc& mh) { return mh.P <= PACK_LDS_FLOATS ? (size_t)mh.P * 4 : 0; }
 static int pack_blocks_of(const ModelDesc& mh) {
-  return (mh.md.blob_frags * 512 + mh.md.aux_floats + PACK_EPB - 1) / PACK_EPB;
+  return (mh.md.blob_frags * 512 + mh.md.aux_floats + (mh.proj_mp + 1) * mh.proj_np + 255) / 256;
 }
 
 void launch_pack(float* const*, const UpdJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
                  hipStream_t st) {
-  hipLaunchKernelGGL(k_pack, dim3(pack_blocks_of(mh), njobs), dim3(256), pack_lds(mh), st, jobs,
-                     md, 0);
+  hipLaunchKernelGGL(k_pack, dim3(pack_blocks_of(mh), njobs), dim3(256), 0, st, jobs, md, 0);
   HIP_OK(hipGetLastError());
 }
 
@@ -220,7 +230,7 @@ __global__ __launch_bounds__(256) void k_adam(const UpdJob* __restrict__ jobs,
   const int p0 = mom ? md->P_sdf : 0, p1 = mom ? md->P : md->P_sdf;
   const float* __restrict__ grads = gp(J.grads);
   float ss = 0.f;
-#pragma unroll 4
+#pragma unroll 16
   for (int i = p0 + threadIdx.x; i < p1; i += 256) { const float g = grads[i]; ss += g * g; }
   ss = block_sum<256>(ss, red);
   const float norm = sqrtf(ss);
@@ -258,7 +268,7 @@ void launch_update(const UpdJob* jobs, int njobs, const ModelDesc* md, const Mod
   hipLaunchKernelGGL(k_adam, dim3((n + ADAM_PB - 1) / ADAM_PB, njobs), dim3(256), 0, st, jobs, md, phase,
                      lr);
   HIP_OK(hipGetLastError());
-  hipLaunchKernelGGL(k_pack, dim3(pack_blocks_of(mh), njobs), dim3(256), pack_lds(mh), st, jobs, md,
+  hipLaunchKernelGGL(k_pack, dim3(pack_blocks_of(mh), njobs), dim3(256), 0, st, jobs, md,
                      phase == 2 ? 2 : 1);
   HIP_OK(hipGetLastError());
 }

@@ -23,7 +23,7 @@ struct MlpJob {
                           //   [tile][layer][lane] = gate(b=0) | gate(b=1) << 16
   uint32_t* mgbits;       // same for the moment tower's hidden layers (phase 2)
   const int* step;        // device step counter (dropout stream)
-  int R, N;
+  int R, N, T;
   unsigned seed;
   int train;              // dropout active
   int do_sdf, do_mom;     // fwd: towers to evaluate
@@ -42,6 +42,7 @@ struct MlpDims {
   int a_sb, a_wo, a_bo, a_pp, a_mb;   // aux offsets: SDF biases [nl][64], out row [64], out
                                       // bias, W0 per-period cols [Dm][64], moment biases [nl][64]
   int blob_frags, aux_floats;
+  int pp_lds_floats;             // >0: per-period inputs [T][Dm] staged in LDS (this many floats)
 };
 
 #define SLAB_EXTRA (DLAP_MAXL * 64 + 64 + 64)

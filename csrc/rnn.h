@@ -1,16 +1,18 @@
 // Job record of the LSTM / prologue kernel (k_rnn.hip).
 #pragma once
+#include <vector>
 #include "common.h"
 
 struct ModelDesc;
 
 struct RnnJob {
   const float* params;   // flat parameters of this job's model
+  const float* wproj;    // packed input-projection matrix (see ModelDesc::proj_mp)
   const float* macro;    // [T][M] standardised macro series of the split
   int T;
   float* out;            // [T][H] last-layer LSTM output (the SDF per-period inputs)
   float* sg;             // train: saved post-activation gates [nrnn][T][4H] (else nullptr)
-  float* sc;             // train: saved cell states [nrnn][T][H]
+  float* sc;             // train: saved cells [nrnn][T][H] (non-null = save for the backward)
   float* sh;             // train: saved layer outputs [nrnn][T][H]
   float* xg;             // scratch [T][4H]
   float* xin;            // scratch [T][H]
@@ -22,3 +24,5 @@ struct RnnJob {
 
 void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* md, const ModelDesc& mh,
                      hipStream_t st);
+
+std::vector<long long> rnn_timestamps();

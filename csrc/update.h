@@ -26,9 +26,10 @@ struct UpdJob {            // one model
   float* gnorm;            // [1] pre-clip gradient norm of the step
   bf16x8* blob;
   float* aux;
+  float* wproj;            // packed input-projection matrix (written by k_pack)
   const float* dpp;        // [T][Dm] d(LSTM output)
   const float* macro;      // [T][M] train macro series
-  const float* sg;         // [nrnn][T][4H] saved gates
+  const float* sg;         // [nrnn][T][4H] saved post-activation gates
   const float* sc;         // [nrnn][T][H]  saved cells
   const float* sh;         // [nrnn][T][H]  saved layer outputs
   float* dg;               // scratch [T][4H]

@@ -1,0 +1,42 @@
+"""In-kernel phase timing of the serial LSTM kernels at the bench config (GPU).
+
+Prints, for the last launch of each kernel: staging / recurrence / tail durations in us
+(wall_clock64 at 100 MHz), with the eval branch pipelined or not.
+"""
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+import bench  # noqa: E402
+from deeplearninginassetpricing_paperreplication_amd.config import default_cli_config  # noqa: E402
+from deeplearninginassetpricing_paperreplication_amd.engine.runner import GANEngine  # noqa: E402
+from deeplearninginassetpricing_paperreplication_amd.models.gan import AssetPricingGAN  # noqa: E402
+from deeplearninginassetpricing_paperreplication_amd.ops import native  # noqa: E402
+
+
+def main():
+    tr, va, te = bench.make_panel(seed=0, device="cuda")
+    cfg = default_cli_config(bench.BENCH["M"], bench.BENCH["F"])
+    eng = GANEngine(AssetPricingGAN(cfg).spec, 1, max_epochs=64)
+    eng.set_data(tr, va, te)
+    torch.manual_seed(0)
+    eng.set_model(0, AssetPricingGAN(cfg), 1)
+    mod = native.load()
+    for pipe in (False, True):
+        eng.eng.set_pipeline(pipe)
+        eng.eng.begin_phase(3)
+        eng.run(3, 6, 1e-3, 1, 1.0, True)
+        eng.eng.sync()
+        ts = np.array(mod.Engine.rnn_timestamps(), dtype=np.int64)
+        us = lambda a, b: (ts[b] - ts[a]) / 100.0  # noqa: E731
+        print(f"pipeline={pipe}")
+        print(f"  k_lstm_gl train: stage {us(0, 1):7.1f}  recur {us(1, 2):7.1f}  tail {us(2, 3):7.1f}  total {us(0, 3):7.1f}")
+        print(f"  k_lstm_gl eval : stage {us(4, 5):7.1f}  recur {us(5, 6):7.1f}  tail {us(6, 7):7.1f}  total {us(4, 7):7.1f}")
+        print(f"  k_lstm_bwd     : stage {us(8, 9):7.1f}  bptt  {us(9, 10):7.1f}  grads {us(10, 11):7.1f} total {us(8, 11):7.1f}")
+        print(f"  k_proj tile0   : total {us(12, 14):7.1f}")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,11 @@
+#!/bin/bash
+# Two PMC passes (kernel-trace only, no sys/runtime trace) over a short sequential bench run.
+# Usage on the GPU box: bash tools/pmc_round.sh <tag>   -> gpurun_out/<tag>_pmc{1,2}/
+tag=${1:-pmc}
+cd /tmp || exit 1
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+DLAP_PIPELINE=0 timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM \
+  --output-format csv -d $R/gpurun_out/${tag}_pmc1 -o run -- python3 $R/bench.py --steps 21 --warmup 3 || exit $?
+DLAP_PIPELINE=0 timeout -k 10 300 rocprofv3 --kernel-trace --pmc SQ_WAVES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_LDS_BANK_CONFLICT SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_BRANCH \
+  --output-format csv -d $R/gpurun_out/${tag}_pmc2 -o run -- python3 $R/bench.py --steps 21 --warmup 3
