@@ -97,10 +97,20 @@ class Engine {
          std::vector<int> mom_hidden, int K, float dropout, bool normalize_w, bool weighted,
          float residual, int G, int max_epochs)
       : G_(G), max_epochs_(max_epochs) {
-    HIP_OK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
-    HIP_OK(hipStreamCreateWithFlags(&st2_, hipStreamNonBlocking));
+    unroll_ = std::max(1, env_int("DLAP_UNROLL", 4));
+    prio_ = env_int("DLAP_PRIO", 0) != 0;
+    if (prio_) {   // the training chain (critical path) ahead of the evaluation branch
+      int lo = 0, hi = 0;
+      HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      HIP_OK(hipStreamCreateWithPriority(&st_, hipStreamNonBlocking, hi));
+      HIP_OK(hipStreamCreateWithPriority(&st2_, hipStreamNonBlocking, lo));
+    } else {
+      HIP_OK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+      HIP_OK(hipStreamCreateWithFlags(&st2_, hipStreamNonBlocking));
+    }
     HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_mid_, hipEventDisableTiming));
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
                residual);
     d_desc_.alloc(sizeof(ModelDesc));
@@ -122,6 +132,7 @@ class Engine {
     for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
     if (ev_fork_) (void)hipEventDestroy(ev_fork_);
     if (ev_join_) (void)hipEventDestroy(ev_join_);
+    if (ev_mid_) (void)hipEventDestroy(ev_mid_);
     if (st2_) (void)hipStreamDestroy(st2_);
     if (st_) (void)hipStreamDestroy(st_);
   }
@@ -306,8 +317,18 @@ class Engine {
                                     [&] { enqueue_pipe(phase, lr, ignore_epoch, sel); });
     hipGraphExec_t tail = graph_for(graph_key(phase, lr, ignore_epoch, sel, 3),
                                     [&] { enqueue_tail(phase, ignore_epoch, sel); });
+    // U pipelined epochs per graph launch: no launch gap between the epochs of one graph
+    const int U = unroll_;
+    hipGraphExec_t bodyU = nullptr;
+    if (U > 1 && n - 1 >= U)
+      bodyU = graph_for(graph_key(phase, lr, ignore_epoch, sel, 100 + U), [&] {
+        for (int u = 0; u < U; ++u) enqueue_pipe(phase, lr, ignore_epoch, sel);
+      });
     HIP_OK(hipGraphLaunch(head, st_));
-    for (int e = 1; e < n; ++e) HIP_OK(hipGraphLaunch(body, st_));
+    int e = 1;
+    if (bodyU)
+      for (; e + U <= n; e += U) HIP_OK(hipGraphLaunch(bodyU, st_));
+    for (; e < n; ++e) HIP_OK(hipGraphLaunch(body, st_));
     HIP_OK(hipGraphLaunch(tail, st_));
   }
   void set_pipeline(bool on) { pipeline_ = on; }
@@ -353,8 +374,10 @@ class Engine {
  private:
   int G_, max_epochs_;
   hipStream_t st_ = nullptr;
+  int unroll_ = 4;                           // pipelined epochs per graph launch (DLAP_UNROLL)
+  bool prio_ = false;                        // stream/node priorities (DLAP_PRIO)
   hipStream_t st2_ = nullptr;                // evaluation branch of the pipelined epoch graph
-  hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr;
+  hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr, ev_mid_ = nullptr;
   ModelDesc md_{};
   DevBuf<char> d_desc_;
   SplitDev splits_[3];
@@ -538,7 +561,7 @@ class Engine {
         W.dpp.alloc((size_t)T * std::max(md_.Dm, 1));
         W.dab.alloc((size_t)T * 64);
         const size_t ntl = (size_t)(R + 31) / 32;
-        W.gb.alloc(std::max<size_t>(ntl * md_.nl_s * 64, 1), false);
+        W.gb.alloc(std::max<size_t>(2 * ntl * md_.nl_s * 64, 1), false);   // two parity halves
         W.mgb.alloc(std::max<size_t>(ntl * std::max(md_.nl_m - 1, 0) * 64, 1), false);
         if (md_.nrnn > 0) {
           W.sg.alloc((size_t)md_.nrnn * T * 4 * H);
@@ -662,7 +685,8 @@ class Engine {
       U.adam_step = S.adam_step.p; U.drop_step = S.drop_step.p; U.gnorm = S.gnorm.p;
       U.blob = reinterpret_cast<bf16x8*>(S.blob.p); U.aux = S.aux.p; U.wproj = S.wproj.p;
       U.dpp = W.dpp.p; U.macro = splits_[0].macro.p; U.sg = W.sg.p; U.sc = W.sc.p; U.sh = W.sh.p;
-      U.dg = W.dg.p; U.dx = W.dx.p; U.dab = W.dab.p; U.T = splits_[0].T; U.seed = S.seed; U.lr = S.lr;
+      U.dg = W.dg.p; U.dx = W.dx.p; U.dab = W.dab.p; U.scal = W.scal.p; U.scal_prev = W.scal_prev.p;
+      U.T = splits_[0].T; U.seed = S.seed; U.lr = S.lr;
       uj.push_back(U);
     }
     n_eval_jobs_ = (int)le.size();
@@ -680,6 +704,7 @@ class Engine {
           if (md_.nl_m > 1) mt.back().mgbits = mb.back().mgbits = ws(g, 0).mgb.p;
         } else {
           mt.back().gbits = mb.back().gbits = ws(g, 0).gb.p;
+          mt.back().gb_half = mb.back().gb_half = ((splits_[0].R + 31) / 32) * md_.nl_s * 64;
         }
         lt.push_back(loss_job(g, 0, phase));
         ModelState& S = models_[g];
@@ -712,13 +737,29 @@ class Engine {
   template <typename T>
   static const T* as(const DevBuf<char>& b) { return reinterpret_cast<const T*>(b.p); }
 
-  void enqueue_train_grads(int phase) {
+  bool dropmask_on(int phase) const { return md_.dropout > 0.f && phase != 2; }
+  // keep masks of the step *drop_step + offset* (phases 1/3: the SDF tower's dropout)
+  void enqueue_dropmask(int phase, int offset, hipStream_t st) {
+    if (!dropmask_on(phase)) return;
+    launch_dropmask(as<MlpJob>(j_mlp_train_[phase]), G_, (splits_[0].R + 31) / 32, md_.md, offset, st);
+  }
+  // side: if non-null, the train split's Sharpe monitor (not needed by the backward) runs
+  // on that stream after the asset pass; the caller joins it before the bookkeeping copy.
+  // premasked: this step's keep masks were generated by the previous epoch graph.
+  void enqueue_train_grads(int phase, hipStream_t side = nullptr, bool premasked = false) {
     const SplitDev& D = splits_[0];
+    if (!premasked) enqueue_dropmask(phase, 0, st_);
     launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_);
     launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, gx_fwd_[0], md_.md, md_.KS1, md_.WMB, st_);
     launch_period_fwd(as<LossJob>(j_loss_train_[phase]), G_, D.T, st_);
     launch_asset(as<LossJob>(j_loss_train_[phase]), G_, D.N, st_);
-    launch_job_metrics(as<LossJob>(j_loss_train_[phase]), G_, st_);
+    if (side) {
+      HIP_OK(hipEventRecord(ev_mid_, st_));
+      HIP_OK(hipStreamWaitEvent(side, ev_mid_, 0));
+      launch_job_metrics(as<LossJob>(j_loss_train_[phase]), G_, side);
+    } else {
+      launch_job_metrics(as<LossJob>(j_loss_train_[phase]), G_, st_);
+    }
     if (phase == 2) {
       launch_mlp_bwd_mom(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_m, 1, md_.md, md_.KS1,
                          md_.WMB, slab_stride(), st_);
@@ -732,7 +773,6 @@ class Engine {
   }
   void enqueue_train(int phase, float lr) {
     enqueue_train_grads(phase);
-    copy_train_scal(st_);
     launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);
   }
   void enqueue_eval(hipStream_t st) {
@@ -744,11 +784,6 @@ class Engine {
     launch_asset(as<LossJob>(j_loss_eval_), n_eval_jobs_, nmax_eval_, st);
     launch_job_metrics(as<LossJob>(j_loss_eval_), n_eval_jobs_, st);
   }
-  void copy_train_scal(hipStream_t st) {
-    for (int g = 0; g < G_; ++g)
-      HIP_OK(hipMemcpyAsync(ws(g, 0).scal_prev.p, ws(g, 0).scal.p, SC_NSCAL * sizeof(float),
-                            hipMemcpyDeviceToDevice, st));
-  }
   void enqueue_epoch_end(int phase, int ignore_epoch, float sel, hipStream_t st) {
     launch_epoch_end(as<EpochJob>(j_epoch_[phase]), G_, phase, ignore_epoch, sel, md_.residual_factor,
                      md_.P, st);
@@ -756,14 +791,13 @@ class Engine {
   // sequential epoch: train step, evaluation, bookkeeping
   void enqueue_epoch(int phase, float lr, int ignore_epoch, float sel) {
     enqueue_train_grads(phase);
-    copy_train_scal(st_);
     launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);
     if (phase != 2) enqueue_eval(st_);
     enqueue_epoch_end(phase, ignore_epoch, sel, st_);
   }
   void enqueue_head(int phase, float lr) {
     enqueue_train_grads(phase);
-    copy_train_scal(st_);
+    enqueue_dropmask(phase, 1, st_);                     // masks of the first pipelined epoch
     launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);
   }
   void enqueue_pipe(int phase, float lr, int ignore_epoch, float sel) {
@@ -771,10 +805,10 @@ class Engine {
     HIP_OK(hipStreamWaitEvent(st2_, ev_fork_, 0));
     enqueue_eval(st2_);                                   // previous epoch's evaluation
     enqueue_epoch_end(phase, ignore_epoch, sel, st2_);    // ... and its bookkeeping
-    HIP_OK(hipEventRecord(ev_join_, st2_));
-    enqueue_train_grads(phase);                           // this epoch's forward/backward
+    enqueue_dropmask(phase, 1, st2_);                     // next epoch's dropout masks
+    enqueue_train_grads(phase, st2_, true);               // this epoch's forward/backward
+    HIP_OK(hipEventRecord(ev_join_, st2_));               // (train monitor ran on st2_ too)
     HIP_OK(hipStreamWaitEvent(st_, ev_join_, 0));
-    copy_train_scal(st_);
     launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);
   }
   void enqueue_tail(int phase, int ignore_epoch, float sel) {
@@ -790,7 +824,7 @@ class Engine {
     enqueue();
     HIP_OK(hipStreamEndCapture(st_, &graph));
     hipGraphExec_t exec;
-    HIP_OK(hipGraphInstantiate(&exec, graph, nullptr, nullptr, 0));
+    HIP_OK(hipGraphInstantiateWithFlags(&exec, graph, prio_ ? hipGraphInstantiateFlagUseNodePriority : 0));
     HIP_OK(hipGraphDestroy(graph));
     graphs_.emplace(key, exec);
     return exec;
@@ -846,6 +880,7 @@ PYBIND11_MODULE(_dlap_hip, m) {
       .def("set_pipeline", &Engine::set_pipeline)
       .def("set_lr", &Engine::set_lr)
       .def_static("rnn_timestamps", []() { return rnn_timestamps(); })
+      .def_static("mlp_timestamps", []() { return mlp_timestamps(); })
       .def("forward_split", &Engine::forward_split)
       .def("train_step", &Engine::train_step)
       .def("backward_only", &Engine::backward_only)

@@ -10,6 +10,8 @@
 //                 portfolio return (evaluate), residual-loss statistics
 //   k_asset       one workgroup per (job, 64 stocks): E, E_unc, dL/dE and partial loss sums;
 //                 the 4 waves split the time axis, then reduce in LDS in a fixed order
+//                 (A fused 'last block reduces' variant was measured 7x slower: the agent-scope
+//                 release fences write back the XCD L2 on every block.)
 //   k_period_bwd  one workgroup per (job, period): dL/dSDF_t and the analytic gradient of
 //                 the zero-mean normalisation, dL/dw_raw = m c_t (R - mean_t R) (+ residual)
 //   k_job_metrics one workgroup per job: scalar losses, Sharpe (unbiased std, 1e-8 guard),
@@ -18,34 +20,68 @@
 #include "loss.h"
 
 // ---------------------------------------------------------------- period forward -------
-__global__ __launch_bounds__(256) void k_period_fwd(const LossJob* __restrict__ jobs) {
+// One workgroup (PER_NT threads) per (job, period). When the period has at most
+// PER_NT * PER_RB compact rows (the usual case), all of its rows are loaded into registers
+// before any use -- one memory round trip instead of one per strided iteration.
+#define PER_NT 512
+#define PER_RB 8
+__global__ __launch_bounds__(PER_NT) void k_period_fwd(const LossJob* __restrict__ jobs) {
   const LossJob& J = jobs[blockIdx.y];
   const int t = blockIdx.x;
   if (t >= J.T) return;
-  __shared__ float red[4];
+  __shared__ float red[PER_NT / 64];
   const int N = J.N;
   const int r0 = gp(J.row_ptr)[t], r1 = gp(J.row_ptr)[t + 1];   // this period's compact rows
-  float sw = 0.f;
-  if (J.normalize) {
-    for (int r = r0 + threadIdx.x; r < r1; r += 256) sw += gp(J.w)[r];
-    sw = block_sum<256>(sw, red);
-  }
-  const float mu = J.normalize ? sw * gp(J.invNt)[t] : 0.f;
-  float s_wr = 0.f, s_abs = 0.f, s_ww = 0.f;
+  const auto w = gp(J.w);
+  const auto Rc = gp(J.Rc);
+  const auto rowti = gp(J.rowti);
+  const float invN = gp(J.invNt)[t];
   float* wn = gp(J.wn) + (size_t)t * N;
-  for (int r = r0 + threadIdx.x; r < r1; r += 256) {
-    const float v = gp(J.w)[r] - mu;
-    wn[gp(J.rowti)[r].y] = v;
-    s_wr += v * gp(J.Rc)[r];
-    s_abs += fabsf(v);
-    s_ww += v * v;
+  float s_wr = 0.f, s_abs = 0.f, s_ww = 0.f, mu = 0.f;
+  if (r1 - r0 <= PER_NT * PER_RB) {
+    float wv[PER_RB], rv[PER_RB];
+    int iv[PER_RB];
+#pragma unroll
+    for (int k = 0; k < PER_RB; ++k) {
+      const int r = r0 + threadIdx.x + PER_NT * k;
+      const int rr = r < r1 ? r : r0;
+      wv[k] = w[rr]; rv[k] = Rc[rr]; iv[k] = rowti[rr].y;
+    }
+    if (J.normalize) {
+      float sw = 0.f;
+#pragma unroll
+      for (int k = 0; k < PER_RB; ++k) sw += (r0 + (int)threadIdx.x + PER_NT * k < r1) ? wv[k] : 0.f;
+      mu = block_sum<PER_NT>(sw, red) * invN;
+    }
+#pragma unroll
+    for (int k = 0; k < PER_RB; ++k) {
+      if (r0 + (int)threadIdx.x + PER_NT * k >= r1) continue;
+      const float v = wv[k] - mu;
+      wn[iv[k]] = v;
+      s_wr += v * rv[k];
+      s_abs += fabsf(v);
+      s_ww += v * v;
+    }
+  } else {                                           // very wide period: two streaming passes
+    if (J.normalize) {
+      float sw = 0.f;
+      for (int r = r0 + threadIdx.x; r < r1; r += PER_NT) sw += w[r];
+      mu = block_sum<PER_NT>(sw, red) * invN;
+    }
+    for (int r = r0 + threadIdx.x; r < r1; r += PER_NT) {
+      const float v = w[r] - mu;
+      wn[rowti[r].y] = v;
+      s_wr += v * Rc[r];
+      s_abs += fabsf(v);
+      s_ww += v * v;
+    }
   }
   if (threadIdx.x == 0) gp(J.mu)[t] = mu;
-  s_wr = block_sum<256>(s_wr, red);
-  s_abs = block_sum<256>(s_abs, red);
-  if (gp(J.rstat)) s_ww = block_sum<256>(s_ww, red);
+  s_wr = block_sum<PER_NT>(s_wr, red);
+  s_abs = block_sum<PER_NT>(s_abs, red);
+  if (gp(J.rstat)) s_ww = block_sum<PER_NT>(s_ww, red);
   if (threadIdx.x == 0) {
-    const float p = J.weighted ? s_wr * gp(J.invNt)[t] * J.Nbar : s_wr;
+    const float p = J.weighted ? s_wr * invN * J.Nbar : s_wr;
     gp(J.P)[t] = p;
     gp(J.sdfv)[t] = 1.f + p;
     if (gp(J.port)) gp(J.port)[t] = s_wr / fmaxf(s_abs, 1e-8f);
@@ -54,6 +90,25 @@ __global__ __launch_bounds__(256) void k_period_fwd(const LossJob* __restrict__ 
       gp(J.rstat)[4 * t + 1] = s_wr;
     }
   }
+}
+
+// ---------------------------------------------------------------- residual loss --------
+// L_res = mean_{t in S1} resid_t / max(mean_{t in S2} Rsq_t, 1e-8)
+//   S2 = {n_t >= 2},  S1 = S2 and ww_t > 1e-8,  resid_t = (RR - Rw^2/ww)/n_t,  Rsq_t = RR/n_t.
+DLAP_DEV void residual_stats(const LossJob& J, float& lres, float& inv_b, float& n1) {
+  float a = 0.f, b = 0.f, c1 = 0.f, c2 = 0.f;
+  for (int t = 0; t < J.T; ++t) {
+    const float n = gp(J.Nt)[t];
+    if (n < 2.f) continue;
+    const float ww = gp(J.rstat)[4 * t + 0], rw = gp(J.rstat)[4 * t + 1], rr = gp(J.RR)[t];
+    b += rr / n; c2 += 1.f;
+    if (ww > 1e-8f) { a += (rr - rw * rw / ww) / n; c1 += 1.f; }
+  }
+  if (c1 == 0.f) { lres = 0.f; inv_b = 0.f; n1 = 0.f; return; }
+  const float B = fmaxf(b / c2, 1e-8f);
+  lres = (a / c1) / B;
+  inv_b = 1.f / B;
+  n1 = c1;
 }
 
 // ---------------------------------------------------------------- asset pass ------------
@@ -80,18 +135,36 @@ __global__ __launch_bounds__(256) void k_asset_part(const LossJob* __restrict__ 
     for (int k = 0; k < 8; ++k) e[k] = 0.f;
     const int kn = J.h ? min(8, K - k0) : 0;
     if (ok) {
-#pragma unroll 4
-      for (int t = t0; t < t1; ++t) {
-        const size_t d = (size_t)t * N + i;
-        const float q = gp(J.Rm)[d] * gp(J.sdfv)[t];
-        if (k0 == 0) eu += q;
-        if (kn == 8 && (K & 3) == 0) {
-          const float* hp = gp(J.h) + d * K + k0;
-          const f32x4 a = *reinterpret_cast<const f32x4*>(hp);
-          const f32x4 b = *reinterpret_cast<const f32x4*>(hp + 4);
+      if (kn == 8 && (K & 3) == 0) {
+        // blocks of AW time steps: every operand of the block is requested before use
+        constexpr int AW = 8;
+        for (int tb = t0; tb < t1; tb += AW) {
+          float rm[AW], sv[AW];
+          f32x4 ha[AW], hb[AW];
 #pragma unroll
-          for (int k = 0; k < 4; ++k) { e[k] += a[k] * q; e[4 + k] += b[k] * q; }
-        } else {
+          for (int u = 0; u < AW; ++u) {
+            const int t = min(tb + u, t1 - 1);
+            const size_t d = (size_t)t * N + i;
+            rm[u] = gp(J.Rm)[d];
+            sv[u] = gp(J.sdfv)[t];
+            const auto hp = gp(J.h) + d * K + k0;
+            ha[u] = ld4(hp);
+            hb[u] = ld4(hp + 4);
+          }
+#pragma unroll
+          for (int u = 0; u < AW; ++u) {
+            const float q = tb + u < t1 ? rm[u] * sv[u] : 0.f;
+            if (k0 == 0) eu += q;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) { e[k] += ha[u][k] * q; e[4 + k] += hb[u][k] * q; }
+          }
+        }
+      } else {
+#pragma unroll 4
+        for (int t = t0; t < t1; ++t) {
+          const size_t d = (size_t)t * N + i;
+          const float q = gp(J.Rm)[d] * gp(J.sdfv)[t];
+          if (k0 == 0) eu += q;
           for (int k = 0; k < kn; ++k) e[k] += gp(J.h)[d * K + k0 + k] * q;
         }
       }
@@ -155,50 +228,72 @@ DLAP_DEV void final_losses(const LossJob& J, float& lc, float& lu) {
   lu = b / (float)J.N;
 }
 
-// ---------------------------------------------------------------- residual loss --------
-// L_res = mean_{t in S1} resid_t / max(mean_{t in S2} Rsq_t, 1e-8)
-//   S2 = {n_t >= 2},  S1 = S2 and ww_t > 1e-8,  resid_t = (RR - Rw^2/ww)/n_t,  Rsq_t = RR/n_t.
-DLAP_DEV void residual_stats(const LossJob& J, float& lres, float& inv_b, float& n1) {
-  float a = 0.f, b = 0.f, c1 = 0.f, c2 = 0.f;
-  for (int t = 0; t < J.T; ++t) {
-    const float n = gp(J.Nt)[t];
-    if (n < 2.f) continue;
-    const float ww = gp(J.rstat)[4 * t + 0], rw = gp(J.rstat)[4 * t + 1], rr = gp(J.RR)[t];
-    b += rr / n; c2 += 1.f;
-    if (ww > 1e-8f) { a += (rr - rw * rw / ww) / n; c1 += 1.f; }
-  }
-  if (c1 == 0.f) { lres = 0.f; inv_b = 0.f; n1 = 0.f; return; }
-  const float B = fmaxf(b / c2, 1e-8f);
-  lres = (a / c1) / B;
-  inv_b = 1.f / B;
-  n1 = c1;
-}
-
 // ---------------------------------------------------------------- period backward ------
-__global__ __launch_bounds__(256) void k_period_bwd(const LossJob* __restrict__ jobs) {
+__global__ __launch_bounds__(PER_NT) void k_period_bwd(const LossJob* __restrict__ jobs) {
   const LossJob& J = jobs[blockIdx.y];
   const int t = blockIdx.x;
   if (t >= J.T) return;
-  __shared__ float red[4];
+  __shared__ float red[PER_NT / 64];
   const int N = J.N, K = J.K;
   const size_t base = (size_t)t * N;
   const int r0 = gp(J.row_ptr)[t], r1 = gp(J.row_ptr)[t + 1];
+  const auto rowti = gp(J.rowti);
+  const auto Rc = gp(J.Rc);
+  const auto invT = gp(J.invT);
+  // per-row dL/dS contribution: g_i R_i / T_i with g = dE_u (phase 1) or sum_k dE[i,k] h[t,i,k]
+  auto row_g = [&](int i) -> float {
+    if (J.phase == 1) return gp(J.dEu)[i];
+    const auto hp = gp(J.h) + (base + i) * K;
+    const auto de = gp(J.dE) + (size_t)i * K;
+    float g = 0.f;
+    for (int k = 0; k < K; ++k) g += de[k] * hp[k];
+    return g;
+  };
+  constexpr int RB = 4;
+  const bool fast = r1 - r0 <= PER_NT * RB;
+  float rv[RB];
   float s = 0.f;
-  for (int rr = r0 + threadIdx.x; rr < r1; rr += 256) {
-    const int i = gp(J.rowti)[rr].y;
-    const float r = gp(J.Rc)[rr];
-    float g;
-    if (J.phase == 1) {
-      g = gp(J.dEu)[i];
-    } else {
-      g = 0.f;
-      const float* hp = gp(J.h) + (base + i) * K;
-      const float* de = gp(J.dE) + (size_t)i * K;
-      for (int k = 0; k < K; ++k) g += de[k] * hp[k];
+  if (fast) {
+    // every row's operands are requested before any is used: 2 dependent round trips total
+    int iv[RB];
+#pragma unroll
+    for (int k = 0; k < RB; ++k) {
+      const int r = r0 + threadIdx.x + PER_NT * k;
+      const int rr = r < r1 ? r : r0;
+      iv[k] = rowti[rr].y;
+      rv[k] = Rc[rr];
     }
-    s += g * r * gp(J.invT)[i];
+    float gv[RB], tv[RB];
+    if (J.phase != 1 && K == 8) {
+      f32x4 d0[RB], d1[RB], h0[RB], h1[RB];
+#pragma unroll
+      for (int k = 0; k < RB; ++k) {
+        const auto hp = gp(J.h) + (base + iv[k]) * 8;
+        const auto de = gp(J.dE) + (size_t)iv[k] * 8;
+        d0[k] = ld4(de); d1[k] = ld4(de + 4); h0[k] = ld4(hp); h1[k] = ld4(hp + 4);
+        tv[k] = invT[iv[k]];
+      }
+#pragma unroll
+      for (int k = 0; k < RB; ++k) {
+        float g = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) g += d0[k][e] * h0[k][e] + d1[k][e] * h1[k][e];
+        gv[k] = g;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < RB; ++k) { gv[k] = row_g(iv[k]); tv[k] = invT[iv[k]]; }
+    }
+#pragma unroll
+    for (int k = 0; k < RB; ++k)
+      if (r0 + (int)threadIdx.x + PER_NT * k < r1) s += gv[k] * rv[k] * tv[k];
+  } else {
+    for (int rr = r0 + threadIdx.x; rr < r1; rr += PER_NT) {
+      const int i = rowti[rr].y;
+      s += row_g(i) * Rc[rr] * invT[i];
+    }
   }
-  s = block_sum<256>(s, red);
+  s = block_sum<PER_NT>(s, red);
   const float c = J.weighted ? s * J.Nbar * gp(J.invNt)[t] : s;   // dL/dS_t with S_t = sum w' R m
   // optional residual-loss gradient wrt w' (valid stocks of period t)
   float rcoef = 0.f, beta = 0.f;
@@ -211,21 +306,28 @@ __global__ __launch_bounds__(256) void k_period_bwd(const LossJob* __restrict__ 
       rcoef = J.res_factor * inv_b / n1 * (-2.f / n) * beta;   // d/dw'_i = rcoef * (R_i - beta w'_i)
     }
   }
-  // mean over valid stocks of the residual gradient (for the normalisation Jacobian)
   const float mu = gp(J.mu)[t];
   float gres_mean = 0.f;
   if (rcoef != 0.f && J.normalize) {
     float sg = 0.f;
-    for (int rr = r0 + threadIdx.x; rr < r1; rr += 256) sg += gp(J.Rc)[rr] - beta * (gp(J.w)[rr] - mu);
-    sg = block_sum<256>(sg, red);
+    for (int rr = r0 + threadIdx.x; rr < r1; rr += PER_NT) sg += Rc[rr] - beta * (gp(J.w)[rr] - mu);
+    sg = block_sum<PER_NT>(sg, red);
     gres_mean = rcoef * sg * gp(J.invNt)[t];
   }
   const float mR = J.normalize ? gp(J.meanR)[t] : 0.f;
-  for (int rr = r0 + threadIdx.x; rr < r1; rr += 256) {
-    const float R = gp(J.Rc)[rr];
-    float g = c * (R - mR);
-    if (rcoef != 0.f) g += rcoef * (R - beta * (gp(J.w)[rr] - mu)) - gres_mean;
-    gp(J.dw)[rr] = g;
+  if (fast && rcoef == 0.f) {
+#pragma unroll
+    for (int k = 0; k < RB; ++k) {
+      const int r = r0 + threadIdx.x + PER_NT * k;
+      if (r < r1) gp(J.dw)[r] = c * (rv[k] - mR);
+    }
+  } else {
+    for (int rr = r0 + threadIdx.x; rr < r1; rr += PER_NT) {
+      const float R = Rc[rr];
+      float g = c * (R - mR);
+      if (rcoef != 0.f) g += rcoef * (R - beta * (gp(J.w)[rr] - mu)) - gres_mean;
+      gp(J.dw)[rr] = g;
+    }
   }
 }
 
@@ -282,7 +384,7 @@ __global__ __launch_bounds__(256) void k_job_metrics(const LossJob* __restrict__
 
 // ---------------------------------------------------------------- launchers ------------
 void launch_period_fwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st) {
-  hipLaunchKernelGGL(k_period_fwd, dim3(tmax, njobs), dim3(256), 0, st, jobs);
+  hipLaunchKernelGGL(k_period_fwd, dim3(tmax, njobs), dim3(PER_NT), 0, st, jobs);
   HIP_OK(hipGetLastError());
 }
 void launch_asset(const LossJob* jobs, int njobs, int nmax, hipStream_t st) {
@@ -292,7 +394,7 @@ void launch_asset(const LossJob* jobs, int njobs, int nmax, hipStream_t st) {
   HIP_OK(hipGetLastError());
 }
 void launch_period_bwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st) {
-  hipLaunchKernelGGL(k_period_bwd, dim3(tmax, njobs), dim3(256), 0, st, jobs);
+  hipLaunchKernelGGL(k_period_bwd, dim3(tmax, njobs), dim3(PER_NT), 0, st, jobs);
   HIP_OK(hipGetLastError());
 }
 void launch_job_metrics(const LossJob* jobs, int njobs, hipStream_t st) {

@@ -34,6 +34,13 @@
 #include "mlp.h"
 
 DLAP_DEV int lane_id() { return threadIdx.x & 63; }
+
+// In-kernel timestamps (wall clock, 100 MHz) of k_mlp_fwd's first / last workgroup, wave 0:
+// [0] start, [1] weights staged, [2] first tile done, [3] loop done; [4..7] same, last block.
+__device__ long long g_mlp_ts[8];
+#define MLP_TS(slot) do { \
+    if ((threadIdx.x & 255) == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1) && J.gbits) \
+      g_mlp_ts[(blockIdx.x == 0 ? 0 : 4) + (slot)] = wall_clock64(); } while (0)
 DLAP_DEV bf16x8 ldsf(const bf16x8* lds, int frag) { return lds[frag * 64 + lane_id()]; }
 DLAP_DEV int perm_unit(int q, int j) { return j < 4 ? 4 * q + j : 16 + 4 * q + (j - 4); }
 
@@ -171,21 +178,21 @@ struct DropCtx {
 };
 
 // bias + ReLU + dropout in place; gate bit (u*4+r) per row block. Branch-free: one hash
-// per unit pair gives both keep decisions (see dropout_pair).
-template <int UB, typename BP>
-DLAP_DEV void relu_dropout(f32x4 (&a)[2][UB], BP bias0, BP bias1,
-                           const DropCtx& dc, int layer_id, const RowInfo& ri, uint32_t (&gate)[2]) {
+// per unit pair gives both keep decisions (see dropout_pair). ``getb(b, u)`` returns the
+// f32x4 bias of units 16u + 4q .. +3 for row block b.
+template <int UB, typename GetB>
+DLAP_DEV void relu_dropout_g(f32x4 (&a)[2][UB], GetB getb, const DropCtx& dc, int layer_id,
+                             const RowInfo& ri, uint32_t (&gate)[2]) {
   const int q = lane_id() >> 4;
   const uint32_t key = dropout_key(dc.seed, dc.step, layer_id);
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
-    const BP bp = b ? bias1 : bias0;
     const uint32_t row = (uint32_t)ri.dense[b];
     const uint32_t rowmix = row * 0xcc9e2d51u ^ (row >> 16);
     uint32_t g = 0;
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
-      const f32x4 bb = ld4(bp + 16 * u + 4 * q);
+      const f32x4 bb = getb(b, u);
       uint32_t keep = 0xFu;
       if (dc.on) {   // wave-uniform
         const uint32_t pair0 = (uint32_t)(8 * u + 2 * q);
@@ -204,6 +211,59 @@ DLAP_DEV void relu_dropout(f32x4 (&a)[2][UB], BP bias0, BP bias1,
     }
     gate[b] = g;
   }
+}
+
+template <int UB, typename BP>
+DLAP_DEV void relu_dropout(f32x4 (&a)[2][UB], BP bias0, BP bias1,
+                           const DropCtx& dc, int layer_id, const RowInfo& ri, uint32_t (&gate)[2]) {
+  const int q = lane_id() >> 4;
+  relu_dropout_g<UB>(a, [&](int b, int u) { return ld4((b ? bias1 : bias0) + 16 * u + 4 * q); },
+                     dc, layer_id, ri, gate);
+}
+
+// bias + ReLU + dropout from pre-generated keep bits (k_dropmask): gate = (z > 0) & keep.
+template <int UB, typename BP>
+DLAP_DEV void relu_keep(f32x4 (&a)[2][UB], BP bias, float scale, uint32_t kw, uint32_t (&gate)[2]) {
+  const int q = lane_id() >> 4;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const uint32_t keep = b ? (kw >> 16) : (kw & 0xFFFFu);
+    uint32_t g = 0;
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const f32x4 bb = ld4(bias + 16 * u + 4 * q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float z = a[b][u][r] + bb[r];
+        const bool on = (z > 0.f) & (((keep >> (u * 4 + r)) & 1u) != 0u);
+        a[b][u][r] = on ? z * scale : 0.f;
+        g |= (on ? 1u : 0u) << (u * 4 + r);
+      }
+    }
+    gate[b] = g;
+  }
+}
+
+// Per-period moment layer-0 bias of a tile's rows (abias[t][16u + 4q .. +3]), loaded one tile
+// ahead from the row periods fetched two tiles ahead, so no dependent load sits on a tile.
+template <int WMB>
+struct AbPre { f32x4 v[2][WMB]; };
+
+template <int WMB>
+DLAP_DEV void issue_abias(const MlpJob& J, const int2 (&ti)[2], AbPre<WMB>& p) {
+  const int q = lane_id() >> 4;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const auto src = gp(J.abias) + ti[b].x * 64 + 4 * q;
+#pragma unroll
+    for (int u = 0; u < WMB; ++u) p.v[b][u] = ld4(src + 16 * u);
+  }
+}
+
+DLAP_DEV void issue_rowti(const MlpJob& J, int tile, int2 (&ti)[2]) {
+  const int l = lane_id();
+#pragma unroll
+  for (int b = 0; b < 2; ++b) ti[b] = gp(J.rowti)[min(tile * 32 + 16 * b + (l & 15), J.R - 1)];
 }
 
 // bias + ReLU + dropout from gate bits stored by the training forward (bit u*4+r per row
@@ -257,20 +317,24 @@ DLAP_DEV void stage_weights(const MlpJob& J, const MlpDims& D, bf16x8* lds, floa
 }
 
 // SDF tower forward on one tile: the raw (pre-normalisation) weight of each row block.
+// gout: gate words of the tile (train). With keep words (kw, pre-generated by k_dropmask) the
+// dropout decisions are read instead of hashed; the gates overwrite the keep words in place.
 template <int KS1>
 DLAP_DEV void sdf_forward_tile(const bf16x8* lds, const float* aux, const MlpDims& D,
                                const DropCtx& dc, const RowInfo& ri, const bf16x8 (&xf)[2][KS1],
-                               DLAP_GLOBAL uint32_t* gout, float (&w)[2]) {
+                               DLAP_GLOBAL uint32_t* gout, const uint32_t* kw, float (&w)[2]) {
   f32x4 a[2][4];
   bf16x8 pf[2][2];
   uint32_t gate[2];
   layer0<KS1, 4>(lds, D.s_fwd0, xf, a);
-  relu_dropout<4>(a, aux + D.a_sb, aux + D.a_sb, dc, 0, ri, gate);
+  if (kw) relu_keep<4>(a, aux + D.a_sb, dc.scale, kw[0], gate);
+  else relu_dropout<4>(a, aux + D.a_sb, aux + D.a_sb, dc, 0, ri, gate);
   if (gout) gout[0] = gate_word(gate);
   for (int j = 1; j < D.nl_sdf; ++j) {
     pack_blocks<4>(a, pf);
     layer_chain<4, 2>(lds, D.s_fwd + (j - 1) * 8, pf, a);
-    relu_dropout<4>(a, aux + D.a_sb + 64 * j, aux + D.a_sb + 64 * j, dc, j, ri, gate);
+    if (kw) relu_keep<4>(a, aux + D.a_sb + 64 * j, dc.scale, kw[j], gate);
+    else relu_dropout<4>(a, aux + D.a_sb + 64 * j, aux + D.a_sb + 64 * j, dc, j, ri, gate);
     if (gout) gout[64 * j] = gate_word(gate);
   }
   const int q = lane_id() >> 4;
@@ -293,17 +357,17 @@ DLAP_DEV void sdf_forward_tile(const bf16x8* lds, const float* aux, const MlpDim
 template <int KS1, int WMB>
 DLAP_DEV void mom_forward_tile(const bf16x8* lds, const float* aux, const MlpDims& D,
                                const MlpJob& J, const DropCtx& dc, const RowInfo& ri,
-                               const bf16x8 (&xf)[2][KS1], DLAP_GLOBAL uint32_t* gout) {
+                               const bf16x8 (&xf)[2][KS1], DLAP_GLOBAL uint32_t* gout,
+                               const AbPre<WMB>& ab) {
   constexpr int KSM = (WMB + 1) / 2;
   f32x4 a[2][WMB];
   bf16x8 pf[2][KSM];
   uint32_t gate[2];
   const int q = lane_id() >> 4;
   layer0<KS1, WMB>(lds, D.m_fwd0, xf, a);
-  // layer-0 bias is per period (global), later biases are staged (LDS)
-  const auto ab0 = gp(J.abias) + ri.t[0] * 64, ab1 = gp(J.abias) + ri.t[1] * 64;
+  // layer-0 bias is per period (prefetched), later biases are staged (LDS)
   for (int j = 0; j + 1 < D.nl_mom; ++j) {
-    if (j == 0) relu_dropout<WMB>(a, ab0, ab1, dc, 16 + j, ri, gate);
+    if (j == 0) relu_dropout_g<WMB>(a, [&](int b, int u) { return ab.v[b][u]; }, dc, 16 + j, ri, gate);
     else relu_dropout<WMB>(a, aux + D.a_mb + 64 * j, aux + D.a_mb + 64 * j, dc, 16 + j, ri, gate);
     if (gout) gout[64 * j] = gate_word(gate);
     pack_blocks<WMB>(a, pf);
@@ -324,8 +388,22 @@ DLAP_DEV void mom_forward_tile(const bf16x8* lds, const float* aux, const MlpDim
         }
     }
   };
-  if (D.nl_mom > 1) emit(aux + D.a_mb + 64 * (D.nl_mom - 1), aux + D.a_mb + 64 * (D.nl_mom - 1));
-  else emit(ab0, ab1);
+  if (D.nl_mom > 1) {
+    emit(aux + D.a_mb + 64 * (D.nl_mom - 1), aux + D.a_mb + 64 * (D.nl_mom - 1));
+  } else {                                   // single layer: its bias is the per-period one
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      if (ri.dense[b] < 0) continue;
+      const auto dst = gp(J.h_out) + (size_t)ri.dense[b] * D.K;
+#pragma unroll
+      for (int u = 0; u < WMB; ++u)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int k = 16 * u + 4 * q + r;
+          if (k < D.K) dst[k] = tanhf(a[b][u][r] + ab.v[b][u][r]);
+        }
+    }
+  }
 }
 
 // ============================== forward ==================================================
@@ -336,23 +414,51 @@ __global__ __launch_bounds__(256, 2) void k_mlp_fwd(const MlpJob* __restrict__ j
   bf16x8* lds = reinterpret_cast<bf16x8*>(smem);
   float* aux = reinterpret_cast<float*>(smem + (size_t)D.blob_frags * 1024);
   float* spp = pp_lds_ptr(smem, D);
+  MLP_TS(0);
   const int wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   const int ntiles = (J.R + 31) >> 5;
   const int q = lane_id() >> 4, lane = lane_id();
   const int stride = gridDim.x * nwaves;
   int tile = blockIdx.x * nwaves + wave;
   TileIn<KS1> cur, nxt;
-  if (tile < ntiles) issue_tile<KS1, false>(J, tile, cur);   // in flight during the staging
+  AbPre<WMB> ab_cur, ab_nxt;
+  int2 ti_ahead[2];                      // periods of the tile after next (for the abias prefetch)
+  const bool mom = J.do_mom;
+  if (tile < ntiles) {
+    issue_tile<KS1, false>(J, tile, cur);                    // in flight during the staging
+    if (mom && tile + stride < ntiles) issue_rowti(J, tile + stride, ti_ahead);
+  }
   stage_weights(J, D, lds, aux, spp);
+  MLP_TS(1);
   const DropCtx dc = drop_ctx(J, D);
+  if (mom && tile < ntiles) issue_abias<WMB>(J, cur.ti, ab_cur);
+  // train forward with dropout: keep words of this step's parity half, prefetched with the tile
+  const bool keep = J.gbits && dc.on;
+  const auto gbase = J.gbits ? gp(J.gbits) + (size_t)(dc.step & 1u) * J.gb_half : nullptr;
+  constexpr int KWM = 4;                           // max SDF hidden layers (engine limit)
+  uint32_t kw_cur[KWM], kw_nxt[KWM];
+  auto issue_kw = [&](int t, uint32_t (&kw)[KWM]) {
+#pragma unroll
+    for (int j = 0; j < KWM; ++j)
+      kw[j] = j < D.nl_sdf ? gbase[((size_t)t * D.nl_sdf + j) * 64 + lane] : 0xFFFFFFFFu;
+  };
+  if (keep && tile < ntiles) issue_kw(tile, kw_cur);
+  bool first = true;
   for (; tile < ntiles; tile += stride) {
-    if (tile + stride < ntiles) issue_tile<KS1, false>(J, tile + stride, nxt);
+    if (tile + stride < ntiles) {
+      issue_tile<KS1, false>(J, tile + stride, nxt);
+      if (keep) issue_kw(tile + stride, kw_nxt);
+      if (mom) {
+        issue_abias<WMB>(J, ti_ahead, ab_nxt);             // periods known since last iteration
+        if (tile + 2 * stride < ntiles) issue_rowti(J, tile + 2 * stride, ti_ahead);
+      }
+    }
     bf16x8 xf[2][KS1];
     const RowInfo ri = finish_tile<KS1>(J, D, tile, cur, xf, spp);
     if (J.do_sdf) {
       float w[2];
-      DLAP_GLOBAL uint32_t* gout = J.gbits ? gp(J.gbits) + (size_t)tile * D.nl_sdf * 64 + lane : nullptr;
-      sdf_forward_tile<KS1>(lds, aux, D, dc, ri, xf, gout, w);
+      DLAP_GLOBAL uint32_t* gout = J.gbits ? gbase + (size_t)tile * D.nl_sdf * 64 + lane : nullptr;
+      sdf_forward_tile<KS1>(lds, aux, D, dc, ri, xf, gout, keep ? kw_cur : nullptr, w);
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         const int r = tile * 32 + 16 * b + (lane & 15);
@@ -362,10 +468,15 @@ __global__ __launch_bounds__(256, 2) void k_mlp_fwd(const MlpJob* __restrict__ j
     if (J.do_mom) {
       DLAP_GLOBAL uint32_t* gout = (J.mgbits && D.nl_mom > 1)
                            ? gp(J.mgbits) + (size_t)tile * (D.nl_mom - 1) * 64 + lane : nullptr;
-      mom_forward_tile<KS1, WMB>(lds, aux, D, J, dc, ri, xf, gout);
+      mom_forward_tile<KS1, WMB>(lds, aux, D, J, dc, ri, xf, gout, ab_cur);
     }
     cur = nxt;
+    ab_cur = ab_nxt;
+#pragma unroll
+    for (int j = 0; j < KWM; ++j) kw_cur[j] = kw_nxt[j];
+    if (first) { MLP_TS(2); first = false; }
   }
+  MLP_TS(3);
 }
 
 // ============================== backward =================================================
@@ -435,10 +546,12 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
   int tile = blockIdx.x * nwaves + wave;
   TileIn<KS1> cur, nxt;
   uint32_t gw_cur[NL], gw_nxt[NL];   // gate words of the forward pass, prefetched with the tile
+  const uint32_t stp = J.step ? (uint32_t)*gp(J.step) : 0u;
+  const auto gbase = gp(J.gbits) + (size_t)(stp & 1u) * J.gb_half;
   if (tile < ntiles) {
     issue_tile<KS1, true>(J, tile, cur);
 #pragma unroll
-    for (int j = 0; j < NL; ++j) gw_cur[j] = gp(J.gbits)[((size_t)tile * NL + j) * 64 + lane];
+    for (int j = 0; j < NL; ++j) gw_cur[j] = gbase[((size_t)tile * NL + j) * 64 + lane];
   }
   stage_weights(J, D, lds, aux, spp);          // first tile's loads are already in flight
   const DropCtx dc = drop_ctx(J, D);
@@ -446,7 +559,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
     if (tile + stride < ntiles) {
       issue_tile<KS1, true>(J, tile + stride, nxt);
 #pragma unroll
-      for (int j = 0; j < NL; ++j) gw_nxt[j] = gp(J.gbits)[((size_t)(tile + stride) * NL + j) * 64 + lane];
+      for (int j = 0; j < NL; ++j) gw_nxt[j] = gbase[((size_t)(tile + stride) * NL + j) * 64 + lane];
     }
     bf16x8 xf[2][KS1];
     const RowInfo ri = finish_tile<KS1>(J, D, tile, cur, xf, spp);
@@ -774,6 +887,54 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
   wg_slab_store(J, red, slab_stride);
 }
 
+// ============================== dropout keep-mask generator ===========================
+// Keep words of every (tile, SDF layer, lane) for the dropout step *step + step_offset*, in
+// that step's parity half of gbits. The decisions are exactly relu_dropout's (same key, row
+// and unit hashing); generating them here lets the next step's masks be produced on an idle
+// branch of the epoch graph while the serial LSTM kernels run, instead of inside the forward.
+__global__ __launch_bounds__(256) void k_dropmask(const MlpJob* __restrict__ jobs, MlpDims D, int step_offset) {
+  const MlpJob& J = jobs[blockIdx.y];
+  const int ntiles = (J.R + 31) >> 5;
+  const int gid = blockIdx.x * 256 + threadIdx.x;
+  const int tile = gid >> 6, lane = gid & 63, q = lane >> 4;
+  if (tile >= ntiles) return;
+  const uint32_t step = (J.step ? (uint32_t)*gp(J.step) : 0u) + (uint32_t)step_offset;
+  const uint32_t thr16 = (uint32_t)(D.dropout * 65536.f + 0.5f);
+  uint32_t rowmix[2];
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int r = min(tile * 32 + 16 * b + (lane & 15), J.R - 1);
+    const int2 ti = gp(J.rowti)[r];
+    const uint32_t row = (uint32_t)(ti.x * J.N + ti.y);
+    rowmix[b] = row * 0xcc9e2d51u ^ (row >> 16);
+  }
+  const auto dst = gp(J.gbits) + (size_t)(step & 1u) * J.gb_half + (size_t)tile * D.nl_sdf * 64 + lane;
+  for (int j = 0; j < D.nl_sdf; ++j) {
+    const uint32_t key = dropout_key(J.seed, step, j);
+    uint32_t word = 0;
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t pair0 = (uint32_t)(8 * u + 2 * q);
+        const uint32_t h0 = dropout_pair(key, rowmix[b], pair0);
+        const uint32_t h1 = dropout_pair(key, rowmix[b], pair0 + 1);
+        const uint32_t keep = ((h0 & 0xFFFFu) >= thr16 ? 1u : 0u) | ((h0 >> 16) >= thr16 ? 2u : 0u) |
+                              ((h1 & 0xFFFFu) >= thr16 ? 4u : 0u) | ((h1 >> 16) >= thr16 ? 8u : 0u);
+        word |= keep << (16 * b + 4 * u);
+      }
+    }
+    dst[64 * j] = word;
+  }
+}
+
+void launch_dropmask(const MlpJob* jobs, int njobs, int ntiles, const MlpDims& D, int step_offset,
+                     hipStream_t st) {
+  hipLaunchKernelGGL(k_dropmask, dim3((ntiles * 64 + 255) / 256, njobs), dim3(256), 0, st, jobs, D,
+                     step_offset);
+  HIP_OK(hipGetLastError());
+}
+
 // ---- host launchers -------------------------------------------------------------------
 size_t mlp_lds_bytes(const MlpDims& D) {
   return (size_t)D.blob_frags * 1024 + (size_t)((D.aux_floats + 3) & ~3) * 4 + (size_t)D.pp_lds_floats * 4;
@@ -817,4 +978,10 @@ void launch_mlp_bwd_mom(const MlpJob* jobs, int njobs, int gx, int nslice, int t
   M_CASE(4, 1, 2) M_CASE(4, 2, 2) M_CASE(4, 4, 2)
 #undef M_CASE
   dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_mom: unsupported depth/width", __FILE__, __LINE__);
+}
+
+std::vector<long long> mlp_timestamps() {
+  std::vector<long long> v(8);
+  HIP_OK(hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(g_mlp_ts), sizeof(long long) * 8));
+  return v;
 }

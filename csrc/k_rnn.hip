@@ -557,12 +557,24 @@ __global__ __launch_bounds__(256) void k_wgrad(const UpdJob* __restrict__ jobs,
 #pragma unroll
   for (int g = 0; g < GM; ++g) acc[g] = 0.f;
   if (col <= M) {
-#pragma unroll 2
-    for (int t = tg; t < T; t += 16) {
-      const float x = col < M ? gp(J.macro)[(size_t)t * M + col] : 1.f;
-      const auto dr = dG + (size_t)t * ldG;
+    // blocks of WG_TB time steps per thread: the macro value of every step is requested
+    // first; the gradient rows are then consumed straight from L2 (16-byte loads)
+    constexpr int WG_TB = 8;
+    for (int tb = tg; tb < T; tb += 16 * WG_TB) {
+      float xv[WG_TB];
 #pragma unroll
-      for (int g = 0; g < GM; ++g) acc[g] += dr[g] * x;
+      for (int u = 0; u < WG_TB; ++u) {
+        const int t = min(tb + 16 * u, T - 1);
+        const float x = col < M ? gp(J.macro)[(size_t)t * M + (col < M ? col : 0)] : 1.f;
+        xv[u] = tb + 16 * u < T ? x : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < WG_TB; ++u) {
+        const int t = min(tb + 16 * u, T - 1);
+        const auto dr = dG + (size_t)t * ldG;
+#pragma unroll
+        for (int g = 0; g < GM; ++g) acc[g] += dr[g] * xv[u];
+      }
     }
   }
 #pragma unroll

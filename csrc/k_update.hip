@@ -226,12 +226,25 @@ __global__ __launch_bounds__(256) void k_adam(const UpdJob* __restrict__ jobs,
                                               const ModelDesc* __restrict__ md, int phase, float lr) {
   const UpdJob& J = jobs[blockIdx.y];
   __shared__ float red[4];
+  // the train split's scalars of this step, kept for the (possibly deferred) bookkeeping
+  if (blockIdx.x == 0 && J.scal && threadIdx.x < SC_NSCAL) gp(J.scal_prev)[threadIdx.x] = gp(J.scal)[threadIdx.x];
   const bool mom = phase == 2;
   const int p0 = mom ? md->P_sdf : 0, p1 = mom ? md->P : md->P_sdf;
   const float* __restrict__ grads = gp(J.grads);
+  // scope norm: the block's whole share of loads is issued before any use (register blocks of
+  // ADAM_NB per thread), so the reduction costs ~one memory round trip per block of 256*ADAM_NB
+  constexpr int ADAM_NB = 48;
   float ss = 0.f;
-#pragma unroll 16
-  for (int i = p0 + threadIdx.x; i < p1; i += 256) { const float g = grads[i]; ss += g * g; }
+  for (int b0 = p0; b0 < p1; b0 += 256 * ADAM_NB) {
+    float gv[ADAM_NB];
+#pragma unroll
+    for (int k = 0; k < ADAM_NB; ++k) {
+      const int i = b0 + k * 256 + threadIdx.x;
+      gv[k] = grads[i < p1 ? i : p0];
+    }
+#pragma unroll
+    for (int k = 0; k < ADAM_NB; ++k) ss += (b0 + k * 256 + (int)threadIdx.x < p1) ? gv[k] * gv[k] : 0.f;
+  }
   ss = block_sum<256>(ss, red);
   const float norm = sqrtf(ss);
   const float coef = fminf(1.f / (norm + 1e-6f), 1.f);

@@ -1,5 +1,6 @@
 // Job / dimension records of the fused tower kernels (k_mlp.hip), shared with the engine.
 #pragma once
+#include <vector>
 #include "common.h"
 
 struct MlpJob {
@@ -19,8 +20,11 @@ struct MlpJob {
   float* slab;            // bwd: per-wave gradient partials
   float* u_out;           // bwd sdf: [R][Dm] dL/d(per-period inputs) per row
   float* v_out;           // bwd mom: [R][64] dL/d(moment layer-0 pre-activation) per row
-  uint32_t* gbits;        // train fwd writes / bwd reads the SDF ReLU*keep gate bits:
-                          //   [tile][layer][lane] = gate(b=0) | gate(b=1) << 16
+  uint32_t* gbits;        // SDF dropout keep -> gate words, two halves by dropout-step parity:
+                          //   [parity][tile][layer][lane] = bits(b=0) | bits(b=1) << 16.
+                          //   k_dropmask writes keep bits, the train forward turns them into
+                          //   ReLU*keep gate bits in place, the backward reads the gates.
+  int gb_half;            // words per parity half (ntiles * nl_sdf * 64)
   uint32_t* mgbits;       // same for the moment tower's hidden layers (phase 2)
   const int* step;        // device step counter (dropout stream)
   int R, N, T;
@@ -52,5 +56,9 @@ void launch_mlp_fwd(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int
                     hipStream_t st);
 void launch_mlp_bwd_sdf(const MlpJob* jobs, int njobs, int gx, int nslice, int tps, const MlpDims& D,
                         int KS1, int slab_stride, hipStream_t st);
+void launch_dropmask(const MlpJob* jobs, int njobs, int ntiles, const MlpDims& D, int step_offset,
+                     hipStream_t st);
 void launch_mlp_bwd_mom(const MlpJob* jobs, int njobs, int gx, int nslice, int tps, const MlpDims& D,
                         int KS1, int WMB, int slab_stride, hipStream_t st);
+
+std::vector<long long> mlp_timestamps();

@@ -35,6 +35,8 @@ struct UpdJob {            // one model
   float* dg;               // scratch [T][4H]
   float* dx;               // scratch [T][H]
   const float* dab;        // [T][64]
+  const float* scal;       // train-split job scalars of this step (SC_NSCAL) ...
+  float* scal_prev;        // ... copied here by k_adam for the epoch bookkeeping
   int T;
   unsigned seed;
   float lr;                // > 0: this model's learning rate (sweeps batch configs that

@@ -36,6 +36,11 @@ def main():
         print(f"  k_lstm_gl eval : stage {us(4, 5):7.1f}  recur {us(5, 6):7.1f}  tail {us(6, 7):7.1f}  total {us(4, 7):7.1f}")
         print(f"  k_lstm_bwd     : stage {us(8, 9):7.1f}  bptt  {us(9, 10):7.1f}  grads {us(10, 11):7.1f} total {us(8, 11):7.1f}")
         print(f"  k_proj tile0   : total {us(12, 14):7.1f}")
+        m = np.array(mod.Engine.mlp_timestamps(), dtype=np.int64)
+        um = lambda a, b: (m[b] - m[a]) / 100.0  # noqa: E731
+        print(f"  k_mlp_fwd blk0 : stage {um(0, 1):7.1f}  tile1 {um(1, 2):7.1f}  rest {um(2, 3):7.1f}")
+        print(f"  k_mlp_fwd last : stage {um(4, 5):7.1f}  tile1 {um(5, 6):7.1f}  rest {um(6, 7):7.1f}  "
+              f"start-lag {(m[4] - m[0]) / 100.0:7.1f}  end-lag {(m[7] - m[3]) / 100.0:7.1f}")
 
 
 if __name__ == "__main__":
