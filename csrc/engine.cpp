@@ -252,6 +252,46 @@ class Engine {
     HIP_OK(hipMemcpy(S.drop_step.p, &drop_step, sizeof(int), hipMemcpyHostToDevice));
   }
 
+  // Bookkeeping state of a model (resume files): epoch counters, per-phase best trackers,
+  // snapshot flags, the two best-model snapshots and the history rows written so far.
+  py::dict get_tracker_state(int g) {
+    ModelState& S = models_[check_g(g)];
+    py::dict d;
+    int ep[2], fl[2];
+    float best[3];
+    sync();
+    HIP_OK(hipMemcpy(ep, S.ep.p, sizeof(ep), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(fl, S.snap_flags.p, sizeof(fl), hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(best, S.best.p, sizeof(best), hipMemcpyDeviceToHost));
+    d["epoch"] = ep[0]; d["epoch_in_phase"] = ep[1];
+    d["snap_loss_taken"] = fl[0]; d["snap_sharpe_taken"] = fl[1];
+    d["best_loss"] = best[0]; d["best_sharpe"] = best[1]; d["best_moment"] = best[2];
+    d["snap_loss"] = down(S.snap_loss); d["snap_sharpe"] = down(S.snap_sharpe);
+    py::array_t<float> h({ep[0], (int)HIST_W});
+    if (ep[0]) HIP_OK(hipMemcpy(h.mutable_data(), S.hist.p, (size_t)ep[0] * HIST_W * 4, hipMemcpyDeviceToHost));
+    d["hist"] = h;
+    return d;
+  }
+  void set_tracker_state(int g, int epoch, int epoch_in_phase, int snap_loss_taken, int snap_sharpe_taken,
+                         float best_loss, float best_sharpe, float best_moment,
+                         py::array_t<float, py::array::c_style> snap_loss,
+                         py::array_t<float, py::array::c_style> snap_sharpe,
+                         py::array_t<float, py::array::c_style> hist) {
+    ModelState& S = models_[check_g(g)];
+    if (epoch < 0 || epoch > max_epochs_) throw std::invalid_argument("epoch count exceeds max_epochs");
+    if (snap_loss.size() != md_.P || snap_sharpe.size() != md_.P) throw std::invalid_argument("snapshot size");
+    if (hist.size() != (size_t)epoch * HIST_W) throw std::invalid_argument("history size");
+    sync();
+    int ep[2] = {epoch, epoch_in_phase}, fl[2] = {snap_loss_taken, snap_sharpe_taken};
+    float best[3] = {best_loss, best_sharpe, best_moment};
+    HIP_OK(hipMemcpy(S.ep.p, ep, sizeof(ep), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(S.snap_flags.p, fl, sizeof(fl), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(S.best.p, best, sizeof(best), hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(S.snap_loss.p, snap_loss.data(), md_.P * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(S.snap_sharpe.p, snap_sharpe.data(), md_.P * 4, hipMemcpyHostToDevice));
+    if (epoch) HIP_OK(hipMemcpy(S.hist.p, hist.data(), (size_t)epoch * HIST_W * 4, hipMemcpyHostToDevice));
+  }
+
   // ---------------------------------------------------------------- phase control -------
   // Reset the per-phase trackers (reference: fresh best values per phase).
   void begin_phase(int phase) {
@@ -872,6 +912,8 @@ PYBIND11_MODULE(_dlap_hip, m) {
       .def("set_seed", &Engine::set_seed)
       .def("get_opt_state", &Engine::get_opt_state)
       .def("set_opt_state", &Engine::set_opt_state)
+      .def("get_tracker_state", &Engine::get_tracker_state)
+      .def("set_tracker_state", &Engine::set_tracker_state)
       .def("begin_phase", &Engine::begin_phase)
       .def("snap_flags", &Engine::snap_flags)
       .def("epoch_count", &Engine::epoch_count)

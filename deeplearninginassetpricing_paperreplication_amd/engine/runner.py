@@ -142,14 +142,28 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
                      num_epochs_unc=256, num_epochs_moment=64, num_epochs=1024, lr=1e-3,
                      print_freq=128, save_dir=None, ignore_epoch=64, seed=None,
                      precision="bf16", selection_sign=1.0, verbose=True, n_models=1,
-                     models=None, seeds=None, save_dirs=None, lrs=None):
+                     models=None, seeds=None, save_dirs=None, lrs=None, resume=False,
+                     resume_path=None, nan_policy="warn", stop_after=None):
     """GPU executor of the 3-phase schedule; with ``n_models > 1`` trains an ensemble batch.
 
     Returns ``(model, history)`` for a single model, or ``(models, histories)`` when
     ``n_models > 1`` (``models``/``seeds``/``save_dirs`` give per-member inputs; ``lrs`` gives
     per-member learning rates, e.g. the lr axis of a hyperparameter sweep).
+
+    Fault tolerance (additions, see ``utils``):
+      resume_path -- where the resume record is written at every print boundary and phase end
+                     (default ``save_dir/resume.pt`` for a single model with a ``save_dir``);
+      resume      -- continue from an existing record at ``resume_path`` (bit-identical to an
+                     uninterrupted run: parameters, Adam state, dropout stream and trackers);
+      nan_policy  -- 'warn' | 'raise' | 'ignore' for non-finite losses / gradient norms,
+                     checked at the print boundaries (``history['nonfinite_epoch']``);
+      stop_after  -- (phase, epochs) : stop once that many epochs of that phase are done
+                     (used to test interruption; the resume record is written first).
     """
     from ..models.gan import AssetPricingGAN
+    from ..utils import checkpoint as ckpt
+    from ..utils.guards import NonFiniteMonitor
+    from ..utils.tracing import Timers, trace_range
     if precision != "bf16":
         raise NotImplementedError("the native engine currently computes the tower GEMMs in bf16 "
                                   "(fp32 accumulation / master weights); use the CPU path for fp32")
@@ -163,6 +177,7 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
     if seeds is None:
         base = torch.initial_seed() if seed is None else seed
         seeds = [int(base) + 7919 * g for g in range(n_models)]
+    seeds = [int(x) for x in seeds]
     if save_dirs is None:
         save_dirs = [save_dir] * n_models if n_models == 1 else [None] * n_models
     spec = models[0].spec
@@ -180,23 +195,64 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
     template = AssetPricingGAN(config)
     t_start = time.time()
     best_state = [False] * n_models
+    schedule = (num_epochs_unc, num_epochs_moment, num_epochs)
+    if resume_path is None and n_models == 1 and save_dirs[0]:
+        resume_path = os.path.join(save_dirs[0], ckpt.RESUME_FILE)
+    timers = Timers()
+    monitor = NonFiniteMonitor(n_models, HIST, nan_policy)
+    start = (1, 0)                  # (phase, epochs done in it) to continue from
+    if resume and resume_path:
+        rec = ckpt.load_resume(resume_path, spec, schedule)
+        if rec is not None:
+            if len(rec["models"]) != n_models:
+                raise ValueError(f"{resume_path}: {len(rec['models'])} models, expected {n_models}")
+            for g, st in enumerate(rec["models"]):
+                ckpt.restore_model(eng.eng, g, st)
+                seeds[g] = int(st["seed"])
+            best_state = list(rec["best_state"])
+            start = (int(rec["phase"]), int(rec["done"]))
+            t_start -= float(rec["elapsed"])
+            say(f"Resumed from {resume_path}: phase {start[0]}, {start[1]} epochs done")
+
+    def write_resume(phase, done):
+        if not resume_path:
+            return
+        with trace_range("resume-checkpoint", timers):
+            lr_of = (lambda g: lrs[g]) if lrs is not None else (lambda g: None)
+            ckpt.save_resume(resume_path, spec=spec, phase=phase, done=done, schedule=schedule,
+                             models=[ckpt.capture_model(eng.eng, g, seeds[g], lr_of(g)) for g in range(n_models)],
+                             best_state=best_state, elapsed=time.time() - t_start)
+
+    class _Stop(Exception):
+        pass
 
     def run_phase(phase, n, title, tag):
+        if phase < start[0]:
+            return
         if verbose:
             print("\n" + "=" * 70 + f"\n{title}\nEpochs: {n}\n" + "=" * 70 + "\n")
-        eng.eng.begin_phase(phase)
-        done = 0
-        ep0 = eng.eng.epoch_count(0)
+        done = start[1] if phase == start[0] else 0
+        if done == 0:
+            eng.eng.begin_phase(phase)
+        ep0 = eng.eng.epoch_count(0) - done
         marks = sorted({0} | set(range(print_freq - 1, n, print_freq)) | {n - 1}) if n > 0 else []
+        if stop_after is not None and stop_after[0] == phase and 0 < stop_after[1] < n:
+            marks = sorted(set(marks) | {stop_after[1] - 1})
         for mk in marks:
             k = mk + 1 - done
             if k <= 0:
                 continue
             t0 = time.time()
-            eng.run(phase, k, lr, ignore_epoch, selection_sign)
-            eng.eng.sync()
+            with trace_range(f"phase{phase}-epochs", timers):
+                eng.run(phase, k, lr, ignore_epoch, selection_sign)
+                eng.eng.sync()
             dt = (time.time() - t0) / k
             done = mk + 1
+            for g in range(n_models):
+                monitor.check(g, eng.history_rows(g), raise_ok=n_models == 1)
+            write_resume(phase, done)
+            if stop_after is not None and tuple(stop_after) == (phase, done):
+                raise _Stop()
             if verbose and ((mk + 1) % print_freq == 0 or mk == 0):
                 r = eng.history_rows(0)[ep0 + mk]
                 if phase == 2:
@@ -220,16 +276,25 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
                 if fl[1]:
                     _save_sd(eng, g, "sharpe", os.path.join(d, "best_model_sharpe.pt"), template)
 
-    run_phase(1, num_epochs_unc, "PHASE 1: Training Unconditional Loss (E[w*R]^2)", "unc")
-    say("\nPhase 1 Complete!")
-    for g in range(n_models):
-        if best_state[g]:
-            eng.eng.load_snapshot(g, 1)
-    if best_state[0]:
-        say("Loaded best model from Phase 1")
-    run_phase(2, num_epochs_moment, "PHASE 2: Updating Moment Conditions", "mom")
-    say("\nPhase 2 Complete!")
-    run_phase(3, num_epochs, "PHASE 3: Training Conditional Loss (E[h*w*R]^2)", "cond")
+    try:
+        run_phase(1, num_epochs_unc, "PHASE 1: Training Unconditional Loss (E[w*R]^2)", "unc")
+        if start[0] <= 1:
+            say("\nPhase 1 Complete!")
+            for g in range(n_models):
+                if best_state[g]:
+                    eng.eng.load_snapshot(g, 1)
+            if best_state[0]:
+                say("Loaded best model from Phase 1")
+            write_resume(2, 0)
+        run_phase(2, num_epochs_moment, "PHASE 2: Updating Moment Conditions", "mom")
+        if start[0] <= 2:
+            say("\nPhase 2 Complete!")
+            write_resume(3, 0)
+        run_phase(3, num_epochs, "PHASE 3: Training Conditional Loss (E[h*w*R]^2)", "cond")
+    except _Stop:
+        say(f"Stopped after {tuple(stop_after)}; resume record at {resume_path}")
+        train_3phase_gpu.last_engine = eng
+        return None
     elapsed = time.time() - t_start
     for g in range(n_models):
         if best_state[g]:
@@ -257,6 +322,8 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
         out_models.append(m)
     train_3phase_gpu.last_engine = eng
     train_3phase_gpu.last_elapsed = elapsed
+    train_3phase_gpu.last_timers = timers
+    train_3phase_gpu.last_nonfinite = monitor.nonfinite_models
     if n_models == 1:
         return out_models[0], hists[0]
     return out_models, hists

@@ -1,7 +1,8 @@
 """``python -m src.train`` command line (flags and defaults of `/root/reference/src/train.py:429-605`).
 
 Additions (never changing reference defaults): ``--device``, ``--precision``,
-``--selection_sign``, ``--resume_dir`` is not needed (checkpoints are final-state only).
+``--selection_sign``, ``--resume`` (continue from ``save_dir/resume.pt``, which every run
+writes at print boundaries and phase ends), ``--nan_policy``.
 """
 from __future__ import annotations
 
@@ -48,6 +49,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--precision", type=str, default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--selection_sign", type=float, default=1.0,
                    help="+1: reference (un-negated Sharpe); -1: paper sign")
+    p.add_argument("--resume", action="store_true",
+                   help="continue an interrupted run from save_dir/resume.pt")
+    p.add_argument("--nan_policy", type=str, default="warn", choices=["warn", "raise", "ignore"],
+                   help="non-finite train loss / grad norm handling")
     return p
 
 
@@ -106,7 +111,8 @@ def main(argv=None):
                                   num_epochs=args.epochs, lr=args.lr, print_freq=args.print_freq,
                                   save_dir=args.save_dir, ignore_epoch=args.ignore_epoch,
                                   save_best_freq=args.save_best_freq, seed=args.seed,
-                                  precision=args.precision, selection_sign=args.selection_sign)
+                                  precision=args.precision, selection_sign=args.selection_sign,
+                                  resume=args.resume, nan_policy=args.nan_policy)
     save_history(history, args.save_dir)
     print(f"\nCheckpoints saved to {args.save_dir}")
     return model, history

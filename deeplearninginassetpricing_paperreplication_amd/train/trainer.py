@@ -116,7 +116,8 @@ def train_3phase(config: dict, train_data: dict, valid_data: dict, test_data: di
                  print_freq: int = 128, save_dir: str = None, ignore_epoch: int = 64,
                  save_best_freq: int = 128, *, seed: Optional[int] = None,
                  precision: str = "bf16", selection_sign: float = 1.0,
-                 verbose: bool = True):
+                 verbose: bool = True, resume: bool = False, resume_path: Optional[str] = None,
+                 nan_policy: str = "warn", stop_after=None):
     """Train with the 3-phase schedule; returns ``(model, history)``.
 
     Extra keyword-only knobs (additions, defaults keep reference behaviour):
@@ -124,7 +125,12 @@ def train_3phase(config: dict, train_data: dict, valid_data: dict, test_data: di
       precision       -- GPU GEMM input precision, 'bf16' (fp32 accumulate/master) or 'fp32'
       selection_sign  -- +1 selects the best epoch by the un-negated Sharpe (reference);
                          −1 by the paper-convention Sharpe of the SDF factor −w·R
-    ``save_best_freq`` is accepted and unused, as in the reference.
+      resume          -- continue from ``resume_path`` (default ``save_dir/resume.pt``), which
+                         both executors write at every print boundary and phase end
+      nan_policy      -- 'warn' | 'raise' | 'ignore' for non-finite train loss / grad norm
+      stop_after      -- (phase, epochs): stop early after writing the resume record (tests)
+    ``save_best_freq`` is accepted and unused, as in the reference. Returns None when
+    ``stop_after`` stopped the run.
     """
     if device is None:
         device = torch.device("cuda" if torch.cuda.is_available() else "cpu")
@@ -138,14 +144,25 @@ def train_3phase(config: dict, train_data: dict, valid_data: dict, test_data: di
                                 num_epochs=num_epochs, lr=lr, print_freq=print_freq,
                                 save_dir=save_dir, ignore_epoch=ignore_epoch, seed=seed,
                                 precision=precision, selection_sign=selection_sign,
-                                verbose=verbose)
+                                verbose=verbose, resume=resume, resume_path=resume_path,
+                                nan_policy=nan_policy, stop_after=stop_after)
     return _train_3phase_cpu(config, train_data, valid_data, test_data, device, num_epochs_unc,
                              num_epochs_moment, num_epochs, lr, print_freq, save_dir,
-                             ignore_epoch, selection_sign, verbose)
+                             ignore_epoch, selection_sign, verbose, resume, resume_path,
+                             nan_policy, stop_after)
+
+
+class _Stop(Exception):
+    pass
 
 
 def _train_3phase_cpu(config, train_data, valid_data, test_data, device, n_unc, n_mom, n_cond,
-                      lr, print_freq, save_dir, ignore_epoch, sel, verbose):
+                      lr, print_freq, save_dir, ignore_epoch, sel, verbose, resume=False,
+                      resume_path=None, nan_policy="warn", stop_after=None):
+    from ..utils.guards import NonFiniteError, POLICIES
+    import warnings
+    if nan_policy not in POLICIES:
+        raise ValueError(f"nan_policy must be one of {POLICIES}")
     say = print if verbose else (lambda *a, **k: None)
     model = AssetPricingGAN(config).to(device)
     n_sdf = sum(p.numel() for p in model.sdf_net.parameters())
@@ -157,13 +174,61 @@ def _train_3phase_cpu(config, train_data, valid_data, test_data, device, n_unc, 
     opt_mom = optim.Adam(model.moment_net.parameters(), lr=lr)
     hist = {k: [] for k in ("train_loss", "train_sharpe", "valid_loss", "valid_sharpe",
                             "test_loss", "test_sharpe", "phase")}
-    best_state = None
-    t0 = time.time()
+    # schedule position + trackers (everything a resume record must carry)
+    st = {"phase": 1, "done": 0, "best_loss": float("inf"), "best_sr": float("-inf"),
+          "best_m": float("-inf"), "best_state": None, "elapsed": 0.0, "nonfinite": -1}
+    schedule = [int(n_unc), int(n_mom), int(n_cond)]
+    if resume_path is None and save_dir:
+        resume_path = os.path.join(save_dir, "resume.pt")
+    if resume and resume_path and os.path.isfile(resume_path):
+        rec = torch.load(resume_path, map_location="cpu", weights_only=True)
+        if rec.get("executor") != "cpu" or list(rec["schedule"]) != schedule:
+            raise ValueError(f"{resume_path}: not a CPU resume record of schedule {schedule}")
+        model.load_state_dict(rec["model"])
+        opt_sdf.load_state_dict(rec["opt_sdf"])
+        opt_mom.load_state_dict(rec["opt_mom"])
+        hist = {k: list(v) for k, v in rec["hist"].items()}
+        st.update(rec["state"])
+        torch.set_rng_state(rec["rng"])
+        say(f"Resumed from {resume_path}: phase {st['phase']}, {st['done']} epochs done")
+    t0 = time.time() - st["elapsed"]
 
-    def run_sdf_phase(n, phase, tag, loss_key):
-        nonlocal best_state
-        best_loss, best_sr = float("inf"), float("-inf")
-        for e in range(n):
+    def write_resume():
+        if not resume_path:
+            return
+        st["elapsed"] = time.time() - t0
+        rec = {"executor": "cpu", "schedule": schedule, "model": model.state_dict(),
+               "opt_sdf": opt_sdf.state_dict(), "opt_mom": opt_mom.state_dict(),
+               "hist": hist, "state": dict(st), "rng": torch.get_rng_state()}
+        tmp = resume_path + ".tmp"
+        torch.save(rec, tmp)
+        os.replace(tmp, resume_path)
+
+    def check_finite(e, tr):
+        if nan_policy == "ignore" or st["nonfinite"] >= 0:
+            return
+        for field in ("loss", "grad_norm"):
+            if not np.isfinite(tr[field]):
+                st["nonfinite"] = len(hist["train_loss"]) - 1
+                if nan_policy == "raise":
+                    raise NonFiniteError(0, e, "train_loss" if field == "loss" else field)
+                warnings.warn(f"non-finite {field} at epoch {e + 1}", RuntimeWarning)
+                return
+
+    def boundary(phase, e, n):
+        """After epoch e of a phase: resume record at print boundaries / phase end."""
+        st["phase"], st["done"] = phase, e + 1
+        if (e + 1) % print_freq == 0 or e + 1 == n:
+            write_resume()
+        if stop_after is not None and tuple(stop_after) == (phase, e + 1):
+            write_resume()
+            raise _Stop()
+
+    def run_sdf_phase(n, phase_id, phase, tag, loss_key):
+        start = st["done"] if st["phase"] == phase_id else 0
+        if start == 0:
+            st["best_loss"], st["best_sr"] = float("inf"), float("-inf")
+        for e in range(start, n):
             te0 = time.time()
             tr = train_epoch(model, opt_sdf, train_data, device, phase=phase, scope="sdf")
             va = evaluate(model, valid_data, device)
@@ -173,52 +238,64 @@ def _train_3phase_cpu(config, train_data, valid_data, test_data, device, n_unc, 
             hist["valid_loss"].append(va[loss_key]); hist["valid_sharpe"].append(va["sharpe"])
             if te is not None:
                 hist["test_loss"].append(te[loss_key]); hist["test_sharpe"].append(te["sharpe"])
+            check_finite(e, tr)
             if e > ignore_epoch:
-                if va[loss_key] < best_loss:
-                    best_loss = va[loss_key]
+                if va[loss_key] < st["best_loss"]:
+                    st["best_loss"] = va[loss_key]
                     _save(model, save_dir, "best_model_loss.pt")
-                if sel * va["sharpe"] > best_sr:
-                    best_sr = sel * va["sharpe"]
-                    best_state = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+                if sel * va["sharpe"] > st["best_sr"]:
+                    st["best_sr"] = sel * va["sharpe"]
+                    st["best_state"] = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
                     _save(model, save_dir, "best_model_sharpe.pt")
             if (e + 1) % print_freq == 0 or e == 0:
                 say(_fmt_line(e, n, time.time() - te0, tr, va, te, loss_key))
-        return best_sr
+            boundary(phase_id, e, n)
+        return st["best_sr"]
 
-    _print_header("PHASE 1: Training Unconditional Loss (E[w*R]^2)", n_unc) if verbose else None
-    b1 = run_sdf_phase(n_unc, "unconditional", "unc", "loss_unc")
-    say("\nPhase 1 Complete!")
-    say(f"Best validation Sharpe (phase 1): {sel * b1:.4f}")
-    if best_state is not None:
-        model.load_state_dict(best_state)
-        say("Loaded best model from Phase 1")
+    try:
+        if st["phase"] == 1:
+            _print_header("PHASE 1: Training Unconditional Loss (E[w*R]^2)", n_unc) if verbose else None
+            b1 = run_sdf_phase(n_unc, 1, "unconditional", "unc", "loss_unc")
+            say("\nPhase 1 Complete!")
+            say(f"Best validation Sharpe (phase 1): {sel * b1:.4f}")
+            if st["best_state"] is not None:
+                model.load_state_dict(st["best_state"])
+                say("Loaded best model from Phase 1")
+            st["phase"], st["done"], st["best_m"] = 2, 0, float("-inf")
+            write_resume()
 
-    _print_header("PHASE 2: Updating Moment Conditions", n_mom) if verbose else None
-    best_m = float("-inf")
-    for p in model.sdf_net.parameters():
-        p.requires_grad_(False)
-    for e in range(n_mom):
-        te0 = time.time()
-        tr = train_epoch(model, opt_mom, train_data, device, phase="moment", scope="moment")
-        if tr["loss_cond"] > best_m:
-            best_m = tr["loss_cond"]
-            _save(model, save_dir, "best_model_loss.pt")
-        if (e + 1) % print_freq == 0 or e == 0:
-            say(f"Epoch {e + 1:4d}/{n_mom} ({time.time() - te0:.1f}s) | Conditional loss: {tr['loss_cond']:.6f}")
-    for p in model.sdf_net.parameters():
-        p.requires_grad_(True)
-    say("\nPhase 2 Complete!")
+        if st["phase"] == 2:
+            _print_header("PHASE 2: Updating Moment Conditions", n_mom) if verbose else None
+            for p in model.sdf_net.parameters():
+                p.requires_grad_(False)
+            for e in range(st["done"], n_mom):
+                te0 = time.time()
+                tr = train_epoch(model, opt_mom, train_data, device, phase="moment", scope="moment")
+                if tr["loss_cond"] > st["best_m"]:
+                    st["best_m"] = tr["loss_cond"]
+                    _save(model, save_dir, "best_model_loss.pt")
+                if (e + 1) % print_freq == 0 or e == 0:
+                    say(f"Epoch {e + 1:4d}/{n_mom} ({time.time() - te0:.1f}s) | Conditional loss: {tr['loss_cond']:.6f}")
+                boundary(2, e, n_mom)
+            for p in model.sdf_net.parameters():
+                p.requires_grad_(True)
+            say("\nPhase 2 Complete!")
+            st["phase"], st["done"] = 3, 0
+            write_resume()
 
-    # Phase 3: the moment net is never stepped again; freezing it skips dead gradient work.
-    for p in model.moment_net.parameters():
-        p.requires_grad_(False)
-    _print_header("PHASE 3: Training Conditional Loss (E[h*w*R]^2)", n_cond) if verbose else None
-    run_sdf_phase(n_cond, "conditional", "cond", "loss_cond")
-    for p in model.moment_net.parameters():
-        p.requires_grad_(True)
+        # Phase 3: the moment net is never stepped again; freezing it skips dead gradient work.
+        for p in model.moment_net.parameters():
+            p.requires_grad_(False)
+        _print_header("PHASE 3: Training Conditional Loss (E[h*w*R]^2)", n_cond) if verbose else None
+        run_sdf_phase(n_cond, 3, "conditional", "cond", "loss_cond")
+        for p in model.moment_net.parameters():
+            p.requires_grad_(True)
+    except _Stop:
+        say(f"Stopped after {tuple(stop_after)}; resume record at {resume_path}")
+        return None
     total = time.time() - t0
-    if best_state is not None:
-        model.load_state_dict(best_state)
+    if st["best_state"] is not None:
+        model.load_state_dict(st["best_state"])
     say("\n" + "=" * 70 + "\nTraining Complete!")
     say(f"Total time: {total / 60:.1f} minutes")
     say(f"Total epochs: {n_unc + n_mom + n_cond} ({n_unc} + {n_mom} + {n_cond})\n" + "=" * 70)

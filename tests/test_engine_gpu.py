@@ -256,3 +256,47 @@ def test_cli_and_ensemble_driver_on_gpu(tmp_path):
                        ignore_epoch=0, save_root=str(tmp_path / "ens"))
     assert res["failed"] == [] and np.isfinite(res["test_sharpe"])
     assert (tmp_path / "ens" / "seed_2" / "best_model_sharpe.pt").exists()
+
+
+@pytest.mark.parametrize("stop", [(1, 3), (2, 1), (3, 4)])
+def test_gpu_resume_equals_uninterrupted(tmp_path, stop):
+    """An interrupted GPU run continued from resume.pt reproduces the uninterrupted run
+    bitwise (parameters, Adam state, dropout stream, trackers, history, checkpoint files)."""
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import train_3phase_gpu
+    b = _batch(T=30, N=120)
+    cfg = default_cli_config(8, 46)
+    kw = dict(num_epochs_unc=5, num_epochs_moment=3, num_epochs=6, print_freq=2, ignore_epoch=0,
+              seed=11, verbose=False)
+    out = {}
+    for name, extra in (("a", {}), ("b", {"stop_after": stop})):
+        d = tmp_path / name
+        d.mkdir()
+        torch.manual_seed(0)
+        out[name] = train_3phase_gpu(cfg, b, b, b, save_dir=str(d), **kw, **extra)
+    assert out["b"] is None and (tmp_path / "b" / "resume.pt").exists()
+    torch.manual_seed(0)
+    mb, hb = train_3phase_gpu(cfg, b, b, b, save_dir=str(tmp_path / "b"), resume=True, **kw)
+    ma, ha = out["a"]
+    for k in ha:
+        assert np.array_equal(np.nan_to_num(np.array(ha[k], dtype=object if k == "phase" else float)),
+                              np.nan_to_num(np.array(hb[k], dtype=object if k == "phase" else float))), k
+    for k, v in ma.state_dict().items():
+        assert torch.equal(v.cpu(), mb.state_dict()[k].cpu()), k
+    for f in ("best_model_sharpe.pt", "best_model_loss.pt", "final_model.pt"):
+        sa = torch.load(tmp_path / "a" / f, weights_only=True)
+        sb = torch.load(tmp_path / "b" / f, weights_only=True)
+        assert all(torch.equal(sa[k], sb[k]) for k in sa), f
+
+
+def test_gpu_nonfinite_guard(tmp_path):
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import train_3phase_gpu
+    from deeplearninginassetpricing_paperreplication_amd.utils.guards import NonFiniteError
+    b = _batch(T=20, N=96)
+    b["individual_features"] = b["individual_features"].clone()
+    b["individual_features"][3, 5, 0] = float("inf")
+    b["mask"] = b["mask"].clone()
+    b["mask"][3, 5] = True
+    cfg = default_cli_config(8, 46)
+    with pytest.raises(NonFiniteError):
+        train_3phase_gpu(cfg, b, b, b, num_epochs_unc=3, num_epochs_moment=1, num_epochs=2,
+                         print_freq=100, ignore_epoch=0, seed=1, verbose=False, nan_policy="raise")
