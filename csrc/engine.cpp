@@ -97,7 +97,7 @@ class Engine {
          std::vector<int> mom_hidden, int K, float dropout, bool normalize_w, bool weighted,
          float residual, int G, int max_epochs)
       : G_(G), max_epochs_(max_epochs) {
-    unroll_ = std::max(1, env_int("DLAP_UNROLL", 4));
+    unroll_ = std::max(1, env_int("DLAP_UNROLL", 1));
     prio_ = env_int("DLAP_PRIO", 0) != 0;
     if (prio_) {   // the training chain (critical path) ahead of the evaluation branch
       int lo = 0, hi = 0;
@@ -111,6 +111,9 @@ class Engine {
     HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_mid_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_a_, hipEventDisableTiming));
+    eval_gx_ = env_int("DLAP_EVAL_GX", 0);
+    b_wait_ = env_int("DLAP_B_WAIT", 0);
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
                residual);
     d_desc_.alloc(sizeof(ModelDesc));
@@ -133,6 +136,7 @@ class Engine {
     if (ev_fork_) (void)hipEventDestroy(ev_fork_);
     if (ev_join_) (void)hipEventDestroy(ev_join_);
     if (ev_mid_) (void)hipEventDestroy(ev_mid_);
+    if (ev_a_) (void)hipEventDestroy(ev_a_);
     if (st2_) (void)hipStreamDestroy(st2_);
     if (st_) (void)hipStreamDestroy(st_);
   }
@@ -414,10 +418,12 @@ class Engine {
  private:
   int G_, max_epochs_;
   hipStream_t st_ = nullptr;
-  int unroll_ = 4;                           // pipelined epochs per graph launch (DLAP_UNROLL)
+  int unroll_ = 1;                           // pipelined epochs per graph launch (DLAP_UNROLL)
   bool prio_ = false;                        // stream/node priorities (DLAP_PRIO)
   hipStream_t st2_ = nullptr;                // evaluation branch of the pipelined epoch graph
-  hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr, ev_mid_ = nullptr;
+  hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr, ev_mid_ = nullptr, ev_a_ = nullptr;
+  int eval_gx_ = 0;                          // cap on the evaluation tower grid (DLAP_EVAL_GX)
+  int b_wait_ = 0;                           // evaluation towers after train towers (DLAP_B_WAIT)
   ModelDesc md_{};
   DevBuf<char> d_desc_;
   SplitDev splits_[3];
@@ -786,11 +792,15 @@ class Engine {
   // side: if non-null, the train split's Sharpe monitor (not needed by the backward) runs
   // on that stream after the asset pass; the caller joins it before the bookkeeping copy.
   // premasked: this step's keep masks were generated by the previous epoch graph.
-  void enqueue_train_grads(int phase, hipStream_t side = nullptr, bool premasked = false) {
+  // mark: record ev_a_ after the tower backward (1) or the tower forward (2);
+  // part1_only: stop before the gradient finalisation (the caller enqueues the tail).
+  void enqueue_train_grads(int phase, hipStream_t side = nullptr, bool premasked = false, int mark = 0,
+                           bool part1_only = false) {
     const SplitDev& D = splits_[0];
     if (!premasked) enqueue_dropmask(phase, 0, st_);
     launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_);
     launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, gx_fwd_[0], md_.md, md_.KS1, md_.WMB, st_);
+    if (mark == 2) HIP_OK(hipEventRecord(ev_a_, st_));
     launch_period_fwd(as<LossJob>(j_loss_train_[phase]), G_, D.T, st_);
     launch_asset(as<LossJob>(j_loss_train_[phase]), G_, D.N, st_);
     if (side) {
@@ -808,6 +818,12 @@ class Engine {
       launch_mlp_bwd_sdf(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_s, md_.tps_s, md_.md, md_.KS1,
                          slab_stride(), st_);
     }
+    if (mark == 1) HIP_OK(hipEventRecord(ev_a_, st_));
+    if (part1_only) return;
+    enqueue_train_tail(phase);
+  }
+  void enqueue_train_tail(int phase) {
+    const SplitDev& D = splits_[0];
     launch_finalize(as<FinJob>(j_fin_), G_, dd(), md_, phase, slab_stride(), D.T, st_);
     launch_lstm_bwd(as<UpdJob>(j_upd_), G_, dd(), md_, D.T, phase, st_);
   }
@@ -816,9 +832,17 @@ class Engine {
     launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);
   }
   void enqueue_eval(hipStream_t st) {
+    enqueue_eval_prologue(st);
+    enqueue_eval_towers(st);
+  }
+  void enqueue_eval_prologue(hipStream_t st) {
     if (n_eval_jobs_ == 0) return;
     launch_prologue(as<RnnJob>(j_rnn_eval_), n_eval_jobs_, tmax_eval_, dd(), md_, st);
+  }
+  void enqueue_eval_towers(hipStream_t st) {
+    if (n_eval_jobs_ == 0) return;
     int gx = std::max(gx_fwd_[1], gx_fwd_[2]);
+    if (eval_gx_ > 0) gx = std::min(gx, eval_gx_);
     launch_mlp_fwd(as<MlpJob>(j_mlp_eval_), n_eval_jobs_, gx, md_.md, md_.KS1, md_.WMB, st);
     launch_period_fwd(as<LossJob>(j_loss_eval_), n_eval_jobs_, tmax_eval_, st);
     launch_asset(as<LossJob>(j_loss_eval_), n_eval_jobs_, nmax_eval_, st);
@@ -843,10 +867,22 @@ class Engine {
   void enqueue_pipe(int phase, float lr, int ignore_epoch, float sel) {
     HIP_OK(hipEventRecord(ev_fork_, st_));
     HIP_OK(hipStreamWaitEvent(st2_, ev_fork_, 0));
-    enqueue_eval(st2_);                                   // previous epoch's evaluation
-    enqueue_epoch_end(phase, ignore_epoch, sel, st2_);    // ... and its bookkeeping
-    enqueue_dropmask(phase, 1, st2_);                     // next epoch's dropout masks
-    enqueue_train_grads(phase, st2_, true);               // this epoch's forward/backward
+    if (b_wait_ == 0) {
+      enqueue_eval(st2_);                                 // previous epoch's evaluation
+      enqueue_epoch_end(phase, ignore_epoch, sel, st2_);  // ... and its bookkeeping
+      enqueue_dropmask(phase, 1, st2_);                   // next epoch's dropout masks
+      enqueue_train_grads(phase, st2_, true);             // this epoch's forward/backward
+    } else {
+      // the evaluation towers start once the training towers (b_wait_ 1: backward, 2:
+      // forward) are done, so the wide kernels of the two branches do not contend
+      enqueue_eval_prologue(st2_);
+      enqueue_train_grads(phase, st2_, true, b_wait_, true);
+      HIP_OK(hipStreamWaitEvent(st2_, ev_a_, 0));
+      enqueue_eval_towers(st2_);
+      enqueue_epoch_end(phase, ignore_epoch, sel, st2_);
+      enqueue_dropmask(phase, 1, st2_);
+      enqueue_train_tail(phase);
+    }
     HIP_OK(hipEventRecord(ev_join_, st2_));               // (train monitor ran on st2_ too)
     HIP_OK(hipStreamWaitEvent(st_, ev_join_, 0));
     launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);

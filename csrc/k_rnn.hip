@@ -230,6 +230,11 @@ __global__ __launch_bounds__(64) void k_lstm(const RnnJob* __restrict__ jobs,
 // the g rows) instead of four per unit lane; the f/g/o values are then gathered onto the unit
 // lanes (DPP row rotates when 4H <= 16, ds_bpermute otherwise). ~3x fewer instructions on
 // the serial chain than the unit-per-lane form. EXACT = HM is H itself (DPP offsets need it).
+template <int CTRL>
+DLAP_DEV float dppf(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
+}
+
 template <int HM, bool DPPG>
 DLAP_DEV float gl_gather(float y, int off_units, int q) {
   if constexpr (DPPG) {
@@ -345,6 +350,134 @@ __global__ __launch_bounds__(64) void k_lstm_gl(const RnnJob* __restrict__ jobs,
   RNN_TS(tsb + 3, tsm);
 }
 
+// ---------------------------------------------------------------------- k_lstm_gls -----
+// k_lstm_gl with every per-step output kept in LDS: the serial loop is branch-free (all 64
+// lanes run the same instructions, results on non-owner lanes are discarded with selects and
+// go to a junk slot) and issues three ds_write per step instead of up to four exec-masked
+// global stores. The saved gates / cells / outputs are flushed to global memory once per
+// layer with coalesced stores; a deeper layer reads its input from the LDS ring directly.
+// Tanh of the g gate and of the cell use 2 sigm(2x) - 1 without the small-|x| Taylor switch:
+// its absolute error (~1e-7) is at fp32 rounding level for the cell update.
+// LDS (floats): xg [T][4H] | gates [T][4H] | cells [T][H] | outputs 2 x [T][H] | junk [64].
+static inline size_t gls_lds_floats(int T, int H) { return (size_t)T * (8 * H + 3 * H) + 64; }
+
+template <int HM, bool DPPG>
+__global__ __launch_bounds__(64) void k_lstm_gls(const RnnJob* __restrict__ jobs,
+                                                 const ModelDesc* __restrict__ md) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const RnnJob& J = jobs[blockIdx.x];
+  const int nrnn = md->nrnn;
+  if (nrnn == 0) return;
+  const int T = J.T, H = DPPG ? HM : md->H, G4 = 4 * H;
+  const int L = threadIdx.x;
+  const bool gl = L < G4, ul = L < H;
+  const int row = gl ? L : 0;
+  const bool is_g = gl && L >= 2 * H && L < 3 * H;
+  // Pre-scaled exponent domain: a gate row's pre-activation is carried as kx * pre with
+  // kx = -ka log2(e), so act = kb / (1 + exp2(.)) + kc needs no multiply on the chain. The
+  // cell is carried as c' = KC c (KC = -2 log2 e), so tanh(c) = 2 / (1 + exp2(c')) - 1; the
+  // g lanes produce KC g directly (kb, kc scaled by KC) so c' = f c' + i (KC g).
+  constexpr float LOG2E = 1.4426950408889634f;
+  constexpr float KC = -2.f * LOG2E;
+  const float kx = is_g ? -2.f * LOG2E : -LOG2E;
+  const float kb = is_g ? 2.f * KC : 1.f, kc = is_g ? -KC : 0.f;
+  const float ysave = is_g ? 1.f / KC : 1.f;      // saved gates are the unscaled activations
+  const bool drop = J.train && md->dropout > 0.f;
+  const uint32_t thr = (uint32_t)(md->dropout * 16777216.f + 0.5f);
+  const float scale = drop ? 1.f / (1.f - md->dropout) : 1.f;
+  const uint32_t step = J.step ? (uint32_t)*gp(J.step) : 0u;
+  const auto params = gp(J.params);
+  const bool save = J.sc != nullptr;
+  const int tsb = save ? 0 : 4;
+  const bool tsm = save || blockIdx.x == gridDim.x - 1;
+  RNN_TS(tsb + 0, tsm);
+  float* sx = sm;
+  float* sgb = sx + (size_t)T * G4;
+  float* scb = sgb + (size_t)T * G4;
+  float* shb0 = scb + (size_t)T * H;
+  float* junk = shb0 + (size_t)2 * T * H;
+  {
+    const auto xg = gp(J.xg);
+    for (int i = L; i < T * G4; i += 64) sx[i] = xg[i];
+  }
+  __syncthreads();
+  for (int l = 0; l < nrnn; ++l) {
+    float whh[HM], wih[HM];
+#pragma unroll
+    for (int j = 0; j < HM; ++j) {
+      const bool ok = gl && j < H;
+      const int jj = j < H ? j : 0;
+      const float a = params[md->lstm_w_hh[l] + row * H + jj];
+      const float b = l > 0 ? params[md->lstm_w_ih[l] + row * H + jj] : 0.f;
+      whh[j] = ok ? a * kx : 0.f;
+      wih[j] = ok ? b * kx : 0.f;
+    }
+    const float bb = l > 0 ? params[md->lstm_b_ih[l] + row] + params[md->lstm_b_hh[l] + row] : 0.f;
+    const float bias = gl ? bb * kx : 0.f;
+    if (l == 0) RNN_TS(tsb + 1, tsm);
+    float* shb = shb0 + (size_t)(l & 1) * T * H;            // this layer's outputs
+    const float* sin = shb0 + (size_t)((l + 1) & 1) * T * H; // previous layer's outputs
+    // per-lane LDS destinations (non-owner lanes write their junk slot)
+    float* gdst = gl ? sgb + L : junk + L;
+    float* udst_c = ul ? scb + L : junk + L;
+    float* udst_h = ul ? shb + L : junk + L;
+    const int gstride = gl ? G4 : 0, ustride = ul ? H : 0;
+    // h / c on lanes >= H are bounded garbage: the broadcast reads lanes j < HM only, and
+    // lanes H <= j < HM carry zero weights
+    float h = 0.f, c = 0.f;
+    auto cell = [&](int t, float pre) {
+      pre += bcast_dot<HM>(whh, h);
+      const float y = kb * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(pre)) + kc;
+      const float gf = gl_gather<HM, DPPG>(y, H, 1);
+      const float gg = gl_gather<HM, DPPG>(y, 2 * H, 2);
+      const float go = gl_gather<HM, DPPG>(y, 3 * H, 3);
+      c = gf * c + y * gg;                                  // y = i on the unit lanes
+      h = go * (2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(c)) - 1.f);
+      gdst[t * gstride] = y * ysave;
+      udst_c[t * ustride] = c * (1.f / KC);
+      udst_h[t * ustride] = h;
+    };
+    if (l == 0) {
+      float nx = sx[row] * kx;
+      for (int t = 0; t < T; ++t) {
+        const float pre = nx;
+        nx = sx[(t + 1 < T ? t + 1 : t) * G4 + row] * kx;   // next step's input, from LDS
+        cell(t, pre);
+      }
+    } else {
+      const uint32_t key_in = dropout_key(J.seed, step, 32 + (l - 1));
+      float nx = ul ? sin[L] : 0.f;
+      for (int t = 0; t < T; ++t) {
+        float xv = ul ? nx : 0.f;
+        nx = sin[(t + 1 < T ? t + 1 : t) * H + (ul ? L : 0)];
+        if (drop) xv = dropout_keep(key_in, (uint32_t)t, (uint32_t)(ul ? L : 0), thr) ? xv * scale : 0.f;
+        float pre = bias;
+#pragma unroll
+        for (int j = 0; j < HM; ++j)
+          pre += wih[j] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), j));
+        cell(t, pre);
+      }
+    }
+    if (l == 0) RNN_TS(tsb + 2, tsm);
+    __syncthreads();
+    // flush: saved gates / cells / outputs (train), tower input (last layer)
+    const bool last = l + 1 == nrnn;
+    if (save) {
+      const auto sg = gp(J.sg) + (size_t)l * T * G4;
+      const auto sc = gp(J.sc) + (size_t)l * T * H;
+      const auto sh = gp(J.sh) + (size_t)l * T * H;
+      for (int i = L; i < T * G4; i += 64) sg[i] = sgb[i];
+      for (int i = L; i < T * H; i += 64) { sc[i] = scb[i]; sh[i] = shb[i]; }
+    }
+    if (last) {
+      const auto out = gp(J.out);
+      for (int i = L; i < T * H; i += 64) out[i] = shb[i];
+    }
+    __syncthreads();
+  }
+  RNN_TS(tsb + 3, tsm);
+}
+
 void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* md, const ModelDesc& mh,
                      hipStream_t st) {
   {
@@ -361,14 +494,24 @@ void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* m
     if (stage) hipLaunchKernelGGL((k_lstm_gl<HM, DP, true>), dim3(njobs), dim3(64), sh, st, jobs, md); \
     else hipLaunchKernelGGL((k_lstm_gl<HM, DP, false>), dim3(njobs), dim3(64), sh, st, jobs, md);
     const char* ul_env = std::getenv("DLAP_LSTM_UNIT_LANES");
+    const char* gls_env = std::getenv("DLAP_LSTM_GLS");
+    const bool gls = !(gls_env && std::atoi(gls_env) == 0) && mh.H <= 16 &&
+                     gls_lds_floats(tmax, mh.H) * sizeof(float) <= 64 * 1024;
+    const size_t shg = gls_lds_floats(tmax, mh.H) * sizeof(float);
+#define S_CASE(HM, DP) hipLaunchKernelGGL((k_lstm_gls<HM, DP>), dim3(njobs), dim3(64), shg, st, jobs, md);
     if (ul_env && std::atoi(ul_env) == 1) {       // unit-per-lane form (reference for tests)
       if (mh.H <= 4) { L_CASE(4) } else if (mh.H <= 8) { L_CASE(8) } else if (mh.H <= 16) { L_CASE(16) } else { L_CASE(32) }
+    } else if (gls) {
+      if (mh.H == 1) { S_CASE(1, true) } else if (mh.H == 2) { S_CASE(2, true) }
+      else if (mh.H == 3) { S_CASE(3, true) } else if (mh.H == 4) { S_CASE(4, true) }
+      else if (mh.H <= 8) { S_CASE(8, false) } else { S_CASE(16, false) }
     } else if (mh.H == 1) { G_CASE(1, true) } else if (mh.H == 2) { G_CASE(2, true) }
     else if (mh.H == 3) { G_CASE(3, true) } else if (mh.H == 4) { G_CASE(4, true) }
     else if (mh.H <= 8) { G_CASE(8, false) } else if (mh.H <= 16) { G_CASE(16, false) }
     else { L_CASE(32) }
 #undef L_CASE
 #undef G_CASE
+#undef S_CASE
     HIP_OK(hipGetLastError());
   }
 }
@@ -424,7 +567,72 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
     }
     __syncthreads();
     if (l == 0) RNN_TS(9, tsm);
-    if (wave == 0) {
+    if (wave == 0 && HM == 4 && H == 4) {
+      // Gate-per-lane BPTT (H = 4): lane L (mod 16) owns gate row L = 4q + k and keeps the
+      // recurrent state of unit k replicated, so d_L = (q == 3 ? dh : dc) * coef is lane-local
+      // and dh_next_j = sum_L W_hh[L][j] d_L is ONE reduce-scatter over the 16 lanes: two DPP
+      // quad exchanges (xor 1: 4 -> 2 values, xor 2: 2 -> 1) and two row rotations, after which
+      // lane L holds the sum for j = L & 3 = its own unit. Branch-free; rows 1..3 of the wave
+      // duplicate row 0 and store to a junk slot.
+      const int L16 = lane & 15, kq = L16 >> 2, ku = L16 & 3;
+      const bool b0 = (lane & 1) != 0, b1 = (lane & 2) != 0, isO = kq == 3;
+      const auto Whh = params + md->lstm_w_hh[l];
+      float w[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = Whh[L16 * 4 + j];
+      float* junk = dgs + T * G4;
+      float* ddst = lane < 16 ? dgs + L16 : junk + lane;
+      const int dstride = lane < 16 ? 16 : 0;
+      const int ci = (1 + kq) * 4 + ku;
+      float dh_next = 0.f, dc_next = 0.f;
+      auto fetch = [&](int t, float (&v)[4]) {
+        const float* q = s_cf + t * (LSTM_NCOEF * 4);
+        v[0] = q[ku]; v[1] = q[20 + ku]; v[2] = q[ci]; v[3] = s_d[t * 4 + ku];
+      };
+      auto step = [&](int t, const float (&v)[4]) {
+        const float dh = v[3] + dh_next;
+        const float dc = dh * v[0] + dc_next;
+        dc_next = dc * v[1];
+        const float d = (isO ? dh : dc) * v[2];
+        ddst[t * dstride] = d;
+        const float p0 = w[0] * d, p1 = w[1] * d, p2 = w[2] * d, p3 = w[3] * d;
+        const float a0 = b0 ? p1 : p0, s0 = b0 ? p0 : p1;
+        const float a1 = b0 ? p3 : p2, s1 = b0 ? p2 : p3;
+        const float n0 = a0 + dppf<0xB1>(s0);             // quad_perm [1,0,3,2]
+        const float n1 = a1 + dppf<0xB1>(s1);
+        const float a = b1 ? n1 : n0, sx = b1 ? n0 : n1;
+        float r = a + dppf<0x4E>(sx);                      // quad_perm [2,3,0,1]
+        r += dppf<0x124>(r);                               // row_ror:4
+        r += dppf<0x128>(r);                               // row_ror:8
+        dh_next = r;
+      };
+      constexpr int U = 8;
+      const int nfull = T / U;
+      int t = T - 1;
+      for (; t >= nfull * U; --t) {
+        float v[4];
+        fetch(t, v);
+        step(t, v);
+      }
+      float A[U][4], B[U][4];
+      auto load_block = [&](int t0, float (&buf)[U][4]) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) fetch(t0 - u, buf[u]);
+      };
+      if (nfull > 0) load_block(t, A);
+      for (int b = 0; b < nfull; b += 2) {
+        if (b + 1 < nfull) load_block(t - U, B);
+#pragma unroll
+        for (int u = 0; u < U; ++u) step(t - u, A[u]);
+        t -= U;
+        if (b + 1 < nfull) {
+          if (b + 2 < nfull) load_block(t - U, A);
+#pragma unroll
+          for (int u = 0; u < U; ++u) step(t - u, B[u]);
+          t -= U;
+        }
+      }
+    } else if (wave == 0) {
       const int k = lane < H ? lane : 0;
       const bool act = lane < H;
       const auto Whh = params + md->lstm_w_hh[l];
@@ -600,7 +808,7 @@ __global__ __launch_bounds__(256) void k_wgrad(const UpdJob* __restrict__ jobs,
 void launch_lstm_bwd(const UpdJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
                      int T, int phase, hipStream_t st) {
   if (phase != 2 && mh.nrnn > 0) {
-    const size_t sh = (size_t)T * (LSTM_NCOEF + 2 + 4) * mh.H * sizeof(float);   // coef, h, d, dgates
+    const size_t sh = ((size_t)T * (LSTM_NCOEF + 2 + 4) * mh.H + 64) * sizeof(float);   // coef, h, d, dgates, junk
     if (sh > 160 * 1024) dlap_throw_hip(hipErrorInvalidValue, "lstm_bwd: T*H too large for LDS", __FILE__, __LINE__);
     if (mh.H <= 4) hipLaunchKernelGGL((k_lstm_bwd<4>), dim3(njobs), dim3(256), sh, st, jobs, md);
     else if (mh.H <= 8) hipLaunchKernelGGL((k_lstm_bwd<8>), dim3(njobs), dim3(256), sh, st, jobs, md);
