@@ -30,6 +30,7 @@
 #include "mlp.h"
 #include "rnn.h"
 #include "update.h"
+#include "wide.h"
 
 namespace py = pybind11;
 
@@ -65,6 +66,7 @@ struct SplitDev {
   DevBuf<uint16_t> X;
   DevBuf<int> rowti, row_ptr;        // rowti: [R] (t, i) int2
   DevBuf<float> Rm, mask, invNt, Nt, meanR, RR, invT, macro, Rc;
+  DevBuf<uint16_t> XT;               // wide path, train split: rows-as-k copy of X (k_wgrad0)
   bool set = false;
 };
 
@@ -74,12 +76,15 @@ struct ModelSplitWS {   // per (model, split)
   DevBuf<float> u, v, dpp, dab, dg, dx;
   DevBuf<uint32_t> gb, mgb;   // forward gate words of the train split (SDF / moment hidden)
   DevBuf<float> scal_prev;    // train split: metrics of the last finished step (bookkeeping)
+  DevBuf<float> z;            // wide path: layer-0 pre-activations [ntiles][zc][64][4]
+  DevBuf<uint16_t> dzs, dzm;  // wide path, train: layer-0 dz fragments (SDF / moment)
+  DevBuf<float> wpart;        // wide path, train: layer-0 weight-gradient partials
 };
 
 struct ModelState {
   DevBuf<float> params, grads, m, v, snap_loss, snap_sharpe, gnorm, best, aux, hist, wproj;
   DevBuf<int> adam_step, drop_step, snap_flags, ep;
-  DevBuf<uint16_t> blob;
+  DevBuf<uint16_t> blob, blob0;
   unsigned seed = 0;
   float lr = 0.f;         // per-model learning rate override (0: use the run's lr)
 };
@@ -127,6 +132,7 @@ class Engine {
       S.hist.alloc((size_t)max_epochs_ * HIST_W);
       S.adam_step.alloc(2); S.drop_step.alloc(1); S.snap_flags.alloc(2); S.ep.alloc(2);
       S.blob.alloc((size_t)md_.md.blob_frags * 512);
+      S.blob0.alloc((size_t)std::max(1, md_.md.b0_frags) * 512);
       S.wproj.alloc((size_t)(md_.proj_mp + 1) * md_.proj_np);
     }
     ws_.resize((size_t)G * 3);
@@ -147,6 +153,7 @@ class Engine {
     d["P"] = md_.P; d["P_sdf"] = md_.P_sdf; d["KP"] = md_.KP; d["KS1"] = md_.KS1; d["WMB"] = md_.WMB;
     d["Dm"] = md_.Dm; d["blob_frags"] = md_.md.blob_frags; d["aux_floats"] = md_.md.aux_floats;
     d["ntile_s"] = md_.ntile_s; d["tps_s"] = md_.tps_s; d["ntile_m"] = md_.ntile_m; d["G"] = G_;
+    d["wide"] = md_.md.wide; d["KX"] = md_.md.KX; d["nsplit"] = nsplit_;
     return d;
   }
 
@@ -210,6 +217,12 @@ class Engine {
     up(D.RR, rr.data(), T); up(D.invT, invt.data(), N);
     D.set = true;
     alloc_ws(s);
+    if (md_.md.wide && s == 0) {    // rows-as-k copy of the train panel for the weight gradient
+      const size_t ntl = (size_t)(R + 31) / 32;
+      D.XT.alloc(std::max<size_t>(ntl * (md_.md.KX / 16) * 512, 1), false);
+      if (R > 0) launch_xt_build(D.X.p, D.XT.p, R, md_.md.KX, st_);
+      sync();
+    }
     graphs_dirty_ = true;
   }
 
@@ -431,11 +444,13 @@ class Engine {
   std::vector<ModelSplitWS> ws_;
   DevBuf<float> slab_;
   int gx_bwd_ = 1, gx_fwd_[3] = {1, 1, 1};
+  int nsplit_ = 1, gx_proj_[3] = {1, 1, 1};  // wide path: wgrad row splits, proj grid per split
   bool graphs_dirty_ = true;
   std::map<std::string, hipGraphExec_t> graphs_;
   // device job tables
   DevBuf<char> j_rnn_train_, j_rnn_eval_, j_mlp_train_[4], j_mlp_eval_, j_mlp_bwd_[4], j_loss_train_[4],
       j_loss_eval_, j_fin_, j_upd_, j_epoch_[4];
+  DevBuf<char> j_wide_train_[4], j_wide_eval_, j_wide_bwd_[4];   // wide path (k_wide.hip)
   int n_eval_jobs_ = 0;
   int tmax_eval_ = 0, nmax_eval_ = 0;
 
@@ -473,6 +488,7 @@ class Engine {
     UpdJob J{};
     J.params = models_[g].params.p;
     J.blob = reinterpret_cast<bf16x8*>(models_[g].blob.p);
+    J.blob0 = reinterpret_cast<bf16x8*>(models_[g].blob0.p);
     J.aux = models_[g].aux.p;
     J.wproj = models_[g].wproj.p;
     DevBuf<char> tmp;
@@ -497,10 +513,19 @@ class Engine {
     d.F = F; d.M = M; d.nrnn = nrnn; d.H = nrnn > 0 ? H : 0; d.K = K;
     d.Dm = nrnn > 0 ? H : (raw_macro_sdf ? M : 0);
     d.KIN = F + d.Dm;
-    int ks = (d.KIN + 31) / 32;
-    if (ks > 4) throw std::invalid_argument("F + per-period inputs must be <= 128 for the native engine");
-    d.KS1 = ks <= 2 ? 2 : 4;
-    d.KP = 32 * d.KS1;
+    const int ks = (d.KIN + 31) / 32;
+    // wide path: layer-0 inputs beyond the 128 columns a fused tower tile holds in registers
+    // (or DLAP_WIDE=1) -> layer 0 runs as the streaming k_proj0 / k_wgrad0 GEMMs
+    const bool wide = ks > 4 || env_int("DLAP_WIDE", 0) != 0;
+    if (wide) {
+      d.KS1 = 2;                                    // template slot of the ZIN tower kernels
+      d.KSB = 0;                                    // no layer-0 fragments in the tower blob
+      d.KP = std::max(32, (F + 31) / 32 * 32);      // panel row = the F characteristics only
+    } else {
+      d.KS1 = ks <= 2 ? 2 : 4;
+      d.KSB = d.KS1;
+      d.KP = 32 * d.KS1;
+    }
     d.dropout = dropout; d.normalize_w = normalize_w; d.weighted_loss = weighted; d.residual_factor = residual;
     int off = 0;
     for (int l = 0; l < nrnn; ++l) {
@@ -540,16 +565,24 @@ class Engine {
     MlpDims& D = d.md;
     D.F = F; D.Dm = d.Dm; D.K = K; D.cm1 = d.cm1; D.nrnn = nrnn;
     D.nl_sdf = d.nl_s; D.nl_mom = d.nl_m; D.dropout = dropout;
-    D.s_fwd0 = 0; D.s_fwd = 4 * d.KS1; D.s_bwd = D.s_fwd + 8 * (d.nl_s - 1);
-    D.m_fwd0 = D.s_bwd + 8 * (d.nl_s - 1); D.m_fwd = D.m_fwd0 + d.WMB * d.KS1;
+    D.s_fwd0 = 0; D.s_fwd = 4 * d.KSB; D.s_bwd = D.s_fwd + 8 * (d.nl_s - 1);
+    D.m_fwd0 = D.s_bwd + 8 * (d.nl_s - 1); D.m_fwd = D.m_fwd0 + d.WMB * d.KSB;
     D.m_bwd = D.m_fwd + (d.nl_m - 1) * d.WMB * KSM;
     D.s_upp = D.m_bwd + (d.nl_m - 1) * d.WMB * KSM;
     D.ubpp = nrnn > 0 ? (d.Dm + 15) / 16 : 0;
     D.blob_frags = D.s_upp + 2 * D.ubpp;
     D.a_sb = 0; D.a_wo = 64 * d.nl_s; D.a_bo = D.a_wo + 64; D.a_pp = D.a_bo + 4;
     D.a_mb = D.a_pp + 64 * d.Dm; D.aux_floats = D.a_mb + 64 * d.nl_m;
-    // gradient tiles: layer-0 chunks first, then one tile per later layer (slice = tile, TPS 1)
-    const int C0 = d.KS1 / 2;
+    D.wide = wide ? 1 : 0;
+    D.KX = wide ? d.KP : 0;
+    D.KSX = D.KX / 32;
+    D.zc = 8 + 2 * d.WMB;
+    D.b0_frags = wide ? (4 + d.WMB) * D.KSX : 0;
+    if ((size_t)D.b0_frags * 1024 > 160 * 1024)
+      throw std::invalid_argument("feature dim too large for the wide layer-0 kernel (LDS budget)");
+    // gradient tiles: layer-0 chunks first (none on the wide path: k_wgrad0), then one tile per
+    // later layer (slice = tile, TPS 1)
+    const int C0 = wide ? 0 : d.KS1 / 2;
     int t = 0;
     for (int c = 0; c < C0; ++c, ++t)
       d.tile_s[t] = GradTile{d.s[0].w_off, d.s[0].ld, 0, d.s[0].out, d.s[0].in, c, t};
@@ -559,16 +592,18 @@ class Engine {
     // two gradient tiles per slice share one forward recompute (fits the 512-register
     // budget of a single wave per SIMD); DLAP_TPS=1 forces one tile per slice
     const char* tps_env = std::getenv("DLAP_TPS");
-    const bool tps2 = d.KS1 == 2 && d.ntile_s == 2 && !(tps_env && std::atoi(tps_env) == 1);
+    const bool tps2 = !wide && d.KS1 == 2 && d.ntile_s == 2 && !(tps_env && std::atoi(tps_env) == 1);
     d.tps_s = tps2 ? 2 : 1;
-    d.nslice_s = (d.ntile_s + d.tps_s - 1) / d.tps_s;
+    // at least one slice: slice 0 also produces the bias / output / per-period gradients
+    d.nslice_s = std::max(1, (d.ntile_s + d.tps_s - 1) / d.tps_s);
     for (int k = 0; k < d.ntile_s; ++k) d.tile_s[k].slice = k / d.tps_s;
     t = 0;
     for (int c = 0; c < C0; ++c, ++t)
       d.tile_m[t] = GradTile{d.m[0].w_off, d.m[0].ld, d.m[0].col0, d.m[0].out, d.m[0].in, c, t};
     for (int j = 1; j < d.nl_m; ++j, ++t)
       d.tile_m[t] = GradTile{d.m[j].w_off, d.m[j].ld, 0, d.m[j].out, d.m[j].in, 0, t};
-    d.ntile_m = d.nslice_m = t;
+    d.ntile_m = t;
+    d.nslice_m = std::max(1, t);
     d.tps_m = 1;
     d.proj_mp = std::max(4, (M + 3) / 4 * 4);
     d.proj_np = ((nrnn > 0 ? 4 * H : 0) + 64 + 15) / 16 * 16;   // whole 16-wide MFMA tiles
@@ -625,6 +660,23 @@ class Engine {
       slab_.alloc((size_t)G_ * nsl * gx_bwd_ * slab_stride());
     }
     gx_fwd_[s] = std::max(1, std::min(((R + 31) / 32 + 3) / 4, env_int("DLAP_GX_FWD", 1024)));
+    if (md_.md.wide) {
+      const size_t ntl = (size_t)(R + 31) / 32;
+      for (int g = 0; g < G_; ++g) {
+        ModelSplitWS& W = ws(g, s);
+        W.z.alloc(std::max<size_t>(ntl * md_.md.zc * 256, 1), false);
+        if (s == 0) {
+          W.dzs.alloc(std::max<size_t>(ntl * 4 * 512, 1), false);
+          W.dzm.alloc(std::max<size_t>(ntl * md_.WMB * 512, 1), false);
+        }
+      }
+      if (s == 0) {
+        // split-K of the layer-0 weight gradient: ~8 tiles per workgroup, at most 2 per CU
+        nsplit_ = std::max(1, std::min((int)((ntl + 7) / 8), env_int("DLAP_WG_SPLIT", 512)));
+        for (int g = 0; g < G_; ++g) ws(g, 0).wpart.alloc(wide_part_floats(md_.md, md_.WMB, nsplit_), false);
+      }
+      gx_proj_[s] = std::max(1, std::min((int)((ntl + 3) / 4), env_int("DLAP_GX_PROJ", 512)));
+    }
     // per-period SDF inputs [T][Dm] are staged in LDS by the tower kernels when small
     int tmax = 0;
     for (int k = 0; k < 3; ++k)
@@ -670,12 +722,32 @@ class Engine {
     J.dw = W.dw.p; J.dE = W.dE.p; J.Rm = D.Rm.p; J.sdfv = W.sdf.p; J.invT = D.invT.p;
     J.slab = slab_.p;
     J.u_out = W.u.p; J.v_out = W.v.p;
+    J.z = reinterpret_cast<const f32x4*>(W.z.p);
     J.step = models_[g].drop_step.p;
     J.R = D.R; J.N = D.N; J.T = D.T;
     J.seed = models_[g].seed;
     J.train = train; J.do_sdf = do_sdf; J.do_mom = do_mom;
     const int nsl = std::max(md_.nslice_s, md_.nslice_m);
     J.slab_base = g * nsl * gx_bwd_;
+    return J;
+  }
+  // wide path: projection (do_sdf / do_mom = towers to project) or weight-gradient job
+  // (do_mom = the moment tower's layer 0, else the SDF's)
+  WideJob wide_job(int g, int s, bool do_sdf, bool do_mom) {
+    ModelSplitWS& W = ws(g, s);
+    SplitDev& D = splits_[s];
+    WideJob J{};
+    J.X = reinterpret_cast<const bf16x8*>(D.X.p);
+    J.XT = reinterpret_cast<const bf16x8*>(D.XT.p);
+    J.rowti = reinterpret_cast<const int2*>(D.rowti.p);
+    J.pp = pp_ptr(g, s);
+    J.blob0 = reinterpret_cast<const bf16x8*>(models_[g].blob0.p);
+    J.z = reinterpret_cast<f32x4*>(W.z.p);
+    J.dz = reinterpret_cast<const bf16x8*>(do_mom ? W.dzm.p : W.dzs.p);
+    J.part = W.wpart.p;
+    J.grads = models_[g].grads.p;
+    J.R = D.R; J.T = D.T;
+    J.do_sdf = do_sdf; J.do_mom = do_mom;
     return J;
   }
   LossJob loss_job(int g, int s, int phase) {
@@ -707,6 +779,7 @@ class Engine {
     std::vector<MlpJob> me;
     std::vector<FinJob> fj;
     std::vector<UpdJob> uj;
+    std::vector<WideJob> we;
     n_eval_jobs_ = 0; tmax_eval_ = 0; nmax_eval_ = 0;
     for (int g = 0; g < G_; ++g) {
       rt.push_back(rnn_job(g, 0, true));
@@ -714,6 +787,7 @@ class Engine {
         if (!splits_[s].set) continue;
         re.push_back(rnn_job(g, s, false));
         me.push_back(mlp_job(g, s, false, true, true));
+        we.push_back(wide_job(g, s, true, true));
         le.push_back(loss_job(g, s, 0));
         tmax_eval_ = std::max(tmax_eval_, splits_[s].T);
         nmax_eval_ = std::max(nmax_eval_, splits_[s].N);
@@ -730,6 +804,7 @@ class Engine {
       U.params = S.params.p; U.grads = S.grads.p; U.m = S.m.p; U.v = S.v.p;
       U.adam_step = S.adam_step.p; U.drop_step = S.drop_step.p; U.gnorm = S.gnorm.p;
       U.blob = reinterpret_cast<bf16x8*>(S.blob.p); U.aux = S.aux.p; U.wproj = S.wproj.p;
+      U.blob0 = reinterpret_cast<bf16x8*>(S.blob0.p);
       U.dpp = W.dpp.p; U.macro = splits_[0].macro.p; U.sg = W.sg.p; U.sc = W.sc.p; U.sh = W.sh.p;
       U.dg = W.dg.p; U.dx = W.dx.p; U.dab = W.dab.p; U.scal = W.scal.p; U.scal_prev = W.scal_prev.p;
       U.T = splits_[0].T; U.seed = S.seed; U.lr = S.lr;
@@ -737,14 +812,18 @@ class Engine {
     }
     n_eval_jobs_ = (int)le.size();
     upload(j_rnn_train_, rt); upload(j_rnn_eval_, re); upload(j_mlp_eval_, me); upload(j_loss_eval_, le);
-    upload(j_fin_, fj); upload(j_upd_, uj);
+    upload(j_fin_, fj); upload(j_upd_, uj); upload(j_wide_eval_, we);
     for (int phase = 1; phase <= 3; ++phase) {
       std::vector<MlpJob> mt, mb;
       std::vector<LossJob> lt;
       std::vector<EpochJob> ej;
+      std::vector<WideJob> wt, wb;
       for (int g = 0; g < G_; ++g) {
         mt.push_back(mlp_job(g, 0, true, true, phase != 1));
         mb.push_back(mlp_job(g, 0, true, true, true));
+        mb.back().dz_out = reinterpret_cast<bf16x8*>(phase == 2 ? ws(g, 0).dzm.p : ws(g, 0).dzs.p);
+        wt.push_back(wide_job(g, 0, true, phase != 1));
+        wb.push_back(wide_job(g, 0, phase != 2, phase == 2));
         // the training forward stores the gate words its backward reuses
         if (phase == 2) {
           if (md_.nl_m > 1) mt.back().mgbits = mb.back().mgbits = ws(g, 0).mgb.p;
@@ -764,18 +843,21 @@ class Engine {
         ej.push_back(E);
       }
       upload(j_mlp_train_[phase], mt); upload(j_mlp_bwd_[phase], mb); upload(j_loss_train_[phase], lt);
-      upload(j_epoch_[phase], ej);
+      upload(j_epoch_[phase], ej); upload(j_wide_train_[phase], wt); upload(j_wide_bwd_[phase], wb);
     }
     // evaluation-only jobs of the train split (module API / final evaluation)
     {
       std::vector<MlpJob> mt;
       std::vector<LossJob> lt;
+      std::vector<WideJob> wt;
       for (int g = 0; g < G_; ++g) {
         mt.push_back(mlp_job(g, 0, false, true, true));
         lt.push_back(loss_job(g, 0, 0));
+        wt.push_back(wide_job(g, 0, true, true));
       }
       upload(j_mlp_train_[0], mt);
       upload(j_loss_train_[0], lt);
+      upload(j_wide_train_[0], wt);
     }
   }
 
@@ -798,6 +880,8 @@ class Engine {
                            bool part1_only = false) {
     const SplitDev& D = splits_[0];
     if (!premasked) enqueue_dropmask(phase, 0, st_);
+    if (md_.md.wide)
+      launch_proj0(as<WideJob>(j_wide_train_[phase]), G_, gx_proj_[0], md_.md, md_.WMB, st_);
     launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_);
     launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, gx_fwd_[0], md_.md, md_.KS1, md_.WMB, st_);
     if (mark == 2) HIP_OK(hipEventRecord(ev_a_, st_));
@@ -818,6 +902,8 @@ class Engine {
       launch_mlp_bwd_sdf(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_s, md_.tps_s, md_.md, md_.KS1,
                          slab_stride(), st_);
     }
+    if (md_.md.wide)   // layer-0 weight gradient from the tower's dz fragments
+      launch_wgrad0(as<WideJob>(j_wide_bwd_[phase]), G_, dd(), md_.md, phase == 2, md_.WMB, nsplit_, st_);
     if (mark == 1) HIP_OK(hipEventRecord(ev_a_, st_));
     if (part1_only) return;
     enqueue_train_tail(phase);
@@ -843,6 +929,8 @@ class Engine {
     if (n_eval_jobs_ == 0) return;
     int gx = std::max(gx_fwd_[1], gx_fwd_[2]);
     if (eval_gx_ > 0) gx = std::min(gx, eval_gx_);
+    if (md_.md.wide)
+      launch_proj0(as<WideJob>(j_wide_eval_), n_eval_jobs_, std::max(gx_proj_[1], gx_proj_[2]), md_.md, md_.WMB, st);
     launch_mlp_fwd(as<MlpJob>(j_mlp_eval_), n_eval_jobs_, gx, md_.md, md_.KS1, md_.WMB, st);
     launch_period_fwd(as<LossJob>(j_loss_eval_), n_eval_jobs_, tmax_eval_, st);
     launch_asset(as<LossJob>(j_loss_eval_), n_eval_jobs_, nmax_eval_, st);
@@ -912,14 +1000,17 @@ class Engine {
     std::vector<RnnJob> rj;
     std::vector<MlpJob> mj;
     std::vector<LossJob> lj;
+    std::vector<WideJob> wj;
     for (int g = 0; g < G_; ++g) {
       rj.push_back(rnn_job(g, s, train_mode));
       mj.push_back(mlp_job(g, s, train_mode, true, do_mom));
       lj.push_back(loss_job(g, s, 0));
+      wj.push_back(wide_job(g, s, true, do_mom));
       if (!do_mom) lj.back().h = nullptr;
     }
-    DevBuf<char> a, b, c;
-    upload(a, rj); upload(b, mj); upload(c, lj);
+    DevBuf<char> a, b, c, w;
+    upload(a, rj); upload(b, mj); upload(c, lj); upload(w, wj);
+    if (md_.md.wide) launch_proj0(as<WideJob>(w), G_, gx_proj_[s], md_.md, md_.WMB, st_);
     launch_prologue(as<RnnJob>(a), G_, D.T, dd(), md_, st_);
     launch_mlp_fwd(as<MlpJob>(b), G_, gx_fwd_[s], md_.md, md_.KS1, md_.WMB, st_);
     launch_period_fwd(as<LossJob>(c), G_, D.T, st_);

@@ -69,6 +69,74 @@ struct RowInfo {
   int t[2], i[2];
 };
 
+// ---- wide path (ZIN instantiations): layer 0 comes from k_proj0 (k_wide.hip) ----------
+// z chunk (tile, c) of lane l is exactly the layer-0 accumulator a[b][u] of that lane, so a
+// tile is 8 + 2*WMB lane-linear 16-byte loads instead of the X row fragments.
+template <int WMB>
+struct ZTile {
+  int2 ti[2];
+  f32x4 zs[2][4];
+  f32x4 zm[2][WMB];
+  float dw[2];
+};
+
+template <int WMB, bool DW>
+DLAP_DEV void issue_ztile(const MlpJob& J, const MlpDims& D, int tile, ZTile<WMB>& in, bool sdf, bool mom) {
+  const int l = lane_id();
+  const auto zt = gp(J.z) + (size_t)tile * D.zc * 64 + l;
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int r = min(tile * 32 + 16 * b + (l & 15), J.R - 1);
+    in.ti[b] = gp(J.rowti)[r];
+    if (DW) in.dw[b] = gp(J.dw)[r];
+    if (sdf) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) in.zs[b][u] = zt[(4 * b + u) * 64];
+    }
+    if (mom) {
+#pragma unroll
+      for (int u = 0; u < WMB; ++u) in.zm[b][u] = zt[(8 + WMB * b + u) * 64];
+    }
+  }
+}
+
+template <int WMB>
+DLAP_DEV RowInfo finish_ztile(const MlpJob& J, int tile, ZTile<WMB>& in) {
+  RowInfo ri;
+  const int l = lane_id();
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const int r = tile * 32 + 16 * b + (l & 15);
+    const bool ok = r < J.R;
+    ri.t[b] = in.ti[b].x;
+    ri.i[b] = in.ti[b].y;
+    ri.dense[b] = ok ? in.ti[b].x * J.N + in.ti[b].y : -1;
+    if (!ok) in.dw[b] = 0.f;
+  }
+  return ri;
+}
+
+// SDF layer 0 of the wide path: a = z + W0[:, F:F+Dm] . pp_t in fp32 (the bias is added by the
+// ReLU step, as in the fused path). W0's per-period columns are the aux block a_pp [Dm][64].
+template <typename PP>
+DLAP_DEV void zin_sdf0(const f32x4 (&zs)[2][4], const RowInfo& ri, PP pp, const float* aux,
+                       const MlpDims& D, f32x4 (&a)[2][4]) {
+  const int q = lane_id() >> 4;
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int u = 0; u < 4; ++u) a[b][u] = zs[b][u];
+  for (int d = 0; d < D.Dm; ++d) {
+    const float p0 = pp[ri.t[0] * D.Dm + d], p1 = pp[ri.t[1] * D.Dm + d];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const f32x4 w = ld4(aux + D.a_pp + 64 * d + 16 * u + 4 * q);
+      a[0][u] += p0 * w;
+      a[1][u] += p1 * w;
+    }
+  }
+}
+
 // Per-tile data that does not depend on other loads: issued one tile ahead (software
 // prefetch) so the HBM latency hides behind the current tile's MFMA/VALU work.
 template <int KS1>
@@ -319,14 +387,15 @@ DLAP_DEV void stage_weights(const MlpJob& J, const MlpDims& D, bf16x8* lds, floa
 // SDF tower forward on one tile: the raw (pre-normalisation) weight of each row block.
 // gout: gate words of the tile (train). With keep words (kw, pre-generated by k_dropmask) the
 // dropout decisions are read instead of hashed; the gates overwrite the keep words in place.
-template <int KS1>
+// layer0_fn(a) fills the layer-0 accumulators (fused: MFMA over the X tile; wide: from z).
+template <typename L0>
 DLAP_DEV void sdf_forward_tile(const bf16x8* lds, const float* aux, const MlpDims& D,
-                               const DropCtx& dc, const RowInfo& ri, const bf16x8 (&xf)[2][KS1],
+                               const DropCtx& dc, const RowInfo& ri, L0&& layer0_fn,
                                DLAP_GLOBAL uint32_t* gout, const uint32_t* kw, float (&w)[2]) {
   f32x4 a[2][4];
   bf16x8 pf[2][2];
   uint32_t gate[2];
-  layer0<KS1, 4>(lds, D.s_fwd0, xf, a);
+  layer0_fn(a);
   if (kw) relu_keep<4>(a, aux + D.a_sb, dc.scale, kw[0], gate);
   else relu_dropout<4>(a, aux + D.a_sb, aux + D.a_sb, dc, 0, ri, gate);
   if (gout) gout[0] = gate_word(gate);
@@ -354,17 +423,17 @@ DLAP_DEV void sdf_forward_tile(const bf16x8* lds, const float* aux, const MlpDim
 }
 
 // Moment tower forward on one tile: writes the K tanh outputs of every valid row.
-template <int KS1, int WMB>
+template <int WMB, typename L0>
 DLAP_DEV void mom_forward_tile(const bf16x8* lds, const float* aux, const MlpDims& D,
                                const MlpJob& J, const DropCtx& dc, const RowInfo& ri,
-                               const bf16x8 (&xf)[2][KS1], DLAP_GLOBAL uint32_t* gout,
+                               L0&& layer0_fn, DLAP_GLOBAL uint32_t* gout,
                                const AbPre<WMB>& ab) {
   constexpr int KSM = (WMB + 1) / 2;
   f32x4 a[2][WMB];
   bf16x8 pf[2][KSM];
   uint32_t gate[2];
   const int q = lane_id() >> 4;
-  layer0<KS1, WMB>(lds, D.m_fwd0, xf, a);
+  layer0_fn(a);
   // layer-0 bias is per period (prefetched), later biases are staged (LDS)
   for (int j = 0; j + 1 < D.nl_mom; ++j) {
     if (j == 0) relu_dropout_g<WMB>(a, [&](int b, int u) { return ab.v[b][u]; }, dc, 16 + j, ri, gate);
@@ -407,7 +476,7 @@ DLAP_DEV void mom_forward_tile(const bf16x8* lds, const float* aux, const MlpDim
 }
 
 // ============================== forward ==================================================
-template <int KS1, int WMB>
+template <int KS1, int WMB, bool ZIN>
 __global__ __launch_bounds__(256, 2) void k_mlp_fwd(const MlpJob* __restrict__ jobs, MlpDims D) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const MlpJob& J = jobs[blockIdx.y];
@@ -421,17 +490,22 @@ __global__ __launch_bounds__(256, 2) void k_mlp_fwd(const MlpJob* __restrict__ j
   const int stride = gridDim.x * nwaves;
   int tile = blockIdx.x * nwaves + wave;
   TileIn<KS1> cur, nxt;
+  ZTile<WMB> zcur, znxt;                 // ZIN: layer-0 pre-activations instead of X rows
   AbPre<WMB> ab_cur, ab_nxt;
   int2 ti_ahead[2];                      // periods of the tile after next (for the abias prefetch)
   const bool mom = J.do_mom;
   if (tile < ntiles) {
-    issue_tile<KS1, false>(J, tile, cur);                    // in flight during the staging
+    if constexpr (ZIN) issue_ztile<WMB, false>(J, D, tile, zcur, J.do_sdf, mom);
+    else issue_tile<KS1, false>(J, tile, cur);               // in flight during the staging
     if (mom && tile + stride < ntiles) issue_rowti(J, tile + stride, ti_ahead);
   }
   stage_weights(J, D, lds, aux, spp);
   MLP_TS(1);
   const DropCtx dc = drop_ctx(J, D);
-  if (mom && tile < ntiles) issue_abias<WMB>(J, cur.ti, ab_cur);
+  if (mom && tile < ntiles) {
+    if constexpr (ZIN) issue_abias<WMB>(J, zcur.ti, ab_cur);
+    else issue_abias<WMB>(J, cur.ti, ab_cur);
+  }
   // train forward with dropout: keep words of this step's parity half, prefetched with the tile
   const bool keep = J.gbits && dc.on;
   const auto gbase = J.gbits ? gp(J.gbits) + (size_t)(dc.step & 1u) * J.gb_half : nullptr;
@@ -446,7 +520,8 @@ __global__ __launch_bounds__(256, 2) void k_mlp_fwd(const MlpJob* __restrict__ j
   bool first = true;
   for (; tile < ntiles; tile += stride) {
     if (tile + stride < ntiles) {
-      issue_tile<KS1, false>(J, tile + stride, nxt);
+      if constexpr (ZIN) issue_ztile<WMB, false>(J, D, tile + stride, znxt, J.do_sdf, mom);
+      else issue_tile<KS1, false>(J, tile + stride, nxt);
       if (keep) issue_kw(tile + stride, kw_nxt);
       if (mom) {
         issue_abias<WMB>(J, ti_ahead, ab_nxt);             // periods known since last iteration
@@ -454,11 +529,21 @@ __global__ __launch_bounds__(256, 2) void k_mlp_fwd(const MlpJob* __restrict__ j
       }
     }
     bf16x8 xf[2][KS1];
-    const RowInfo ri = finish_tile<KS1>(J, D, tile, cur, xf, spp);
+    RowInfo ri;
+    if constexpr (ZIN) ri = finish_ztile<WMB>(J, tile, zcur);
+    else ri = finish_tile<KS1>(J, D, tile, cur, xf, spp);
     if (J.do_sdf) {
       float w[2];
       DLAP_GLOBAL uint32_t* gout = J.gbits ? gbase + (size_t)tile * D.nl_sdf * 64 + lane : nullptr;
-      sdf_forward_tile<KS1>(lds, aux, D, dc, ri, xf, gout, keep ? kw_cur : nullptr, w);
+      auto l0 = [&](f32x4 (&a)[2][4]) {
+        if constexpr (ZIN) {
+          if (D.pp_lds_floats > 0) zin_sdf0(zcur.zs, ri, spp, aux, D, a);
+          else zin_sdf0(zcur.zs, ri, gp(J.pp), aux, D, a);
+        } else {
+          layer0<KS1, 4>(lds, D.s_fwd0, xf, a);
+        }
+      };
+      sdf_forward_tile(lds, aux, D, dc, ri, l0, gout, keep ? kw_cur : nullptr, w);
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         const int r = tile * 32 + 16 * b + (lane & 15);
@@ -468,9 +553,20 @@ __global__ __launch_bounds__(256, 2) void k_mlp_fwd(const MlpJob* __restrict__ j
     if (J.do_mom) {
       DLAP_GLOBAL uint32_t* gout = (J.mgbits && D.nl_mom > 1)
                            ? gp(J.mgbits) + (size_t)tile * (D.nl_mom - 1) * 64 + lane : nullptr;
-      mom_forward_tile<KS1, WMB>(lds, aux, D, J, dc, ri, xf, gout, ab_cur);
+      auto l0 = [&](f32x4 (&a)[2][WMB]) {
+        if constexpr (ZIN) {
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int u = 0; u < WMB; ++u) a[b][u] = zcur.zm[b][u];
+        } else {
+          layer0<KS1, WMB>(lds, D.m_fwd0, xf, a);
+        }
+      };
+      mom_forward_tile<WMB>(lds, aux, D, J, dc, ri, l0, gout, ab_cur);
     }
-    cur = nxt;
+    if constexpr (ZIN) zcur = znxt;
+    else cur = nxt;
     ab_cur = ab_nxt;
 #pragma unroll
     for (int j = 0; j < KWM; ++j) kw_cur[j] = kw_nxt[j];
@@ -508,7 +604,9 @@ DLAP_DEV void wg_slab_store(const MlpJob& J, const float* red, int slab_stride) 
 }
 
 // SDF backward. NL = number of hidden (MFMA) layers, all 64 wide.
-template <int KS1, int NL, int TPS>
+// ZIN (wide path): layer 0 is recomputed from z, its weight gradient is left to k_wgrad0: the
+// kernel stores the layer-0 dz as rows-as-k fragments instead (J.dz_out [tile][4][64]).
+template <int KS1, int NL, int TPS, bool ZIN>
 __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict__ jobs, MlpDims D,
                                                         int slab_stride) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -519,7 +617,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
   const int lane = lane_id(), q = lane >> 4, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   const int ntiles = (J.R + 31) >> 5;
   const int slice = blockIdx.z;
-  constexpr int C0 = KS1 / 2;                // 64-column chunks of layer 0
+  constexpr int C0 = ZIN ? 0 : KS1 / 2;      // 64-column chunks of layer 0
   const bf16x8 selP0 = make_sel(true, 0), selP1 = make_sel(true, 1);
   const bf16x8 selN0 = make_sel(false, 0), selN1 = make_sel(false, 1);
 
@@ -545,11 +643,13 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
   const int stride = gridDim.x * nwaves;
   int tile = blockIdx.x * nwaves + wave;
   TileIn<KS1> cur, nxt;
+  ZTile<1> zcur, znxt;
   uint32_t gw_cur[NL], gw_nxt[NL];   // gate words of the forward pass, prefetched with the tile
   const uint32_t stp = J.step ? (uint32_t)*gp(J.step) : 0u;
   const auto gbase = gp(J.gbits) + (size_t)(stp & 1u) * J.gb_half;
   if (tile < ntiles) {
-    issue_tile<KS1, true>(J, tile, cur);
+    if constexpr (ZIN) issue_ztile<1, true>(J, D, tile, zcur, true, false);
+    else issue_tile<KS1, true>(J, tile, cur);
 #pragma unroll
     for (int j = 0; j < NL; ++j) gw_cur[j] = gbase[((size_t)tile * NL + j) * 64 + lane];
   }
@@ -557,17 +657,25 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
   const DropCtx dc = drop_ctx(J, D);
   for (; tile < ntiles; tile += stride) {
     if (tile + stride < ntiles) {
-      issue_tile<KS1, true>(J, tile + stride, nxt);
+      if constexpr (ZIN) issue_ztile<1, true>(J, D, tile + stride, znxt, true, false);
+      else issue_tile<KS1, true>(J, tile + stride, nxt);
 #pragma unroll
       for (int j = 0; j < NL; ++j) gw_nxt[j] = gbase[((size_t)(tile + stride) * NL + j) * 64 + lane];
     }
     bf16x8 xf[2][KS1];
-    const RowInfo ri = finish_tile<KS1>(J, D, tile, cur, xf, spp);
+    RowInfo ri;
+    if constexpr (ZIN) ri = finish_ztile<1>(J, tile, zcur);
+    else ri = finish_tile<KS1>(J, D, tile, cur, xf, spp);
     // ---- forward recompute from the stored gates, keep packed activations ----
     bf16x8 act[NL][2][2];
     uint32_t gates[NL][2];
     f32x4 a[2][4];
-    layer0<KS1, 4>(lds, D.s_fwd0, xf, a);
+    if constexpr (ZIN) {
+      if (D.pp_lds_floats > 0) zin_sdf0(zcur.zs, ri, spp, aux, D, a);
+      else zin_sdf0(zcur.zs, ri, gp(J.pp), aux, D, a);
+    } else {
+      layer0<KS1, 4>(lds, D.s_fwd0, xf, a);
+    }
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
       if (j > 0) layer_chain<4, 2>(lds, D.s_fwd + (j - 1) * 8, act[j - 1], a);
@@ -577,7 +685,9 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
       pack_blocks<4>(a, act[j]);
     }
     // ---- output layer: w = wo . a_last + bo ----
-    const float dwr[2] = {cur.dw[0], cur.dw[1]};
+    float dwr[2];
+    if constexpr (ZIN) { dwr[0] = zcur.dw[0]; dwr[1] = zcur.dw[1]; }
+    else { dwr[0] = cur.dw[0]; dwr[1] = cur.dw[1]; }
     f32x4 dz[2][4];
     const float* wo = aux + D.a_wo;
 #pragma unroll
@@ -607,19 +717,28 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
 #pragma unroll
         for (int u = 0; u < 4; ++u) gbias[u] = mfma16(dzN[u], oh, gbias[u]);
       }
+      if constexpr (ZIN) {
+        if (j == 0 && slice == 0) {                 // layer-0 dz for k_wgrad0
+          const auto dzo = gp(J.dz_out) + (size_t)tile * 4 * 64 + lane;
+#pragma unroll
+          for (int u = 0; u < 4; ++u) dzo[u * 64] = dzN[u];
+        }
+      }
 #pragma unroll
       for (int t = 0; t < TPS; ++t) {
         if (tl[t] == j) {
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
-            bf16x8 aN;
+            bf16x8 aN = zero8();
             if (j == 0) {
-              const int blk = 4 * tc[t] + v;
-              bf16x8 x0 = zero8(), x1 = zero8();
+              if constexpr (!ZIN) {
+                const int blk = 4 * tc[t] + v;
+                bf16x8 x0 = zero8(), x1 = zero8();
 #pragma unroll
-              for (int s = 0; s < KS1; ++s)
-                if (s == (blk >> 1)) { x0 = xf[0][s]; x1 = xf[1][s]; }
-              x_rows_k(x0, x1, blk, selN0, selN1, aN);
+                for (int s = 0; s < KS1; ++s)
+                  if (s == (blk >> 1)) { x0 = xf[0][s]; x1 = xf[1][s]; }
+                x_rows_k(x0, x1, blk, selN0, selN1, aN);
+              }
             } else {
               to_rows_k<4>(act[j > 0 ? j - 1 : 0], v, selP0, selP1, aN);
             }
@@ -664,7 +783,8 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
         }
       }
     }
-    cur = nxt;
+    if constexpr (ZIN) zcur = znxt;
+    else cur = nxt;
 #pragma unroll
     for (int j = 0; j < NL; ++j) gw_cur[j] = gw_nxt[j];
   }
@@ -703,7 +823,8 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
 }
 
 // Moment backward (phase 2). NLM MFMA layers of WM = 16*WMB units; tanh on the last.
-template <int KS1, int WMB, int NLM, int TPS>
+// ZIN: as k_mlp_bwd_sdf (layer 0 from z, layer-0 dz stored as J.dz_out [tile][WMB][64]).
+template <int KS1, int WMB, int NLM, int TPS, bool ZIN>
 __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict__ jobs, MlpDims D,
                                                         int slab_stride) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -714,7 +835,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
   const int lane = lane_id(), q = lane >> 4, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   const int ntiles = (J.R + 31) >> 5;
   const int slice = blockIdx.z;
-  constexpr int C0 = KS1 / 2;
+  constexpr int C0 = ZIN ? 0 : KS1 / 2;
   const bf16x8 selP0 = make_sel(true, 0), selP1 = make_sel(true, 1);
   const bf16x8 selN0 = make_sel(false, 0), selN1 = make_sel(false, 1);
 
@@ -740,9 +861,11 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
   int tile = blockIdx.x * nwaves + wave;
   constexpr int NH = NLM > 1 ? NLM - 1 : 1;   // hidden layers with stored gate words
   TileIn<KS1> cur, nxt;
+  ZTile<WMB> zcur, znxt;
   uint32_t gw_cur[NH], gw_nxt[NH];
   if (tile < ntiles) {
-    issue_tile<KS1, false>(J, tile, cur);
+    if constexpr (ZIN) issue_ztile<WMB, false>(J, D, tile, zcur, false, true);
+    else issue_tile<KS1, false>(J, tile, cur);
 #pragma unroll
     for (int j = 0; j + 1 < NLM; ++j) gw_cur[j] = gp(J.mgbits)[((size_t)tile * (NLM - 1) + j) * 64 + lane];
   }
@@ -750,17 +873,27 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
   const DropCtx dc = drop_ctx(J, D);
   for (; tile < ntiles; tile += stride) {
     if (tile + stride < ntiles) {
-      issue_tile<KS1, false>(J, tile + stride, nxt);
+      if constexpr (ZIN) issue_ztile<WMB, false>(J, D, tile + stride, znxt, false, true);
+      else issue_tile<KS1, false>(J, tile + stride, nxt);
 #pragma unroll
       for (int j = 0; j + 1 < NLM; ++j)
         gw_nxt[j] = gp(J.mgbits)[((size_t)(tile + stride) * (NLM - 1) + j) * 64 + lane];
     }
     bf16x8 xf[2][KS1];
-    const RowInfo ri = finish_tile<KS1, false>(J, D, tile, cur, xf);   // moment tower: no per-period cols
+    RowInfo ri;
+    if constexpr (ZIN) ri = finish_ztile<WMB>(J, tile, zcur);
+    else ri = finish_tile<KS1, false>(J, D, tile, cur, xf);   // moment tower: no per-period cols
     bf16x8 act[NLM][2][KSM];
     uint32_t gates[NLM][2];
     f32x4 a[2][WMB];
-    layer0<KS1, WMB>(lds, D.m_fwd0, xf, a);
+    if constexpr (ZIN) {
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int u = 0; u < WMB; ++u) a[b][u] = zcur.zm[b][u];
+    } else {
+      layer0<KS1, WMB>(lds, D.m_fwd0, xf, a);
+    }
 #pragma unroll
     for (int j = 0; j < NLM; ++j) {
       if (j > 0) layer_chain<WMB, KSM>(lds, D.m_fwd + (j - 1) * WMB * KSM, act[j - 1], a);
@@ -811,20 +944,29 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
 #pragma unroll
         for (int u = 0; u < WMB; ++u) gbias[u] = mfma16(dzN[u], oh, gbias[u]);
       }
+      if constexpr (ZIN) {
+        if (j == 0 && slice == 0) {                 // layer-0 dz for k_wgrad0
+          const auto dzo = gp(J.dz_out) + (size_t)tile * WMB * 64 + lane;
+#pragma unroll
+          for (int u = 0; u < WMB; ++u) dzo[u * 64] = dzN[u];
+        }
+      }
 #pragma unroll
       for (int t = 0; t < TPS; ++t) {
         if (tl[t] == j) {
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
             if (j > 0 && v >= WMB) continue;
-            bf16x8 aN;
+            bf16x8 aN = zero8();
             if (j == 0) {
-              const int blk = 4 * tc[t] + v;
-              bf16x8 x0 = zero8(), x1 = zero8();
+              if constexpr (!ZIN) {
+                const int blk = 4 * tc[t] + v;
+                bf16x8 x0 = zero8(), x1 = zero8();
 #pragma unroll
-              for (int s = 0; s < KS1; ++s)
-                if (s == (blk >> 1)) { x0 = xf[0][s]; x1 = xf[1][s]; }
-              x_rows_k(x0, x1, blk, selN0, selN1, aN);
+                for (int s = 0; s < KS1; ++s)
+                  if (s == (blk >> 1)) { x0 = xf[0][s]; x1 = xf[1][s]; }
+                x_rows_k(x0, x1, blk, selN0, selN1, aN);
+              }
             } else {
               to_rows_k<WMB>(act[j > 0 ? j - 1 : 0], v, selP0, selP1, aN);
             }
@@ -857,7 +999,8 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
         }
       }
     }
-    cur = nxt;
+    if constexpr (ZIN) zcur = znxt;
+    else cur = nxt;
 #pragma unroll
     for (int j = 0; j < NH; ++j) gw_cur[j] = gw_nxt[j];
   }
@@ -948,7 +1091,12 @@ void launch_mlp_fwd(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int
                     hipStream_t st) {
   dim3 grid(gx, njobs), block(256);
   size_t sh = mlp_lds_bytes(D);
-#define F_CASE(K, W) if (KS1 == K && WMB == W) { hipLaunchKernelGGL((k_mlp_fwd<K, W>), grid, block, sh, st, jobs, D); HIP_OK(hipGetLastError()); return; }
+  if (D.wide) {
+#define FZ_CASE(W) if (WMB == W) { hipLaunchKernelGGL((k_mlp_fwd<2, W, true>), grid, block, sh, st, jobs, D); HIP_OK(hipGetLastError()); return; }
+    FZ_CASE(1) FZ_CASE(2) FZ_CASE(4)
+#undef FZ_CASE
+  }
+#define F_CASE(K, W) if (!D.wide && KS1 == K && WMB == W) { hipLaunchKernelGGL((k_mlp_fwd<K, W, false>), grid, block, sh, st, jobs, D); HIP_OK(hipGetLastError()); return; }
   F_CASE(2, 1) F_CASE(2, 2) F_CASE(2, 4) F_CASE(4, 1) F_CASE(4, 2) F_CASE(4, 4)
 #undef F_CASE
   dlap_throw_hip(hipErrorInvalidValue, "mlp_fwd: unsupported (KS1, WMB)", __FILE__, __LINE__);
@@ -958,7 +1106,13 @@ void launch_mlp_bwd_sdf(const MlpJob* jobs, int njobs, int gx, int nslice, int t
                         int KS1, int slab_stride, hipStream_t st) {
   dim3 grid(gx, njobs, nslice), block(256);
   size_t sh = bwd_lds_bytes(D, slab_stride);
-#define S_CASE(K, N, T) if (KS1 == K && D.nl_sdf == N && tps == T) { hipLaunchKernelGGL((k_mlp_bwd_sdf<K, N, T>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
+  if (D.wide) {
+#define SZ_CASE(N) if (D.nl_sdf == N && tps == 1) { hipLaunchKernelGGL((k_mlp_bwd_sdf<2, N, 1, true>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
+    SZ_CASE(1) SZ_CASE(2) SZ_CASE(3) SZ_CASE(4)
+#undef SZ_CASE
+    dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_sdf: unsupported depth (wide)", __FILE__, __LINE__);
+  }
+#define S_CASE(K, N, T) if (KS1 == K && D.nl_sdf == N && tps == T) { hipLaunchKernelGGL((k_mlp_bwd_sdf<K, N, T, false>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
   S_CASE(2, 1, 1) S_CASE(2, 2, 1) S_CASE(2, 3, 1) S_CASE(2, 4, 1)
   S_CASE(2, 2, 2)
   S_CASE(4, 1, 1) S_CASE(4, 2, 1) S_CASE(4, 3, 1) S_CASE(4, 4, 1)
@@ -970,7 +1124,15 @@ void launch_mlp_bwd_mom(const MlpJob* jobs, int njobs, int gx, int nslice, int t
                         int KS1, int WMB, int slab_stride, hipStream_t st) {
   dim3 grid(gx, njobs, nslice), block(256);
   size_t sh = bwd_lds_bytes(D, slab_stride);
-#define M_CASE(K, W, N) if (KS1 == K && WMB == W && D.nl_mom == N && tps == 1) { hipLaunchKernelGGL((k_mlp_bwd_mom<K, W, N, 1>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
+  if (D.wide) {
+#define MZ_CASE(W, N) if (WMB == W && D.nl_mom == N && tps == 1) { hipLaunchKernelGGL((k_mlp_bwd_mom<2, W, N, 1, true>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
+    MZ_CASE(1, 1) MZ_CASE(2, 1) MZ_CASE(4, 1)
+    MZ_CASE(1, 2) MZ_CASE(2, 2) MZ_CASE(4, 2)
+    MZ_CASE(1, 3) MZ_CASE(2, 3) MZ_CASE(4, 3)
+#undef MZ_CASE
+    dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_mom: unsupported depth/width (wide)", __FILE__, __LINE__);
+  }
+#define M_CASE(K, W, N) if (KS1 == K && WMB == W && D.nl_mom == N && tps == 1) { hipLaunchKernelGGL((k_mlp_bwd_mom<K, W, N, 1, false>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
   M_CASE(2, 1, 1) M_CASE(2, 2, 1) M_CASE(2, 4, 1)
   M_CASE(2, 1, 2) M_CASE(2, 2, 2) M_CASE(2, 4, 2)
   M_CASE(2, 1, 3) M_CASE(2, 2, 3) M_CASE(2, 4, 3)

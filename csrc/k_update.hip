@@ -100,7 +100,7 @@ DLAP_DEV int perm_u(int q, int j) { return j < 4 ? 4 * q + j : 16 + 4 * q + (j -
 template <typename PP>
 DLAP_DEV float pack_blob_elem(const ModelDesc* __restrict__ md, PP P, int e) {
   const MlpDims& D = md->md;
-  const int KS1 = md->KS1, WMB = md->WMB, KSM = (WMB + 1) / 2;
+  const int KS1 = md->KSB, WMB = md->WMB, KSM = (WMB + 1) / 2;   // (no layer-0 range if KSB = 0)
   const int frag = e >> 9, lane = (e >> 3) & 63, j = e & 7;
   const int q = lane >> 4, n = lane & 15;
   float val = 0.f;
@@ -186,6 +186,27 @@ DLAP_DEV float pack_proj_elem(const ModelDesc* __restrict__ md, PP P, int f) {
   return om < md->cm1 ? P[L0.w_off + om * L0.ld + m] : 0.f;
 }
 
+// Wide path: k_proj0's layer-0 weight fragments (natural k, as the tower blob's layer 0):
+// fragment (u, s) with u < 4 the SDF W0[16u + n][32s + 8q + j], u >= 4 the moment layer 0's
+// x columns; columns >= F and units beyond the layer width are zero.
+template <typename PP>
+DLAP_DEV float pack_blob0_elem(const ModelDesc* __restrict__ md, PP P, int e) {
+  const int KSX = md->md.KSX;
+  const int frag = e >> 9, lane = (e >> 3) & 63, j = e & 7;
+  const int q = lane >> 4, n = lane & 15;
+  const int u = frag / KSX, s = frag - u * KSX;
+  const int k = 32 * s + 8 * q + j;
+  if (k >= md->F) return 0.f;
+  if (u < 4) {
+    const PackLayer& L = md->s[0];
+    const int o = 16 * u + n;
+    return o < L.out ? P[L.w_off + o * L.ld + k] : 0.f;
+  }
+  const PackLayer& L = md->m[0];
+  const int o = 16 * (u - 4) + n;
+  return o < L.out ? P[L.w_off + o * L.ld + L.col0 + k] : 0.f;
+}
+
 // Re-pack the bf16 MFMA weight fragments + fp32 aux of every model after an update.
 // grid (ceil(elements / 256), models): one packed element per thread, gathered straight from
 // the (L2-resident) parameter vector -- a single memory round trip per launch.
@@ -195,12 +216,14 @@ __global__ __launch_bounds__(256) void k_pack(const UpdJob* __restrict__ jobs,
   const UpdJob& J = jobs[blockIdx.y];
   const int nel = md->md.blob_frags * 512, naux = nel + md->md.aux_floats;
   const int NP = md->proj_np, MP = md->proj_mp;
-  const int total = naux + (MP + 1) * NP;
+  const int nproj = naux + (MP + 1) * NP;
+  const int total = nproj + md->md.b0_frags * 512;
   const int e = blockIdx.x * 256 + threadIdx.x;
   const auto src = gp(static_cast<const float*>(J.params));
   if (e < nel) ((DLAP_GLOBAL __bf16*)(J.blob))[e] = (__bf16)pack_blob_elem(md, src, e);
   else if (e < naux) gp(J.aux)[e - nel] = pack_aux_elem(md, src, e - nel);
-  else if (e < total) gp(J.wproj)[e - naux] = pack_proj_elem(md, src, e - naux);
+  else if (e < nproj) gp(J.wproj)[e - naux] = pack_proj_elem(md, src, e - naux);
+  else if (e < total) ((DLAP_GLOBAL __bf16*)(J.blob0))[e - nproj] = (__bf16)pack_blob0_elem(md, src, e - nproj);
   if (bump && blockIdx.x == 0 && threadIdx.x == 0) {
     gp(J.adam_step)[bump - 1] = gp(J.adam_step)[bump - 1] + 1;
     gp(J.drop_step)[0] = gp(J.drop_step)[0] + 1;
@@ -208,7 +231,8 @@ __global__ __launch_bounds__(256) void k_pack(const UpdJob* __restrict__ jobs,
 }
 
 static int pack_blocks_of(const ModelDesc& mh) {
-  return (mh.md.blob_frags * 512 + mh.md.aux_floats + (mh.proj_mp + 1) * mh.proj_np + 255) / 256;
+  return (mh.md.blob_frags * 512 + mh.md.aux_floats + (mh.proj_mp + 1) * mh.proj_np + mh.md.b0_frags * 512 +
+          255) / 256;
 }
 
 void launch_pack(float* const*, const UpdJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,

@@ -34,6 +34,7 @@ struct GradTile {
 struct ModelDesc {
   // dimensions
   int F, M, Dm, KIN, KP, KS1, WMB;
+  int KSB;                  // layer-0 k-steps packed into the tower blob (KS1; 0 on the wide path)
   int K, cm1;
   int nrnn, H;
   int P, P_sdf;

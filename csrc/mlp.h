@@ -27,6 +27,8 @@ struct MlpJob {
   int gb_half;            // words per parity half (ntiles * nl_sdf * 64)
   uint32_t* mgbits;       // same for the moment tower's hidden layers (phase 2)
   const int* step;        // device step counter (dropout stream)
+  const f32x4* z;         // wide path: [ntiles][zc][64] layer-0 pre-activations (k_proj0)
+  bf16x8* dz_out;         // wide path, bwd: [ntiles][UB][64] layer-0 dz fragments (rows as k)
   int R, N, T;
   unsigned seed;
   int train;              // dropout active
@@ -47,6 +49,26 @@ struct MlpDims {
                                       // bias, W0 per-period cols [Dm][64], moment biases [nl][64]
   int blob_frags, aux_floats;
   int pp_lds_floats;             // >0: per-period inputs [T][Dm] staged in LDS (this many floats)
+  // wide path (F + Dm > 128): layer 0 of both towers runs as k_proj0 / k_wgrad0 (k_wide.hip)
+  int wide;                      // 1: the tower kernels read layer-0 pre-activations from z
+  int KX, KSX;                   // panel row width (multiple of 32) and its 32-column k-steps
+  int zc;                        // f32x4 chunks per tile in z: SDF (4 b + u), moment 8 + WMB b + u
+  int b0_frags;                  // layer-0 x-column fragments: SDF [4][KSX], moment [WMB][KSX]
+};
+
+// One model x split of the wide layer-0 kernels.
+struct WideJob {
+  const bf16x8* X;        // [R][KX/8] bf16 panel rows
+  const bf16x8* XT;       // train split: [ntiles][KX/16][64] rows-as-k fragments of X
+  const int2* rowti;      // [R] (t, i)
+  const float* pp;        // [T][Dm] per-period SDF inputs (wgrad per-period column blocks)
+  const bf16x8* blob0;    // packed layer-0 x-column weight fragments
+  f32x4* z;               // proj out: [ntiles][zc][64]
+  const bf16x8* dz;       // wgrad in: [ntiles][UB][64] (SDF UB = 4, moment UB = WMB)
+  float* part;            // wgrad partials [nsplit][16 UB][16 ncb]
+  float* grads;           // flat gradient vector of the model
+  int R, T;
+  int do_sdf, do_mom;     // proj: towers to project; wgrad: do_mom selects the moment tower
 };
 
 #define SLAB_EXTRA (DLAP_MAXL * 64 + 64 + 64)

@@ -25,6 +25,7 @@ struct UpdJob {            // one model
   int* drop_step;          // dropout stream counter
   float* gnorm;            // [1] pre-clip gradient norm of the step
   bf16x8* blob;
+  bf16x8* blob0;           // wide path: layer-0 x-column fragments of k_proj0 (nullptr: none)
   float* aux;
   float* wproj;            // packed input-projection matrix (written by k_pack)
   const float* dpp;        // [T][Dm] d(LSTM output)

@@ -300,3 +300,69 @@ def test_gpu_nonfinite_guard(tmp_path):
     with pytest.raises(NonFiniteError):
         train_3phase_gpu(cfg, b, b, b, num_epochs_unc=3, num_epochs_moment=1, num_epochs=2,
                          print_freq=100, ignore_epoch=0, seed=1, verbose=False, nan_policy="raise")
+
+
+# ---- wide panels: layer 0 as the streaming k_proj0 / k_wgrad0 GEMMs (F + Dm > 128) ----------
+def _wide_engine(monkeypatch, cfg, data, force, seeds=(7,), n_models=1):
+    monkeypatch.setenv("DLAP_WIDE", "1" if force else "0")
+    eng, b = _engine(cfg, n_models=n_models, seeds=seeds, data=data)
+    assert int(eng.desc["wide"]) == 1
+    return eng, b
+
+
+@pytest.mark.parametrize("F,M,force,rnn,hm,K", [(46, 8, True, [4], [], 8), (200, 8, False, [4], [], 8),
+                                                (300, 12, False, [2, 3], [16], 4), (140, 6, False, [], [], 8)])
+def test_wide_forward_and_gradients_match_fp32_reference(monkeypatch, F, M, force, rnn, hm, K):
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import flatten_state
+    cfg = default_cli_config(M, F, rnn_dim=rnn or [4], use_lstm=bool(rnn), num_moments=K,
+                             hidden_dim_moment=hm, dropout=0.0)
+    data = _batch(T=30, N=150, F=F, M=M)
+    eng, b = _wide_engine(monkeypatch, cfg, data, force)
+    torch.manual_seed(0)
+    model = AssetPricingGAN(cfg)
+    eng.set_model(0, model, 7)
+    with torch.no_grad():
+        out = model(b["macro_features"], b["individual_features"], b["returns"], b["mask"], phase="conditional")
+    eng.eng.forward_split(0, False, True)
+    T, N = b["mask"].shape
+    m = b["mask"].numpy()
+    assert _rel(eng.eng.read_ws(0, 0, "wn").reshape(T, N), out["weights"].numpy()) < 3e-2
+    h = eng.eng.read_ws(0, 0, "h").reshape(T, N, K)
+    assert _rel(h[m], out["moments"].permute(1, 2, 0).numpy()[m]) < 3e-2
+    sc = eng.eng.read_ws(0, 0, "scal")
+    assert _rel(sc[0], out["loss_conditional"].item()) < 3e-2
+    P_sdf = model.spec.param_counts()[0]
+    for phase, pname in ((1, "unconditional"), (3, "conditional"), (2, "moment")):
+        model.zero_grad()
+        o = model(b["macro_features"], b["individual_features"], b["returns"], b["mask"], phase=pname)
+        o["loss"].backward()
+        ref = flatten_state({k: (p.grad if p.grad is not None else torch.zeros_like(p))
+                             for k, p in model.named_parameters()}, model.spec)
+        eng.eng.backward_only(phase)
+        got = eng.eng.get_grads(0)
+        sl = slice(0, P_sdf) if phase != 2 else slice(P_sdf, None)
+        err = np.linalg.norm(got[sl] - ref[sl]) / np.linalg.norm(ref[sl])
+        cos = np.dot(got[sl], ref[sl]) / (np.linalg.norm(got[sl]) * np.linalg.norm(ref[sl]))
+        # bf16 layer-0 operands over F up to 300 inputs: slightly looser than the F=46 bound
+        assert err < 0.08 and cos > 0.997, (phase, err, cos)
+
+
+def test_wide_path_tracks_fused_path_and_is_deterministic(monkeypatch):
+    cfg = default_cli_config(8, 46)
+    data = _batch()
+    runs = {}
+    for force in (False, True, True):
+        monkeypatch.setenv("DLAP_WIDE", "1" if force else "0")
+        eng, _ = _engine(cfg, data=data)
+        for ph, n in ((1, 4), (2, 2), (3, 4)):
+            eng.eng.begin_phase(ph)
+            eng.run(ph, n, 1e-3, 1, 1.0, True)
+        eng.eng.sync()
+        runs.setdefault(force, []).append((eng.history_rows(0), eng.params(0)))
+    (hw0, pw0), (hw1, pw1) = runs[True]
+    np.testing.assert_array_equal(pw0, pw1)                       # bitwise reproducible
+    np.testing.assert_array_equal(np.nan_to_num(hw0), np.nan_to_num(hw1))
+    hf, pf = runs[False][0]
+    assert np.isfinite(hw0[:, 1]).all()
+    # same math, different rounding (fp32 per-period terms): close, not bitwise
+    assert np.abs(pw0 - pf).max() < 5e-3, np.abs(pw0 - pf).max()
