@@ -11,6 +11,7 @@
 //     from device counters, so it is captured ONCE per phase into a hipGraph and replayed;
 //   * history, best-epoch tracking and checkpoint snapshots are device-side: the host only
 //     synchronises at print intervals / phase boundaries.
+#include <cstdint>
 #include <cstdlib>
 #include <hip/hip_runtime.h>
 #include <pybind11/numpy.h>
@@ -162,16 +163,40 @@ class Engine {
                  py::array_t<int, py::array::c_style> row_ptr, py::array_t<float, py::array::c_style> Rm,
                  py::array_t<float, py::array::c_style> mask, py::array_t<float, py::array::c_style> macro,
                  int T, int N) {
+    const long R = (long)rowti.size() / 2;
+    if ((long)X.size() != R * md_.KP) throw std::invalid_argument("X must be [R][KP] bf16 bits");
+    set_split_impl(s, X.data(), false, rowti, row_ptr, Rm, mask, macro, T, N);
+  }
+  // Same, with the compacted panel X already in device memory (x_ptr: R * KP bf16 values, e.g.
+  // a torch CUDA tensor built on the GPU): the scaled panels never round-trip through the host.
+  void set_split_dev(int s, uintptr_t x_ptr, long x_elems, py::array_t<int, py::array::c_style> rowti,
+                     py::array_t<int, py::array::c_style> row_ptr, py::array_t<float, py::array::c_style> Rm,
+                     py::array_t<float, py::array::c_style> mask, py::array_t<float, py::array::c_style> macro,
+                     int T, int N) {
+    const long R = (long)rowti.size() / 2;
+    if (x_elems != R * md_.KP) throw std::invalid_argument("X must be [R][KP] bf16 values");
+    set_split_impl(s, reinterpret_cast<const uint16_t*>(x_ptr), true, rowti, row_ptr, Rm, mask, macro, T, N);
+  }
+  void set_split_impl(int s, const uint16_t* Xp, bool x_on_device, py::array_t<int, py::array::c_style> rowti,
+                      py::array_t<int, py::array::c_style> row_ptr, py::array_t<float, py::array::c_style> Rm,
+                      py::array_t<float, py::array::c_style> mask, py::array_t<float, py::array::c_style> macro,
+                      int T, int N) {
     if (s < 0 || s > 2) throw std::invalid_argument("split must be 0, 1 or 2");
     if (T > DLAP_MAX_T) throw std::invalid_argument("T exceeds DLAP_MAX_T");
     SplitDev& D = splits_[s];
-    const int R = (int)rowti.size() / 2;
-    if ((long)X.size() != (long)R * md_.KP) throw std::invalid_argument("X must be [R][KP] bf16 bits");
+    if ((long)rowti.size() / 2 > (long)INT32_MAX) throw std::invalid_argument("too many panel rows");
+    const int R = (int)(rowti.size() / 2);
     if ((long)Rm.size() != (long)T * N || (long)mask.size() != (long)T * N) throw std::invalid_argument("Rm/mask must be [T*N]");
     if ((int)row_ptr.size() != T + 1) throw std::invalid_argument("row_ptr must be [T+1]");
     if (md_.M > 0 && (long)macro.size() != (long)T * md_.M) throw std::invalid_argument("macro must be [T][M]");
     D.T = T; D.N = N; D.R = R;
-    up(D.X, X.data(), X.size());
+    const size_t nx = (size_t)R * md_.KP;
+    if (x_on_device) {
+      D.X.alloc(nx, false);
+      if (nx) HIP_OK(hipMemcpy(D.X.p, Xp, nx * sizeof(uint16_t), hipMemcpyDeviceToDevice));
+    } else {
+      up(D.X, Xp, nx);
+    }
     up(D.rowti, rowti.data(), (size_t)2 * R);
     {
       std::vector<float> rc(R);
@@ -1031,6 +1056,7 @@ PYBIND11_MODULE(_dlap_hip, m) {
            py::arg("max_epochs"))
       .def("describe", &Engine::describe)
       .def("set_split", &Engine::set_split)
+      .def("set_split_dev", &Engine::set_split_dev)
       .def("set_params", &Engine::set_params)
       .def("get_params", &Engine::get_params)
       .def("get_grads", &Engine::get_grads)

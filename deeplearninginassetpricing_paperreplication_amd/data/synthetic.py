@@ -232,6 +232,23 @@ def generate_all_splits(output_dir: str, n_periods_train: int = 120, n_periods_v
 # --------------------------------------------------------------------------------------
 # Fast generator (torch, float32, CPU or GPU) for the scaled BASELINE panels
 # --------------------------------------------------------------------------------------
+def _row_quantiles(x, qs):
+    """Per-row quantiles with torch.quantile's default linear interpolation, via one sort:
+    torch.quantile refuses inputs above 2^24 elements (a 16-period chunk of a 30000 x 512
+    panel is 2.5e8), and sorting once serves both percentiles."""
+    import torch
+    n = x.shape[1]
+    srt = torch.sort(x, dim=1).values
+    out = []
+    for q in qs:
+        pos = q * (n - 1)
+        lo = int(pos)
+        hi = min(lo + 1, n - 1)
+        frac = pos - lo
+        out.append(torch.lerp(srt[:, lo], srt[:, hi], torch.full((), frac, device=x.device, dtype=x.dtype)))
+    return torch.stack(out)
+
+
 def generate_panel_fast(T: int, N: int, F: int, M: int, seed: int = 0, device: str = "cpu",
                         n_factors: int = 5, chunk: int = 16):
     """Return (returns [T,N] f32, features [T,N,F] f32, mask [T,N] bool, macro [T,M] f32).
@@ -262,8 +279,7 @@ def generate_panel_fast(T: int, N: int, F: int, M: int, seed: int = 0, device: s
         c = torch.randn(z - a, N, F, generator=g, device=dev)
         c[:, :, :npred] = (b[:, sel][None] + c[:, :, :npred] * 0.5
                            + torch.randn(z - a, 1, npred, generator=g, device=dev) * 0.1)
-        q = torch.quantile(c.transpose(1, 2).reshape(-1, N),
-                           torch.tensor([0.05, 0.95], device=dev), dim=1)  # [2, (z-a)*F]
+        q = _row_quantiles(c.transpose(1, 2).reshape(-1, N), (0.05, 0.95))  # [2, (z-a)*F]
         lo = q[0].reshape(z - a, 1, F)
         hi = q[1].reshape(z - a, 1, F)
         c = torch.minimum(torch.maximum(c, lo), hi)

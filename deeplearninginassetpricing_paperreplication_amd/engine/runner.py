@@ -17,7 +17,7 @@ import torch
 
 from ..config import ModelSpec
 from ..ops.native import load as load_native
-from .panel import prepare_split
+from .panel import prepare_split, prepare_split_device
 
 HIST = dict(phase=0, train_loss=1, train_sharpe=2, valid_loss=3, valid_sharpe=4, test_loss=5,
             test_sharpe=6, train_loss_unc=7, train_loss_cond=8, grad_norm=9, valid_loss_unc=10,
@@ -69,9 +69,17 @@ class GANEngine:
         for s, b in enumerate((train, valid, test)):
             if b is None:
                 continue
-            ps = prepare_split(b, self.KP)
-            self.eng.set_split(s, ps.X.reshape(-1), ps.rowti.reshape(-1), ps.row_ptr, ps.Rm, ps.mask,
-                               ps.macro.reshape(-1), ps.T, ps.N)
+            x = b["individual_features"]
+            if isinstance(x, torch.Tensor) and x.is_cuda:
+                # compact on the GPU, hand the engine a device pointer (no host copy of X)
+                ps = prepare_split_device(b, self.KP)
+                self.eng.set_split_dev(s, ps.X.data_ptr(), ps.X.numel(), ps.rowti.reshape(-1), ps.row_ptr,
+                                       ps.Rm, ps.mask, ps.macro.reshape(-1), ps.T, ps.N)
+                ps.X = None                                  # the engine keeps its own copy
+            else:
+                ps = prepare_split(b, self.KP)
+                self.eng.set_split(s, ps.X.reshape(-1), ps.rowti.reshape(-1), ps.row_ptr, ps.Rm, ps.mask,
+                                   ps.macro.reshape(-1), ps.T, ps.N)
             self.splits[s] = ps
 
     # ---- parameters -----------------------------------------------------------------
