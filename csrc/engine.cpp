@@ -607,23 +607,26 @@ class Engine {
       throw std::invalid_argument("feature dim too large for the wide layer-0 kernel (LDS budget)");
     // gradient tiles: layer-0 chunks first (none on the wide path: k_wgrad0), then one tile per
     // later layer (slice = tile, TPS 1)
-    const int C0 = wide ? 0 : d.KS1 / 2;
+    // (wide path: only the per-period input columns W0[:, F:F+Dm] have layer-0 tiles)
+    const int C0 = wide ? (d.Dm + 63) / 64 : d.KS1 / 2;
     int t = 0;
     for (int c = 0; c < C0; ++c, ++t)
-      d.tile_s[t] = GradTile{d.s[0].w_off, d.s[0].ld, 0, d.s[0].out, d.s[0].in, c, t};
+      d.tile_s[t] = wide ? GradTile{d.s[0].w_off, d.s[0].ld, F, d.s[0].out, d.Dm, c, t}
+                         : GradTile{d.s[0].w_off, d.s[0].ld, 0, d.s[0].out, d.s[0].in, c, t};
     for (int j = 1; j < d.nl_s; ++j, ++t)
       d.tile_s[t] = GradTile{d.s[j].w_off, d.s[j].ld, 0, d.s[j].out, d.s[j].in, 0, t};
     d.ntile_s = t;
     // two gradient tiles per slice share one forward recompute (fits the 512-register
     // budget of a single wave per SIMD); DLAP_TPS=1 forces one tile per slice
     const char* tps_env = std::getenv("DLAP_TPS");
-    const bool tps2 = !wide && d.KS1 == 2 && d.ntile_s == 2 && !(tps_env && std::atoi(tps_env) == 1);
+    const bool tps2 = (wide || d.KS1 == 2) && d.ntile_s == 2 && !(tps_env && std::atoi(tps_env) == 1);
     d.tps_s = tps2 ? 2 : 1;
     // at least one slice: slice 0 also produces the bias / output / per-period gradients
     d.nslice_s = std::max(1, (d.ntile_s + d.tps_s - 1) / d.tps_s);
     for (int k = 0; k < d.ntile_s; ++k) d.tile_s[k].slice = k / d.tps_s;
     t = 0;
-    for (int c = 0; c < C0; ++c, ++t)
+    const int C0m = wide ? 0 : d.KS1 / 2;
+    for (int c = 0; c < C0m; ++c, ++t)
       d.tile_m[t] = GradTile{d.m[0].w_off, d.m[0].ld, d.m[0].col0, d.m[0].out, d.m[0].in, c, t};
     for (int j = 1; j < d.nl_m; ++j, ++t)
       d.tile_m[t] = GradTile{d.m[j].w_off, d.m[j].ld, 0, d.m[j].out, d.m[j].in, 0, t};

@@ -241,6 +241,21 @@ DLAP_DEV void pack_blocks(const f32x4 (&a)[2][UB], bf16x8 (&pf)[2][(UB + 1) / 2]
       pf[b][s] = pack8(a[b][2 * s], (2 * s + 1 < UB) ? a[b][2 * s + 1] : zero4());
 }
 
+// Natural-k fragment of the per-period SDF inputs of k-step s for a row of period t (lane:
+// columns 32 s + 8 q + j of pp[t], zero beyond Dm), bf16 as the fused path inserts them: the
+// wide path's operand for the W0[:, F:F+Dm] weight-gradient tile (transposed by x_rows_k).
+template <typename PP>
+DLAP_DEV bf16x8 pp_xfrag(PP pp, int t, int s, const MlpDims& D) {
+  const int q = lane_id() >> 4;
+  bf16x8 f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int col = 32 * s + 8 * q + j;
+    f[j] = (__bf16)(col < D.Dm ? pp[t * D.Dm + col] : 0.f);
+  }
+  return f;
+}
+
 struct DropCtx {
   bool on; uint32_t thr16; float scale; uint32_t seed, step;
 };
@@ -617,7 +632,9 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
   const int lane = lane_id(), q = lane >> 4, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   const int ntiles = (J.R + 31) >> 5;
   const int slice = blockIdx.z;
-  constexpr int C0 = ZIN ? 0 : KS1 / 2;      // 64-column chunks of layer 0
+  // 64-column chunks of layer 0 with a gradient tile: the X chunks (fused) or, on the wide
+  // path, only the per-period input columns (the X columns are k_wgrad0's)
+  const int C0 = ZIN ? (D.Dm + 63) / 64 : KS1 / 2;
   const bf16x8 selP0 = make_sel(true, 0), selP1 = make_sel(true, 1);
   const bf16x8 selN0 = make_sel(false, 0), selN1 = make_sel(false, 1);
 
@@ -731,12 +748,21 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
           for (int v = 0; v < 4; ++v) {
             bf16x8 aN = zero8();
             if (j == 0) {
+              const int blk = 4 * tc[t] + v;
               if constexpr (!ZIN) {
-                const int blk = 4 * tc[t] + v;
                 bf16x8 x0 = zero8(), x1 = zero8();
 #pragma unroll
                 for (int s = 0; s < KS1; ++s)
                   if (s == (blk >> 1)) { x0 = xf[0][s]; x1 = xf[1][s]; }
+                x_rows_k(x0, x1, blk, selN0, selN1, aN);
+              } else {
+                if (16 * blk >= D.Dm) continue;             // wave-uniform: no columns here
+                bf16x8 x0, x1;
+                if (D.pp_lds_floats > 0) {
+                  x0 = pp_xfrag(spp, ri.t[0], blk >> 1, D); x1 = pp_xfrag(spp, ri.t[1], blk >> 1, D);
+                } else {
+                  x0 = pp_xfrag(gp(J.pp), ri.t[0], blk >> 1, D); x1 = pp_xfrag(gp(J.pp), ri.t[1], blk >> 1, D);
+                }
                 x_rows_k(x0, x1, blk, selN0, selN1, aN);
               }
             } else {
@@ -1107,8 +1133,8 @@ void launch_mlp_bwd_sdf(const MlpJob* jobs, int njobs, int gx, int nslice, int t
   dim3 grid(gx, njobs, nslice), block(256);
   size_t sh = bwd_lds_bytes(D, slab_stride);
   if (D.wide) {
-#define SZ_CASE(N) if (D.nl_sdf == N && tps == 1) { hipLaunchKernelGGL((k_mlp_bwd_sdf<2, N, 1, true>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
-    SZ_CASE(1) SZ_CASE(2) SZ_CASE(3) SZ_CASE(4)
+#define SZ_CASE(N, T) if (D.nl_sdf == N && tps == T) { hipLaunchKernelGGL((k_mlp_bwd_sdf<2, N, T, true>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
+    SZ_CASE(1, 1) SZ_CASE(2, 1) SZ_CASE(3, 1) SZ_CASE(4, 1) SZ_CASE(2, 2)
 #undef SZ_CASE
     dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_sdf: unsupported depth (wide)", __FILE__, __LINE__);
   }

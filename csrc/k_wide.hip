@@ -14,8 +14,8 @@
 //              k_xt_build: with 288 GB of HBM the second copy is free), so both operands are
 //              plain lane-linear 16-byte loads. Split-K over row tiles into per-workgroup
 //              partials, then k_wgrad0_fin sums them in a fixed order (deterministic) straight
-//              into the flat gradient vector. The per-period columns of the SDF layer 0 are
-//              extra column blocks whose rows-as-k operand is gathered from pp[t(row)].
+//              into the flat gradient vector. (The SDF layer 0's per-period columns keep a
+//              gradient tile in the tower backward, which has pp staged in LDS.)
 //
 // One train step at 600 x 30000 x 512 streams the train panel twice (forward, weight
 // gradient): HBM-bound, the MFMA work (2 x R x 512 x 72 flop per pass) is ~1 % of the chip.
@@ -163,9 +163,7 @@ void launch_proj0(const WideJob* jobs, int njobs, int gx, const MlpDims& D, int 
 }
 
 // ------------------------------------------------------------------- weight gradient ----
-int wide_ncb(const MlpDims& D, bool mom) {
-  return (D.KX >> 4) + (mom ? 0 : (D.Dm + 15) / 16);
-}
+int wide_ncb(const MlpDims& D, bool) { return D.KX >> 4; }
 
 #define WG_WAVES 8
 #define WG_VPW_MAX 5
@@ -175,21 +173,6 @@ static int wg_vpw(int ncb) { return std::min(WG_VPW_MAX, std::max(1, (ncb + WG_W
 size_t wide_part_floats(const MlpDims& D, int WMB, int nsplit) {
   const size_t s = (size_t)64 * 16 * wide_ncb(D, false), m = (size_t)16 * WMB * 16 * wide_ncb(D, true);
   return (size_t)nsplit * std::max(s, m);
-}
-
-// Rows-as-k operand of a per-period column block p: lane l element j = pp[t(row)][16 p + (l & 15)]
-// (bf16, as the fused path rounds the inserted per-period columns), row as in XT.
-DLAP_DEV bf16x8 pp_frag(const WideJob& J, const MlpDims& D, int tile, int p, int q, int n) {
-  bf16x8 f;
-  const int d = 16 * p + n;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int row = tile * 32 + 16 * (j >> 2) + 4 * q + (j & 3);
-    float v = 0.f;
-    if (row < J.R && d < D.Dm) v = gp(J.pp)[gp(J.rowti)[row].x * D.Dm + d];
-    f[j] = (__bf16)v;
-  }
-  return f;
 }
 
 // grid (nsplit, jobs, passes), WG_WAVES waves. Workgroup `split` accumulates the row tiles
@@ -219,11 +202,7 @@ __global__ __launch_bounds__(WG_WAVES * 64) void k_wgrad0(const WideJob* __restr
 #pragma unroll
     for (int u = 0; u < UB; ++u) dz[u] = dzp[u * 64];
 #pragma unroll
-    for (int k = 0; k < VPW; ++k) {
-      if (vb[k] < NVX) xt[k] = gp(J.XT)[((size_t)tile * NVX + vb[k]) * 64 + lane];
-      else if (vb[k] < ncb) xt[k] = pp_frag(J, D, tile, vb[k] - NVX, q, n);
-      else xt[k] = zero8();
-    }
+    for (int k = 0; k < VPW; ++k) xt[k] = vb[k] < NVX ? gp(J.XT)[((size_t)tile * NVX + vb[k]) * 64 + lane] : zero8();
   };
   bf16x8 dzc[UB], xc[VPW], dzn[UB], xn[VPW];
   if (t0 < t1) load(t0, dzc, xc);
@@ -274,13 +253,7 @@ __global__ __launch_bounds__(256) void k_wgrad0_fin(const WideJob* __restrict__ 
   const bool mom = J.do_mom;
   const PackLayer& L = mom ? md->m[0] : md->s[0];
   if (unit >= L.out) return;
-  const int KX = md->md.KX;
-  if (col < KX) {
-    if (col < md->F) gp(J.grads)[L.w_off + unit * L.ld + L.col0 + col] = v;
-  } else if (!mom) {
-    const int d = col - KX;
-    if (d < md->Dm) gp(J.grads)[L.w_off + unit * L.ld + md->F + d] = v;
-  }
+  if (col < md->F) gp(J.grads)[L.w_off + unit * L.ld + L.col0 + col] = v;
 }
 
 void launch_wgrad0(const WideJob* jobs, int njobs, const ModelDesc* md, const MlpDims& D, bool mom,

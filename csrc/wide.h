@@ -9,12 +9,12 @@ struct ModelDesc;
 void launch_xt_build(const u16* X, u16* XT, int R, int KX, hipStream_t st);
 // z = X . W0x^T of the SDF (do_sdf) and moment (do_mom) towers for every job.
 void launch_proj0(const WideJob* jobs, int njobs, int gx, const MlpDims& D, int WMB, hipStream_t st);
-// Column blocks (16 wide) of the layer-0 weight gradient: the KX panel columns plus, for the
-// SDF tower, the per-period input columns.
+// Column blocks (16 wide) of the layer-0 weight gradient: the KX panel columns (the SDF's
+// per-period input columns have a gradient tile in the tower backward instead).
 int wide_ncb(const MlpDims& D, bool mom);
 // Floats of one model's weight-gradient partials for nsplit row splits.
 size_t wide_part_floats(const MlpDims& D, int WMB, int nsplit);
-// dW0x (+ the per-period columns) of the SDF (mom = false) or moment tower into the flat
+// dW0x of the SDF (mom = false) or moment tower into the flat
 // gradient vectors: split-K MFMA over the train split, then a fixed-order reduce.
 void launch_wgrad0(const WideJob* jobs, int njobs, const ModelDesc* md, const MlpDims& D, bool mom,
                    int WMB, int nsplit, hipStream_t st);
