@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import os
 import time
+from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -47,6 +48,26 @@ def unflatten_state(flat: np.ndarray, spec: ModelSpec) -> Dict[str, torch.Tensor
     return out
 
 
+_PREP_CACHE: "OrderedDict[tuple, object]" = OrderedDict()
+
+
+def _prepared(batch: Dict, KP: int):
+    """Host compaction of a split, memoised on the identity/version of its input tensors: the
+    ensemble and sweep drivers build one engine per architecture bucket over the same panel."""
+    def tk(t):
+        return (id(t), t.data_ptr(), t._version) if isinstance(t, torch.Tensor) else (id(t),)
+    key = (KP,) + tuple(tk(batch.get(k)) for k in ("individual_features", "returns", "mask", "macro_features"))
+    hit = _PREP_CACHE.get(key)
+    if hit is None:
+        # the entry keeps the inputs alive, so their ids cannot be reused while it exists
+        hit = (prepare_split(batch, KP), [batch.get(k) for k in ("individual_features", "returns", "mask",
+                                                                   "macro_features")])
+        _PREP_CACHE[key] = hit
+        while len(_PREP_CACHE) > 6:
+            _PREP_CACHE.popitem(last=False)
+    return hit[0]
+
+
 class GANEngine:
     """Native multi-model trainer for one architecture (``spec``) on the current GPU."""
 
@@ -77,7 +98,7 @@ class GANEngine:
                                        ps.Rm, ps.mask, ps.macro.reshape(-1), ps.T, ps.N)
                 ps.X = None                                  # the engine keeps its own copy
             else:
-                ps = prepare_split(b, self.KP)
+                ps = _prepared(b, self.KP)
                 self.eng.set_split(s, ps.X.reshape(-1), ps.rowti.reshape(-1), ps.row_ptr, ps.Rm, ps.mask,
                                    ps.macro.reshape(-1), ps.T, ps.N)
             self.splits[s] = ps

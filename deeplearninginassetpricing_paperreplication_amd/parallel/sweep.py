@@ -11,9 +11,9 @@ Grid (paper Table A.VIII):
     LR  {1e-3,5e-4,2e-4,1e-4}
 3 * 2 * 2 * 2 * 4 * 4 = 384 configurations.
 
-Execution: configurations that share an architecture (everything but LR) form a *bucket*; a
-bucket is trained as ONE batched native-engine run with one member per LR (per-member learning
-rates, ``Engine.set_lr``), so the 384 configs are 96 engine runs. Buckets are dealt round-robin
+Execution: configurations that build the same network form a *bucket* (LR and the no-op CSMV
+vary inside it); a bucket is trained as ONE batched native-engine run, one member per config
+(per-member learning rates, ``Engine.set_lr``), so the 384 configs are 48 engine runs. Buckets are dealt round-robin
 over ranks. A bucket that raises marks its configs failed (metrics NaN) without stopping the
 sweep; the per-config metric table is exchanged with one all-gather and every rank ranks the
 configs identically (best = highest validation Sharpe of the paper-sign SDF factor by default).
@@ -29,7 +29,7 @@ from typing import Dict, List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
-from ..config import default_cli_config
+from ..config import ModelSpec, default_cli_config
 from . import comm
 from .ensemble import SPLITS, _init_models, _load_batches
 
@@ -52,10 +52,15 @@ def paper_grid(M: int, F: int, grid: Dict = GRID, dropout: float = 0.05) -> List
 
 
 def buckets(entries: Sequence[Tuple[Dict, float, Dict]]) -> List[List[int]]:
-    """Group config indices that differ only in lr (same architecture -> one batched run)."""
-    groups: Dict[str, List[int]] = {}
+    """Group config indices that build the same network (one batched engine run each).
+
+    The key is the ``ModelSpec`` the config produces, so configs that differ only in lr or in
+    keys the model ignores -- CSMV (``num_units_rnn_moment``) is such a no-op in the reference
+    (`/root/reference/src/model.py:309-311`) -- share a bucket: the paper grid's 384 configs
+    are 48 architectures x 8 members."""
+    groups: Dict[object, List[int]] = {}
     for i, (cfg, _, _) in enumerate(entries):
-        groups.setdefault(json.dumps(cfg, sort_keys=True), []).append(i)
+        groups.setdefault(ModelSpec.from_config(cfg), []).append(i)
     return list(groups.values())
 
 
@@ -102,17 +107,21 @@ def run_bucket(entries, idx: List[int], batches: Dict[str, Dict], device: torch.
 
 def run_sweep(batches: Dict[str, Dict], entries, dist: Optional[comm.Dist] = None, epochs=(256, 64, 1024),
               ignore_epoch: int = 64, seed: int = 42, selection_sign: float = 1.0,
-              rank_sign: float = -1.0, fail_buckets: Sequence[int] = ()) -> Dict:
+              rank_sign: float = -1.0, fail_buckets: Sequence[int] = (), verbose: bool = False) -> Dict:
     d = dist or comm.Dist()
     bks = buckets(entries)
     mine = comm.shard(len(bks), d.rank, d.world)
     local = {}
     errors = {}
-    for b in mine:
+    t_start = time.time()
+    for k, b in enumerate(mine):
         try:
             if b in set(fail_buckets):
                 raise RuntimeError("injected failure")
             local[b] = run_bucket(entries, bks[b], batches, d.device, epochs, ignore_epoch, seed, selection_sign)
+            if verbose:
+                print(f"[sweep rank {d.rank}] bucket {k + 1}/{len(mine)} ({len(bks[b])} configs) "
+                      f"done, {time.time() - t_start:.1f} s", flush=True)
         except Exception as e:  # isolate: this bucket's configs report NaN
             errors[b] = f"{type(e).__name__}: {e}"
             z = np.full((len(bks[b]), len(METRICS)), np.nan)
@@ -130,7 +139,9 @@ def run_sweep(batches: Dict[str, Dict], entries, dist: Optional[comm.Dist] = Non
     ok = table[:, 0] > 0.5
     score = np.where(ok, rank_sign * table[:, 1], -np.inf)
     best = int(np.argmax(score)) if ok.any() else -1
+    walls = comm.all_gather_rows(d, np.array([[time.time() - t_start]]), d.world, [d.rank])[:, 0]
     return {"n_configs": len(entries), "n_buckets": len(bks), "n_ok": int(ok.sum()),
+            "world_size": d.world, "wall_s": float(walls.max()),
             "failed": [int(i) for i in np.where(~ok)[0]], "best_index": best,
             "best_point": entries[best][2] if best >= 0 else None,
             "best_valid_sharpe": float(table[best, 1]) if best >= 0 else None,
@@ -162,7 +173,8 @@ def main(argv=None):
     entries = paper_grid(M, F)
     if a.limit:
         entries = entries[:a.limit]
-    res = run_sweep(batches, entries, d, (a.epochs_unc, a.epochs_moment, a.epochs), a.ignore_epoch, a.seed)
+    res = run_sweep(batches, entries, d, (a.epochs_unc, a.epochs_moment, a.epochs), a.ignore_epoch, a.seed,
+                    verbose=True)
     if d.is_main:
         if a.out:
             np.savez(a.out, table=res["table"], metrics=np.array(METRICS))

@@ -116,10 +116,11 @@ def test_sweep_sharding_and_failure_isolation(tmp_path):
     assert np.all(np.isfinite(t[ok, 1]))
 
 
-def test_paper_grid_is_384_configs_in_96_buckets():
+def test_paper_grid_is_384_configs_in_48_buckets():
     from deeplearninginassetpricing_paperreplication_amd.parallel.sweep import buckets, paper_grid
     e = paper_grid(178, 46)
-    assert len(e) == 384 and len(buckets(e)) == 96
+    # 3 HL x 2 SMV x 2 CHL x 4 CHU architectures; LR and the no-op CSMV vary inside a bucket
+    assert len(e) == 384 and len(buckets(e)) == 48
     cfg, lr, pt = e[0]
     assert cfg["hidden_dim"] == [64, 64] and cfg["num_units_rnn"] == [4] and lr == 1e-3
-    assert {len(b) for b in buckets(e)} == {4}
+    assert {len(b) for b in buckets(e)} == {8}
