@@ -120,6 +120,7 @@ class Engine {
     HIP_OK(hipEventCreateWithFlags(&ev_a_, hipEventDisableTiming));
     eval_gx_ = env_int("DLAP_EVAL_GX", 0);
     b_wait_ = env_int("DLAP_B_WAIT", 0);
+    side_metrics_ = env_int("DLAP_SIDE_METRICS", 0) != 0;
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
                residual);
     d_desc_.alloc(sizeof(ModelDesc));
@@ -462,6 +463,7 @@ class Engine {
   hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr, ev_mid_ = nullptr, ev_a_ = nullptr;
   int eval_gx_ = 0;                          // cap on the evaluation tower grid (DLAP_EVAL_GX)
   int b_wait_ = 0;                           // evaluation towers after train towers (DLAP_B_WAIT)
+  bool side_metrics_ = false;                // train Sharpe monitor on a graph side branch (DLAP_SIDE_METRICS)
   ModelDesc md_{};
   DevBuf<char> d_desc_;
   SplitDev splits_[3];
@@ -987,7 +989,7 @@ class Engine {
       enqueue_eval(st2_);                                 // previous epoch's evaluation
       enqueue_epoch_end(phase, ignore_epoch, sel, st2_);  // ... and its bookkeeping
       enqueue_dropmask(phase, 1, st2_);                   // next epoch's dropout masks
-      enqueue_train_grads(phase, st2_, true);             // this epoch's forward/backward
+      enqueue_train_grads(phase, side_metrics_ ? st2_ : nullptr, true);   // this epoch's fwd/bwd
     } else {
       // the evaluation towers start once the training towers (b_wait_ 1: backward, 2:
       // forward) are done, so the wide kernels of the two branches do not contend
