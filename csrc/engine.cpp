@@ -1080,6 +1080,7 @@ PYBIND11_MODULE(_dlap_hip, m) {
       .def("set_pipeline", &Engine::set_pipeline)
       .def("set_lr", &Engine::set_lr)
       .def_static("rnn_timestamps", []() { return rnn_timestamps(); })
+      .def_static("loss_timestamps", []() { return loss_timestamps(); })
       .def_static("mlp_timestamps", []() { return mlp_timestamps(); })
       .def("forward_split", &Engine::forward_split)
       .def("train_step", &Engine::train_step)

@@ -220,10 +220,15 @@ __global__ __launch_bounds__(256) void k_asset_red(const LossJob* __restrict__ j
   }
 }
 
-DLAP_DEV void final_losses(const LossJob& J, float& lc, float& lu) {
+// Block-wide (256 threads) fixed-order sum of the asset blocks' loss partials: every thread
+// takes a strided share (all loads in flight at once, instead of 2 * nblk dependent round trips
+// on one thread), then the fixed-order block reduction.
+DLAP_DEV void final_losses(const LossJob& J, float& lc, float& lu, float* red) {
   const int nblk = (J.N + 255) >> 8;
   float a = 0.f, b = 0.f;
-  for (int k = 0; k < nblk; ++k) { a += gp(J.part)[2 * k]; b += gp(J.part)[2 * k + 1]; }
+  for (int k = threadIdx.x; k < nblk; k += 256) { a += gp(J.part)[2 * k]; b += gp(J.part)[2 * k + 1]; }
+  a = block_sum<256>(a, red);
+  b = block_sum<256>(b, red);
   lc = J.h ? a / ((float)J.K * (float)J.N) : 0.f;
   lu = b / (float)J.N;
 }
@@ -331,6 +336,11 @@ __global__ __launch_bounds__(PER_NT) void k_period_bwd(const LossJob* __restrict
   }
 }
 
+// In-kernel timestamps of k_job_metrics, last block (Engine.loss_timestamps, 100 MHz clock):
+// [0] start, [1] losses reduced, [2] pass 0 (train monitor) done, [3] pass 1 done.
+__device__ long long g_loss_ts[4];
+#define MET_TS(slot) do { if (threadIdx.x == 0 && blockIdx.x == gridDim.x - 1) g_loss_ts[slot] = wall_clock64(); } while (0)
+
 // ---------------------------------------------------------------- per-job scalars -------
 // scal layout: see loss.h (SC_*).
 __global__ __launch_bounds__(256) void k_job_metrics(const LossJob* __restrict__ jobs) {
@@ -338,9 +348,11 @@ __global__ __launch_bounds__(256) void k_job_metrics(const LossJob* __restrict__
   __shared__ float red[4];
   __shared__ float ret[DLAP_MAX_T];
   const int T = J.T;
+  MET_TS(0);
+  float lc, lu;
+  final_losses(J, lc, lu, red);
+  MET_TS(1);
   if (threadIdx.x == 0) {
-    float lc, lu;
-    final_losses(J, lc, lu);
     float lres = 0.f, inv_b, n1;
     if (J.res_factor > 0.f) residual_stats(J, lres, inv_b, n1);
     gp(J.scal)[SC_LCOND] = lc;
@@ -369,17 +381,53 @@ __global__ __launch_bounds__(256) void k_job_metrics(const LossJob* __restrict__
         gp(J.scal)[SC_SHARPE] = sharpe;
         gp(J.scal)[SC_MEAN] = mean;
         gp(J.scal)[SC_STD] = sqrtf(v / (float)T);
-        float cum = 1.f, peak = 1.f, mdd = 0.f;
-        for (int t = 0; t < T; ++t) {
-          cum *= 1.f + ret[t];
-          peak = t == 0 ? cum : fmaxf(peak, cum);
-          mdd = fminf(mdd, (cum - peak) / peak);
-        }
-        gp(J.scal)[SC_MDD] = mdd;
       }
     }
+    if (pass == 1 && threadIdx.x < 64) {
+      // max drawdown of cumprod(1 + r) on wave 0: each lane owns a contiguous run of periods;
+      // prefix product and prefix running-max across lanes by shuffle scans (replaces a
+      // T-step serial loop on one thread; products associate differently: fp32 rounding only)
+      const int lane = threadIdx.x, per = (T + 63) >> 6;
+      const int t0 = min(T, lane * per), t1 = min(T, t0 + per);
+      float prod = 1.f;
+      for (int t = t0; t < t1; ++t) prod *= 1.f + ret[t];
+      float incl = prod;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const float u = __shfl_up(incl, o, 64);
+        if (lane >= o) incl *= u;
+      }
+      float base = __shfl_up(incl, 1, 64);
+      if (lane == 0) base = 1.f;
+      float cum = base, lmax = -INFINITY;
+      for (int t = t0; t < t1; ++t) { cum *= 1.f + ret[t]; lmax = fmaxf(lmax, cum); }
+      float pmax = lmax;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const float u = __shfl_up(pmax, o, 64);
+        if (lane >= o) pmax = fmaxf(pmax, u);
+      }
+      float peak = __shfl_up(pmax, 1, 64);
+      if (lane == 0) peak = -INFINITY;
+      cum = base;
+      float mdd = 0.f;
+      for (int t = t0; t < t1; ++t) {
+        cum *= 1.f + ret[t];
+        peak = t == 0 ? cum : fmaxf(peak, cum);
+        mdd = fminf(mdd, (cum - peak) / peak);
+      }
+      mdd = wave_min(mdd);
+      if (lane == 0) gp(J.scal)[SC_MDD] = mdd;
+    }
     __syncthreads();
+    MET_TS(2 + pass);
   }
+}
+
+std::vector<long long> loss_timestamps() {
+  std::vector<long long> v(4);
+  HIP_OK(hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(g_loss_ts), sizeof(long long) * 4));
+  return v;
 }
 
 // ---------------------------------------------------------------- launchers ------------

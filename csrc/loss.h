@@ -1,5 +1,6 @@
 // Job record of the loss / metric kernels (k_loss.hip), shared with the engine.
 #pragma once
+#include <vector>
 #include "common.h"
 
 #define DLAP_MAX_T 2048   // max periods per split handled by the LDS-staged passes
@@ -53,3 +54,4 @@ void launch_period_fwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st)
 void launch_asset(const LossJob* jobs, int njobs, int nmax, hipStream_t st);
 void launch_period_bwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st);
 void launch_job_metrics(const LossJob* jobs, int njobs, hipStream_t st);
+std::vector<long long> loss_timestamps();

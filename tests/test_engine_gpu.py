@@ -366,3 +366,17 @@ def test_wide_path_tracks_fused_path_and_is_deterministic(monkeypatch):
     assert np.isfinite(hw0[:, 1]).all()
     # same math, different rounding (fp32 per-period terms): close, not bitwise
     assert np.abs(pw0 - pf).max() < 5e-3, np.abs(pw0 - pf).max()
+
+
+def test_device_eval_metrics_match_numpy():
+    """Sharpe (unbiased std), mean/std and the scan-based max drawdown of the device metric
+    kernel vs the numpy formulas of `/root/reference/src/train.py:29-42` on its own portfolio."""
+    from deeplearninginassetpricing_paperreplication_amd.train.metrics import compute_max_drawdown
+    cfg = default_cli_config(8, 46)
+    for T in (36, 300):
+        eng, _ = _engine(cfg, data=_batch(T=T, N=120))
+        ev = eng.evaluate(0)[0]
+        port = ev["portfolio_returns"].astype(np.float64)
+        assert abs(ev["max_drawdown"] - compute_max_drawdown(port)) < 1e-5
+        assert abs(ev["mean_return"] - port.mean()) < 1e-6
+        assert abs(ev["std_return"] - port.std()) < 1e-5
