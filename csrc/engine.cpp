@@ -910,9 +910,10 @@ class Engine {
                            bool part1_only = false) {
     const SplitDev& D = splits_[0];
     if (!premasked) enqueue_dropmask(phase, 0, st_);
+    // the latency-bound LSTM first, before the streaming projection loads the memory system
+    launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_);
     if (md_.md.wide)
       launch_proj0(as<WideJob>(j_wide_train_[phase]), G_, gx_proj_[0], md_.md, md_.WMB, st_);
-    launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_);
     launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, gx_fwd_[0], md_.md, md_.KS1, md_.WMB, st_);
     if (mark == 2) HIP_OK(hipEventRecord(ev_a_, st_));
     launch_period_fwd(as<LossJob>(j_loss_train_[phase]), G_, D.T, st_);

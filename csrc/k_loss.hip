@@ -62,18 +62,41 @@ __global__ __launch_bounds__(PER_NT) void k_period_fwd(const LossJob* __restrict
       s_abs += fabsf(v);
       s_ww += v * v;
     }
-  } else {                                           // very wide period: two streaming passes
+  } else {          // very wide period: two passes in chunks of PER_NT * PER_RB rows, each
+                    // chunk's loads issued before use (the chunk is L2-hot for the second pass)
+    constexpr int CH = PER_NT * PER_RB;
     if (J.normalize) {
       float sw = 0.f;
-      for (int r = r0 + threadIdx.x; r < r1; r += PER_NT) sw += w[r];
+      for (int c0 = r0; c0 < r1; c0 += CH) {
+        float wv[PER_RB];
+#pragma unroll
+        for (int k = 0; k < PER_RB; ++k) {
+          const int r = c0 + threadIdx.x + PER_NT * k;
+          wv[k] = w[r < r1 ? r : r0];
+        }
+#pragma unroll
+        for (int k = 0; k < PER_RB; ++k) sw += (c0 + (int)threadIdx.x + PER_NT * k < r1) ? wv[k] : 0.f;
+      }
       mu = block_sum<PER_NT>(sw, red) * invN;
     }
-    for (int r = r0 + threadIdx.x; r < r1; r += PER_NT) {
-      const float v = w[r] - mu;
-      wn[rowti[r].y] = v;
-      s_wr += v * Rc[r];
-      s_abs += fabsf(v);
-      s_ww += v * v;
+    for (int c0 = r0; c0 < r1; c0 += CH) {
+      float wv[PER_RB], rv[PER_RB];
+      int iv[PER_RB];
+#pragma unroll
+      for (int k = 0; k < PER_RB; ++k) {
+        const int r = c0 + threadIdx.x + PER_NT * k;
+        const int rr = r < r1 ? r : r0;
+        wv[k] = w[rr]; rv[k] = Rc[rr]; iv[k] = rowti[rr].y;
+      }
+#pragma unroll
+      for (int k = 0; k < PER_RB; ++k) {
+        if (c0 + (int)threadIdx.x + PER_NT * k >= r1) continue;
+        const float v = wv[k] - mu;
+        wn[iv[k]] = v;
+        s_wr += v * rv[k];
+        s_abs += fabsf(v);
+        s_ww += v * v;
+      }
     }
   }
   if (threadIdx.x == 0) gp(J.mu)[t] = mu;
@@ -256,14 +279,13 @@ __global__ __launch_bounds__(PER_NT) void k_period_bwd(const LossJob* __restrict
   };
   constexpr int RB = 4;
   const bool fast = r1 - r0 <= PER_NT * RB;
-  float rv[RB];
-  float s = 0.f;
-  if (fast) {
-    // every row's operands are requested before any is used: 2 dependent round trips total
+  // one chunk of PER_NT * RB rows: every row's operands are requested before any is used
+  // (2 dependent round trips per chunk); periods wider than one chunk loop over chunks
+  auto chunk_sum = [&](int c0, float (&rv)[RB]) -> float {
     int iv[RB];
 #pragma unroll
     for (int k = 0; k < RB; ++k) {
-      const int r = r0 + threadIdx.x + PER_NT * k;
+      const int r = c0 + threadIdx.x + PER_NT * k;
       const int rr = r < r1 ? r : r0;
       iv[k] = rowti[rr].y;
       rv[k] = Rc[rr];
@@ -289,13 +311,20 @@ __global__ __launch_bounds__(PER_NT) void k_period_bwd(const LossJob* __restrict
 #pragma unroll
       for (int k = 0; k < RB; ++k) { gv[k] = row_g(iv[k]); tv[k] = invT[iv[k]]; }
     }
+    float part = 0.f;
 #pragma unroll
     for (int k = 0; k < RB; ++k)
-      if (r0 + (int)threadIdx.x + PER_NT * k < r1) s += gv[k] * rv[k] * tv[k];
+      if (c0 + (int)threadIdx.x + PER_NT * k < r1) part += gv[k] * rv[k] * tv[k];
+    return part;
+  };
+  float rv[RB];
+  float s = 0.f;
+  if (fast) {
+    s = chunk_sum(r0, rv);
   } else {
-    for (int rr = r0 + threadIdx.x; rr < r1; rr += PER_NT) {
-      const int i = rowti[rr].y;
-      s += row_g(i) * Rc[rr] * invT[i];
+    for (int c0 = r0; c0 < r1; c0 += PER_NT * RB) {
+      float rt[RB];
+      s += chunk_sum(c0, rt);
     }
   }
   s = block_sum<PER_NT>(s, red);
@@ -325,6 +354,20 @@ __global__ __launch_bounds__(PER_NT) void k_period_bwd(const LossJob* __restrict
     for (int k = 0; k < RB; ++k) {
       const int r = r0 + threadIdx.x + PER_NT * k;
       if (r < r1) gp(J.dw)[r] = c * (rv[k] - mR);
+    }
+  } else if (rcoef == 0.f) {
+    for (int c0 = r0; c0 < r1; c0 += PER_NT * RB) {
+      float rt[RB];
+#pragma unroll
+      for (int k = 0; k < RB; ++k) {
+        const int r = c0 + threadIdx.x + PER_NT * k;
+        rt[k] = Rc[r < r1 ? r : r0];
+      }
+#pragma unroll
+      for (int k = 0; k < RB; ++k) {
+        const int r = c0 + threadIdx.x + PER_NT * k;
+        if (r < r1) gp(J.dw)[r] = c * (rt[k] - mR);
+      }
     }
   } else {
     for (int rr = r0 + threadIdx.x; rr < r1; rr += PER_NT) {

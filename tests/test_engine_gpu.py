@@ -380,3 +380,32 @@ def test_device_eval_metrics_match_numpy():
         assert abs(ev["max_drawdown"] - compute_max_drawdown(port)) < 1e-5
         assert abs(ev["mean_return"] - port.mean()) < 1e-6
         assert abs(ev["std_return"] - port.std()) < 1e-5
+
+
+def test_wide_periods_use_chunked_loss_passes():
+    """Periods with more valid rows than one register block (>4096 fwd / >2048 bwd) take the
+    chunked streaming paths of k_period_fwd / k_period_bwd: same results as the fp32 model."""
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import flatten_state
+    cfg = default_cli_config(8, 46, dropout=0.0)
+    b = _batch(T=8, N=12000)
+    assert b["mask"].sum(1).min() > 4096
+    eng, _ = _engine(cfg, data=b)
+    torch.manual_seed(0)
+    model = AssetPricingGAN(cfg)
+    eng.set_model(0, model, 7)
+    with torch.no_grad():
+        out = model(b["macro_features"], b["individual_features"], b["returns"], b["mask"], phase="conditional")
+    eng.eng.forward_split(0, False, True)
+    T, N = b["mask"].shape
+    assert _rel(eng.eng.read_ws(0, 0, "wn").reshape(T, N), out["weights"].numpy()) < 3e-2
+    assert _rel(eng.eng.read_ws(0, 0, "scal")[0], out["loss_conditional"].item()) < 3e-2
+    model.zero_grad()
+    o = model(b["macro_features"], b["individual_features"], b["returns"], b["mask"], phase="conditional")
+    o["loss"].backward()
+    ref = flatten_state({k: (p.grad if p.grad is not None else torch.zeros_like(p))
+                         for k, p in model.named_parameters()}, model.spec)
+    eng.eng.backward_only(3)
+    got = eng.eng.get_grads(0)
+    sl = slice(0, model.spec.param_counts()[0])
+    cos = np.dot(got[sl], ref[sl]) / (np.linalg.norm(got[sl]) * np.linalg.norm(ref[sl]))
+    assert cos > 0.998, cos
