@@ -121,6 +121,8 @@ class Engine {
     eval_gx_ = env_int("DLAP_EVAL_GX", 0);
     b_wait_ = env_int("DLAP_B_WAIT", 0);
     side_metrics_ = env_int("DLAP_SIDE_METRICS", 0) != 0;
+    zx_eval_ = env_int("DLAP_ZX_EVAL", 1) != 0;
+    zx_gx_ = std::max(1, env_int("DLAP_ZX_GX", 256));
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
                residual);
     d_desc_.alloc(sizeof(ModelDesc));
@@ -463,6 +465,8 @@ class Engine {
   hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr, ev_mid_ = nullptr, ev_a_ = nullptr;
   int eval_gx_ = 0;                          // cap on the evaluation tower grid (DLAP_EVAL_GX)
   int b_wait_ = 0;                           // evaluation towers after train towers (DLAP_B_WAIT)
+  bool zx_eval_ = true;                      // wide path: fused layer-0 evaluation towers (DLAP_ZX_EVAL)
+  int zx_gx_ = 256;                          // their workgroups over all evaluation jobs (DLAP_ZX_GX)
   bool side_metrics_ = false;                // train Sharpe monitor on a graph side branch (DLAP_SIDE_METRICS)
   ModelDesc md_{};
   DevBuf<char> d_desc_;
@@ -747,6 +751,7 @@ class Engine {
     J.pp = pp_ptr(g, s);
     J.abias = W.abias.p;
     J.blob = reinterpret_cast<const bf16x8*>(models_[g].blob.p);
+    J.blob0 = reinterpret_cast<const bf16x8*>(models_[g].blob0.p);
     J.aux = models_[g].aux.p;
     J.w_out = W.w.p; J.h_out = W.h.p;
     J.dw = W.dw.p; J.dE = W.dE.p; J.Rm = D.Rm.p; J.sdfv = W.sdf.p; J.invT = D.invT.p;
@@ -904,7 +909,8 @@ class Engine {
   // side: if non-null, the train split's Sharpe monitor (not needed by the backward) runs
   // on that stream after the asset pass; the caller joins it before the bookkeeping copy.
   // premasked: this step's keep masks were generated by the previous epoch graph.
-  // mark: record ev_a_ after the tower backward (1) or the tower forward (2);
+  // mark: record ev_a_ after the tower backward (1), the tower forward (2) or the wide
+  // layer-0 projection (3);
   // part1_only: stop before the gradient finalisation (the caller enqueues the tail).
   void enqueue_train_grads(int phase, hipStream_t side = nullptr, bool premasked = false, int mark = 0,
                            bool part1_only = false) {
@@ -914,6 +920,7 @@ class Engine {
     launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_);
     if (md_.md.wide)
       launch_proj0(as<WideJob>(j_wide_train_[phase]), G_, gx_proj_[0], md_.md, md_.WMB, st_);
+    if (mark == 3) HIP_OK(hipEventRecord(ev_a_, st_));
     launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, gx_fwd_[0], md_.md, md_.KS1, md_.WMB, st_);
     if (mark == 2) HIP_OK(hipEventRecord(ev_a_, st_));
     launch_period_fwd(as<LossJob>(j_loss_train_[phase]), G_, D.T, st_);
@@ -960,9 +967,13 @@ class Engine {
     if (n_eval_jobs_ == 0) return;
     int gx = std::max(gx_fwd_[1], gx_fwd_[2]);
     if (eval_gx_ > 0) gx = std::min(gx, eval_gx_);
-    if (md_.md.wide)
-      launch_proj0(as<WideJob>(j_wide_eval_), n_eval_jobs_, std::max(gx_proj_[1], gx_proj_[2]), md_.md, md_.WMB, st);
-    launch_mlp_fwd(as<MlpJob>(j_mlp_eval_), n_eval_jobs_, gx, md_.md, md_.KS1, md_.WMB, st);
+    if (md_.md.wide && zx_eval_) {     // layer 0 streamed inside the evaluation towers
+      launch_mlp_fwd_zx(as<MlpJob>(j_mlp_eval_), n_eval_jobs_, std::max(1, zx_gx_ / n_eval_jobs_), md_.md, md_.WMB, st);
+    } else {
+      if (md_.md.wide)
+        launch_proj0(as<WideJob>(j_wide_eval_), n_eval_jobs_, std::max(gx_proj_[1], gx_proj_[2]), md_.md, md_.WMB, st);
+      launch_mlp_fwd(as<MlpJob>(j_mlp_eval_), n_eval_jobs_, gx, md_.md, md_.KS1, md_.WMB, st);
+    }
     launch_period_fwd(as<LossJob>(j_loss_eval_), n_eval_jobs_, tmax_eval_, st);
     launch_asset(as<LossJob>(j_loss_eval_), n_eval_jobs_, nmax_eval_, st);
     launch_job_metrics(as<LossJob>(j_loss_eval_), n_eval_jobs_, st);
@@ -995,7 +1006,7 @@ class Engine {
       // the evaluation towers start once the training towers (b_wait_ 1: backward, 2:
       // forward) are done, so the wide kernels of the two branches do not contend
       enqueue_eval_prologue(st2_);
-      enqueue_train_grads(phase, st2_, true, b_wait_, true);
+      enqueue_train_grads(phase, side_metrics_ ? st2_ : nullptr, true, b_wait_, true);
       HIP_OK(hipStreamWaitEvent(st2_, ev_a_, 0));
       enqueue_eval_towers(st2_);
       enqueue_epoch_end(phase, ignore_epoch, sel, st2_);
@@ -1041,9 +1052,11 @@ class Engine {
     }
     DevBuf<char> a, b, c, w;
     upload(a, rj); upload(b, mj); upload(c, lj); upload(w, wj);
-    if (md_.md.wide) launch_proj0(as<WideJob>(w), G_, gx_proj_[s], md_.md, md_.WMB, st_);
+    const bool zx = md_.md.wide && zx_eval_ && !train_mode;
+    if (md_.md.wide && !zx) launch_proj0(as<WideJob>(w), G_, gx_proj_[s], md_.md, md_.WMB, st_);
     launch_prologue(as<RnnJob>(a), G_, D.T, dd(), md_, st_);
-    launch_mlp_fwd(as<MlpJob>(b), G_, gx_fwd_[s], md_.md, md_.KS1, md_.WMB, st_);
+    if (zx) launch_mlp_fwd_zx(as<MlpJob>(b), G_, std::max(1, zx_gx_ / G_), md_.md, md_.WMB, st_);
+    else launch_mlp_fwd(as<MlpJob>(b), G_, gx_fwd_[s], md_.md, md_.KS1, md_.WMB, st_);
     launch_period_fwd(as<LossJob>(c), G_, D.T, st_);
     launch_asset(as<LossJob>(c), G_, D.N, st_);
     launch_job_metrics(as<LossJob>(c), G_, st_);

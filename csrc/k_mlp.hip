@@ -388,6 +388,10 @@ DLAP_DEV DropCtx drop_ctx(const MlpJob& J, const MlpDims& D) {
   return dc;
 }
 
+// LDS image of the tower kernels: blob fragments, aux floats, per-period inputs.
+__host__ __device__ inline size_t lds_bytes_of(const MlpDims& D) {
+  return (size_t)D.blob_frags * 1024 + (size_t)((D.aux_floats + 3) & ~3) * 4 + (size_t)D.pp_lds_floats * 4;
+}
 DLAP_DEV float* pp_lds_ptr(char* smem, const MlpDims& D) {
   return reinterpret_cast<float*>(smem + (size_t)D.blob_frags * 1024 + (size_t)((D.aux_floats + 3) & ~3) * 4);
 }
@@ -588,6 +592,131 @@ __global__ __launch_bounds__(256, 2) void k_mlp_fwd(const MlpJob* __restrict__ j
     if (first) { MLP_TS(2); first = false; }
   }
   MLP_TS(3);
+}
+
+// ============================== wide evaluation forward ==================================
+// Evaluation (no dropout, no backward) on the wide path: layer 0 of both towers is streamed
+// from the panel rows inside the tower kernel -- k_proj0's loop with the layer-0 fragments
+// staged in LDS next to the tower blob -- so the pre-activations never go through HBM (the
+// z round trip is 2 x 320 B per row; an evaluation row is read once). grid (gx, jobs), 8 waves,
+// one workgroup per CU (the layer-0 fragments take up to (4 + WMB) x KSX KiB of LDS). The
+// next tile's first k-chunk is in flight while the tower runs on the current one.
+template <int WMB>
+__global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict__ jobs, MlpDims D) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NU = 4 + WMB;
+  const MlpJob& J = jobs[blockIdx.y];
+  bf16x8* lds = reinterpret_cast<bf16x8*>(smem);
+  float* aux = reinterpret_cast<float*>(smem + (size_t)D.blob_frags * 1024);
+  float* spp = pp_lds_ptr(smem, D);
+  bf16x8* lds0 = reinterpret_cast<bf16x8*>(smem + ((lds_bytes_of(D) + 15) & ~(size_t)15));
+  const int lane = lane_id(), q = lane >> 4, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  const int KSX = D.KSX, rstride = D.KX >> 3;
+  const int u0 = J.do_sdf ? 0 : 4, u1 = J.do_mom ? NU : 4;
+  for (int i = threadIdx.x; i < (u1 - u0) * KSX * 64; i += blockDim.x) lds0[i] = gp(J.blob0)[u0 * KSX * 64 + i];
+  stage_weights(J, D, lds, aux, spp);                      // (ends with the barrier)
+  const DropCtx dc = drop_ctx(J, D);
+  const int ntiles = (J.R + 31) >> 5;
+  const int nch = (KSX + 3) >> 2;
+  const int stride = gridDim.x * nwaves;
+  int tile = blockIdx.x * nwaves + wave;
+  if (tile >= ntiles) return;
+  auto issue = [&](int tl, int ch, bf16x8 (&x)[2][4]) {
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int r = min(tl * 32 + 16 * b + (lane & 15), J.R - 1);
+      const auto row = gp(J.X) + (size_t)r * rstride;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const int ks = 4 * ch + s;
+        x[b][s] = ks < KSX ? row[4 * ks + q] : zero8();
+      }
+    }
+  };
+  bf16x8 xc[2][4], xn[2][4];
+  f32x4 acc[2][NU];
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int u = 0; u < NU; ++u) acc[b][u] = zero4();
+  int2 ti[2];
+  issue_rowti(J, tile, ti);
+  issue(tile, 0, xc);
+  int ch = 0;
+  for (;;) {
+    int ntl = tile, nc = ch + 1;
+    if (nc == nch) { nc = 0; ntl += stride; }
+    const bool more = ntl < ntiles;
+    if (more) issue(ntl, nc, xn);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int ks = 4 * ch + s;
+      if (ks < KSX) {
+#pragma unroll
+        for (int u = 0; u < NU; ++u) {
+          if (u >= u0 && u < u1) {
+            const bf16x8 w = lds0[((u - u0) * KSX + ks) * 64 + lane];
+            acc[0][u] = mfma16(w, xc[0][s], acc[0][u]);
+            acc[1][u] = mfma16(w, xc[1][s], acc[1][u]);
+          }
+        }
+      }
+    }
+    if (nc == 0) {                                        // layer 0 of the tile is complete
+      RowInfo ri;
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int r = tile * 32 + 16 * b + (lane & 15);
+        ri.t[b] = ti[b].x;
+        ri.i[b] = ti[b].y;
+        ri.dense[b] = r < J.R ? ti[b].x * J.N + ti[b].y : -1;
+      }
+      int2 tn[2];
+      if (more) issue_rowti(J, ntl, tn);
+      if (J.do_sdf) {
+        f32x4 zs[2][4];
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int u = 0; u < 4; ++u) zs[b][u] = acc[b][u];
+        auto l0 = [&](f32x4 (&a)[2][4]) {
+          if (D.pp_lds_floats > 0) zin_sdf0(zs, ri, spp, aux, D, a);
+          else zin_sdf0(zs, ri, gp(J.pp), aux, D, a);
+        };
+        float w[2];
+        sdf_forward_tile(lds, aux, D, dc, ri, l0, nullptr, nullptr, w);
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          const int r = tile * 32 + 16 * b + (lane & 15);
+          if (q == 0 && r < J.R) gp(J.w_out)[r] = w[b];
+        }
+      }
+      if (J.do_mom) {
+        AbPre<WMB> ab;
+        issue_abias<WMB>(J, ti, ab);
+        auto l0m = [&](f32x4 (&a)[2][WMB]) {
+#pragma unroll
+          for (int b = 0; b < 2; ++b)
+#pragma unroll
+            for (int u = 0; u < WMB; ++u) a[b][u] = acc[b][4 + u];
+        };
+        mom_forward_tile<WMB>(lds, aux, D, J, dc, ri, l0m, nullptr, ab);
+      }
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+#pragma unroll
+        for (int u = 0; u < NU; ++u) acc[b][u] = zero4();
+        if (more) ti[b] = tn[b];
+      }
+    }
+    if (!more) break;
+    tile = ntl;
+    ch = nc;
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int s = 0; s < 4; ++s) xc[b][s] = xn[b][s];
+  }
 }
 
 // ============================== backward =================================================
@@ -1105,9 +1234,7 @@ void launch_dropmask(const MlpJob* jobs, int njobs, int ntiles, const MlpDims& D
 }
 
 // ---- host launchers -------------------------------------------------------------------
-size_t mlp_lds_bytes(const MlpDims& D) {
-  return (size_t)D.blob_frags * 1024 + (size_t)((D.aux_floats + 3) & ~3) * 4 + (size_t)D.pp_lds_floats * 4;
-}
+size_t mlp_lds_bytes(const MlpDims& D) { return lds_bytes_of(D); }
 static size_t bwd_lds_bytes(const MlpDims& D, int slab_stride) {
   size_t a = mlp_lds_bytes(D), b = (size_t)slab_stride * 4;
   return a > b ? a : b;
@@ -1126,6 +1253,15 @@ void launch_mlp_fwd(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int
   F_CASE(2, 1) F_CASE(2, 2) F_CASE(2, 4) F_CASE(4, 1) F_CASE(4, 2) F_CASE(4, 4)
 #undef F_CASE
   dlap_throw_hip(hipErrorInvalidValue, "mlp_fwd: unsupported (KS1, WMB)", __FILE__, __LINE__);
+}
+
+void launch_mlp_fwd_zx(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int WMB, hipStream_t st) {
+  dim3 grid(gx, njobs), block(512);
+  const size_t sh = ((lds_bytes_of(D) + 15) & ~(size_t)15) + (size_t)(4 + WMB) * D.KSX * 1024;
+#define ZX_CASE(W) if (WMB == W) { hipLaunchKernelGGL((k_mlp_fwd_zx<W>), grid, block, sh, st, jobs, D); HIP_OK(hipGetLastError()); return; }
+  ZX_CASE(1) ZX_CASE(2) ZX_CASE(4)
+#undef ZX_CASE
+  dlap_throw_hip(hipErrorInvalidValue, "mlp_fwd_zx: unsupported moment width", __FILE__, __LINE__);
 }
 
 void launch_mlp_bwd_sdf(const MlpJob* jobs, int njobs, int gx, int nslice, int tps, const MlpDims& D,

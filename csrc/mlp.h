@@ -9,6 +9,7 @@ struct MlpJob {
   const float* pp;        // [T][Dm] per-period SDF inputs (LSTM output or raw macro)
   const float* abias;     // [T][64] moment layer-0 per-period bias (W_macro . m_t + b)
   const bf16x8* blob;     // packed weight fragments of this job's model
+  const bf16x8* blob0;    // wide path: layer-0 x-column fragments (k_mlp_fwd_zx / k_proj0)
   const float* aux;       // fp32 biases / output row of this job's model
   float* w_out;           // fwd: compact [R] raw SDF weights
   float* h_out;           // fwd: dense [T*N][K] moments (valid rows written)
@@ -76,6 +77,8 @@ struct WideJob {
 size_t mlp_lds_bytes(const MlpDims& D);
 void launch_mlp_fwd(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int KS1, int WMB,
                     hipStream_t st);
+// wide path, evaluation forward: layer 0 streamed from X inside the tower kernel (no z)
+void launch_mlp_fwd_zx(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int WMB, hipStream_t st);
 void launch_mlp_bwd_sdf(const MlpJob* jobs, int njobs, int gx, int nslice, int tps, const MlpDims& D,
                         int KS1, int slab_stride, hipStream_t st);
 void launch_dropmask(const MlpJob* jobs, int njobs, int ntiles, const MlpDims& D, int step_offset,
