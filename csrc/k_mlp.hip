@@ -35,6 +35,11 @@
 
 DLAP_DEV int lane_id() { return threadIdx.x & 63; }
 
+// Waves per SIMD the forward tower kernel is compiled for (its VGPR budget = 512 / this).
+#ifndef DLAP_FWD_WPS
+#define DLAP_FWD_WPS 2
+#endif
+
 // In-kernel timestamps (wall clock, 100 MHz) of k_mlp_fwd's first / last workgroup, wave 0:
 // [0] start, [1] weights staged, [2] first tile done, [3] loop done; [4..7] same, last block.
 __device__ long long g_mlp_ts[8];
@@ -418,7 +423,10 @@ DLAP_DEV void sdf_forward_tile(const bf16x8* lds, const float* aux, const MlpDim
   if (kw) relu_keep<4>(a, aux + D.a_sb, dc.scale, kw[0], gate);
   else relu_dropout<4>(a, aux + D.a_sb, aux + D.a_sb, dc, 0, ri, gate);
   if (gout) gout[0] = gate_word(gate);
-  for (int j = 1; j < D.nl_sdf; ++j) {
+  // fully unrolled to the engine's 4-layer limit so kw[j] is a register, not scratch
+#pragma unroll
+  for (int j = 1; j < 4; ++j) {
+    if (j >= D.nl_sdf) break;
     pack_blocks<4>(a, pf);
     layer_chain<4, 2>(lds, D.s_fwd + (j - 1) * 8, pf, a);
     if (kw) relu_keep<4>(a, aux + D.a_sb + 64 * j, dc.scale, kw[j], gate);
@@ -496,7 +504,7 @@ DLAP_DEV void mom_forward_tile(const bf16x8* lds, const float* aux, const MlpDim
 
 // ============================== forward ==================================================
 template <int KS1, int WMB, bool ZIN>
-__global__ __launch_bounds__(256, 2) void k_mlp_fwd(const MlpJob* __restrict__ jobs, MlpDims D) {
+__global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __restrict__ jobs, MlpDims D) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const MlpJob& J = jobs[blockIdx.y];
   bf16x8* lds = reinterpret_cast<bf16x8*>(smem);
