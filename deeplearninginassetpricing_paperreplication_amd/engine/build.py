@@ -50,26 +50,39 @@ def _compile(src: Path, obj: Path, flags):
     return obj
 
 
-def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> Path:
+# Host-side undefined-behaviour checks in trap mode (no sanitizer runtime to preload into the
+# Python process; any UB in the C++ runtime or the launchers stops the process with SIGILL).
+# GPU sanitizers are not available on the MI355X pool, the device code is unchanged.
+UBSAN_FLAGS = ["-Xarch_host", "-fsanitize=undefined", "-Xarch_host", "-fsanitize-trap=undefined",
+               "-Xarch_host", "-fno-sanitize=vptr"]
+
+
+def build(force: bool = False, jobs: int = 8, verbose: bool = True, ubsan: bool = False) -> Path:
     srcs = sorted(CSRC.glob("*.hip")) + [CSRC / "engine.cpp"]
     headers = sorted(CSRC.glob("*.h"))
     out = ext_path()
-    stamp = BUILD / "stamp"
+    build_dir = BUILD
+    if ubsan:       # a separate artefact, swapped in by tools/ubsan_gpu_tests.sh on the GPU box
+        out = PKG / "ubsan" / out.name
+        out.parent.mkdir(exist_ok=True)
+        build_dir = BUILD / "ubsan"
+    stamp = build_dir / "stamp"
     key = _hash(srcs + headers)
     if not force and out.exists() and stamp.exists() and stamp.read_text() == key:
         if verbose:
             print(f"[dlap] native extension up to date: {out.name}")
         return out
-    BUILD.mkdir(parents=True, exist_ok=True)
-    flags = _includes() + ["-Wno-unused-result"]
+    build_dir.mkdir(parents=True, exist_ok=True)
+    flags = _includes() + ["-Wno-unused-result"] + (UBSAN_FLAGS if ubsan else [])
     objs = []
     with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(srcs)))) as ex:
-        futs = {ex.submit(_compile, s, BUILD / (s.stem + ".o"), flags): s for s in srcs}
+        futs = {ex.submit(_compile, s, build_dir / (s.stem + ".o"), flags): s for s in srcs}
         for f in cf.as_completed(futs):
             objs.append(f.result())
             if verbose:
                 print(f"[dlap] compiled {futs[f].name}")
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, sorted(objs)), "-o", str(out)]
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *(UBSAN_FLAGS if ubsan else []),
+           *map(str, sorted(objs)), "-o", str(out)]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
@@ -80,4 +93,4 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True) -> Path:
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    build(force="--force" in sys.argv, ubsan="--ubsan" in sys.argv)
