@@ -21,7 +21,7 @@ import torch
 
 from ..data.dataset import load_splits
 from ..models.gan import AssetPricingGAN
-from .portfolio import PAPER_TEST_SHARPE, ensemble_sharpes
+from .portfolio import PAPER_TEST_SHARPE, average_weights, ensemble_sharpes, paper_metrics
 from .portfolio import sharpe_ddof0 as compute_sharpe  # noqa: F401  (reference name)
 
 SPLITS = ("train", "valid", "test")
@@ -72,7 +72,9 @@ def weights_batched_gpu(models: Sequence, batches: Dict[str, Dict]) -> List[Dict
 
 
 def evaluate_ensemble(checkpoint_dirs: Sequence[str], data_dir: str, device: str = "cpu",
-                      verbose: bool = True) -> Dict:
+                      verbose: bool = True, paper: bool = False) -> Dict:
+    """Reference output and return value; ``paper=True`` (CLI ``--paper_metrics``) adds the
+    paper's EV / XS-R² / turnover / max 1-month loss of the ensemble's SDF factor per split."""
     say = print if verbose else (lambda *a, **k: None)
     bar = "=" * 70
     say(bar); say(f"ENSEMBLE EVALUATION ({len(checkpoint_dirs)} models, averaged weights)"); say(bar); say()
@@ -108,8 +110,20 @@ def evaluate_ensemble(checkpoint_dirs: Sequence[str], data_dir: str, device: str
     say(f"  Our Ensemble Test Sharpe:  {res['test_sharpe']:.4f}")
     say(f"  Ratio (Our / Paper):       {res['test_sharpe'] / PAPER_TEST_SHARPE:.1%}")
     say()
-    return {"train_sharpe": res["train_sharpe"], "valid_sharpe": res["valid_sharpe"],
-            "test_sharpe": res["test_sharpe"], "individual_sharpes": ind}
+    out = {"train_sharpe": res["train_sharpe"], "valid_sharpe": res["valid_sharpe"],
+           "test_sharpe": res["test_sharpe"], "individual_sharpes": ind}
+    if paper:
+        out["paper_metrics"] = {}
+        say(bar); say("PAPER METRICS OF THE ENSEMBLE SDF FACTOR (Table I / A.VI / A.VII)"); say(bar); say()
+        for s in SPLITS:
+            b = np_batches[s]
+            avg = average_weights([w[s] for w in weights], b["mask"])
+            pm = paper_metrics(avg, b["returns"], b["mask"])
+            out["paper_metrics"][s] = pm
+            say(f"  {s.capitalize():5s}  SR {pm['sharpe']:7.4f}  EV {pm['ev']:7.4f}  XS-R2 {pm['xs_r2']:7.4f}  "
+                f"turnover {pm['turnover']:6.3f}  max 1m loss {pm['max_1m_loss_std']:5.2f} sd")
+        say()
+    return out
 
 
 def main(argv=None):
@@ -117,8 +131,9 @@ def main(argv=None):
     p.add_argument("--data_dir", type=str, required=True)
     p.add_argument("--checkpoint_dirs", type=str, nargs="+", required=True)
     p.add_argument("--device", type=str, default="cpu", help="cpu | cuda (batched native engine)")
+    p.add_argument("--paper_metrics", action="store_true", help="also print EV / XS-R2 / turnover / max loss")
     a = p.parse_args(argv)
-    return evaluate_ensemble(a.checkpoint_dirs, a.data_dir, a.device)
+    return evaluate_ensemble(a.checkpoint_dirs, a.data_dir, a.device, paper=a.paper_metrics)
 
 
 if __name__ == "__main__":

@@ -74,3 +74,70 @@ def ensemble_sharpes(weights_by_model: Sequence[Dict[str, np.ndarray]], batches:
     out["individual_sharpes"] = [
         -sharpe_ddof0(portfolio_returns(w["test"], tb["returns"], tb["mask"])) for w in weights_by_model]
     return out
+
+
+# ------------------------------------------------------------------------------------------
+# Paper metrics the reference does not implement (EV and XS-R² of Table I,
+# turnover of Table A.VII, max 1-month loss of Table A.VI). The paper's loadings come from a
+# separate beta network; here the loading direction of period t is the SDF weight vector itself
+# (the cross-sectional projection the reference's residual loss uses, `model.py:435-483`),
+# which makes the metrics computable from any checkpoint's weights.
+# ------------------------------------------------------------------------------------------
+def _projection_residuals(weights: np.ndarray, returns: np.ndarray, mask: np.ndarray) -> np.ndarray:
+    m = mask.astype(np.float64)
+    w = weights.astype(np.float64) * m
+    r = returns.astype(np.float64) * m
+    ww = (w * w).sum(axis=1, keepdims=True)
+    rw = (r * w).sum(axis=1, keepdims=True)
+    beta = np.divide(rw, ww, out=np.zeros_like(rw), where=ww > 1e-12)
+    return (r - beta * w) * m
+
+
+def explained_variation(weights: np.ndarray, returns: np.ndarray, mask: np.ndarray) -> float:
+    """EV = 1 - sum_t mean_i eps^2 / sum_t mean_i R^2 over valid stocks (paper eq. for Table I)."""
+    m = mask.astype(np.float64)
+    n = np.maximum(m.sum(axis=1), 1.0)
+    eps = _projection_residuals(weights, returns, mask)
+    r = returns.astype(np.float64) * m
+    den = ((r * r).sum(axis=1) / n).sum()
+    return float(1.0 - ((eps * eps).sum(axis=1) / n).sum() / den) if den > 0 else float("nan")
+
+
+def cross_sectional_r2(weights: np.ndarray, returns: np.ndarray, mask: np.ndarray) -> float:
+    """XS-R² = 1 - mean_i (T_i/T) mean_t(eps_i)^2 / mean_i (T_i/T) mean_t(R_i)^2."""
+    m = mask.astype(np.float64)
+    T = m.shape[0]
+    ti = m.sum(axis=0)
+    ok = ti > 0
+    eps = _projection_residuals(weights, returns, mask)
+    r = returns.astype(np.float64) * m
+    e_bar = np.divide(eps.sum(axis=0), ti, out=np.zeros_like(ti), where=ok)
+    r_bar = np.divide(r.sum(axis=0), ti, out=np.zeros_like(ti), where=ok)
+    num = ((ti / T) * e_bar ** 2)[ok].mean()
+    den = ((ti / T) * r_bar ** 2)[ok].mean()
+    return float(1.0 - num / den) if den > 0 else float("nan")
+
+
+def turnover(weights: np.ndarray, returns: np.ndarray, mask: np.ndarray) -> float:
+    """Mean over t of sum_i |w_{t+1,i} - w_{t,i} (1 + R_{t,i}) / (1 + sum_j w_{t,j} R_{t,j})|."""
+    m = mask.astype(np.float64)
+    w = weights.astype(np.float64) * m
+    r = returns.astype(np.float64) * m
+    if w.shape[0] < 2:
+        return 0.0
+    gross = 1.0 + (w * r).sum(axis=1, keepdims=True)
+    drift = np.divide(w * (1.0 + r), gross, out=np.zeros_like(w), where=np.abs(gross) > 1e-12)
+    return float(np.abs(w[1:] - drift[:-1]).sum(axis=1).mean())
+
+
+def paper_metrics(weights: np.ndarray, returns: np.ndarray, mask: np.ndarray) -> Dict[str, float]:
+    """Sharpe / EV / XS-R² / turnover / max 1-month loss (std units) of the SDF factor F = -w.R."""
+    f = -portfolio_returns(weights, returns, mask).astype(np.float64)
+    sd = f.std()
+    return {
+        "sharpe": sharpe_ddof0(f),
+        "ev": explained_variation(weights, returns, mask),
+        "xs_r2": cross_sectional_r2(weights, returns, mask),
+        "turnover": turnover(weights, returns, mask),
+        "max_1m_loss_std": float(-f.min() / sd) if sd > 0 else float("nan"),
+    }

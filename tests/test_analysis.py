@@ -91,3 +91,14 @@ def test_download_check_and_graceful_failure(shipped_data, tmp_path, capsys):
     r = subprocess.run([sys.executable, "-m", "src.download_data", "--check", "-o", shipped_data], cwd=ROOT,
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0
+
+
+def test_evaluate_ensemble_paper_metrics(shipped_data, two_checkpoints, capsys):
+    b = ens.evaluate_ensemble(two_checkpoints, shipped_data, verbose=True, paper=True)
+    out = capsys.readouterr().out
+    assert "PAPER METRICS" in out
+    pm = b["paper_metrics"]
+    assert set(pm) == {"train", "valid", "test"}
+    for s in pm:
+        assert abs(pm[s]["sharpe"] - b[f"{s}_sharpe"]) < 1e-6       # same factor, same ddof=0 Sharpe
+        assert -1.0 < pm[s]["ev"] <= 1.0 and pm[s]["turnover"] >= 0
