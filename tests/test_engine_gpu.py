@@ -409,3 +409,8 @@ def test_wide_periods_use_chunked_loss_passes():
     sl = slice(0, model.spec.param_counts()[0])
     cos = np.dot(got[sl], ref[sl]) / (np.linalg.norm(got[sl]) * np.linalg.norm(ref[sl]))
     assert cos > 0.998, cos
+
+
+def test_wide_model_batching_matches_single_models(monkeypatch):
+    monkeypatch.setenv("DLAP_WIDE", "1")
+    test_model_batching_matches_single_models()
