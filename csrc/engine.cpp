@@ -122,6 +122,7 @@ class Engine {
     b_wait_ = env_int("DLAP_B_WAIT", 0);
     side_metrics_ = env_int("DLAP_SIDE_METRICS", 0) != 0;
     zx_eval_ = env_int("DLAP_ZX_EVAL", 1) != 0;
+    zx_train_ = env_int("DLAP_ZX_TRAIN", 1) != 0;
     zx_gx_ = std::max(1, env_int("DLAP_ZX_GX", 256));
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
                residual);
@@ -466,6 +467,7 @@ class Engine {
   int eval_gx_ = 0;                          // cap on the evaluation tower grid (DLAP_EVAL_GX)
   int b_wait_ = 0;                           // evaluation towers after train towers (DLAP_B_WAIT)
   bool zx_eval_ = true;                      // wide path: fused layer-0 evaluation towers (DLAP_ZX_EVAL)
+  bool zx_train_ = true;                     // ... and training forward (DLAP_ZX_TRAIN)
   int zx_gx_ = 256;                          // their workgroups over all evaluation jobs (DLAP_ZX_GX)
   bool side_metrics_ = false;                // train Sharpe monitor on a graph side branch (DLAP_SIDE_METRICS)
   ModelDesc md_{};
@@ -857,6 +859,8 @@ class Engine {
         mt.push_back(mlp_job(g, 0, true, true, phase != 1));
         mb.push_back(mlp_job(g, 0, true, true, true));
         mb.back().dz_out = reinterpret_cast<bf16x8*>(phase == 2 ? ws(g, 0).dzm.p : ws(g, 0).dzs.p);
+        mt.back().z_out = reinterpret_cast<f32x4*>(ws(g, 0).z.p);
+        mt.back().store_mz = phase == 2;
         wt.push_back(wide_job(g, 0, true, phase != 1));
         wb.push_back(wide_job(g, 0, phase != 2, phase == 2));
         // the training forward stores the gate words its backward reuses
@@ -918,10 +922,14 @@ class Engine {
     if (!premasked) enqueue_dropmask(phase, 0, st_);
     // the latency-bound LSTM first, before the streaming projection loads the memory system
     launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_);
-    if (md_.md.wide)
+    const bool zx_train = md_.md.wide && zx_train_;
+    if (md_.md.wide && !zx_train)
       launch_proj0(as<WideJob>(j_wide_train_[phase]), G_, gx_proj_[0], md_.md, md_.WMB, st_);
     if (mark == 3) HIP_OK(hipEventRecord(ev_a_, st_));
-    launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, gx_fwd_[0], md_.md, md_.KS1, md_.WMB, st_);
+    if (zx_train)      // layer 0 streamed inside the training towers, z stored for the backward
+      launch_mlp_fwd_zx(as<MlpJob>(j_mlp_train_[phase]), G_, std::max(1, zx_gx_ / G_), md_.md, md_.WMB, st_, true);
+    else
+      launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, gx_fwd_[0], md_.md, md_.KS1, md_.WMB, st_);
     if (mark == 2) HIP_OK(hipEventRecord(ev_a_, st_));
     launch_period_fwd(as<LossJob>(j_loss_train_[phase]), G_, D.T, st_);
     launch_asset(as<LossJob>(j_loss_train_[phase]), G_, D.N, st_);

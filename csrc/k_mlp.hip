@@ -609,7 +609,10 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __r
 // z round trip is 2 x 320 B per row; an evaluation row is read once). grid (gx, jobs), 8 waves,
 // one workgroup per CU (the layer-0 fragments take up to (4 + WMB) x KSX KiB of LDS). The
 // next tile's first k-chunk is in flight while the tower runs on the current one.
-template <int WMB>
+// TRAIN: the training forward of the same kind -- dropout from the pre-generated keep words,
+// gate words for the backward, and the layer-0 pre-activations stored to z (SDF blocks; the
+// moment blocks too when J.store_mz, i.e. in phase 2) for the ZIN backward kernels.
+template <int WMB, bool TRAIN>
 __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict__ jobs, MlpDims D) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NU = 4 + WMB;
@@ -629,6 +632,8 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
   const int stride = gridDim.x * nwaves;
   int tile = blockIdx.x * nwaves + wave;
   if (tile >= ntiles) return;
+  const bool keep = TRAIN && J.gbits && dc.on;
+  const auto gbase = (TRAIN && J.gbits) ? gp(J.gbits) + (size_t)(dc.step & 1u) * J.gb_half : nullptr;
   auto issue = [&](int tl, int ch, bf16x8 (&x)[2][4]) {
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
@@ -681,6 +686,24 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
       }
       int2 tn[2];
       if (more) issue_rowti(J, ntl, tn);
+      uint32_t kw[4];
+      if constexpr (TRAIN) {
+        const auto zt = gp(J.z_out) + (size_t)tile * D.zc * 64 + lane;
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) zt[(4 * b + u) * 64] = acc[b][u];
+          if (J.store_mz) {
+#pragma unroll
+            for (int u = 0; u < WMB; ++u) zt[(8 + WMB * b + u) * 64] = acc[b][4 + u];
+          }
+        }
+        if (keep) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            kw[j] = j < D.nl_sdf ? gbase[((size_t)tile * D.nl_sdf + j) * 64 + lane] : 0xFFFFFFFFu;
+        }
+      }
       if (J.do_sdf) {
         f32x4 zs[2][4];
 #pragma unroll
@@ -692,7 +715,8 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
           else zin_sdf0(zs, ri, gp(J.pp), aux, D, a);
         };
         float w[2];
-        sdf_forward_tile(lds, aux, D, dc, ri, l0, nullptr, nullptr, w);
+        DLAP_GLOBAL uint32_t* gout = (TRAIN && J.gbits) ? gbase + (size_t)tile * D.nl_sdf * 64 + lane : nullptr;
+        sdf_forward_tile(lds, aux, D, dc, ri, l0, gout, keep ? kw : nullptr, w);
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
           const int r = tile * 32 + 16 * b + (lane & 15);
@@ -708,7 +732,9 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
 #pragma unroll
             for (int u = 0; u < WMB; ++u) a[b][u] = acc[b][4 + u];
         };
-        mom_forward_tile<WMB>(lds, aux, D, J, dc, ri, l0m, nullptr, ab);
+        DLAP_GLOBAL uint32_t* mgout = (TRAIN && J.mgbits && D.nl_mom > 1)
+                                          ? gp(J.mgbits) + (size_t)tile * (D.nl_mom - 1) * 64 + lane : nullptr;
+        mom_forward_tile<WMB>(lds, aux, D, J, dc, ri, l0m, mgout, ab);
       }
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
@@ -1263,11 +1289,12 @@ void launch_mlp_fwd(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int
   dlap_throw_hip(hipErrorInvalidValue, "mlp_fwd: unsupported (KS1, WMB)", __FILE__, __LINE__);
 }
 
-void launch_mlp_fwd_zx(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int WMB, hipStream_t st) {
+void launch_mlp_fwd_zx(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int WMB, hipStream_t st,
+                       bool train) {
   dim3 grid(gx, njobs), block(512);
   const size_t sh = ((lds_bytes_of(D) + 15) & ~(size_t)15) + (size_t)(4 + WMB) * D.KSX * 1024;
-#define ZX_CASE(W) if (WMB == W) { hipLaunchKernelGGL((k_mlp_fwd_zx<W>), grid, block, sh, st, jobs, D); HIP_OK(hipGetLastError()); return; }
-  ZX_CASE(1) ZX_CASE(2) ZX_CASE(4)
+#define ZX_CASE(W, TR) if (WMB == W && train == TR) { hipLaunchKernelGGL((k_mlp_fwd_zx<W, TR>), grid, block, sh, st, jobs, D); HIP_OK(hipGetLastError()); return; }
+  ZX_CASE(1, false) ZX_CASE(2, false) ZX_CASE(4, false) ZX_CASE(1, true) ZX_CASE(2, true) ZX_CASE(4, true)
 #undef ZX_CASE
   dlap_throw_hip(hipErrorInvalidValue, "mlp_fwd_zx: unsupported moment width", __FILE__, __LINE__);
 }

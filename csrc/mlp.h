@@ -30,6 +30,8 @@ struct MlpJob {
   const int* step;        // device step counter (dropout stream)
   const f32x4* z;         // wide path: [ntiles][zc][64] layer-0 pre-activations (k_proj0)
   bf16x8* dz_out;         // wide path, bwd: [ntiles][UB][64] layer-0 dz fragments (rows as k)
+  f32x4* z_out;           // wide path, fused training forward: where it stores the layer-0 z
+  int store_mz;           // ... including the moment blocks (phase 2: the moment backward reads them)
   int R, N, T;
   unsigned seed;
   int train;              // dropout active
@@ -78,7 +80,8 @@ size_t mlp_lds_bytes(const MlpDims& D);
 void launch_mlp_fwd(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int KS1, int WMB,
                     hipStream_t st);
 // wide path, evaluation forward: layer 0 streamed from X inside the tower kernel (no z)
-void launch_mlp_fwd_zx(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int WMB, hipStream_t st);
+void launch_mlp_fwd_zx(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int WMB, hipStream_t st,
+                       bool train = false);
 void launch_mlp_bwd_sdf(const MlpJob* jobs, int njobs, int gx, int nslice, int tps, const MlpDims& D,
                         int KS1, int slab_stride, hipStream_t st);
 void launch_dropmask(const MlpJob* jobs, int njobs, int ntiles, const MlpDims& D, int step_offset,
