@@ -109,10 +109,13 @@ def all_gather_rows(d: Dist, local: np.ndarray, n_total: int, owner_index: Seque
     return out
 
 
-def broadcast_arrays(d: Dist, arrays: Optional[dict], src: int = 0) -> dict:
+def broadcast_arrays(d: Dist, arrays: Optional[dict], src: int = 0, as_tensors: bool = False) -> dict:
     """Broadcast a dict of numpy arrays from ``src`` (e.g. a panel read once from disk): one
-    metadata object broadcast, then one tensor broadcast per array."""
+    metadata object broadcast, then one tensor broadcast per array. ``as_tensors`` returns the
+    received tensors where they landed (the rank's GPU under RCCL: no host copy on the peers)."""
     if not d.active:
+        if as_tensors and arrays is not None:
+            return {k: torch.as_tensor(np.ascontiguousarray(v)).to(d.comm_device()) for k, v in arrays.items()}
         return arrays
     meta = [None]
     if d.rank == src:
@@ -126,5 +129,20 @@ def broadcast_arrays(d: Dist, arrays: Optional[dict], src: int = 0) -> dict:
         else:
             t = torch.empty(shape, dtype=torch.from_numpy(np.empty(0, np.dtype(dt))).dtype, device=dev)
         tdist.broadcast(t, src=src)
-        out[k] = t.cpu().numpy()
+        out[k] = t if as_tensors else t.cpu().numpy()
+    return out
+
+
+def broadcast_batches(d: Dist, batches: Optional[dict], src: int = 0) -> dict:
+    """Split dicts ``{split: {key: array/tensor}}`` read on ``src`` only, delivered to every
+    rank as tensors on its collective device (one RCCL broadcast per array over xGMI)."""
+    flat = None
+    if d.rank == src:
+        flat = {f"{sp}/{k}": (v.cpu().numpy() if isinstance(v, torch.Tensor) else np.asarray(v))
+                for sp, b in batches.items() for k, v in b.items() if v is not None}
+    got = broadcast_arrays(d, flat, src, as_tensors=True)
+    out: dict = {}
+    for key, t in got.items():
+        sp, k = key.split("/", 1)
+        out.setdefault(sp, {})[k] = t
     return out

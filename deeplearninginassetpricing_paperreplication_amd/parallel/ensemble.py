@@ -134,8 +134,7 @@ def run_ensemble(config: Dict, batches: Dict[str, Dict], seeds: Sequence[int] = 
             weights[i][sp] = allw[i]
     walls = comm.all_gather_rows(d, np.array([[t_train]], np.float64), d.world, [d.rank])[:, 0]
     good = [i for i in range(len(seeds)) if ok[i]]
-    np_b = {sp: {"returns": np.asarray(batches[sp]["returns"]), "mask": np.asarray(batches[sp]["mask"])}
-            for sp in SPLITS}
+    np_b = {sp: {"returns": _host(batches[sp]["returns"]), "mask": _host(batches[sp]["mask"])} for sp in SPLITS}
     out = {"seeds": [int(s) for s in seeds], "ok": ok.tolist(),
            "failed": [int(seeds[i]) for i in range(len(seeds)) if not ok[i]],
            "world_size": d.world, "train_wall_s_per_rank": walls.tolist(),
@@ -148,6 +147,20 @@ def run_ensemble(config: Dict, batches: Dict[str, Dict], seeds: Sequence[int] = 
         out["individual_sharpes"] = ind.tolist()
     out["errors"] = {int(r["seed"]): r["error"] for r in recs if r["error"]}
     return out
+
+
+def _host(a) -> np.ndarray:
+    return a.detach().cpu().numpy() if isinstance(a, torch.Tensor) else np.asarray(a)
+
+
+def load_batches(args, d: Optional[comm.Dist] = None) -> Dict[str, Dict]:
+    """The three splits for a driver run. With a process group, only rank 0 reads the .npz
+    files / generates the panel and RCCL broadcasts it (peers receive it straight into their
+    GPU's memory, where the engine compacts it without a host round trip)."""
+    if d is None or not d.active:
+        return _load_batches(args)
+    b = _load_batches(args) if d.rank == 0 else None
+    return comm.broadcast_batches(d, b)
 
 
 def _load_batches(args) -> Dict[str, Dict]:
@@ -186,7 +199,7 @@ def main(argv=None):
     if not a.synthetic and not a.data_dir:
         p.error("--data_dir or --synthetic is required")
     d = comm.init(use_gpu=not a.cpu and torch.cuda.is_available())
-    batches = _load_batches(a)
+    batches = load_batches(a, d)
     cfg = default_cli_config(batches["train"]["macro_features"].shape[-1] if "macro_features" in batches["train"] else 0,
                              batches["train"]["individual_features"].shape[-1])
     res = run_ensemble(cfg, batches, a.seeds, d, (a.epochs_unc, a.epochs_moment, a.epochs), a.lr,

@@ -31,7 +31,7 @@ import torch
 
 from ..config import ModelSpec, default_cli_config
 from . import comm
-from .ensemble import SPLITS, _init_models, _load_batches
+from .ensemble import SPLITS, _init_models, load_batches
 
 GRID = {"HL": (2, 3, 4), "SMV": (4, 8), "CSMV": (16, 32), "CHL": (0, 1), "CHU": (4, 8, 16, 32),
         "LR": (1e-3, 5e-4, 2e-4, 1e-4)}
@@ -167,7 +167,7 @@ def main(argv=None):
     if not a.synthetic and not a.data_dir:
         p.error("--data_dir or --synthetic is required")
     d = comm.init(use_gpu=not a.cpu and torch.cuda.is_available())
-    batches = _load_batches(a)
+    batches = load_batches(a, d)
     M = batches["train"]["macro_features"].shape[-1] if "macro_features" in batches["train"] else 0
     F = batches["train"]["individual_features"].shape[-1]
     entries = paper_grid(M, F)

@@ -50,6 +50,19 @@ def _worker(rank, world, port, outdir, job):
         arr = {"x": np.arange(6, dtype=np.int32).reshape(2, 3), "m": np.array([True, False])} if d.rank == 0 else None
         got = comm.broadcast_arrays(d, arr)
         out["bcast"] = [got["x"].tolist(), got["m"].tolist()]
+    elif job in ("load_local", "load_bcast"):
+        import argparse
+        from deeplearninginassetpricing_paperreplication_amd.parallel.ensemble import (
+            _load_batches, load_batches, run_ensemble)
+        args = argparse.Namespace(synthetic=[10, 4, 5, 30, 6, 3], data_seed=1, data_dir=None)
+        b = load_batches(args, d) if job == "load_bcast" else _load_batches(args)
+        if job == "load_bcast":
+            ref = _load_batches(args)            # what every rank would have read itself
+            for sp in ref:
+                for k in ref[sp]:
+                    assert torch.equal(torch.as_tensor(b[sp][k]), torch.as_tensor(ref[sp][k])), (sp, k)
+        res = run_ensemble(_cfg(b), b, seeds=(3, 4, 5), dist=d, epochs=(2, 1, 2), ignore_epoch=0, print_freq=100)
+        out = {k: v for k, v in res.items() if k not in ("errors", "train_wall_s_per_rank", "train_wall_s")}
     elif job in ("ensemble", "ensemble_fail"):
         from deeplearninginassetpricing_paperreplication_amd.parallel.ensemble import run_ensemble
         b = _batches()
@@ -124,3 +137,11 @@ def test_paper_grid_is_384_configs_in_48_buckets():
     cfg, lr, pt = e[0]
     assert cfg["hidden_dim"] == [64, 64] and cfg["num_units_rnn"] == [4] and lr == 1e-3
     assert {len(b) for b in buckets(e)} == {8}
+
+
+def test_rank0_load_and_broadcast_equals_local_loading(tmp_path):
+    (tmp_path / "a").mkdir()
+    (tmp_path / "b").mkdir()
+    a = _run("load_local", tmp_path / "a")
+    b = _run("load_bcast", tmp_path / "b")
+    assert a[0] == b[0] == b[1]
