@@ -414,3 +414,43 @@ def test_wide_periods_use_chunked_loss_passes():
 def test_wide_model_batching_matches_single_models(monkeypatch):
     monkeypatch.setenv("DLAP_WIDE", "1")
     test_model_batching_matches_single_models()
+
+
+@pytest.mark.parametrize("wide", ["0", "1"])
+def test_edge_panels_all_masked_period_single_observation_asset(monkeypatch, wide):
+    """SURVEY §7.4 edge cases through the native engine: a fully masked period, an asset with a
+    single observation, N not a multiple of the tile, T = 2 (the shortest split with a Sharpe)."""
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import flatten_state
+    monkeypatch.setenv("DLAP_WIDE", wide)
+    cfg = default_cli_config(8, 46, dropout=0.0)
+    for T, N in ((7, 77), (2, 45)):
+        b = _batch(T=T, N=N, seed=3)
+        mask = b["mask"].clone()
+        mask[T // 2] = False                          # no valid stock in this period
+        mask[:, 5] = False
+        mask[0, 5] = True                             # one observation for asset 5
+        b["mask"] = mask
+        b["returns"] = b["returns"] * mask
+        b["individual_features"] = b["individual_features"] * mask[..., None]
+        eng, _ = _engine(cfg, data=b)
+        torch.manual_seed(0)
+        model = AssetPricingGAN(cfg)
+        eng.set_model(0, model, 7)
+        with torch.no_grad():
+            out = model(b["macro_features"], b["individual_features"], b["returns"], b["mask"], phase="conditional")
+        eng.eng.forward_split(0, False, True)
+        assert _rel(eng.eng.read_ws(0, 0, "wn").reshape(T, N), out["weights"].numpy()) < 3e-2
+        sc = eng.eng.read_ws(0, 0, "scal")
+        assert _rel(sc[0], out["loss_conditional"].item()) < 3e-2
+        assert _rel(sc[1], out["loss_unconditional"].item()) < 3e-2
+        model.zero_grad()
+        o = model(b["macro_features"], b["individual_features"], b["returns"], b["mask"], phase="conditional")
+        o["loss"].backward()
+        ref = flatten_state({k: (p.grad if p.grad is not None else torch.zeros_like(p))
+                             for k, p in model.named_parameters()}, model.spec)
+        eng.eng.backward_only(3)
+        got = eng.eng.get_grads(0)
+        sl = slice(0, model.spec.param_counts()[0])
+        assert np.isfinite(got).all()
+        cos = np.dot(got[sl], ref[sl]) / (np.linalg.norm(got[sl]) * np.linalg.norm(ref[sl]))
+        assert cos > 0.995, (T, N, cos)
