@@ -22,6 +22,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -40,6 +41,17 @@ void dlap_throw_hip(hipError_t e, const char* what, const char* file, int line) 
                            std::to_string(line) + " (" + what + ")");
 }
 
+// Engines of several threads (the sweep runs architecture buckets concurrently) must not issue
+// legacy-stream operations (synchronous hipMemcpy / hipMemset / hipMalloc / hipFree) while
+// another thread is capturing an epoch graph: every such call and every capture takes this lock.
+// Graph replays, the long part of a run, are outside it.
+static std::mutex g_legacy_mu;
+#define HIP_LEGACY(expr)                                \
+  do {                                                  \
+    std::lock_guard<std::mutex> _legacy_guard(g_legacy_mu); \
+    HIP_OK(expr);                                       \
+  } while (0)
+
 namespace {
 
 template <typename T>
@@ -50,11 +62,11 @@ struct DevBuf {
     free();
     n = count;
     if (count == 0) return;
-    HIP_OK(hipMalloc(&p, count * sizeof(T)));
-    if (zero) HIP_OK(hipMemset(p, 0, count * sizeof(T)));
+    HIP_LEGACY(hipMalloc(&p, count * sizeof(T)));
+    if (zero) HIP_LEGACY(hipMemset(p, 0, count * sizeof(T)));
   }
   void free() {
-    if (p) (void)hipFree(p);
+    if (p) { std::lock_guard<std::mutex> g(g_legacy_mu); (void)hipFree(p); }
     p = nullptr;
     n = 0;
   }
@@ -127,7 +139,7 @@ class Engine {
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
                residual);
     d_desc_.alloc(sizeof(ModelDesc));
-    HIP_OK(hipMemcpy(d_desc_.p, &md_, sizeof(ModelDesc), hipMemcpyHostToDevice));
+    HIP_LEGACY(hipMemcpy(d_desc_.p, &md_, sizeof(ModelDesc), hipMemcpyHostToDevice));
     models_.resize(G);
     for (int g = 0; g < G; ++g) {
       ModelState& S = models_[g];
@@ -197,7 +209,7 @@ class Engine {
     const size_t nx = (size_t)R * md_.KP;
     if (x_on_device) {
       D.X.alloc(nx, false);
-      if (nx) HIP_OK(hipMemcpy(D.X.p, Xp, nx * sizeof(uint16_t), hipMemcpyDeviceToDevice));
+      if (nx) HIP_LEGACY(hipMemcpy(D.X.p, Xp, nx * sizeof(uint16_t), hipMemcpyDeviceToDevice));
     } else {
       up(D.X, Xp, nx);
     }
@@ -283,19 +295,19 @@ class Engine {
     py::dict d;
     d["m"] = down(S.m); d["v"] = down(S.v);
     int hs[2], ds[1];
-    HIP_OK(hipMemcpy(hs, S.adam_step.p, sizeof(hs), hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(ds, S.drop_step.p, sizeof(ds), hipMemcpyDeviceToHost));
+    HIP_LEGACY(hipMemcpy(hs, S.adam_step.p, sizeof(hs), hipMemcpyDeviceToHost));
+    HIP_LEGACY(hipMemcpy(ds, S.drop_step.p, sizeof(ds), hipMemcpyDeviceToHost));
     d["step_sdf"] = hs[0]; d["step_moment"] = hs[1]; d["drop_step"] = ds[0];
     return d;
   }
   void set_opt_state(int g, py::array_t<float, py::array::c_style> m, py::array_t<float, py::array::c_style> v,
                      int step_sdf, int step_mom, int drop_step) {
     ModelState& S = models_[check_g(g)];
-    HIP_OK(hipMemcpy(S.m.p, m.data(), md_.P * 4, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(S.v.p, v.data(), md_.P * 4, hipMemcpyHostToDevice));
+    HIP_LEGACY(hipMemcpy(S.m.p, m.data(), md_.P * 4, hipMemcpyHostToDevice));
+    HIP_LEGACY(hipMemcpy(S.v.p, v.data(), md_.P * 4, hipMemcpyHostToDevice));
     int hs[2] = {step_sdf, step_mom};
-    HIP_OK(hipMemcpy(S.adam_step.p, hs, sizeof(hs), hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(S.drop_step.p, &drop_step, sizeof(int), hipMemcpyHostToDevice));
+    HIP_LEGACY(hipMemcpy(S.adam_step.p, hs, sizeof(hs), hipMemcpyHostToDevice));
+    HIP_LEGACY(hipMemcpy(S.drop_step.p, &drop_step, sizeof(int), hipMemcpyHostToDevice));
   }
 
   // Bookkeeping state of a model (resume files): epoch counters, per-phase best trackers,
@@ -306,15 +318,15 @@ class Engine {
     int ep[2], fl[2];
     float best[3];
     sync();
-    HIP_OK(hipMemcpy(ep, S.ep.p, sizeof(ep), hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(fl, S.snap_flags.p, sizeof(fl), hipMemcpyDeviceToHost));
-    HIP_OK(hipMemcpy(best, S.best.p, sizeof(best), hipMemcpyDeviceToHost));
+    HIP_LEGACY(hipMemcpy(ep, S.ep.p, sizeof(ep), hipMemcpyDeviceToHost));
+    HIP_LEGACY(hipMemcpy(fl, S.snap_flags.p, sizeof(fl), hipMemcpyDeviceToHost));
+    HIP_LEGACY(hipMemcpy(best, S.best.p, sizeof(best), hipMemcpyDeviceToHost));
     d["epoch"] = ep[0]; d["epoch_in_phase"] = ep[1];
     d["snap_loss_taken"] = fl[0]; d["snap_sharpe_taken"] = fl[1];
     d["best_loss"] = best[0]; d["best_sharpe"] = best[1]; d["best_moment"] = best[2];
     d["snap_loss"] = down(S.snap_loss); d["snap_sharpe"] = down(S.snap_sharpe);
     py::array_t<float> h({ep[0], (int)HIST_W});
-    if (ep[0]) HIP_OK(hipMemcpy(h.mutable_data(), S.hist.p, (size_t)ep[0] * HIST_W * 4, hipMemcpyDeviceToHost));
+    if (ep[0]) HIP_LEGACY(hipMemcpy(h.mutable_data(), S.hist.p, (size_t)ep[0] * HIST_W * 4, hipMemcpyDeviceToHost));
     d["hist"] = h;
     return d;
   }
@@ -330,12 +342,12 @@ class Engine {
     sync();
     int ep[2] = {epoch, epoch_in_phase}, fl[2] = {snap_loss_taken, snap_sharpe_taken};
     float best[3] = {best_loss, best_sharpe, best_moment};
-    HIP_OK(hipMemcpy(S.ep.p, ep, sizeof(ep), hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(S.snap_flags.p, fl, sizeof(fl), hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(S.best.p, best, sizeof(best), hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(S.snap_loss.p, snap_loss.data(), md_.P * 4, hipMemcpyHostToDevice));
-    HIP_OK(hipMemcpy(S.snap_sharpe.p, snap_sharpe.data(), md_.P * 4, hipMemcpyHostToDevice));
-    if (epoch) HIP_OK(hipMemcpy(S.hist.p, hist.data(), (size_t)epoch * HIST_W * 4, hipMemcpyHostToDevice));
+    HIP_LEGACY(hipMemcpy(S.ep.p, ep, sizeof(ep), hipMemcpyHostToDevice));
+    HIP_LEGACY(hipMemcpy(S.snap_flags.p, fl, sizeof(fl), hipMemcpyHostToDevice));
+    HIP_LEGACY(hipMemcpy(S.best.p, best, sizeof(best), hipMemcpyHostToDevice));
+    HIP_LEGACY(hipMemcpy(S.snap_loss.p, snap_loss.data(), md_.P * 4, hipMemcpyHostToDevice));
+    HIP_LEGACY(hipMemcpy(S.snap_sharpe.p, snap_sharpe.data(), md_.P * 4, hipMemcpyHostToDevice));
+    if (epoch) HIP_LEGACY(hipMemcpy(S.hist.p, hist.data(), (size_t)epoch * HIST_W * 4, hipMemcpyHostToDevice));
   }
 
   // ---------------------------------------------------------------- phase control -------
@@ -346,12 +358,12 @@ class Engine {
       ModelState& S = models_[g];
       const float inf = INFINITY;
       float best[3] = {inf, -inf, -inf};
-      HIP_OK(hipMemcpy(S.best.p, best, sizeof(best), hipMemcpyHostToDevice));
-      HIP_OK(hipMemset(S.snap_flags.p, 0, 2 * sizeof(int)));
+      HIP_LEGACY(hipMemcpy(S.best.p, best, sizeof(best), hipMemcpyHostToDevice));
+      HIP_LEGACY(hipMemset(S.snap_flags.p, 0, 2 * sizeof(int)));
       int ep[2];
-      HIP_OK(hipMemcpy(ep, S.ep.p, sizeof(ep), hipMemcpyDeviceToHost));
+      HIP_LEGACY(hipMemcpy(ep, S.ep.p, sizeof(ep), hipMemcpyDeviceToHost));
       ep[1] = 0;
-      HIP_OK(hipMemcpy(S.ep.p, ep, sizeof(ep), hipMemcpyHostToDevice));
+      HIP_LEGACY(hipMemcpy(S.ep.p, ep, sizeof(ep), hipMemcpyHostToDevice));
     }
     sync();
     (void)phase;
@@ -360,19 +372,19 @@ class Engine {
     ModelState& S = models_[check_g(g)];
     sync();
     py::array_t<int> out(2);
-    HIP_OK(hipMemcpy(out.mutable_data(), S.snap_flags.p, 2 * sizeof(int), hipMemcpyDeviceToHost));
+    HIP_LEGACY(hipMemcpy(out.mutable_data(), S.snap_flags.p, 2 * sizeof(int), hipMemcpyDeviceToHost));
     return out;
   }
   int epoch_count(int g) {
     sync();
     int ep[2];
-    HIP_OK(hipMemcpy(ep, models_[check_g(g)].ep.p, sizeof(ep), hipMemcpyDeviceToHost));
+    HIP_LEGACY(hipMemcpy(ep, models_[check_g(g)].ep.p, sizeof(ep), hipMemcpyDeviceToHost));
     return ep[0];
   }
   py::array_t<float> history(int g) {
     const int n = epoch_count(g);
     py::array_t<float> out({n, (int)HIST_W});
-    if (n) HIP_OK(hipMemcpy(out.mutable_data(), models_[g].hist.p, (size_t)n * HIST_W * 4, hipMemcpyDeviceToHost));
+    if (n) HIP_LEGACY(hipMemcpy(out.mutable_data(), models_[g].hist.p, (size_t)n * HIST_W * 4, hipMemcpyDeviceToHost));
     return out;
   }
 
@@ -451,7 +463,7 @@ class Engine {
     sync();  // (already synchronous)
     ModelState& S = models_[check_g(g)];
     py::array_t<uint16_t> out(S.blob.n);
-    HIP_OK(hipMemcpy(out.mutable_data(), S.blob.p, S.blob.n * 2, hipMemcpyDeviceToHost));
+    HIP_LEGACY(hipMemcpy(out.mutable_data(), S.blob.p, S.blob.n * 2, hipMemcpyDeviceToHost));
     return out;
   }
   void sync() { HIP_OK(hipStreamSynchronize(st_)); }
@@ -502,18 +514,18 @@ class Engine {
   template <typename T>
   void up(DevBuf<T>& b, const T* src, size_t n) {
     b.alloc(n, false);
-    if (n) HIP_OK(hipMemcpy(b.p, src, n * sizeof(T), hipMemcpyHostToDevice));
+    if (n) HIP_LEGACY(hipMemcpy(b.p, src, n * sizeof(T), hipMemcpyHostToDevice));
   }
   py::array_t<float> down(const DevBuf<float>& b) {
     sync();
     py::array_t<float> out(b.n);
-    if (b.n) HIP_OK(hipMemcpy(out.mutable_data(), b.p, b.n * sizeof(float), hipMemcpyDeviceToHost));
+    if (b.n) HIP_LEGACY(hipMemcpy(out.mutable_data(), b.p, b.n * sizeof(float), hipMemcpyDeviceToHost));
     return out;
   }
   template <typename T>
   DevBuf<char>& upload(DevBuf<char>& b, const std::vector<T>& v) {
     b.alloc(v.size() * sizeof(T), false);
-    if (!v.empty()) HIP_OK(hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    if (!v.empty()) HIP_LEGACY(hipMemcpy(b.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
     return b;
   }
 
@@ -1034,9 +1046,12 @@ class Engine {
     auto it = graphs_.find(key);
     if (it != graphs_.end()) return it->second;
     hipGraph_t graph;
-    HIP_OK(hipStreamBeginCapture(st_, hipStreamCaptureModeThreadLocal));
-    enqueue();
-    HIP_OK(hipStreamEndCapture(st_, &graph));
+    {
+      std::lock_guard<std::mutex> g(g_legacy_mu);
+      HIP_OK(hipStreamBeginCapture(st_, hipStreamCaptureModeThreadLocal));
+      enqueue();
+      HIP_OK(hipStreamEndCapture(st_, &graph));
+    }
     hipGraphExec_t exec;
     HIP_OK(hipGraphInstantiateWithFlags(&exec, graph, prio_ ? hipGraphInstantiateFlagUseNodePriority : 0));
     HIP_OK(hipGraphDestroy(graph));

@@ -9,6 +9,7 @@ final on-disk state equals the reference's "last writer wins" sequence.
 from __future__ import annotations
 
 import os
+import threading
 import time
 from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence
@@ -51,12 +52,20 @@ def unflatten_state(flat: np.ndarray, spec: ModelSpec) -> Dict[str, torch.Tensor
 _PREP_CACHE: "OrderedDict[tuple, object]" = OrderedDict()
 
 
+_PREP_LOCK = threading.Lock()
+
+
 def _prepared(batch: Dict, KP: int):
     """Host compaction of a split, memoised on the identity/version of its input tensors: the
     ensemble and sweep drivers build one engine per architecture bucket over the same panel."""
     def tk(t):
         return (id(t), t.data_ptr(), t._version) if isinstance(t, torch.Tensor) else (id(t),)
     key = (KP,) + tuple(tk(batch.get(k)) for k in ("individual_features", "returns", "mask", "macro_features"))
+    with _PREP_LOCK:       # drivers may build engines from several threads
+        return _prepared_locked(batch, KP, key)
+
+
+def _prepared_locked(batch: Dict, KP: int, key):
     hit = _PREP_CACHE.get(key)
     if hit is None:
         # the entry keeps the inputs alive, so their ids cannot be reused while it exists
