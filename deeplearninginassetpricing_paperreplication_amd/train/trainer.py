@@ -158,13 +158,19 @@ class _Stop(Exception):
 
 def _train_3phase_cpu(config, train_data, valid_data, test_data, device, n_unc, n_mom, n_cond,
                       lr, print_freq, save_dir, ignore_epoch, sel, verbose, resume=False,
-                      resume_path=None, nan_policy="warn", stop_after=None):
+                      resume_path=None, nan_policy="warn", stop_after=None, *, model=None,
+                      train_fn=None, eval_fn=None):
+    """``model`` / ``train_fn`` / ``eval_fn`` substitute the module and the step / evaluation
+    functions (the cross-sectionally sharded executor of ``parallel.xsection`` passes its own)."""
     from ..utils.guards import NonFiniteError, POLICIES
     import warnings
     if nan_policy not in POLICIES:
         raise ValueError(f"nan_policy must be one of {POLICIES}")
     say = print if verbose else (lambda *a, **k: None)
-    model = AssetPricingGAN(config).to(device)
+    train_epoch_ = train_fn or train_epoch
+    evaluate_ = eval_fn or evaluate
+    if model is None:
+        model = AssetPricingGAN(config).to(device)
     n_sdf = sum(p.numel() for p in model.sdf_net.parameters())
     n_mom_p = sum(p.numel() for p in model.moment_net.parameters())
     say(f"Model has {n_sdf + n_mom_p:,} trainable parameters")
@@ -230,9 +236,9 @@ def _train_3phase_cpu(config, train_data, valid_data, test_data, device, n_unc, 
             st["best_loss"], st["best_sr"] = float("inf"), float("-inf")
         for e in range(start, n):
             te0 = time.time()
-            tr = train_epoch(model, opt_sdf, train_data, device, phase=phase, scope="sdf")
-            va = evaluate(model, valid_data, device)
-            te = evaluate(model, test_data, device) if test_data is not None else None
+            tr = train_epoch_(model, opt_sdf, train_data, device, phase=phase, scope="sdf")
+            va = evaluate_(model, valid_data, device)
+            te = evaluate_(model, test_data, device) if test_data is not None else None
             hist["train_loss"].append(tr["loss"]); hist["train_sharpe"].append(tr["sharpe"])
             hist["phase"].append(tag)
             hist["valid_loss"].append(va[loss_key]); hist["valid_sharpe"].append(va["sharpe"])
@@ -270,7 +276,7 @@ def _train_3phase_cpu(config, train_data, valid_data, test_data, device, n_unc, 
                 p.requires_grad_(False)
             for e in range(st["done"], n_mom):
                 te0 = time.time()
-                tr = train_epoch(model, opt_mom, train_data, device, phase="moment", scope="moment")
+                tr = train_epoch_(model, opt_mom, train_data, device, phase="moment", scope="moment")
                 if tr["loss_cond"] > st["best_m"]:
                     st["best_m"] = tr["loss_cond"]
                     _save(model, save_dir, "best_model_loss.pt")
@@ -300,7 +306,7 @@ def _train_3phase_cpu(config, train_data, valid_data, test_data, device, n_unc, 
     say(f"Total time: {total / 60:.1f} minutes")
     say(f"Total epochs: {n_unc + n_mom + n_cond} ({n_unc} + {n_mom} + {n_cond})\n" + "=" * 70)
     if verbose:
-        print_final(lambda d: evaluate(model, d, device), train_data, valid_data, test_data)
+        print_final(lambda d: evaluate_(model, d, device), train_data, valid_data, test_data)
     _save(model, save_dir, "final_model.pt")
     return model, hist
 
