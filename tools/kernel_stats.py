@@ -11,6 +11,21 @@ from collections import defaultdict
 from pathlib import Path
 
 
+def demangle(names):
+    """Demangled kernel names (rocprofv3 writes mangled ``_Z...kd`` symbols with some options)."""
+    import shutil
+    import subprocess
+    names = list(names)
+    raw = [n[:-3] if n.endswith(".kd") else n for n in names]
+    tool = shutil.which("c++filt") or "/opt/rocm/lib/llvm/bin/llvm-cxxfilt"
+    try:
+        out = subprocess.run([tool], input="\n".join(raw), capture_output=True, text=True, check=True).stdout
+        dem = out.split("\n")[:len(raw)]
+        return dict(zip(names, dem)) if len(dem) == len(raw) else dict(zip(names, raw))
+    except (OSError, subprocess.CalledProcessError):
+        return dict(zip(names, raw))
+
+
 def from_db(path: Path):
     c = sqlite3.connect(str(path))
     q = ("select s.kernel_name, d.end - d.start, s.arch_vgpr_count, s.accum_vgpr_count, s.sgpr_count, "
@@ -41,7 +56,9 @@ def main():
     for f in d.glob("*kernel_trace.csv"):
         rows += list(from_csv(f))
     agg = defaultdict(lambda: [0, 0.0, None])
+    dm = demangle({r[0] for r in rows})
     for name, ns, info in rows:
+        name = dm[name]
         e = agg[name]
         e[0] += 1
         e[1] += ns
