@@ -50,12 +50,16 @@ def init(backend: Optional[str] = None, timeout_s: float = 600.0, use_gpu: Optio
     local = int(os.environ.get("LOCAL_RANK", str(rank)))
     if use_gpu is None:
         use_gpu = torch.cuda.is_available()
+    if use_gpu and os.environ.get("DLAP_SHARE_GPU", "0") == "1":
+        # rehearsal of a multi-rank job on fewer GPUs (with DLAP_DIST_BACKEND=gloo: RCCL
+        # refuses two ranks on one device)
+        local = local % max(1, torch.cuda.device_count())
     dev = torch.device("cuda", local) if use_gpu else torch.device("cpu")
     if use_gpu:
         torch.cuda.set_device(dev)
     if world <= 1:
         return Dist(0, 1, 0, "none", dev)
-    backend = backend or ("nccl" if use_gpu else "gloo")
+    backend = backend or os.environ.get("DLAP_DIST_BACKEND") or ("nccl" if use_gpu else "gloo")
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     if not tdist.is_initialized():
         kw = dict(backend=backend, timeout=datetime.timedelta(seconds=timeout_s))

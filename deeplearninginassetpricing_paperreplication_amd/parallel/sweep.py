@@ -130,6 +130,9 @@ def run_sweep(batches: Dict[str, Dict], entries, dist: Optional[comm.Dist] = Non
 
     def one(b):
         try:
+            if d.device.type == "cuda":
+                # HIP's current device is per host thread: a pool thread starts on device 0
+                torch.cuda.set_device(d.device)
             if b in set(fail_buckets):
                 raise RuntimeError("injected failure")
             res = run_bucket(entries, bks[b], batches, d.device, epochs, ignore_epoch, seed, selection_sign,
