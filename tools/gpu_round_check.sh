@@ -1,0 +1,5 @@
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/r1e_gpu_tests.log 2>&1 && \
+timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/r1e_smoke.log 2>&1 && \
+timeout -k 10 300 python bench.py > gpurun_out/r1e_bench.log 2>&1
