@@ -155,6 +155,9 @@ class Engine {
     ws_.resize((size_t)G * 3);
   }
   ~Engine() {
+    // drain both streams before the graphs, events and (member) buffers go away
+    if (st2_) (void)hipStreamSynchronize(st2_);
+    if (st_) (void)hipStreamSynchronize(st_);
     for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
     if (ev_fork_) (void)hipEventDestroy(ev_fork_);
     if (ev_join_) (void)hipEventDestroy(ev_join_);
