@@ -328,8 +328,9 @@ class Engine {
     d["snap_loss_taken"] = fl[0]; d["snap_sharpe_taken"] = fl[1];
     d["best_loss"] = best[0]; d["best_sharpe"] = best[1]; d["best_moment"] = best[2];
     d["snap_loss"] = down(S.snap_loss); d["snap_sharpe"] = down(S.snap_sharpe);
-    py::array_t<float> h({ep[0], (int)HIST_W});
-    if (ep[0]) HIP_LEGACY(hipMemcpy(h.mutable_data(), S.hist.p, (size_t)ep[0] * HIST_W * 4, hipMemcpyDeviceToHost));
+    const int nh = std::min(ep[0], max_epochs_);     // rows past the capacity were not kept
+    py::array_t<float> h({nh, (int)HIST_W});
+    if (nh) HIP_LEGACY(hipMemcpy(h.mutable_data(), S.hist.p, (size_t)nh * HIST_W * 4, hipMemcpyDeviceToHost));
     d["hist"] = h;
     return d;
   }
@@ -385,7 +386,7 @@ class Engine {
     return ep[0];
   }
   py::array_t<float> history(int g) {
-    const int n = epoch_count(g);
+    const int n = std::min(epoch_count(g), max_epochs_);   // rows past the capacity were not kept
     py::array_t<float> out({n, (int)HIST_W});
     if (n) HIP_LEGACY(hipMemcpy(out.mutable_data(), models_[g].hist.p, (size_t)n * HIST_W * 4, hipMemcpyDeviceToHost));
     return out;
@@ -894,6 +895,7 @@ class Engine {
         E.gnorm = S.gnorm.p; E.hist = S.hist.p; E.ep = S.ep.p; E.best = S.best.p;
         E.snap_flags = S.snap_flags.p; E.params = S.params.p;
         E.snap_loss = S.snap_loss.p; E.snap_sharpe = S.snap_sharpe.p;
+        E.max_ep = max_epochs_;
         ej.push_back(E);
       }
       upload(j_mlp_train_[phase], mt); upload(j_mlp_bwd_[phase], mb); upload(j_loss_train_[phase], lt);

@@ -317,7 +317,9 @@ __global__ __launch_bounds__(256) void k_epoch_end(const EpochJob* __restrict__ 
   __shared__ int dec[2];
   if (threadIdx.x == 0) {
     const int ep = gp(J.ep)[0], ep_ph = gp(J.ep)[1];
-    float* row = gp(J.hist) + (size_t)ep * HIST_W;
+    // past the history capacity the row goes to a per-block scratch instead of out of bounds
+    __shared__ float spill[HIST_W];
+    float* row = ep < J.max_ep ? gp(J.hist) + (size_t)ep * HIST_W : spill;
     const float* tr = gp(J.sc_train);
     const float lres = tr[SC_LRES] * res_factor;
     float tloss;

@@ -64,6 +64,7 @@ struct EpochJob {          // one model
   const float* params;
   float* snap_loss;        // [P]
   float* snap_sharpe;      // [P]
+  int max_ep;              // rows of hist: epochs past the capacity are not recorded
 };
 
 void launch_finalize(const FinJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,

@@ -454,3 +454,20 @@ def test_edge_panels_all_masked_period_single_observation_asset(monkeypatch, wid
         assert np.isfinite(got).all()
         cos = np.dot(got[sl], ref[sl]) / (np.linalg.norm(got[sl]) * np.linalg.norm(ref[sl]))
         assert cos > 0.995, (T, N, cos)
+
+
+def test_epochs_past_history_capacity_are_dropped_not_written_out_of_bounds():
+    """More epochs than ``max_epochs``: k_epoch_end keeps the first max_epochs history rows and
+    sends later rows to scratch (no write past the history buffer); training itself continues."""
+    cfg = default_cli_config(8, 46)
+    eng, _ = _engine(cfg, max_epochs=4)
+    before = eng.params(0).copy()
+    for ph, n in ((1, 3), (3, 4)):
+        eng.eng.begin_phase(ph)
+        eng.run(ph, n, 1e-3, 0, 1.0, True)
+    eng.eng.sync()
+    h = eng.history_rows(0)
+    assert h.shape[0] == 4
+    assert np.isfinite(h[:, 1]).all()
+    after = eng.params(0)
+    assert np.isfinite(after).all() and np.abs(after - before).max() > 0
