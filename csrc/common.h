@@ -42,6 +42,16 @@ DLAP_DEV DLAP_GLOBAL T* gp(T* p) { return (DLAP_GLOBAL T*)p; }
 
 void dlap_throw_hip(hipError_t e, const char* what, const char* file, int line);
 
+// Device-side bounds checks (build with DLAP_DEBUG=1: `engine.build --debug`): an index that
+// leaves its allocation stops the kernel with a printed assertion instead of corrupting or
+// faulting somewhere else. Compiled out of the production extension.
+#if defined(DLAP_DEBUG) && DLAP_DEBUG
+#include <cassert>
+#define DLAP_ASSERT(cond) assert(cond)
+#else
+#define DLAP_ASSERT(cond) ((void)0)
+#endif
+
 DLAP_DEV f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }

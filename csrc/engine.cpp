@@ -136,6 +136,7 @@ class Engine {
     zx_eval_ = env_int("DLAP_ZX_EVAL", 1) != 0;
     zx_train_ = env_int("DLAP_ZX_TRAIN", 1) != 0;
     zx_gx_ = std::max(1, env_int("DLAP_ZX_GX", 256));
+    train_first_ = env_int("DLAP_TRAIN_FIRST", 0) != 0;
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
                residual);
     d_desc_.alloc(sizeof(ModelDesc));
@@ -340,9 +341,12 @@ class Engine {
                          py::array_t<float, py::array::c_style> snap_sharpe,
                          py::array_t<float, py::array::c_style> hist) {
     ModelState& S = models_[check_g(g)];
-    if (epoch < 0 || epoch > max_epochs_) throw std::invalid_argument("epoch count exceeds max_epochs");
+    // a record taken past the history capacity holds only the first max_epochs rows (the
+    // device drops later rows, get_tracker_state reads min(epoch, max_epochs) of them)
+    const int nh = std::min(epoch, max_epochs_);
+    if (epoch < 0) throw std::invalid_argument("negative epoch count");
     if (snap_loss.size() != md_.P || snap_sharpe.size() != md_.P) throw std::invalid_argument("snapshot size");
-    if (hist.size() != (size_t)epoch * HIST_W) throw std::invalid_argument("history size");
+    if (hist.size() != (size_t)nh * HIST_W) throw std::invalid_argument("history size");
     sync();
     int ep[2] = {epoch, epoch_in_phase}, fl[2] = {snap_loss_taken, snap_sharpe_taken};
     float best[3] = {best_loss, best_sharpe, best_moment};
@@ -351,7 +355,7 @@ class Engine {
     HIP_LEGACY(hipMemcpy(S.best.p, best, sizeof(best), hipMemcpyHostToDevice));
     HIP_LEGACY(hipMemcpy(S.snap_loss.p, snap_loss.data(), md_.P * 4, hipMemcpyHostToDevice));
     HIP_LEGACY(hipMemcpy(S.snap_sharpe.p, snap_sharpe.data(), md_.P * 4, hipMemcpyHostToDevice));
-    if (epoch) HIP_LEGACY(hipMemcpy(S.hist.p, hist.data(), (size_t)epoch * HIST_W * 4, hipMemcpyHostToDevice));
+    if (nh) HIP_LEGACY(hipMemcpy(S.hist.p, hist.data(), (size_t)nh * HIST_W * 4, hipMemcpyHostToDevice));
   }
 
   // ---------------------------------------------------------------- phase control -------
@@ -486,6 +490,7 @@ class Engine {
   bool zx_train_ = true;                     // ... and training forward (DLAP_ZX_TRAIN)
   int zx_gx_ = 256;                          // their workgroups over all evaluation jobs (DLAP_ZX_GX)
   bool side_metrics_ = false;                // train Sharpe monitor on a graph side branch (DLAP_SIDE_METRICS)
+  bool train_first_ = false;                 // capture the training chain before the evaluation branch
   ModelDesc md_{};
   DevBuf<char> d_desc_;
   SplitDev splits_[3];
@@ -808,7 +813,7 @@ class Engine {
     SplitDev& D = splits_[s];
     LossJob J{};
     J.Rm = D.Rm.p; J.mask = D.mask.p; J.invNt = D.invNt.p; J.Nt = D.Nt.p; J.meanR = D.meanR.p;
-    J.RR = D.RR.p; J.invT = D.invT.p; J.Nbar = D.Nbar; J.T = D.T; J.N = D.N; J.K = md_.K;
+    J.RR = D.RR.p; J.invT = D.invT.p; J.Nbar = D.Nbar; J.T = D.T; J.N = D.N; J.K = md_.K; J.R = D.R;
     J.row_ptr = D.row_ptr.p; J.rowti = reinterpret_cast<const int2*>(D.rowti.p); J.Rc = D.Rc.p; J.mu = W.mu.p;
     J.normalize = md_.normalize_w; J.weighted = md_.weighted_loss; J.phase = phase;
     J.res_factor = md_.residual_factor;
@@ -1022,7 +1027,13 @@ class Engine {
   void enqueue_pipe(int phase, float lr, int ignore_epoch, float sel) {
     HIP_OK(hipEventRecord(ev_fork_, st_));
     HIP_OK(hipStreamWaitEvent(st2_, ev_fork_, 0));
-    if (b_wait_ == 0) {
+    if (b_wait_ == 0 && train_first_) {
+      // same graph topology, training-chain nodes first (they land on the graph's first queue)
+      enqueue_train_grads(phase, side_metrics_ ? st2_ : nullptr, true);   // this epoch's fwd/bwd
+      enqueue_eval(st2_);                                 // previous epoch's evaluation
+      enqueue_epoch_end(phase, ignore_epoch, sel, st2_);  // ... and its bookkeeping
+      enqueue_dropmask(phase, 1, st2_);                   // next epoch's dropout masks
+    } else if (b_wait_ == 0) {
       enqueue_eval(st2_);                                 // previous epoch's evaluation
       enqueue_epoch_end(phase, ignore_epoch, sel, st2_);  // ... and its bookkeeping
       enqueue_dropmask(phase, 1, st2_);                   // next epoch's dropout masks

@@ -32,13 +32,19 @@ __global__ __launch_bounds__(PER_NT) void k_period_fwd(const LossJob* __restrict
   __shared__ float red[PER_NT / 64];
   const int N = J.N;
   const int r0 = gp(J.row_ptr)[t], r1 = gp(J.row_ptr)[t + 1];   // this period's compact rows
+  DLAP_ASSERT(0 <= r0 && r0 <= r1 && r1 <= J.R);
   const auto w = gp(J.w);
   const auto Rc = gp(J.Rc);
   const auto rowti = gp(J.rowti);
   const float invN = gp(J.invNt)[t];
   float* wn = gp(J.wn) + (size_t)t * N;
   float s_wr = 0.f, s_abs = 0.f, s_ww = 0.f, mu = 0.f;
-  if (r1 - r0 <= PER_NT * PER_RB) {
+  // A period without valid stocks has no compact rows: r0 == r1, possibly == R (the last
+  // period of the split), so the clamped `rr = r0` below would read one element past the end of
+  // w / Rc / rowti (and then index wn with a garbage stock). Its sums are all zero.
+  if (r1 == r0) {
+    // (block-uniform: every thread takes this branch; no barrier is skipped by some threads)
+  } else if (r1 - r0 <= PER_NT * PER_RB) {
     float wv[PER_RB], rv[PER_RB];
     int iv[PER_RB];
 #pragma unroll
@@ -265,6 +271,10 @@ __global__ __launch_bounds__(PER_NT) void k_period_bwd(const LossJob* __restrict
   const int N = J.N, K = J.K;
   const size_t base = (size_t)t * N;
   const int r0 = gp(J.row_ptr)[t], r1 = gp(J.row_ptr)[t + 1];
+  DLAP_ASSERT(0 <= r0 && r0 <= r1 && r1 <= J.R);
+  // no compact rows in this period (all stocks masked): no dL/dw to write, and the clamped
+  // row index of the loads below would point past the end of the arrays when r0 == R
+  if (r1 == r0) return;            // block-uniform, before any barrier
   const auto rowti = gp(J.rowti);
   const auto Rc = gp(J.Rc);
   const auto invT = gp(J.invT);

@@ -115,6 +115,7 @@ DLAP_DEV RowInfo finish_ztile(const MlpJob& J, int tile, ZTile<WMB>& in) {
     const bool ok = r < J.R;
     ri.t[b] = in.ti[b].x;
     ri.i[b] = in.ti[b].y;
+    DLAP_ASSERT(J.R > 0 && (unsigned)ri.t[b] < (unsigned)J.T && (unsigned)ri.i[b] < (unsigned)J.N);
     ri.dense[b] = ok ? in.ti[b].x * J.N + in.ti[b].y : -1;
     if (!ok) in.dw[b] = 0.f;
   }
@@ -179,6 +180,7 @@ DLAP_DEV RowInfo finish_tile(const MlpJob& J, const MlpDims& D, int tile, TileIn
     const bool ok = r < J.R;
     ri.t[b] = in.ti[b].x;
     ri.i[b] = in.ti[b].y;
+    DLAP_ASSERT(J.R > 0 && (unsigned)ri.t[b] < (unsigned)J.T && (unsigned)ri.i[b] < (unsigned)J.N);
     ri.dense[b] = ok ? in.ti[b].x * J.N + in.ti[b].y : -1;
 #pragma unroll
     for (int s = 0; s < KS1; ++s) xf[b][s] = ok ? in.x[b][s] : zero8();
@@ -682,6 +684,7 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
         const int r = tile * 32 + 16 * b + (lane & 15);
         ri.t[b] = ti[b].x;
         ri.i[b] = ti[b].y;
+        DLAP_ASSERT((unsigned)ri.t[b] < (unsigned)J.T && (unsigned)ri.i[b] < (unsigned)J.N);
         ri.dense[b] = r < J.R ? ti[b].x * J.N + ti[b].y : -1;
       }
       int2 tn[2];

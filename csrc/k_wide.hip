@@ -198,6 +198,7 @@ __global__ __launch_bounds__(WG_WAVES * 64) void k_wgrad0(const WideJob* __restr
 #pragma unroll
     for (int u = 0; u < UB; ++u) acc[k][u] = zero4();
   auto load = [&](int tile, bf16x8 (&dz)[UB], bf16x8 (&xt)[VPW]) {
+    DLAP_ASSERT(tile >= 0 && tile < ntiles);
     const auto dzp = gp(J.dz) + (size_t)tile * UB * 64 + lane;
 #pragma unroll
     for (int u = 0; u < UB; ++u) dz[u] = dzp[u * 64];
@@ -253,6 +254,7 @@ __global__ __launch_bounds__(256) void k_wgrad0_fin(const WideJob* __restrict__ 
   const bool mom = J.do_mom;
   const PackLayer& L = mom ? md->m[0] : md->s[0];
   if (unit >= L.out) return;
+  DLAP_ASSERT(L.col0 + col < L.ld || col >= md->F);
   if (col < md->F) gp(J.grads)[L.w_off + unit * L.ld + L.col0 + col] = v;
 }
 

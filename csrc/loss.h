@@ -27,6 +27,7 @@ struct LossJob {
   float* mu;             // [T] cross-sectional mean of the raw weights
   float Nbar;
   int T, N, K;
+  int R;                 // compact rows of the split (bounds of w / Rc / rowti / dw)
   int normalize, weighted;
   int phase;             // 1: unconditional, 2: moment, 3: conditional, 0: evaluation
   float res_factor;      // residual_loss_factor (gradient only in training jobs)

@@ -57,15 +57,28 @@ UBSAN_FLAGS = ["-Xarch_host", "-fsanitize=undefined", "-Xarch_host", "-fsanitize
                "-Xarch_host", "-fno-sanitize=vptr"]
 
 
-def build(force: bool = False, jobs: int = 8, verbose: bool = True, ubsan: bool = False) -> Path:
+# Device-side bounds assertions (DLAP_ASSERT in csrc/common.h) for fault hunting: a kernel index
+# that leaves its allocation aborts with the failing condition printed.
+DEBUG_FLAGS = ["-DDLAP_DEBUG=1"]
+
+
+def variant_path(variant: str) -> Path:
+    """Where a non-default build lives (``PKG/<variant>/_dlap_hip*.so``); ``ops.native.load``
+    imports it instead of the production module when ``DLAP_NATIVE=<variant>``."""
+    return PKG / variant / ext_path().name
+
+
+def build(force: bool = False, jobs: int = 8, verbose: bool = True, ubsan: bool = False,
+          debug: bool = False) -> Path:
     srcs = sorted(CSRC.glob("*.hip")) + [CSRC / "engine.cpp"]
     headers = sorted(CSRC.glob("*.h"))
     out = ext_path()
     build_dir = BUILD
-    if ubsan:       # a separate artefact, swapped in by tools/ubsan_gpu_tests.sh on the GPU box
-        out = PKG / "ubsan" / out.name
+    variant = "ubsan" if ubsan else ("debug" if debug else None)
+    if variant:     # a separate artefact next to the production one (selected by DLAP_NATIVE)
+        out = variant_path(variant)
         out.parent.mkdir(exist_ok=True)
-        build_dir = BUILD / "ubsan"
+        build_dir = BUILD / variant
     stamp = build_dir / "stamp"
     key = _hash(srcs + headers)
     if not force and out.exists() and stamp.exists() and stamp.read_text() == key:
@@ -73,7 +86,7 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True, ubsan: bool 
             print(f"[dlap] native extension up to date: {out.name}")
         return out
     build_dir.mkdir(parents=True, exist_ok=True)
-    flags = _includes() + ["-Wno-unused-result"] + (UBSAN_FLAGS if ubsan else [])
+    flags = _includes() + ["-Wno-unused-result"] + (UBSAN_FLAGS if ubsan else []) + (DEBUG_FLAGS if debug else [])
     objs = []
     with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(srcs)))) as ex:
         futs = {ex.submit(_compile, s, build_dir / (s.stem + ".o"), flags): s for s in srcs}
@@ -93,4 +106,4 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True, ubsan: bool 
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, ubsan="--ubsan" in sys.argv)
+    build(force="--force" in sys.argv, ubsan="--ubsan" in sys.argv, debug="--debug" in sys.argv)

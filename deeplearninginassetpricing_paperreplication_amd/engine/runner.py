@@ -239,8 +239,10 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
     timers = Timers()
     monitor = NonFiniteMonitor(n_models, HIST, nan_policy)
     start = (1, 0)                  # (phase, epochs done in it) to continue from
+    run_fp = ckpt.run_fingerprint(lr, ignore_epoch, selection_sign,
+                                  ckpt.data_fingerprint(train_data, valid_data, test_data)) if resume_path else None
     if resume and resume_path:
-        rec = ckpt.load_resume(resume_path, spec, schedule)
+        rec = ckpt.load_resume(resume_path, spec, schedule, run=run_fp)
         if rec is not None:
             if len(rec["models"]) != n_models:
                 raise ValueError(f"{resume_path}: {len(rec['models'])} models, expected {n_models}")
@@ -259,7 +261,7 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
             lr_of = (lambda g: lrs[g]) if lrs is not None else (lambda g: None)
             ckpt.save_resume(resume_path, spec=spec, phase=phase, done=done, schedule=schedule,
                              models=[ckpt.capture_model(eng.eng, g, seeds[g], lr_of(g)) for g in range(n_models)],
-                             best_state=best_state, elapsed=time.time() - t_start)
+                             best_state=best_state, elapsed=time.time() - t_start, run=run_fp)
 
     class _Stop(Exception):
         pass

@@ -9,7 +9,9 @@ GPU engine needs to continue a 3-phase run bit-for-bit where it stopped:
     the per-phase best trackers and snapshot flags, both best-model snapshots, the device
     history rows, the per-model learning rate,
   * a fingerprint of the architecture (``ModelSpec``) so a file is never applied to a
-    different model.
+    different model, and a run fingerprint (learning rate, ``ignore_epoch``, selection sign and a
+    cheap checksum of every split's shape / mask / returns) so it is never continued with other
+    hyperparameters or data.
 
 The file is written atomically (temp file + ``os.replace``) at every print boundary and phase
 end, so a crash leaves either the previous or the new complete state. It contains only tensors,
@@ -66,21 +68,42 @@ def spec_fingerprint(spec) -> str:
     return repr(spec)
 
 
+def data_fingerprint(*batches) -> str:
+    """Cheap identity of the training data: per split its [T, N] shape, the number of valid
+    entries, and float64 sums of the mask pattern (weighted by position) and of the returns."""
+    parts = []
+    for b in batches:
+        if b is None:
+            parts.append("-")
+            continue
+        m = torch.as_tensor(b["mask"]).detach().to("cpu", torch.float64)
+        r = torch.as_tensor(b["returns"]).detach().to("cpu", torch.float64) * m
+        pos = torch.arange(m.numel(), dtype=torch.float64).reshape(m.shape)
+        parts.append(f"{tuple(m.shape)}:{int(m.sum())}:{float((m * pos).sum()):.6e}:{float(r.sum()):.9e}")
+    return "|".join(parts)
+
+
+def run_fingerprint(lr: float, ignore_epoch: int, selection_sign: float, data: str) -> Dict:
+    return {"lr": float(lr), "ignore_epoch": int(ignore_epoch), "selection_sign": float(selection_sign),
+            "data": str(data)}
+
+
 def save_resume(path: str, *, spec, phase: int, done: int, schedule, models: List[Dict],
-                best_state: List[bool], elapsed: float):
+                best_state: List[bool], elapsed: float, run: Optional[Dict] = None):
     rec = {
         "format": FORMAT_VERSION, "spec": spec_fingerprint(spec), "phase": int(phase),
         "done": int(done), "schedule": [int(x) for x in schedule], "models": models,
         "best_state": [bool(b) for b in best_state], "elapsed": float(elapsed),
+        "run": dict(run) if run is not None else {},
     }
     tmp = path + ".tmp"
     torch.save(rec, tmp)
     os.replace(tmp, path)
 
 
-def load_resume(path: str, spec=None, schedule=None) -> Optional[Dict]:
+def load_resume(path: str, spec=None, schedule=None, run: Optional[Dict] = None) -> Optional[Dict]:
     """The resume record at ``path`` (None if absent). Raises if it belongs to another
-    architecture or schedule."""
+    architecture, schedule, or (``run``) learning rate / ignore_epoch / selection sign / data."""
     if not os.path.isfile(path):
         return None
     rec = torch.load(path, map_location="cpu", weights_only=True)
@@ -90,4 +113,11 @@ def load_resume(path: str, spec=None, schedule=None) -> Optional[Dict]:
         raise ValueError(f"{path}: saved for a different model architecture")
     if schedule is not None and list(rec["schedule"]) != [int(x) for x in schedule]:
         raise ValueError(f"{path}: saved for schedule {rec['schedule']}, not {list(schedule)}")
+    if run is not None:
+        saved = rec.get("run") or {}
+        for k, v in run.items():
+            if k not in saved:
+                raise ValueError(f"{path}: record has no run fingerprint entry {k!r}")
+            if saved[k] != v:
+                raise ValueError(f"{path}: saved with {k}={saved[k]!r}, this run has {k}={v!r}")
     return rec

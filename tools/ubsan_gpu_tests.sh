@@ -1,14 +1,18 @@
 #!/bin/bash
-# Run the GPU test suite against the host-UBSan (trap mode) build of the native extension.
-# Build it first on the CPU side:  python -m deeplearninginassetpricing_paperreplication_amd.engine.build --ubsan
-# Usage on the GPU box: bash tools/ubsan_gpu_tests.sh   (restores the normal .so afterwards)
+# Run the GPU test suite against a checking build of the native extension:
+#   ubsan (default): host UBSan in trap mode;   debug: device-side bounds assertions.
+# Build it first on the CPU side:
+#   python -m deeplearninginassetpricing_paperreplication_amd.engine.build --ubsan   (or --debug)
+# Usage on the GPU box: bash tools/ubsan_gpu_tests.sh [ubsan|debug] [pytest -k expression]
 set -u
-PKG=deeplearninginassetpricing_paperreplication_amd
-SO=$(ls $PKG/_dlap_hip*.so)
-cp "$SO" /tmp/_dlap_hip_normal.so || exit 1
-cp $PKG/ubsan/$(basename "$SO") "$SO" || exit 1
-timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+VARIANT=${1:-ubsan}
+SEL=${2:-}
+export DLAP_NATIVE=$VARIANT DLAP_AUTOBUILD=0
+if [ -n "$SEL" ]; then
+  timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -k "$SEL"
+else
+  timeout -k 10 500 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread
+fi
 rc=$?
-cp /tmp/_dlap_hip_normal.so "$SO"
-echo "ubsan gpu tests rc=$rc"
+echo "$VARIANT gpu tests rc=$rc"
 exit $rc
