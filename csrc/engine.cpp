@@ -136,7 +136,8 @@ class Engine {
     zx_eval_ = env_int("DLAP_ZX_EVAL", 1) != 0;
     zx_train_ = env_int("DLAP_ZX_TRAIN", 1) != 0;
     zx_gx_ = std::max(1, env_int("DLAP_ZX_GX", 256));
-    train_first_ = env_int("DLAP_TRAIN_FIRST", 0) != 0;
+    train_first_ = env_int("DLAP_TRAIN_FIRST", 1) != 0;
+    h_cache_ = env_int("DLAP_H_CACHE", 1) != 0;
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
                residual);
     d_desc_.alloc(sizeof(ModelDesc));
@@ -261,6 +262,7 @@ class Engine {
     up(D.Nt, nt.data(), T); up(D.invNt, inv_nt.data(), T); up(D.meanR, meanr.data(), T);
     up(D.RR, rr.data(), T); up(D.invT, invt.data(), N);
     D.set = true;
+    h_valid_ = false;
     alloc_ws(s);
     if (md_.md.wide && s == 0) {    // rows-as-k copy of the train panel for the weight gradient
       const size_t ntl = (size_t)(R + 31) / 32;
@@ -278,6 +280,7 @@ class Engine {
     HIP_OK(hipMemcpyAsync(models_[g].params.p, p.data(), md_.P * sizeof(float), hipMemcpyHostToDevice, st_));
     pack(g);
     sync();
+    h_valid_ = false;
   }
   py::array_t<float> get_params(int g) { return down(models_[check_g(g)].params); }
   py::array_t<float> get_grads(int g) { return down(models_[check_g(g)].grads); }
@@ -291,6 +294,7 @@ class Engine {
                           hipMemcpyDeviceToDevice, st_));
     pack(g);
     sync();
+    h_valid_ = false;
   }
   void set_seed(int g, unsigned seed) { models_[check_g(g)].seed = seed; graphs_dirty_ = true; }
   void set_lr(int g, float lr) { models_[check_g(g)].lr = lr; graphs_dirty_ = true; }
@@ -407,6 +411,8 @@ class Engine {
     if (!splits_[0].set) throw std::runtime_error("train split not set");
     if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
     if (n <= 0) return;
+    if (phase == 2) h_valid_ = false;     // the moment net trains: the cached moments go stale
+    else ensure_moments();
     const bool pipe = phase != 2 && n_eval_jobs_ > 0 && pipeline_;
     if (!use_graph) {
       for (int e = 0; e < n; ++e) enqueue_epoch(phase, lr, ignore_epoch, sel);
@@ -446,10 +452,13 @@ class Engine {
   }
   void train_step(int phase, float lr) {
     if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
+    if (phase == 2) h_valid_ = false;
+    else ensure_moments();
     enqueue_train(phase, lr);
   }
   void backward_only(int phase) {   // losses + gradients, no optimiser step
     if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
+    if (phase != 2) ensure_moments();
     enqueue_train_grads(phase);
     sync();
   }
@@ -490,7 +499,14 @@ class Engine {
   bool zx_train_ = true;                     // ... and training forward (DLAP_ZX_TRAIN)
   int zx_gx_ = 256;                          // their workgroups over all evaluation jobs (DLAP_ZX_GX)
   bool side_metrics_ = false;                // train Sharpe monitor on a graph side branch (DLAP_SIDE_METRICS)
-  bool train_first_ = false;                 // capture the training chain before the evaluation branch
+  bool train_first_ = true;                  // capture the training chain before the evaluation branch
+  // Moment cache: the moment net only changes in phase 2, so outside it the moments h of every
+  // split are constant (eval mode has no dropout; the train split's only if the moment tower has
+  // no dropout-carrying hidden layer). They are computed once (refresh_moments) when the moment
+  // parameters may have changed, and the phase-1/3 towers run the SDF tower only.
+  bool h_cache_ = true;                      // DLAP_H_CACHE
+  bool h_valid_ = false;                     // cached h matches the current moment parameters
+  bool cache_train_h() const { return h_cache_ && (md_.nl_m == 1 || md_.dropout == 0.f); }
   ModelDesc md_{};
   DevBuf<char> d_desc_;
   SplitDev splits_[3];
@@ -505,6 +521,8 @@ class Engine {
   DevBuf<char> j_rnn_train_, j_rnn_eval_, j_mlp_train_[4], j_mlp_eval_, j_mlp_bwd_[4], j_loss_train_[4],
       j_loss_eval_, j_fin_, j_upd_, j_epoch_[4];
   DevBuf<char> j_wide_train_[4], j_wide_eval_, j_wide_bwd_[4];   // wide path (k_wide.hip)
+  DevBuf<char> j_rnn_mom_, j_mlp_mom_, j_wide_mom_;             // moment refresh (every split)
+  int n_mom_jobs_ = 0, tmax_all_ = 0, gx_mom_ = 1;
   int n_eval_jobs_ = 0;
   int tmax_eval_ = 0, nmax_eval_ = 0;
 
@@ -687,7 +705,7 @@ class Engine {
       W.w.alloc((size_t)std::max(R, 1)); W.wn.alloc((size_t)T * N); W.h.alloc((size_t)T * N * K);
       W.P.alloc(T); W.port.alloc(T); W.sdf.alloc(T); W.mu.alloc(T);
       W.E.alloc((size_t)N * K); W.Eu.alloc(N); W.dE.alloc((size_t)N * K); W.dEu.alloc(N);
-      W.part.alloc(2 * ((N + 255) / 256));
+      W.part.alloc(2 * (((size_t)N * (K + 1) + 255) / 256));
       W.pe.alloc((size_t)DLAP_TCH * N * K); W.pu.alloc((size_t)DLAP_TCH * N);
       W.scal.alloc(SC_NSCAL);
       if (s == 0) W.scal_prev.alloc(SC_NSCAL);
@@ -844,8 +862,8 @@ class Engine {
       for (int s = 1; s < 3; ++s) {
         if (!splits_[s].set) continue;
         re.push_back(rnn_job(g, s, false));
-        me.push_back(mlp_job(g, s, false, true, true));
-        we.push_back(wide_job(g, s, true, true));
+        me.push_back(mlp_job(g, s, false, true, !h_cache_));
+        we.push_back(wide_job(g, s, true, !h_cache_));
         le.push_back(loss_job(g, s, 0));
         tmax_eval_ = std::max(tmax_eval_, splits_[s].T);
         nmax_eval_ = std::max(nmax_eval_, splits_[s].N);
@@ -871,18 +889,35 @@ class Engine {
     n_eval_jobs_ = (int)le.size();
     upload(j_rnn_train_, rt); upload(j_rnn_eval_, re); upload(j_mlp_eval_, me); upload(j_loss_eval_, le);
     upload(j_fin_, fj); upload(j_upd_, uj); upload(j_wide_eval_, we);
+    {   // moment refresh: eval-mode moment tower (and its per-period bias) of every split
+      std::vector<RnnJob> rm;
+      std::vector<MlpJob> mm;
+      std::vector<WideJob> wm;
+      tmax_all_ = 0; gx_mom_ = 1;
+      for (int g = 0; g < G_; ++g)
+        for (int s = 0; s < 3; ++s) {
+          if (!splits_[s].set) continue;
+          rm.push_back(rnn_job(g, s, false));
+          mm.push_back(mlp_job(g, s, false, false, true));
+          wm.push_back(wide_job(g, s, false, true));
+          tmax_all_ = std::max(tmax_all_, splits_[s].T);
+          gx_mom_ = std::max(gx_mom_, gx_fwd_[s]);
+        }
+      n_mom_jobs_ = (int)mm.size();
+      upload(j_rnn_mom_, rm); upload(j_mlp_mom_, mm); upload(j_wide_mom_, wm);
+    }
     for (int phase = 1; phase <= 3; ++phase) {
       std::vector<MlpJob> mt, mb;
       std::vector<LossJob> lt;
       std::vector<EpochJob> ej;
       std::vector<WideJob> wt, wb;
       for (int g = 0; g < G_; ++g) {
-        mt.push_back(mlp_job(g, 0, true, true, phase != 1));
+        mt.push_back(mlp_job(g, 0, true, true, phase == 2 || (phase == 3 && !cache_train_h())));
         mb.push_back(mlp_job(g, 0, true, true, true));
         mb.back().dz_out = reinterpret_cast<bf16x8*>(phase == 2 ? ws(g, 0).dzm.p : ws(g, 0).dzs.p);
         mt.back().z_out = reinterpret_cast<f32x4*>(ws(g, 0).z.p);
         mt.back().store_mz = phase == 2;
-        wt.push_back(wide_job(g, 0, true, phase != 1));
+        wt.push_back(wide_job(g, 0, true, phase == 2 || (phase == 3 && !cache_train_h())));
         wb.push_back(wide_job(g, 0, phase != 2, phase == 2));
         // the training forward stores the gate words its backward reuses
         if (phase == 2) {
@@ -926,6 +961,20 @@ class Engine {
   template <typename T>
   static const T* as(const DevBuf<char>& b) { return reinterpret_cast<const T*>(b.p); }
 
+  // Recompute the cached moments of every split (enqueued on st_, ahead of the epochs that
+  // read them) if the moment parameters may have changed since they were computed.
+  void ensure_moments() {
+    if (!h_cache_ || h_valid_ || n_mom_jobs_ == 0) return;
+    launch_prologue(as<RnnJob>(j_rnn_mom_), n_mom_jobs_, tmax_all_, dd(), md_, st_);
+    if (md_.md.wide && zx_eval_) {
+      launch_mlp_fwd_zx(as<MlpJob>(j_mlp_mom_), n_mom_jobs_, std::max(1, zx_gx_ / n_mom_jobs_), md_.md, md_.WMB, st_);
+    } else {
+      if (md_.md.wide) launch_proj0(as<WideJob>(j_wide_mom_), n_mom_jobs_, std::max({gx_proj_[0], gx_proj_[1], gx_proj_[2]}),
+                                    md_.md, md_.WMB, st_);
+      launch_mlp_fwd(as<MlpJob>(j_mlp_mom_), n_mom_jobs_, gx_mom_, md_.md, md_.KS1, md_.WMB, st_);
+    }
+    h_valid_ = true;
+  }
   bool dropmask_on(int phase) const { return md_.dropout > 0.f && phase != 2; }
   // keep masks of the step *drop_step + offset* (phases 1/3: the SDF tower's dropout)
   void enqueue_dropmask(int phase, int offset, hipStream_t st) {
@@ -954,7 +1003,7 @@ class Engine {
       launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, gx_fwd_[0], md_.md, md_.KS1, md_.WMB, st_);
     if (mark == 2) HIP_OK(hipEventRecord(ev_a_, st_));
     launch_period_fwd(as<LossJob>(j_loss_train_[phase]), G_, D.T, st_);
-    launch_asset(as<LossJob>(j_loss_train_[phase]), G_, D.N, st_);
+    launch_asset(as<LossJob>(j_loss_train_[phase]), G_, D.N, md_.K, st_);
     if (side) {
       HIP_OK(hipEventRecord(ev_mid_, st_));
       HIP_OK(hipStreamWaitEvent(side, ev_mid_, 0));
@@ -1005,7 +1054,7 @@ class Engine {
       launch_mlp_fwd(as<MlpJob>(j_mlp_eval_), n_eval_jobs_, gx, md_.md, md_.KS1, md_.WMB, st);
     }
     launch_period_fwd(as<LossJob>(j_loss_eval_), n_eval_jobs_, tmax_eval_, st);
-    launch_asset(as<LossJob>(j_loss_eval_), n_eval_jobs_, nmax_eval_, st);
+    launch_asset(as<LossJob>(j_loss_eval_), n_eval_jobs_, nmax_eval_, md_.K, st);
     launch_job_metrics(as<LossJob>(j_loss_eval_), n_eval_jobs_, st);
   }
   void enqueue_epoch_end(int phase, int ignore_epoch, float sel, hipStream_t st) {
@@ -1097,7 +1146,7 @@ class Engine {
     if (zx) launch_mlp_fwd_zx(as<MlpJob>(b), G_, std::max(1, zx_gx_ / G_), md_.md, md_.WMB, st_);
     else launch_mlp_fwd(as<MlpJob>(b), G_, gx_fwd_[s], md_.md, md_.KS1, md_.WMB, st_);
     launch_period_fwd(as<LossJob>(c), G_, D.T, st_);
-    launch_asset(as<LossJob>(c), G_, D.N, st_);
+    launch_asset(as<LossJob>(c), G_, D.N, md_.K, st_);
     launch_job_metrics(as<LossJob>(c), G_, st_);
     sync();
   }

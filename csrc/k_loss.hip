@@ -212,33 +212,40 @@ __global__ __launch_bounds__(256) void k_asset_part(const LossJob* __restrict__ 
   }
 }
 
-// Pass 2, grid (ceil(N/256), jobs): thread per stock; sums the chunks in order, writes
-// E, E_unc, dL/dE and the block's loss partial sums.
+// Pass 2, grid (ceil(N (K+1) / 256), jobs): one thread per output (stock i, moment k), the
+// last "moment" k = K being the unconditional E_unc; the DLAP_TCH chunk partials of an output are
+// all requested before they are summed (in chunk order), so the pass is one memory round trip.
+// Writes E, E_unc, dL/dE and the block's loss partial sums. Without moments (h == nullptr: the
+// unconditional training loss) only the E_unc outputs exist.
+DLAP_DEV int asset_red_blocks(const LossJob& J) { return (J.N * (J.h ? J.K + 1 : 1) + 255) >> 8; }
+
 __global__ __launch_bounds__(256) void k_asset_red(const LossJob* __restrict__ jobs) {
   const LossJob& J = jobs[blockIdx.y];
-  const int N = J.N, K = J.K;
-  if ((int)blockIdx.x * 256 >= N) return;
+  const int N = J.N, K = J.K, kk = J.h ? K + 1 : 1;
+  if ((int)blockIdx.x >= asset_red_blocks(J)) return;          // block-uniform
   __shared__ float red[4];
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  const bool ok = i < N;
+  const int o = blockIdx.x * 256 + threadIdx.x;
+  const bool ok = o < N * kk;
+  const int i = ok ? o / kk : 0, k = ok ? o - i * kk : 0;
+  const bool unc = k == kk - 1;
   float lc = 0.f, lu = 0.f;
   if (ok) {
-    const float invT = gp(J.invT)[i];
-    float u = 0.f;
-    for (int ch = 0; ch < DLAP_TCH; ++ch) u += gp(J.pu)[(size_t)ch * N + i];
-    u *= invT;
-    gp(J.Eu)[i] = u;
-    if (gp(J.dEu)) gp(J.dEu)[i] = J.coef_u * u;
-    lu = u * u;
-    if (gp(J.h)) {
-      for (int k = 0; k < K; ++k) {
-        float v = 0.f;
-        for (int ch = 0; ch < DLAP_TCH; ++ch) v += gp(J.pe)[((size_t)ch * N + i) * K + k];
-        v *= invT;
-        gp(J.E)[(size_t)i * K + k] = v;
-        if (gp(J.dE)) gp(J.dE)[(size_t)i * K + k] = J.coef_c * v;
-        lc += v * v;
-      }
+    float p[DLAP_TCH];
+#pragma unroll
+    for (int ch = 0; ch < DLAP_TCH; ++ch)
+      p[ch] = unc ? gp(J.pu)[(size_t)ch * N + i] : gp(J.pe)[((size_t)ch * N + i) * K + k];
+    float v = 0.f;
+#pragma unroll
+    for (int ch = 0; ch < DLAP_TCH; ++ch) v += p[ch];
+    v *= gp(J.invT)[i];
+    if (unc) {
+      gp(J.Eu)[i] = v;
+      if (gp(J.dEu)) gp(J.dEu)[i] = J.coef_u * v;
+      lu = v * v;
+    } else {
+      gp(J.E)[(size_t)i * K + k] = v;
+      if (gp(J.dE)) gp(J.dE)[(size_t)i * K + k] = J.coef_c * v;
+      lc = v * v;
     }
   }
   lc = block_sum<256>(lc, red);
@@ -253,7 +260,7 @@ __global__ __launch_bounds__(256) void k_asset_red(const LossJob* __restrict__ j
 // takes a strided share (all loads in flight at once, instead of 2 * nblk dependent round trips
 // on one thread), then the fixed-order block reduction.
 DLAP_DEV void final_losses(const LossJob& J, float& lc, float& lu, float* red) {
-  const int nblk = (J.N + 255) >> 8;
+  const int nblk = asset_red_blocks(J);
   float a = 0.f, b = 0.f;
   for (int k = threadIdx.x; k < nblk; k += 256) { a += gp(J.part)[2 * k]; b += gp(J.part)[2 * k + 1]; }
   a = block_sum<256>(a, red);
@@ -488,10 +495,10 @@ void launch_period_fwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st)
   hipLaunchKernelGGL(k_period_fwd, dim3(tmax, njobs), dim3(PER_NT), 0, st, jobs);
   HIP_OK(hipGetLastError());
 }
-void launch_asset(const LossJob* jobs, int njobs, int nmax, hipStream_t st) {
+void launch_asset(const LossJob* jobs, int njobs, int nmax, int kmax, hipStream_t st) {
   hipLaunchKernelGGL(k_asset_part, dim3((nmax + 63) / 64, DLAP_TCH, njobs), dim3(256), 0, st, jobs);
   HIP_OK(hipGetLastError());
-  hipLaunchKernelGGL(k_asset_red, dim3((nmax + 255) / 256, njobs), dim3(256), 0, st, jobs);
+  hipLaunchKernelGGL(k_asset_red, dim3((nmax * (kmax + 1) + 255) / 256, njobs), dim3(256), 0, st, jobs);
   HIP_OK(hipGetLastError());
 }
 void launch_period_bwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st) {

@@ -103,6 +103,7 @@ __global__ __launch_bounds__(64) void k_proj(const RnnJob* __restrict__ jobs,
 // Layout [t][6][H]: A = o (1 - tanh(c)^2), Bi = g i (1 - i), Bf = c_prev f (1 - f),
 // Bg = i (1 - g^2), Bo = tanh(c) o (1 - o), F = f.
 #define LSTM_NCOEF 6
+#define LSTM_GSEG 8        // max time segments of the k_lstm_bwd weight-gradient sums
 
 // ------------------------------------------------------------------------ k_lstm -------
 // STAGE: layer-0 input projections staged in LDS (T*4H <= 12288). The layer-0 and deeper
@@ -121,6 +122,27 @@ DLAP_DEV float bcast_dot(const float (&w)[HM], float v) {
 #pragma unroll
     for (int j = 0; j + w2 < HM; j += 2 * w2) p[j] += p[j + w2];
   return p[0];
+}
+
+// Same dot product with h_j taken from lane j of the lane's own 16-lane row by a DPP
+// row_newbcast operand (gfx90a+): no VALU -> SGPR -> VALU round trip through v_readlane on the
+// recurrence's critical path. Valid when every lane that uses the result sits in row 0 and the
+// source units are lanes 0..HM-1 (the gate-per-lane form with 4H <= 16).
+template <int J>
+DLAP_DEV float row_bcast(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + J, 0xF, 0xF, true));
+}
+template <int HM>
+DLAP_DEV float bcast_dot_row(const float (&w)[HM], float v) {
+  static_assert(HM >= 1 && HM <= 4, "row-broadcast dot: 1..4 units");
+  float p0 = w[0] * row_bcast<0>(v);
+  if constexpr (HM == 1) return p0;
+  float p1 = w[1] * row_bcast<1>(v);
+  if constexpr (HM == 2) return p0 + p1;
+  p0 = fmaf(w[2], row_bcast<2>(v), p0);
+  if constexpr (HM == 3) return p0 + p1;
+  p1 = fmaf(w[3], row_bcast<3>(v), p1);
+  return p0 + p1;
 }
 
 template <int HM, bool STAGE>
@@ -426,7 +448,8 @@ __global__ __launch_bounds__(64) void k_lstm_gls(const RnnJob* __restrict__ jobs
     // lanes H <= j < HM carry zero weights
     float h = 0.f, c = 0.f;
     auto cell = [&](int t, float pre) {
-      pre += bcast_dot<HM>(whh, h);
+      if constexpr (DPPG) pre += bcast_dot_row<HM>(whh, h);
+      else pre += bcast_dot<HM>(whh, h);
       const float y = kb * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(pre)) + kc;
       const float gf = gl_gather<HM, DPPG>(y, H, 1);
       const float gg = gl_gather<HM, DPPG>(y, 2 * H, 2);
@@ -702,30 +725,49 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
       const auto dg = gp(J.dg);
       for (int i = threadIdx.x; i < T * G4; i += 256) dg[i] = dgs[i];   // for k_wgrad
     }
-    // W_hh [4H][H] and the biases: thread per (gate, column)
+    // W_hh [4H][H] and the biases: (gate, column) outputs x S time segments over the 256
+    // threads (S = 3 at H = 4: 240 of them busy instead of 80), segment partials summed in
+    // segment order from LDS (fixed order: deterministic)
     const int in_dim = l == 0 ? M : H;
     const uint32_t key_below = l > 0 ? dropout_key(J.seed, step, 32 + (l - 1)) : 0u;
     const auto hb = gp(J.sh) + (size_t)(l > 0 ? l - 1 : 0) * T * H;
     const int ncol = H + 1 + (l > 0 ? H : 0);
-    for (int idx = threadIdx.x; idx < G4 * ncol; idx += 256) {
-      const int g = idx % G4, col = idx / G4;
+    const int nout = G4 * ncol;
+    const int S = max(1, min(LSTM_GSEG, 256 / max(nout, 1)));
+    float* gpart = dgs + T * G4 + 64;                 // [S][nout] (after the junk slots)
+    for (int idx0 = 0; idx0 < nout; idx0 += 256 / S) {
+      const int lt = (int)threadIdx.x % (256 / S), seg = (int)threadIdx.x / (256 / S);
+      const int idx = idx0 + lt;
       float acc = 0.f;
-      if (col < H) {
-        for (int t = 1; t < T; ++t) acc += dgs[t * G4 + g] * s_h[(t - 1) * H + col];
-        grads[md->lstm_w_hh[l] + g * H + col] = acc;
-      } else if (col == H) {
-        for (int t = 0; t < T; ++t) acc += dgs[t * G4 + g];
-        grads[md->lstm_b_ih[l] + g] = acc;
-        grads[md->lstm_b_hh[l] + g] = acc;
-      } else {
-        const int m = col - H - 1;     // W_ih of layer l > 0 (input = dropout(h_{l-1}))
-        for (int t = 0; t < T; ++t) {
-          float x = hb[(size_t)t * H + m];
-          if (drop) x = dropout_keep(key_below, (uint32_t)t, (uint32_t)m, thr) ? x * scale : 0.f;
-          acc += dgs[t * G4 + g] * x;
+      if (idx < nout && seg < S) {
+        const int g = idx % G4, col = idx / G4;
+        const int ta = (T * seg) / S, tb = (T * (seg + 1)) / S;
+        if (col < H) {
+#pragma unroll 4
+          for (int t = max(ta, 1); t < tb; ++t) acc += dgs[t * G4 + g] * s_h[(t - 1) * H + col];
+        } else if (col == H) {
+#pragma unroll 4
+          for (int t = ta; t < tb; ++t) acc += dgs[t * G4 + g];
+        } else {
+          const int m = col - H - 1;     // W_ih of layer l > 0 (input = dropout(h_{l-1}))
+          for (int t = ta; t < tb; ++t) {
+            float x = hb[(size_t)t * H + m];
+            if (drop) x = dropout_keep(key_below, (uint32_t)t, (uint32_t)m, thr) ? x * scale : 0.f;
+            acc += dgs[t * G4 + g] * x;
+          }
         }
-        grads[md->lstm_w_ih[l] + g * in_dim + m] = acc;
+        gpart[seg * nout + idx] = acc;
       }
+      __syncthreads();
+      if ((int)threadIdx.x < 256 / S && idx0 + (int)threadIdx.x < nout) {
+        const int o = idx0 + threadIdx.x, g = o % G4, col = o / G4;
+        float v = 0.f;
+        for (int q = 0; q < S; ++q) v += gpart[q * nout + o];
+        if (col < H) grads[md->lstm_w_hh[l] + g * H + col] = v;
+        else if (col == H) { grads[md->lstm_b_ih[l] + g] = v; grads[md->lstm_b_hh[l] + g] = v; }
+        else grads[md->lstm_w_ih[l] + g * in_dim + (col - H - 1)] = v;
+      }
+      __syncthreads();
     }
     if (l > 0) {
       const auto Wih = params + md->lstm_w_ih[l];
@@ -745,62 +787,73 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
 }
 
 // --------------------------------------------------------------------------- k_wgrad ---
-// out[g][col] = sum_t dG[t][g] * macro[t][col] (+ the bias column, x = 1) for the layer-0
-// LSTM input weights (phases 1/3, dG = gate gradients) or the moment layer-0 macro columns
-// (phase 2, dG = per-period sums of the pre-activation gradient). grid (ceil((M+1)/16), models):
-// 16 columns per block, 16 time groups; fixed-order LDS reduction over the time groups.
-template <int GM>
+// out[g][col] = sum_t dG[t][g] * x[t][col] (x = macro, or 1 for the bias column col = M) for the
+// layer-0 LSTM input weights (phases 1/3, dG = gate gradients) or the moment layer-0 macro
+// columns + bias (phase 2, dG = per-period sums of the pre-activation gradient).
+// fp32 MFMA (v_mfma_f32_16x16x4f32: exact fp32 products): C^T[col][g] = sum_t A[col][t] B[t][g],
+//   A lane l -> x[t = t0 + (l>>4)][col = c0 + (l&15)],  B lane l -> dG[t0 + (l>>4)][g0 + (l&15)],
+//   C lane l -> (col = c0 + 4(l>>4) + r, g = g0 + (l&15)).
+// grid (ceil((M+1)/16), models), 4 waves split the time axis, every operand of a wave's 16
+// k-steps is requested before the first MFMA; the 4 partial tiles are summed in LDS in wave order.
+template <int GT>
 __global__ __launch_bounds__(256) void k_wgrad(const UpdJob* __restrict__ jobs,
                                                const ModelDesc* __restrict__ md, int phase) {
-  __shared__ float red[16][16][GM + 1];
+  __shared__ f32x4 red[4][GT][64];
   const UpdJob& J = jobs[blockIdx.y];
   const int T = J.T, M = md->M;
   const bool mom = phase == 2;
   const int G = mom ? md->m[0].out : 4 * md->H;
   const int ldG = mom ? 64 : G;
   const auto dG = gp(mom ? J.dab : J.dg);
-  const int cl = threadIdx.x & 15, tg = threadIdx.x >> 4;
-  const int col = blockIdx.x * 16 + cl;
-  float acc[GM];
+  const auto X = gp(J.macro);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, n = lane & 15, kq = lane >> 4;
+  const int c0 = blockIdx.x * 16, col = c0 + n;
+  const int ta = (T * wave) / 4, tb = (T * (wave + 1)) / 4;
+  f32x4 acc[GT];
 #pragma unroll
-  for (int g = 0; g < GM; ++g) acc[g] = 0.f;
-  if (col <= M) {
-    // blocks of WG_TB time steps per thread: the macro value of every step is requested
-    // first; the gradient rows are then consumed straight from L2 (16-byte loads)
-    constexpr int WG_TB = 8;
-    for (int tb = tg; tb < T; tb += 16 * WG_TB) {
-      float xv[WG_TB];
+  for (int gt = 0; gt < GT; ++gt) acc[gt] = zero4();
+  constexpr int KC = 16;
+  for (int t0 = ta; t0 < tb; t0 += 4 * KC) {
+    float a[KC], b[KC][GT];
 #pragma unroll
-      for (int u = 0; u < WG_TB; ++u) {
-        const int t = min(tb + 16 * u, T - 1);
-        const float x = col < M ? gp(J.macro)[(size_t)t * M + (col < M ? col : 0)] : 1.f;
-        xv[u] = tb + 16 * u < T ? x : 0.f;
-      }
+    for (int s = 0; s < KC; ++s) {
+      const int t = t0 + 4 * s + kq;
+      const bool ok = t < tb;
+      const int tc = ok ? t : ta;
+      const float x = X[(size_t)tc * M + (col < M ? col : 0)];
+      a[s] = ok ? (col < M ? x : (col == M ? 1.f : 0.f)) : 0.f;
 #pragma unroll
-      for (int u = 0; u < WG_TB; ++u) {
-        const int t = min(tb + 16 * u, T - 1);
-        const auto dr = dG + (size_t)t * ldG;
-#pragma unroll
-        for (int g = 0; g < GM; ++g) acc[g] += dr[g] * xv[u];
+      for (int gt = 0; gt < GT; ++gt) {
+        const int g = gt * 16 + n;
+        const float v = dG[(size_t)tc * ldG + (g < G ? g : 0)];
+        b[s][gt] = ok && g < G ? v : 0.f;
       }
     }
+#pragma unroll
+    for (int s = 0; s < KC; ++s)
+#pragma unroll
+      for (int gt = 0; gt < GT; ++gt) acc[gt] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s][gt], acc[gt], 0, 0, 0);
   }
 #pragma unroll
-  for (int g = 0; g < GM; ++g) red[tg][cl][g] = acc[g];
+  for (int gt = 0; gt < GT; ++gt) red[wave][gt][lane] = acc[gt];
   __syncthreads();
-  // thread (cl, g-slice) sums the 16 time groups in order
-  for (int idx = threadIdx.x; idx < 16 * G; idx += 256) {
-    const int c = idx & 15, g = idx >> 4;
-    const int cc = blockIdx.x * 16 + c;
-    if (cc > M) continue;
-    float s = 0.f;
-    for (int q = 0; q < 16; ++q) s += red[q][c][g];
-    if (mom) {
-      const PackLayer& L0 = md->m[0];
-      if (cc < M) gp(J.grads)[L0.w_off + (size_t)g * L0.ld + cc] = s;
-      else gp(J.grads)[L0.b_off + g] = s;
-    } else if (cc < M) {
-      gp(J.grads)[md->lstm_w_ih[0] + (size_t)g * M + cc] = s;
+  if (wave != 0) return;
+#pragma unroll
+  for (int gt = 0; gt < GT; ++gt) {
+    const f32x4 v = red[0][gt][lane] + red[1][gt][lane] + red[2][gt][lane] + red[3][gt][lane];
+    const int g = gt * 16 + n;
+    if (g >= G) continue;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int cc = c0 + 4 * kq + r;
+      if (cc > M) continue;
+      if (mom) {
+        const PackLayer& L0 = md->m[0];
+        if (cc < M) gp(J.grads)[L0.w_off + (size_t)g * L0.ld + cc] = v[r];
+        else gp(J.grads)[L0.b_off + g] = v[r];
+      } else if (cc < M) {
+        gp(J.grads)[md->lstm_w_ih[0] + (size_t)g * M + cc] = v[r];
+      }
     }
   }
 }
@@ -808,7 +861,8 @@ __global__ __launch_bounds__(256) void k_wgrad(const UpdJob* __restrict__ jobs,
 void launch_lstm_bwd(const UpdJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
                      int T, int phase, hipStream_t st) {
   if (phase != 2 && mh.nrnn > 0) {
-    const size_t sh = ((size_t)T * (LSTM_NCOEF + 2 + 4) * mh.H + 64) * sizeof(float);   // coef, h, d, dgates, junk
+    // coef, h, d, dgates, junk, weight-gradient segment partials
+    const size_t sh = ((size_t)T * (LSTM_NCOEF + 2 + 4) * mh.H + 64 + 256 + 16 * mh.H * (2 * mh.H + 1)) * sizeof(float);
     if (sh > 160 * 1024) dlap_throw_hip(hipErrorInvalidValue, "lstm_bwd: T*H too large for LDS", __FILE__, __LINE__);
     if (mh.H <= 4) hipLaunchKernelGGL((k_lstm_bwd<4>), dim3(njobs), dim3(256), sh, st, jobs, md);
     else if (mh.H <= 8) hipLaunchKernelGGL((k_lstm_bwd<8>), dim3(njobs), dim3(256), sh, st, jobs, md);
@@ -820,9 +874,10 @@ void launch_lstm_bwd(const UpdJob* jobs, int njobs, const ModelDesc* md, const M
   if (phase != 2 && mh.nrnn == 0) return;
   const int G = phase == 2 ? mh.m[0].out : 4 * mh.H;
   dim3 grid((mh.M + 1 + 15) / 16, njobs);
-  if (G <= 16) hipLaunchKernelGGL((k_wgrad<16>), grid, dim3(256), 0, st, jobs, md, phase);
-  else if (G <= 32) hipLaunchKernelGGL((k_wgrad<32>), grid, dim3(256), 0, st, jobs, md, phase);
-  else hipLaunchKernelGGL((k_wgrad<64>), grid, dim3(256), 0, st, jobs, md, phase);
+  if (G <= 16) hipLaunchKernelGGL((k_wgrad<1>), grid, dim3(256), 0, st, jobs, md, phase);
+  else if (G <= 32) hipLaunchKernelGGL((k_wgrad<2>), grid, dim3(256), 0, st, jobs, md, phase);
+  else if (G <= 64) hipLaunchKernelGGL((k_wgrad<4>), grid, dim3(256), 0, st, jobs, md, phase);
+  else hipLaunchKernelGGL((k_wgrad<8>), grid, dim3(256), 0, st, jobs, md, phase);
   HIP_OK(hipGetLastError());
 }
 

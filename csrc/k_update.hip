@@ -272,12 +272,20 @@ __global__ __launch_bounds__(256) void k_adam(const UpdJob* __restrict__ jobs,
   ss = block_sum<256>(ss, red);
   const float norm = sqrtf(ss);
   const float coef = fminf(1.f / (norm + 1e-6f), 1.f);
-  const int step = gp(J.adam_step)[mom ? 1 : 0] + 1;
-  const double bc1 = 1.0 - pow(0.9, (double)step);
-  const double bc2 = 1.0 - pow(0.999, (double)step);
-  const float lr_g = J.lr > 0.f ? J.lr : lr;
-  const float step_size = (float)(lr_g / bc1);
-  const float bc2s = (float)sqrt(bc2);
+  // bias corrections in double like torch's Python-float scalars; one thread evaluates the
+  // (slow) double pow and shares the two fp32 scalars through LDS
+  __shared__ float sc2[2];
+  if (threadIdx.x == 0) {
+    const int step = gp(J.adam_step)[mom ? 1 : 0] + 1;
+    const double bc1 = 1.0 - pow(0.9, (double)step);
+    const double bc2 = 1.0 - pow(0.999, (double)step);
+    const float lr_g = J.lr > 0.f ? J.lr : lr;
+    sc2[0] = (float)(lr_g / bc1);
+    sc2[1] = (float)sqrt(bc2);
+  }
+  __syncthreads();
+  const float step_size = sc2[0];
+  const float bc2s = sc2[1];
   const int i = p0 + blockIdx.x * ADAM_PB;
   float* __restrict__ pm = gp(J.m);
   float* __restrict__ pv = gp(J.v);

@@ -43,7 +43,7 @@ struct LossJob {
   float* Eu;             // [N]
   float* dE;             // [N*K] (nullptr: skip)
   float* dEu;            // [N]   (nullptr: skip)
-  float* part;           // [2 * ceil(N/256)] partial loss sums
+  float* part;           // [2 * ceil(N (K+1) / 256)] partial loss sums
   float* pe;             // [DLAP_TCH][N][K] chunk partials of E
   float* pu;             // [DLAP_TCH][N] chunk partials of E_unc
   float* dw;             // [R] dL/dw_raw (compact rows)
@@ -52,7 +52,8 @@ struct LossJob {
 };
 
 void launch_period_fwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st);
-void launch_asset(const LossJob* jobs, int njobs, int nmax, hipStream_t st);
+// kmax: the moment count K of the jobs (sizes the output grid of the reduction pass)
+void launch_asset(const LossJob* jobs, int njobs, int nmax, int kmax, hipStream_t st);
 void launch_period_bwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st);
 void launch_job_metrics(const LossJob* jobs, int njobs, hipStream_t st);
 std::vector<long long> loss_timestamps();
