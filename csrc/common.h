@@ -80,6 +80,42 @@ DLAP_DEV bf16x8 zero8() {
   return r;
 }
 
+// ---- tower precision policies ------------------------------------------------------------
+// The tower kernels are written once over an operand "fragment" of 8 k-values per lane (the
+// 16x16x32 MFMA operand map above) and instantiated for two precisions:
+//   PrecBF16  production: bf16 operands, one v_mfma_f32_16x16x32_bf16 per fragment pair;
+//   PrecF32   reference precision (`--precision fp32`): fp32 operands, the same 32-deep product
+//             as eight v_mfma_f32_16x16x4_f32 (exact fp32 products, fp32 accumulation). MFMA j
+//             takes element j of every lane's fragment, i.e. k = 8q + j for lane group q, so
+//             the eight of them together cover k = 0..31 once: the same operand layouts, panel
+//             rows, weight blob and selector tricks work unchanged, at 2x the register / LDS /
+//             HBM bytes per fragment.
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+
+struct PrecBF16 {
+  using Frag = bf16x8;
+  static constexpr bool kF32 = false;
+  DLAP_DEV static f32x4 mma(const Frag& a, const Frag& b, const f32x4& c) { return mfma16(a, b, c); }
+  DLAP_DEV static Frag pack(const f32x4& lo, const f32x4& hi) { return pack8(lo, hi); }
+  DLAP_DEV static Frag zero() { return zero8(); }
+  DLAP_DEV static void set(Frag& f, int j, float v) { f[j] = (__bf16)v; }
+};
+
+struct PrecF32 {
+  using Frag = f32x8;
+  static constexpr bool kF32 = true;
+  DLAP_DEV static f32x4 mma(const Frag& a, const Frag& b, f32x4 c) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[j], b[j], c, 0, 0, 0);
+    return c;
+  }
+  DLAP_DEV static Frag pack(const f32x4& lo, const f32x4& hi) {
+    return Frag{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  }
+  DLAP_DEV static Frag zero() { return Frag{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}; }
+  DLAP_DEV static void set(Frag& f, int j, float v) { f[j] = v; }
+};
+
 // ---- counter-based RNG for dropout (murmur3 finaliser on a mixed counter) -------------
 DLAP_DEV uint32_t fmix32(uint32_t h) {
   h ^= h >> 16; h *= 0x85ebca6bu; h ^= h >> 13; h *= 0xc2b2ae35u; h ^= h >> 16;

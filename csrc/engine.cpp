@@ -113,7 +113,7 @@ class Engine {
  public:
   Engine(int F, int M, int nrnn, int H, bool raw_macro_sdf, std::vector<int> hidden,
          std::vector<int> mom_hidden, int K, float dropout, bool normalize_w, bool weighted,
-         float residual, int G, int max_epochs)
+         float residual, int G, int max_epochs, bool fp32)
       : G_(G), max_epochs_(max_epochs) {
     unroll_ = std::max(1, env_int("DLAP_UNROLL", 1));
     prio_ = env_int("DLAP_PRIO", 0) != 0;
@@ -130,7 +130,7 @@ class Engine {
     HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_mid_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_a_, hipEventDisableTiming));
-    eval_gx_ = env_int("DLAP_EVAL_GX", 0);
+    eval_gx_ = env_int("DLAP_EVAL_GX", 512);
     b_wait_ = env_int("DLAP_B_WAIT", 0);
     side_metrics_ = env_int("DLAP_SIDE_METRICS", 0) != 0;
     zx_eval_ = env_int("DLAP_ZX_EVAL", 1) != 0;
@@ -139,7 +139,7 @@ class Engine {
     train_first_ = env_int("DLAP_TRAIN_FIRST", 1) != 0;
     h_cache_ = env_int("DLAP_H_CACHE", 1) != 0;
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
-               residual);
+               residual, fp32);
     d_desc_.alloc(sizeof(ModelDesc));
     HIP_LEGACY(hipMemcpy(d_desc_.p, &md_, sizeof(ModelDesc), hipMemcpyHostToDevice));
     models_.resize(G);
@@ -150,7 +150,7 @@ class Engine {
       S.gnorm.alloc(1); S.best.alloc(3); S.aux.alloc(md_.md.aux_floats);
       S.hist.alloc((size_t)max_epochs_ * HIST_W);
       S.adam_step.alloc(2); S.drop_step.alloc(1); S.snap_flags.alloc(2); S.ep.alloc(2);
-      S.blob.alloc((size_t)md_.md.blob_frags * 512);
+      S.blob.alloc((size_t)md_.md.blob_frags * 512 * xw());       // bf16 (or fp32: 2 u16 each)
       S.blob0.alloc((size_t)std::max(1, md_.md.b0_frags) * 512);
       S.wproj.alloc((size_t)(md_.proj_mp + 1) * md_.proj_np);
     }
@@ -175,7 +175,7 @@ class Engine {
     d["P"] = md_.P; d["P_sdf"] = md_.P_sdf; d["KP"] = md_.KP; d["KS1"] = md_.KS1; d["WMB"] = md_.WMB;
     d["Dm"] = md_.Dm; d["blob_frags"] = md_.md.blob_frags; d["aux_floats"] = md_.md.aux_floats;
     d["ntile_s"] = md_.ntile_s; d["tps_s"] = md_.tps_s; d["ntile_m"] = md_.ntile_m; d["G"] = G_;
-    d["wide"] = md_.md.wide; d["KX"] = md_.md.KX; d["nsplit"] = nsplit_;
+    d["wide"] = md_.md.wide; d["KX"] = md_.md.KX; d["nsplit"] = nsplit_; d["fp32"] = md_.md.fp32;
     return d;
   }
 
@@ -185,7 +185,8 @@ class Engine {
                  py::array_t<float, py::array::c_style> mask, py::array_t<float, py::array::c_style> macro,
                  int T, int N) {
     const long R = (long)rowti.size() / 2;
-    if ((long)X.size() != R * md_.KP) throw std::invalid_argument("X must be [R][KP] bf16 bits");
+    if ((long)X.size() != R * md_.KP * xw())
+      throw std::invalid_argument(md_.md.fp32 ? "X must be [R][KP] fp32 (as 2 x uint16)" : "X must be [R][KP] bf16 bits");
     set_split_impl(s, X.data(), false, rowti, row_ptr, Rm, mask, macro, T, N);
   }
   // Same, with the compacted panel X already in device memory (x_ptr: R * KP bf16 values, e.g.
@@ -195,7 +196,7 @@ class Engine {
                      py::array_t<float, py::array::c_style> mask, py::array_t<float, py::array::c_style> macro,
                      int T, int N) {
     const long R = (long)rowti.size() / 2;
-    if (x_elems != R * md_.KP) throw std::invalid_argument("X must be [R][KP] bf16 values");
+    if (x_elems != R * md_.KP * xw()) throw std::invalid_argument("X must be [R][KP] bf16 (fp32: 2x) elements");
     set_split_impl(s, reinterpret_cast<const uint16_t*>(x_ptr), true, rowti, row_ptr, Rm, mask, macro, T, N);
   }
   void set_split_impl(int s, const uint16_t* Xp, bool x_on_device, py::array_t<int, py::array::c_style> rowti,
@@ -211,7 +212,7 @@ class Engine {
     if ((int)row_ptr.size() != T + 1) throw std::invalid_argument("row_ptr must be [T+1]");
     if (md_.M > 0 && (long)macro.size() != (long)T * md_.M) throw std::invalid_argument("macro must be [T][M]");
     D.T = T; D.N = N; D.R = R;
-    const size_t nx = (size_t)R * md_.KP;
+    const size_t nx = (size_t)R * md_.KP * xw();
     if (x_on_device) {
       D.X.alloc(nx, false);
       if (nx) HIP_LEGACY(hipMemcpy(D.X.p, Xp, nx * sizeof(uint16_t), hipMemcpyDeviceToDevice));
@@ -514,6 +515,7 @@ class Engine {
   std::vector<ModelSplitWS> ws_;
   DevBuf<float> slab_;
   int gx_bwd_ = 1, gx_fwd_[3] = {1, 1, 1};
+  int gx_fwd13_ = 1;                         // training forward grid of phases 1 / 3
   int nsplit_ = 1, gx_proj_[3] = {1, 1, 1};  // wide path: wgrad row splits, proj grid per split
   bool graphs_dirty_ = true;
   std::map<std::string, hipGraphExec_t> graphs_;
@@ -532,6 +534,8 @@ class Engine {
     return b;
   }
   bool pipeline_ = true;
+  // uint16 elements per panel / blob value: 1 (bf16) or 2 (fp32 reference-precision towers)
+  long xw() const { return md_.md.fp32 ? 2 : 1; }
   int check_g(int g) const {
     if (g < 0 || g >= G_) throw std::out_of_range("model index");
     return g;
@@ -573,7 +577,7 @@ class Engine {
   // ------------------------------------------------------------ model descriptor ------
   void build_desc(int F, int M, int nrnn, int H, bool raw_macro_sdf, const std::vector<int>& hs,
                   const std::vector<int>& hm, int K, float dropout, bool normalize_w, bool weighted,
-                  float residual) {
+                  float residual, bool fp32) {
     ModelDesc& d = md_;
     std::memset(&d, 0, sizeof d);
     if (hs.empty() || (int)hs.size() > 4) throw std::invalid_argument("native engine supports 1..4 SDF hidden layers");
@@ -650,6 +654,11 @@ class Engine {
     D.KSX = D.KX / 32;
     D.zc = 8 + 2 * d.WMB;
     D.b0_frags = wide ? (4 + d.WMB) * D.KSX : 0;
+    D.fp32 = fp32 ? 1 : 0;
+    if (fp32 && wide)
+      throw std::invalid_argument("precision fp32: the wide layer-0 path (F + per-period inputs > 128) is bf16 only");
+    if (fp32 && (size_t)D.blob_frags * 2048 + (size_t)D.aux_floats * 4 > 150 * 1024)
+      throw std::invalid_argument("precision fp32: this architecture's fp32 weight fragments exceed the LDS budget");
     if ((size_t)D.b0_frags * 1024 > 160 * 1024)
       throw std::invalid_argument("feature dim too large for the wide layer-0 kernel (LDS budget)");
     // gradient tiles: layer-0 chunks first (none on the wide path: k_wgrad0), then one tile per
@@ -734,7 +743,13 @@ class Engine {
       const int nsl = std::max(md_.nslice_s, md_.nslice_m);
       slab_.alloc((size_t)G_ * nsl * gx_bwd_ * slab_stride());
     }
+    // tower-forward grids (measured, 600x3000x46 epoch graph): the phase-1/3 training forward
+    // runs SDF-only (moments cached) beside the evaluation branch and is fastest with one
+    // workgroup per CU (256); phase 2 (moment tower, no evaluation branch) with 1024
     gx_fwd_[s] = std::max(1, std::min(((R + 31) / 32 + 3) / 4, env_int("DLAP_GX_FWD", 1024)));
+    if (s == 0) {
+      gx_fwd13_ = std::max(1, std::min(((R + 31) / 32 + 3) / 4, env_int("DLAP_GX_FWD13", 256)));
+    }
     if (md_.md.wide) {
       const size_t ntl = (size_t)(R + 31) / 32;
       for (int g = 0; g < G_; ++g) {
@@ -1000,7 +1015,8 @@ class Engine {
     if (zx_train)      // layer 0 streamed inside the training towers, z stored for the backward
       launch_mlp_fwd_zx(as<MlpJob>(j_mlp_train_[phase]), G_, std::max(1, zx_gx_ / G_), md_.md, md_.WMB, st_, true);
     else
-      launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, gx_fwd_[0], md_.md, md_.KS1, md_.WMB, st_);
+      launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, phase == 2 ? gx_fwd_[0] : gx_fwd13_, md_.md, md_.KS1,
+                     md_.WMB, st_);
     if (mark == 2) HIP_OK(hipEventRecord(ev_a_, st_));
     launch_period_fwd(as<LossJob>(j_loss_train_[phase]), G_, D.T, st_);
     launch_asset(as<LossJob>(j_loss_train_[phase]), G_, D.N, md_.K, st_);
@@ -1156,11 +1172,11 @@ PYBIND11_MODULE(_dlap_hip, m) {
   m.doc() = "DLAP MI355X native engine (HIP kernels for gfx950 + hipGraph epoch executor)";
   py::class_<Engine>(m, "Engine")
       .def(py::init<int, int, int, int, bool, std::vector<int>, std::vector<int>, int, float, bool, bool,
-                    float, int, int>(),
+                    float, int, int, bool>(),
            py::arg("F"), py::arg("M"), py::arg("nrnn"), py::arg("H"), py::arg("raw_macro_sdf"),
            py::arg("hidden"), py::arg("mom_hidden"), py::arg("K"), py::arg("dropout"),
            py::arg("normalize_w"), py::arg("weighted"), py::arg("residual"), py::arg("G"),
-           py::arg("max_epochs"))
+           py::arg("max_epochs"), py::arg("fp32") = false)
       .def("describe", &Engine::describe)
       .def("set_split", &Engine::set_split)
       .def("set_split_dev", &Engine::set_split_dev)

@@ -46,27 +46,36 @@ __device__ long long g_mlp_ts[8];
 #define MLP_TS(slot) do { \
     if ((threadIdx.x & 255) == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1) && J.gbits) \
       g_mlp_ts[(blockIdx.x == 0 ? 0 : 4) + (slot)] = wall_clock64(); } while (0)
-DLAP_DEV bf16x8 ldsf(const bf16x8* lds, int frag) { return lds[frag * 64 + lane_id()]; }
+template <typename F>
+DLAP_DEV F ldsf(const F* lds, int frag) { return lds[frag * 64 + lane_id()]; }
 DLAP_DEV int perm_unit(int q, int j) { return j < 4 ? 4 * q + j : 16 + 4 * q + (j - 4); }
 
 // 0/1 selectors (constant per lane) that transpose a packed T fragment (permuted k) or a
 // natural-k X fragment into N layout, and a one-hot column selector for bias sums.
-DLAP_DEV bf16x8 make_sel(bool permuted, int c) {
+template <class P>
+DLAP_DEV typename P::Frag make_sel(bool permuted, int c) {
   const int l = lane_id(), q = l >> 4, n = l & 15;
-  bf16x8 s;
+  typename P::Frag s = P::zero();
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     int k = permuted ? perm_unit(q, j) : 8 * q + j;
-    s[j] = (__bf16)((k == 16 * c + n) ? 1.f : 0.f);
+    P::set(s, j, (k == 16 * c + n) ? 1.f : 0.f);
   }
   return s;
 }
-DLAP_DEV bf16x8 make_onehot(int col) {
+template <class P>
+DLAP_DEV typename P::Frag make_onehot(int col) {
   const bool on = (lane_id() & 15) == col;
-  bf16x8 s;
+  typename P::Frag s = P::zero();
 #pragma unroll
-  for (int j = 0; j < 8; ++j) s[j] = (__bf16)(on ? 1.f : 0.f);
+  for (int j = 0; j < 8; ++j) P::set(s, j, on ? 1.f : 0.f);
   return s;
+}
+
+// The compacted panel rows as fragments of the precision's operand type (bf16 or fp32 rows).
+template <class P>
+DLAP_DEV const DLAP_GLOBAL typename P::Frag* xrows(const MlpJob& J) {
+  return gp(reinterpret_cast<const typename P::Frag*>(J.X));
 }
 
 struct RowInfo {
@@ -145,21 +154,21 @@ DLAP_DEV void zin_sdf0(const f32x4 (&zs)[2][4], const RowInfo& ri, PP pp, const 
 
 // Per-tile data that does not depend on other loads: issued one tile ahead (software
 // prefetch) so the HBM latency hides behind the current tile's MFMA/VALU work.
-template <int KS1>
+template <class P, int KS1>
 struct TileIn {
   int2 ti[2];
-  bf16x8 x[2][KS1];
+  typename P::Frag x[2][KS1];
   float dw[2];
 };
 
-template <int KS1, bool DW>
-DLAP_DEV void issue_tile(const MlpJob& J, int tile, TileIn<KS1>& in) {
+template <class P, int KS1, bool DW>
+DLAP_DEV void issue_tile(const MlpJob& J, int tile, TileIn<P, KS1>& in) {
   const int l = lane_id(), q = l >> 4;
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
     const int r = min(tile * 32 + 16 * b + (l & 15), J.R - 1);   // clamp: no divergent loads
     in.ti[b] = gp(J.rowti)[r];
-    const auto row = gp(J.X) + (size_t)r * (4 * KS1);
+    const auto row = xrows<P>(J) + (size_t)r * (4 * KS1);
 #pragma unroll
     for (int s = 0; s < KS1; ++s) in.x[b][s] = row[4 * s + q];
     if (DW) in.dw[b] = gp(J.dw)[r];
@@ -168,9 +177,9 @@ DLAP_DEV void issue_tile(const MlpJob& J, int tile, TileIn<KS1>& in) {
 
 // Finish a prefetched tile: row info, zero rows beyond R, insert the per-period columns
 // (INS; from the LDS copy staged with the weights when it fits, else from global memory).
-template <int KS1, bool INS = true>
-DLAP_DEV RowInfo finish_tile(const MlpJob& J, const MlpDims& D, int tile, TileIn<KS1>& in,
-                             bf16x8 (&xf)[2][KS1], const float* spp = nullptr) {
+template <class P, int KS1, bool INS = true>
+DLAP_DEV RowInfo finish_tile(const MlpJob& J, const MlpDims& D, int tile, TileIn<P, KS1>& in,
+                             typename P::Frag (&xf)[2][KS1], const float* spp = nullptr) {
   RowInfo ri;
   const int l = lane_id(), q = l >> 4;
   const int s_lo = D.F >> 5, s_hi = (D.F + D.Dm - 1) >> 5;
@@ -183,7 +192,7 @@ DLAP_DEV RowInfo finish_tile(const MlpJob& J, const MlpDims& D, int tile, TileIn
     DLAP_ASSERT(J.R > 0 && (unsigned)ri.t[b] < (unsigned)J.T && (unsigned)ri.i[b] < (unsigned)J.N);
     ri.dense[b] = ok ? in.ti[b].x * J.N + in.ti[b].y : -1;
 #pragma unroll
-    for (int s = 0; s < KS1; ++s) xf[b][s] = ok ? in.x[b][s] : zero8();
+    for (int s = 0; s < KS1; ++s) xf[b][s] = ok ? in.x[b][s] : P::zero();
     if (INS && D.Dm > 0) {
       auto insert = [&](auto pp) {
 #pragma unroll
@@ -194,7 +203,7 @@ DLAP_DEV RowInfo finish_tile(const MlpJob& J, const MlpDims& D, int tile, TileIn
               const int col = 32 * s + 8 * q + j - D.F;
               const bool in_rng = (unsigned)col < (unsigned)D.Dm;
               const float v = pp[min(max(col, 0), D.Dm - 1)];
-              if (in_rng && ok) xf[b][s][j] = (__bf16)v;
+              if (in_rng && ok) P::set(xf[b][s], j, v);
             }
           }
         }
@@ -208,57 +217,59 @@ DLAP_DEV RowInfo finish_tile(const MlpJob& J, const MlpDims& D, int tile, TileIn
 }
 
 // acc[b][u] = W0 . X^T  (UB output blocks)
-template <int KS1, int UB>
-DLAP_DEV void layer0(const bf16x8* lds, int off, const bf16x8 (&xf)[2][KS1], f32x4 (&acc)[2][UB]) {
+template <class P, int KS1, int UB>
+DLAP_DEV void layer0(const typename P::Frag* lds, int off, const typename P::Frag (&xf)[2][KS1],
+                     f32x4 (&acc)[2][UB]) {
 #pragma unroll
   for (int u = 0; u < UB; ++u) {
     f32x4 c0 = zero4(), c1 = zero4();
 #pragma unroll
     for (int s = 0; s < KS1; ++s) {
-      bf16x8 w = ldsf(lds, off + u * KS1 + s);
-      c0 = mfma16(w, xf[0][s], c0);
-      c1 = mfma16(w, xf[1][s], c1);
+      const typename P::Frag w = ldsf(lds, off + u * KS1 + s);
+      c0 = P::mma(w, xf[0][s], c0);
+      c1 = P::mma(w, xf[1][s], c1);
     }
     acc[0][u] = c0; acc[1][u] = c1;
   }
 }
 
 // acc = W . prev^T, prev as KS packed fragments per row block, UB output blocks.
-template <int UB, int KS>
-DLAP_DEV void layer_chain(const bf16x8* lds, int off, const bf16x8 (&pf)[2][KS], f32x4 (&acc)[2][UB]) {
+template <class P, int UB, int KS>
+DLAP_DEV void layer_chain(const typename P::Frag* lds, int off, const typename P::Frag (&pf)[2][KS],
+                          f32x4 (&acc)[2][UB]) {
 #pragma unroll
   for (int u = 0; u < UB; ++u) {
     f32x4 c0 = zero4(), c1 = zero4();
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
-      bf16x8 w = ldsf(lds, off + u * KS + s);
-      c0 = mfma16(w, pf[0][s], c0);
-      c1 = mfma16(w, pf[1][s], c1);
+      const typename P::Frag w = ldsf(lds, off + u * KS + s);
+      c0 = P::mma(w, pf[0][s], c0);
+      c1 = P::mma(w, pf[1][s], c1);
     }
     acc[0][u] = c0; acc[1][u] = c1;
   }
 }
 
-template <int UB>
-DLAP_DEV void pack_blocks(const f32x4 (&a)[2][UB], bf16x8 (&pf)[2][(UB + 1) / 2]) {
+template <class P, int UB>
+DLAP_DEV void pack_blocks(const f32x4 (&a)[2][UB], typename P::Frag (&pf)[2][(UB + 1) / 2]) {
 #pragma unroll
   for (int b = 0; b < 2; ++b)
 #pragma unroll
     for (int s = 0; s < (UB + 1) / 2; ++s)
-      pf[b][s] = pack8(a[b][2 * s], (2 * s + 1 < UB) ? a[b][2 * s + 1] : zero4());
+      pf[b][s] = P::pack(a[b][2 * s], (2 * s + 1 < UB) ? a[b][2 * s + 1] : zero4());
 }
 
 // Natural-k fragment of the per-period SDF inputs of k-step s for a row of period t (lane:
 // columns 32 s + 8 q + j of pp[t], zero beyond Dm), bf16 as the fused path inserts them: the
 // wide path's operand for the W0[:, F:F+Dm] weight-gradient tile (transposed by x_rows_k).
-template <typename PP>
-DLAP_DEV bf16x8 pp_xfrag(PP pp, int t, int s, const MlpDims& D) {
+template <class P, typename PP>
+DLAP_DEV typename P::Frag pp_xfrag(PP pp, int t, int s, const MlpDims& D) {
   const int q = lane_id() >> 4;
-  bf16x8 f;
+  typename P::Frag f = P::zero();
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int col = 32 * s + 8 * q + j;
-    f[j] = (__bf16)(col < D.Dm ? pp[t * D.Dm + col] : 0.f);
+    P::set(f, j, col < D.Dm ? pp[t * D.Dm + col] : 0.f);
   }
   return f;
 }
@@ -395,15 +406,25 @@ DLAP_DEV DropCtx drop_ctx(const MlpJob& J, const MlpDims& D) {
   return dc;
 }
 
-// LDS image of the tower kernels: blob fragments, aux floats, per-period inputs.
+// LDS image of the tower kernels: blob fragments (1 KiB bf16 / 2 KiB fp32 each), aux floats,
+// per-period inputs.
+__host__ __device__ inline size_t blob_bytes_of(const MlpDims& D) {
+  return (size_t)D.blob_frags * (D.fp32 ? 2048 : 1024);
+}
 __host__ __device__ inline size_t lds_bytes_of(const MlpDims& D) {
-  return (size_t)D.blob_frags * 1024 + (size_t)((D.aux_floats + 3) & ~3) * 4 + (size_t)D.pp_lds_floats * 4;
+  return blob_bytes_of(D) + (size_t)((D.aux_floats + 3) & ~3) * 4 + (size_t)D.pp_lds_floats * 4;
+}
+DLAP_DEV float* aux_lds_ptr(char* smem, const MlpDims& D) {
+  return reinterpret_cast<float*>(smem + blob_bytes_of(D));
 }
 DLAP_DEV float* pp_lds_ptr(char* smem, const MlpDims& D) {
-  return reinterpret_cast<float*>(smem + (size_t)D.blob_frags * 1024 + (size_t)((D.aux_floats + 3) & ~3) * 4);
+  return reinterpret_cast<float*>(smem + blob_bytes_of(D) + (size_t)((D.aux_floats + 3) & ~3) * 4);
 }
-DLAP_DEV void stage_weights(const MlpJob& J, const MlpDims& D, bf16x8* lds, float* aux, float* spp = nullptr) {
-  for (int i = threadIdx.x; i < D.blob_frags * 64; i += blockDim.x) lds[i] = gp(J.blob)[i];
+template <class P>
+DLAP_DEV void stage_weights(const MlpJob& J, const MlpDims& D, typename P::Frag* lds, float* aux,
+                            float* spp = nullptr) {
+  const auto blob = gp(reinterpret_cast<const typename P::Frag*>(J.blob));
+  for (int i = threadIdx.x; i < D.blob_frags * 64; i += blockDim.x) lds[i] = blob[i];
   for (int i = threadIdx.x; i < D.aux_floats; i += blockDim.x) aux[i] = gp(J.aux)[i];
   if (spp && D.pp_lds_floats > 0 && D.Dm > 0)
     for (int i = threadIdx.x; i < J.T * D.Dm; i += blockDim.x) spp[i] = gp(J.pp)[i];
@@ -414,12 +435,12 @@ DLAP_DEV void stage_weights(const MlpJob& J, const MlpDims& D, bf16x8* lds, floa
 // gout: gate words of the tile (train). With keep words (kw, pre-generated by k_dropmask) the
 // dropout decisions are read instead of hashed; the gates overwrite the keep words in place.
 // layer0_fn(a) fills the layer-0 accumulators (fused: MFMA over the X tile; wide: from z).
-template <typename L0>
-DLAP_DEV void sdf_forward_tile(const bf16x8* lds, const float* aux, const MlpDims& D,
+template <class P, typename L0>
+DLAP_DEV void sdf_forward_tile(const typename P::Frag* lds, const float* aux, const MlpDims& D,
                                const DropCtx& dc, const RowInfo& ri, L0&& layer0_fn,
                                DLAP_GLOBAL uint32_t* gout, const uint32_t* kw, float (&w)[2]) {
   f32x4 a[2][4];
-  bf16x8 pf[2][2];
+  typename P::Frag pf[2][2];
   uint32_t gate[2];
   layer0_fn(a);
   if (kw) relu_keep<4>(a, aux + D.a_sb, dc.scale, kw[0], gate);
@@ -429,8 +450,8 @@ DLAP_DEV void sdf_forward_tile(const bf16x8* lds, const float* aux, const MlpDim
 #pragma unroll
   for (int j = 1; j < 4; ++j) {
     if (j >= D.nl_sdf) break;
-    pack_blocks<4>(a, pf);
-    layer_chain<4, 2>(lds, D.s_fwd + (j - 1) * 8, pf, a);
+    pack_blocks<P, 4>(a, pf);
+    layer_chain<P, 4, 2>(lds, D.s_fwd + (j - 1) * 8, pf, a);
     if (kw) relu_keep<4>(a, aux + D.a_sb + 64 * j, dc.scale, kw[j], gate);
     else relu_dropout<4>(a, aux + D.a_sb + 64 * j, aux + D.a_sb + 64 * j, dc, j, ri, gate);
     if (gout) gout[64 * j] = gate_word(gate);
@@ -452,14 +473,14 @@ DLAP_DEV void sdf_forward_tile(const bf16x8* lds, const float* aux, const MlpDim
 }
 
 // Moment tower forward on one tile: writes the K tanh outputs of every valid row.
-template <int WMB, typename L0>
-DLAP_DEV void mom_forward_tile(const bf16x8* lds, const float* aux, const MlpDims& D,
+template <class P, int WMB, typename L0>
+DLAP_DEV void mom_forward_tile(const typename P::Frag* lds, const float* aux, const MlpDims& D,
                                const MlpJob& J, const DropCtx& dc, const RowInfo& ri,
                                L0&& layer0_fn, DLAP_GLOBAL uint32_t* gout,
                                const AbPre<WMB>& ab) {
   constexpr int KSM = (WMB + 1) / 2;
   f32x4 a[2][WMB];
-  bf16x8 pf[2][KSM];
+  typename P::Frag pf[2][KSM];
   uint32_t gate[2];
   const int q = lane_id() >> 4;
   layer0_fn(a);
@@ -468,8 +489,8 @@ DLAP_DEV void mom_forward_tile(const bf16x8* lds, const float* aux, const MlpDim
     if (j == 0) relu_dropout_g<WMB>(a, [&](int b, int u) { return ab.v[b][u]; }, dc, 16 + j, ri, gate);
     else relu_dropout<WMB>(a, aux + D.a_mb + 64 * j, aux + D.a_mb + 64 * j, dc, 16 + j, ri, gate);
     if (gout) gout[64 * j] = gate_word(gate);
-    pack_blocks<WMB>(a, pf);
-    layer_chain<WMB, KSM>(lds, D.m_fwd + j * WMB * KSM, pf, a);
+    pack_blocks<P, WMB>(a, pf);
+    layer_chain<P, WMB, KSM>(lds, D.m_fwd + j * WMB * KSM, pf, a);
   }
   auto emit = [&](auto pb0, auto pb1) {
 #pragma unroll
@@ -505,12 +526,13 @@ DLAP_DEV void mom_forward_tile(const bf16x8* lds, const float* aux, const MlpDim
 }
 
 // ============================== forward ==================================================
-template <int KS1, int WMB, bool ZIN>
+template <class P, int KS1, int WMB, bool ZIN>
 __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __restrict__ jobs, MlpDims D) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  using Frag = typename P::Frag;
   const MlpJob& J = jobs[blockIdx.y];
-  bf16x8* lds = reinterpret_cast<bf16x8*>(smem);
-  float* aux = reinterpret_cast<float*>(smem + (size_t)D.blob_frags * 1024);
+  Frag* lds = reinterpret_cast<Frag*>(smem);
+  float* aux = aux_lds_ptr(smem, D);
   float* spp = pp_lds_ptr(smem, D);
   MLP_TS(0);
   const int wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
@@ -518,17 +540,17 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __r
   const int q = lane_id() >> 4, lane = lane_id();
   const int stride = gridDim.x * nwaves;
   int tile = blockIdx.x * nwaves + wave;
-  TileIn<KS1> cur, nxt;
+  TileIn<P, KS1> cur, nxt;
   ZTile<WMB> zcur, znxt;                 // ZIN: layer-0 pre-activations instead of X rows
   AbPre<WMB> ab_cur, ab_nxt;
   int2 ti_ahead[2];                      // periods of the tile after next (for the abias prefetch)
   const bool mom = J.do_mom;
   if (tile < ntiles) {
     if constexpr (ZIN) issue_ztile<WMB, false>(J, D, tile, zcur, J.do_sdf, mom);
-    else issue_tile<KS1, false>(J, tile, cur);               // in flight during the staging
+    else issue_tile<P, KS1, false>(J, tile, cur);            // in flight during the staging
     if (mom && tile + stride < ntiles) issue_rowti(J, tile + stride, ti_ahead);
   }
-  stage_weights(J, D, lds, aux, spp);
+  stage_weights<P>(J, D, lds, aux, spp);
   MLP_TS(1);
   const DropCtx dc = drop_ctx(J, D);
   if (mom && tile < ntiles) {
@@ -550,17 +572,17 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __r
   for (; tile < ntiles; tile += stride) {
     if (tile + stride < ntiles) {
       if constexpr (ZIN) issue_ztile<WMB, false>(J, D, tile + stride, znxt, J.do_sdf, mom);
-      else issue_tile<KS1, false>(J, tile + stride, nxt);
+      else issue_tile<P, KS1, false>(J, tile + stride, nxt);
       if (keep) issue_kw(tile + stride, kw_nxt);
       if (mom) {
         issue_abias<WMB>(J, ti_ahead, ab_nxt);             // periods known since last iteration
         if (tile + 2 * stride < ntiles) issue_rowti(J, tile + 2 * stride, ti_ahead);
       }
     }
-    bf16x8 xf[2][KS1];
+    Frag xf[2][KS1];
     RowInfo ri;
     if constexpr (ZIN) ri = finish_ztile<WMB>(J, tile, zcur);
-    else ri = finish_tile<KS1>(J, D, tile, cur, xf, spp);
+    else ri = finish_tile<P, KS1>(J, D, tile, cur, xf, spp);
     if (J.do_sdf) {
       float w[2];
       DLAP_GLOBAL uint32_t* gout = J.gbits ? gbase + (size_t)tile * D.nl_sdf * 64 + lane : nullptr;
@@ -569,10 +591,10 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __r
           if (D.pp_lds_floats > 0) zin_sdf0(zcur.zs, ri, spp, aux, D, a);
           else zin_sdf0(zcur.zs, ri, gp(J.pp), aux, D, a);
         } else {
-          layer0<KS1, 4>(lds, D.s_fwd0, xf, a);
+          layer0<P, KS1, 4>(lds, D.s_fwd0, xf, a);
         }
       };
-      sdf_forward_tile(lds, aux, D, dc, ri, l0, gout, keep ? kw_cur : nullptr, w);
+      sdf_forward_tile<P>(lds, aux, D, dc, ri, l0, gout, keep ? kw_cur : nullptr, w);
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         const int r = tile * 32 + 16 * b + (lane & 15);
@@ -589,10 +611,10 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __r
 #pragma unroll
             for (int u = 0; u < WMB; ++u) a[b][u] = zcur.zm[b][u];
         } else {
-          layer0<KS1, WMB>(lds, D.m_fwd0, xf, a);
+          layer0<P, KS1, WMB>(lds, D.m_fwd0, xf, a);
         }
       };
-      mom_forward_tile<WMB>(lds, aux, D, J, dc, ri, l0, gout, ab_cur);
+      mom_forward_tile<P, WMB>(lds, aux, D, J, dc, ri, l0, gout, ab_cur);
     }
     if constexpr (ZIN) zcur = znxt;
     else cur = nxt;
@@ -620,14 +642,14 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
   constexpr int NU = 4 + WMB;
   const MlpJob& J = jobs[blockIdx.y];
   bf16x8* lds = reinterpret_cast<bf16x8*>(smem);
-  float* aux = reinterpret_cast<float*>(smem + (size_t)D.blob_frags * 1024);
+  float* aux = aux_lds_ptr(smem, D);
   float* spp = pp_lds_ptr(smem, D);
   bf16x8* lds0 = reinterpret_cast<bf16x8*>(smem + ((lds_bytes_of(D) + 15) & ~(size_t)15));
   const int lane = lane_id(), q = lane >> 4, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   const int KSX = D.KSX, rstride = D.KX >> 3;
   const int u0 = J.do_sdf ? 0 : 4, u1 = J.do_mom ? NU : 4;
   for (int i = threadIdx.x; i < (u1 - u0) * KSX * 64; i += blockDim.x) lds0[i] = gp(J.blob0)[u0 * KSX * 64 + i];
-  stage_weights(J, D, lds, aux, spp);                      // (ends with the barrier)
+  stage_weights<PrecBF16>(J, D, lds, aux, spp);           // (ends with the barrier)
   const DropCtx dc = drop_ctx(J, D);
   const int ntiles = (J.R + 31) >> 5;
   const int nch = (KSX + 3) >> 2;
@@ -719,7 +741,7 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
         };
         float w[2];
         DLAP_GLOBAL uint32_t* gout = (TRAIN && J.gbits) ? gbase + (size_t)tile * D.nl_sdf * 64 + lane : nullptr;
-        sdf_forward_tile(lds, aux, D, dc, ri, l0, gout, keep ? kw : nullptr, w);
+        sdf_forward_tile<PrecBF16>(lds, aux, D, dc, ri, l0, gout, keep ? kw : nullptr, w);
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
           const int r = tile * 32 + 16 * b + (lane & 15);
@@ -737,7 +759,7 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
         };
         DLAP_GLOBAL uint32_t* mgout = (TRAIN && J.mgbits && D.nl_mom > 1)
                                           ? gp(J.mgbits) + (size_t)tile * (D.nl_mom - 1) * 64 + lane : nullptr;
-        mom_forward_tile<WMB>(lds, aux, D, J, dc, ri, l0m, mgout, ab);
+        mom_forward_tile<PrecBF16, WMB>(lds, aux, D, J, dc, ri, l0m, mgout, ab);
       }
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
@@ -757,17 +779,18 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
 }
 
 // ============================== backward =================================================
-template <int UB>
-DLAP_DEV void to_rows_k(const bf16x8 (&pf)[2][(UB + 1) / 2], int blk, const bf16x8& s0,
-                        const bf16x8& s1, bf16x8& out) {
-  const bf16x8 sel = (blk & 1) ? s1 : s0;
-  out = pack8(mfma16(pf[0][blk >> 1], sel, zero4()), mfma16(pf[1][blk >> 1], sel, zero4()));
+template <class P, int UB>
+DLAP_DEV void to_rows_k(const typename P::Frag (&pf)[2][(UB + 1) / 2], int blk, const typename P::Frag& s0,
+                        const typename P::Frag& s1, typename P::Frag& out) {
+  const typename P::Frag sel = (blk & 1) ? s1 : s0;
+  out = P::pack(P::mma(pf[0][blk >> 1], sel, zero4()), P::mma(pf[1][blk >> 1], sel, zero4()));
 }
 
-DLAP_DEV void x_rows_k(const bf16x8& x0, const bf16x8& x1, int blk, const bf16x8& s0,
-                       const bf16x8& s1, bf16x8& out) {
-  const bf16x8 sel = (blk & 1) ? s1 : s0;
-  out = pack8(mfma16(x0, sel, zero4()), mfma16(x1, sel, zero4()));
+template <class P>
+DLAP_DEV void x_rows_k(const typename P::Frag& x0, const typename P::Frag& x1, int blk,
+                       const typename P::Frag& s0, const typename P::Frag& s1, typename P::Frag& out) {
+  const typename P::Frag sel = (blk & 1) ? s1 : s0;
+  out = P::pack(P::mma(x0, sel, zero4()), P::mma(x1, sel, zero4()));
 }
 
 // One slab per workgroup: zero an LDS image (reusing the weight staging area), let the
@@ -787,13 +810,14 @@ DLAP_DEV void wg_slab_store(const MlpJob& J, const float* red, int slab_stride) 
 // SDF backward. NL = number of hidden (MFMA) layers, all 64 wide.
 // ZIN (wide path): layer 0 is recomputed from z, its weight gradient is left to k_wgrad0: the
 // kernel stores the layer-0 dz as rows-as-k fragments instead (J.dz_out [tile][4][64]).
-template <int KS1, int NL, int TPS, bool ZIN>
+template <class P, int KS1, int NL, int TPS, bool ZIN>
 __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict__ jobs, MlpDims D,
                                                         int slab_stride) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  using Frag = typename P::Frag;
   const MlpJob& J = jobs[blockIdx.y];
-  bf16x8* lds = reinterpret_cast<bf16x8*>(smem);
-  float* aux = reinterpret_cast<float*>(smem + (size_t)D.blob_frags * 1024);
+  Frag* lds = reinterpret_cast<Frag*>(smem);
+  float* aux = aux_lds_ptr(smem, D);
   float* spp = pp_lds_ptr(smem, D);
   const int lane = lane_id(), q = lane >> 4, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   const int ntiles = (J.R + 31) >> 5;
@@ -801,8 +825,8 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
   // 64-column chunks of layer 0 with a gradient tile: the X chunks (fused) or, on the wide
   // path, only the per-period input columns (the X columns are k_wgrad0's)
   const int C0 = ZIN ? (D.Dm + 63) / 64 : KS1 / 2;
-  const bf16x8 selP0 = make_sel(true, 0), selP1 = make_sel(true, 1);
-  const bf16x8 selN0 = make_sel(false, 0), selN1 = make_sel(false, 1);
+  const Frag selP0 = make_sel<P>(true, 0), selP1 = make_sel<P>(true, 1);
+  const Frag selN0 = make_sel<P>(false, 0), selN1 = make_sel<P>(false, 1);
 
   f32x4 dW[TPS][4][4];
 #pragma unroll
@@ -825,47 +849,47 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
 
   const int stride = gridDim.x * nwaves;
   int tile = blockIdx.x * nwaves + wave;
-  TileIn<KS1> cur, nxt;
+  TileIn<P, KS1> cur, nxt;
   ZTile<1> zcur, znxt;
   uint32_t gw_cur[NL], gw_nxt[NL];   // gate words of the forward pass, prefetched with the tile
   const uint32_t stp = J.step ? (uint32_t)*gp(J.step) : 0u;
   const auto gbase = gp(J.gbits) + (size_t)(stp & 1u) * J.gb_half;
   if (tile < ntiles) {
     if constexpr (ZIN) issue_ztile<1, true>(J, D, tile, zcur, true, false);
-    else issue_tile<KS1, true>(J, tile, cur);
+    else issue_tile<P, KS1, true>(J, tile, cur);
 #pragma unroll
     for (int j = 0; j < NL; ++j) gw_cur[j] = gbase[((size_t)tile * NL + j) * 64 + lane];
   }
-  stage_weights(J, D, lds, aux, spp);          // first tile's loads are already in flight
+  stage_weights<P>(J, D, lds, aux, spp);       // first tile's loads are already in flight
   const DropCtx dc = drop_ctx(J, D);
   for (; tile < ntiles; tile += stride) {
     if (tile + stride < ntiles) {
       if constexpr (ZIN) issue_ztile<1, true>(J, D, tile + stride, znxt, true, false);
-      else issue_tile<KS1, true>(J, tile + stride, nxt);
+      else issue_tile<P, KS1, true>(J, tile + stride, nxt);
 #pragma unroll
       for (int j = 0; j < NL; ++j) gw_nxt[j] = gbase[((size_t)(tile + stride) * NL + j) * 64 + lane];
     }
-    bf16x8 xf[2][KS1];
+    Frag xf[2][KS1];
     RowInfo ri;
     if constexpr (ZIN) ri = finish_ztile<1>(J, tile, zcur);
-    else ri = finish_tile<KS1>(J, D, tile, cur, xf, spp);
+    else ri = finish_tile<P, KS1>(J, D, tile, cur, xf, spp);
     // ---- forward recompute from the stored gates, keep packed activations ----
-    bf16x8 act[NL][2][2];
+    Frag act[NL][2][2];
     uint32_t gates[NL][2];
     f32x4 a[2][4];
     if constexpr (ZIN) {
       if (D.pp_lds_floats > 0) zin_sdf0(zcur.zs, ri, spp, aux, D, a);
       else zin_sdf0(zcur.zs, ri, gp(J.pp), aux, D, a);
     } else {
-      layer0<KS1, 4>(lds, D.s_fwd0, xf, a);
+      layer0<P, KS1, 4>(lds, D.s_fwd0, xf, a);
     }
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
-      if (j > 0) layer_chain<4, 2>(lds, D.s_fwd + (j - 1) * 8, act[j - 1], a);
+      if (j > 0) layer_chain<P, 4, 2>(lds, D.s_fwd + (j - 1) * 8, act[j - 1], a);
       gates[j][0] = gw_cur[j] & 0xFFFFu;
       gates[j][1] = gw_cur[j] >> 16;
       relu_gates<4>(a, aux + D.a_sb + 64 * j, aux + D.a_sb + 64 * j, dc.scale, gates[j]);
-      pack_blocks<4>(a, act[j]);
+      pack_blocks<P, 4>(a, act[j]);
     }
     // ---- output layer: w = wo . a_last + bo ----
     float dwr[2];
@@ -890,15 +914,15 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
     // ---- backward chain ----
 #pragma unroll
     for (int j = NL - 1; j >= 0; --j) {
-      bf16x8 dzf[2][2];
-      pack_blocks<4>(dz, dzf);
-      bf16x8 dzN[4];
+      Frag dzf[2][2];
+      pack_blocks<P, 4>(dz, dzf);
+      Frag dzN[4];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) to_rows_k<4>(dzf, u, selP0, selP1, dzN[u]);
+      for (int u = 0; u < 4; ++u) to_rows_k<P, 4>(dzf, u, selP0, selP1, dzN[u]);
       if (slice == 0) {
-        const bf16x8 oh = make_onehot(j);
+        const Frag oh = make_onehot<P>(j);
 #pragma unroll
-        for (int u = 0; u < 4; ++u) gbias[u] = mfma16(dzN[u], oh, gbias[u]);
+        for (int u = 0; u < 4; ++u) gbias[u] = P::mma(dzN[u], oh, gbias[u]);
       }
       if constexpr (ZIN) {
         if (j == 0 && slice == 0) {                 // layer-0 dz for k_wgrad0
@@ -912,36 +936,36 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
         if (tl[t] == j) {
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
-            bf16x8 aN = zero8();
+            Frag aN = P::zero();
             if (j == 0) {
               const int blk = 4 * tc[t] + v;
               if constexpr (!ZIN) {
-                bf16x8 x0 = zero8(), x1 = zero8();
+                Frag x0 = P::zero(), x1 = P::zero();
 #pragma unroll
                 for (int s = 0; s < KS1; ++s)
                   if (s == (blk >> 1)) { x0 = xf[0][s]; x1 = xf[1][s]; }
-                x_rows_k(x0, x1, blk, selN0, selN1, aN);
+                x_rows_k<P>(x0, x1, blk, selN0, selN1, aN);
               } else {
                 if (16 * blk >= D.Dm) continue;             // wave-uniform: no columns here
-                bf16x8 x0, x1;
+                Frag x0, x1;
                 if (D.pp_lds_floats > 0) {
-                  x0 = pp_xfrag(spp, ri.t[0], blk >> 1, D); x1 = pp_xfrag(spp, ri.t[1], blk >> 1, D);
+                  x0 = pp_xfrag<P>(spp, ri.t[0], blk >> 1, D); x1 = pp_xfrag<P>(spp, ri.t[1], blk >> 1, D);
                 } else {
-                  x0 = pp_xfrag(gp(J.pp), ri.t[0], blk >> 1, D); x1 = pp_xfrag(gp(J.pp), ri.t[1], blk >> 1, D);
+                  x0 = pp_xfrag<P>(gp(J.pp), ri.t[0], blk >> 1, D); x1 = pp_xfrag<P>(gp(J.pp), ri.t[1], blk >> 1, D);
                 }
-                x_rows_k(x0, x1, blk, selN0, selN1, aN);
+                x_rows_k<P>(x0, x1, blk, selN0, selN1, aN);
               }
             } else {
-              to_rows_k<4>(act[j > 0 ? j - 1 : 0], v, selP0, selP1, aN);
+              to_rows_k<P, 4>(act[j > 0 ? j - 1 : 0], v, selP0, selP1, aN);
             }
 #pragma unroll
-            for (int u = 0; u < 4; ++u) dW[t][u][v] = mfma16(dzN[u], aN, dW[t][u][v]);
+            for (int u = 0; u < 4; ++u) dW[t][u][v] = P::mma(dzN[u], aN, dW[t][u][v]);
           }
         }
       }
       if (j > 0) {
         f32x4 da[2][4];
-        layer_chain<4, 2>(lds, D.s_bwd + (j - 1) * 8, dzf, da);
+        layer_chain<P, 4, 2>(lds, D.s_bwd + (j - 1) * 8, dzf, da);
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
@@ -958,9 +982,9 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
           f32x4 c0 = zero4(), c1 = zero4();
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
-            const bf16x8 w = ldsf(lds, D.s_upp + 2 * ub + s);
-            c0 = mfma16(w, dzf[0][s], c0);
-            c1 = mfma16(w, dzf[1][s], c1);
+            const Frag w = ldsf(lds, D.s_upp + 2 * ub + s);
+            c0 = P::mma(w, dzf[0][s], c0);
+            c1 = P::mma(w, dzf[1][s], c1);
           }
 #pragma unroll
           for (int b = 0; b < 2; ++b) {
@@ -1016,20 +1040,21 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
 
 // Moment backward (phase 2). NLM MFMA layers of WM = 16*WMB units; tanh on the last.
 // ZIN: as k_mlp_bwd_sdf (layer 0 from z, layer-0 dz stored as J.dz_out [tile][WMB][64]).
-template <int KS1, int WMB, int NLM, int TPS, bool ZIN>
+template <class P, int KS1, int WMB, int NLM, int TPS, bool ZIN>
 __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict__ jobs, MlpDims D,
                                                         int slab_stride) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KSM = (WMB + 1) / 2;
+  using Frag = typename P::Frag;
   const MlpJob& J = jobs[blockIdx.y];
-  bf16x8* lds = reinterpret_cast<bf16x8*>(smem);
-  float* aux = reinterpret_cast<float*>(smem + (size_t)D.blob_frags * 1024);
+  Frag* lds = reinterpret_cast<Frag*>(smem);
+  float* aux = aux_lds_ptr(smem, D);
   const int lane = lane_id(), q = lane >> 4, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   const int ntiles = (J.R + 31) >> 5;
   const int slice = blockIdx.z;
   constexpr int C0 = ZIN ? 0 : KS1 / 2;
-  const bf16x8 selP0 = make_sel(true, 0), selP1 = make_sel(true, 1);
-  const bf16x8 selN0 = make_sel(false, 0), selN1 = make_sel(false, 1);
+  const Frag selP0 = make_sel<P>(true, 0), selP1 = make_sel<P>(true, 1);
+  const Frag selN0 = make_sel<P>(false, 0), selN1 = make_sel<P>(false, 1);
 
   f32x4 dW[TPS][WMB][4];
 #pragma unroll
@@ -1052,30 +1077,30 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
   const int stride = gridDim.x * nwaves;
   int tile = blockIdx.x * nwaves + wave;
   constexpr int NH = NLM > 1 ? NLM - 1 : 1;   // hidden layers with stored gate words
-  TileIn<KS1> cur, nxt;
+  TileIn<P, KS1> cur, nxt;
   ZTile<WMB> zcur, znxt;
   uint32_t gw_cur[NH], gw_nxt[NH];
   if (tile < ntiles) {
     if constexpr (ZIN) issue_ztile<WMB, false>(J, D, tile, zcur, false, true);
-    else issue_tile<KS1, false>(J, tile, cur);
+    else issue_tile<P, KS1, false>(J, tile, cur);
 #pragma unroll
     for (int j = 0; j + 1 < NLM; ++j) gw_cur[j] = gp(J.mgbits)[((size_t)tile * (NLM - 1) + j) * 64 + lane];
   }
-  stage_weights(J, D, lds, aux);
+  stage_weights<P>(J, D, lds, aux);
   const DropCtx dc = drop_ctx(J, D);
   for (; tile < ntiles; tile += stride) {
     if (tile + stride < ntiles) {
       if constexpr (ZIN) issue_ztile<WMB, false>(J, D, tile + stride, znxt, false, true);
-      else issue_tile<KS1, false>(J, tile + stride, nxt);
+      else issue_tile<P, KS1, false>(J, tile + stride, nxt);
 #pragma unroll
       for (int j = 0; j + 1 < NLM; ++j)
         gw_nxt[j] = gp(J.mgbits)[((size_t)(tile + stride) * (NLM - 1) + j) * 64 + lane];
     }
-    bf16x8 xf[2][KS1];
+    Frag xf[2][KS1];
     RowInfo ri;
     if constexpr (ZIN) ri = finish_ztile<WMB>(J, tile, zcur);
-    else ri = finish_tile<KS1, false>(J, D, tile, cur, xf);   // moment tower: no per-period cols
-    bf16x8 act[NLM][2][KSM];
+    else ri = finish_tile<P, KS1, false>(J, D, tile, cur, xf);   // moment tower: no per-period cols
+    Frag act[NLM][2][KSM];
     uint32_t gates[NLM][2];
     f32x4 a[2][WMB];
     if constexpr (ZIN) {
@@ -1084,17 +1109,17 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
 #pragma unroll
         for (int u = 0; u < WMB; ++u) a[b][u] = zcur.zm[b][u];
     } else {
-      layer0<KS1, WMB>(lds, D.m_fwd0, xf, a);
+      layer0<P, KS1, WMB>(lds, D.m_fwd0, xf, a);
     }
 #pragma unroll
     for (int j = 0; j < NLM; ++j) {
-      if (j > 0) layer_chain<WMB, KSM>(lds, D.m_fwd + (j - 1) * WMB * KSM, act[j - 1], a);
+      if (j > 0) layer_chain<P, WMB, KSM>(lds, D.m_fwd + (j - 1) * WMB * KSM, act[j - 1], a);
       auto body = [&](auto b0, auto b1) {
         if (j + 1 < NLM) {
           gates[j][0] = gw_cur[j < NH ? j : 0] & 0xFFFFu;
           gates[j][1] = gw_cur[j < NH ? j : 0] >> 16;
           relu_gates<WMB>(a, b0, b1, dc.scale, gates[j]);
-          pack_blocks<WMB>(a, act[j]);
+          pack_blocks<P, WMB>(a, act[j]);
         } else {
           // h = tanh(z); dz = dh (1 - h^2), dh = dE[i][k] R SDF_t / T_i
 #pragma unroll
@@ -1126,15 +1151,15 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
       for (int u = 0; u < WMB; ++u) dz[b][u] = a[b][u];
 #pragma unroll
     for (int j = NLM - 1; j >= 0; --j) {
-      bf16x8 dzf[2][KSM];
-      pack_blocks<WMB>(dz, dzf);
-      bf16x8 dzN[WMB];
+      Frag dzf[2][KSM];
+      pack_blocks<P, WMB>(dz, dzf);
+      Frag dzN[WMB];
 #pragma unroll
-      for (int u = 0; u < WMB; ++u) to_rows_k<WMB>(dzf, u, selP0, selP1, dzN[u]);
+      for (int u = 0; u < WMB; ++u) to_rows_k<P, WMB>(dzf, u, selP0, selP1, dzN[u]);
       if (slice == 0 && j > 0) {
-        const bf16x8 oh = make_onehot(j);
+        const Frag oh = make_onehot<P>(j);
 #pragma unroll
-        for (int u = 0; u < WMB; ++u) gbias[u] = mfma16(dzN[u], oh, gbias[u]);
+        for (int u = 0; u < WMB; ++u) gbias[u] = P::mma(dzN[u], oh, gbias[u]);
       }
       if constexpr (ZIN) {
         if (j == 0 && slice == 0) {                 // layer-0 dz for k_wgrad0
@@ -1149,27 +1174,27 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
 #pragma unroll
           for (int v = 0; v < 4; ++v) {
             if (j > 0 && v >= WMB) continue;
-            bf16x8 aN = zero8();
+            Frag aN = P::zero();
             if (j == 0) {
               if constexpr (!ZIN) {
                 const int blk = 4 * tc[t] + v;
-                bf16x8 x0 = zero8(), x1 = zero8();
+                Frag x0 = P::zero(), x1 = P::zero();
 #pragma unroll
                 for (int s = 0; s < KS1; ++s)
                   if (s == (blk >> 1)) { x0 = xf[0][s]; x1 = xf[1][s]; }
-                x_rows_k(x0, x1, blk, selN0, selN1, aN);
+                x_rows_k<P>(x0, x1, blk, selN0, selN1, aN);
               }
             } else {
-              to_rows_k<WMB>(act[j > 0 ? j - 1 : 0], v, selP0, selP1, aN);
+              to_rows_k<P, WMB>(act[j > 0 ? j - 1 : 0], v, selP0, selP1, aN);
             }
 #pragma unroll
-            for (int u = 0; u < WMB; ++u) dW[t][u][v] = mfma16(dzN[u], aN, dW[t][u][v]);
+            for (int u = 0; u < WMB; ++u) dW[t][u][v] = P::mma(dzN[u], aN, dW[t][u][v]);
           }
         }
       }
       if (j > 0) {
         f32x4 da[2][WMB];
-        layer_chain<WMB, KSM>(lds, D.m_bwd + (j - 1) * WMB * KSM, dzf, da);
+        layer_chain<P, WMB, KSM>(lds, D.m_bwd + (j - 1) * WMB * KSM, dzf, da);
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
@@ -1277,19 +1302,28 @@ static size_t bwd_lds_bytes(const MlpDims& D, int slab_stride) {
   return a > b ? a : b;
 }
 
+template <class P>
+static bool launch_mlp_fwd_p(const MlpJob* jobs, dim3 grid, dim3 block, size_t sh, const MlpDims& D, int KS1,
+                             int WMB, hipStream_t st) {
+#define F_CASE(K, W) if (KS1 == K && WMB == W) { hipLaunchKernelGGL((k_mlp_fwd<P, K, W, false>), grid, block, sh, st, jobs, D); HIP_OK(hipGetLastError()); return true; }
+  F_CASE(2, 1) F_CASE(2, 2) F_CASE(2, 4) F_CASE(4, 1) F_CASE(4, 2) F_CASE(4, 4)
+#undef F_CASE
+  return false;
+}
+
 void launch_mlp_fwd(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int KS1, int WMB,
                     hipStream_t st) {
   dim3 grid(gx, njobs), block(256);
   size_t sh = mlp_lds_bytes(D);
   if (D.wide) {
-#define FZ_CASE(W) if (WMB == W) { hipLaunchKernelGGL((k_mlp_fwd<2, W, true>), grid, block, sh, st, jobs, D); HIP_OK(hipGetLastError()); return; }
+    if (D.fp32) dlap_throw_hip(hipErrorInvalidValue, "mlp_fwd: fp32 towers need the fused path", __FILE__, __LINE__);
+#define FZ_CASE(W) if (WMB == W) { hipLaunchKernelGGL((k_mlp_fwd<PrecBF16, 2, W, true>), grid, block, sh, st, jobs, D); HIP_OK(hipGetLastError()); return; }
     FZ_CASE(1) FZ_CASE(2) FZ_CASE(4)
 #undef FZ_CASE
   }
-#define F_CASE(K, W) if (!D.wide && KS1 == K && WMB == W) { hipLaunchKernelGGL((k_mlp_fwd<K, W, false>), grid, block, sh, st, jobs, D); HIP_OK(hipGetLastError()); return; }
-  F_CASE(2, 1) F_CASE(2, 2) F_CASE(2, 4) F_CASE(4, 1) F_CASE(4, 2) F_CASE(4, 4)
-#undef F_CASE
-  dlap_throw_hip(hipErrorInvalidValue, "mlp_fwd: unsupported (KS1, WMB)", __FILE__, __LINE__);
+  const bool ok = D.fp32 ? launch_mlp_fwd_p<PrecF32>(jobs, grid, block, sh, D, KS1, WMB, st)
+                         : launch_mlp_fwd_p<PrecBF16>(jobs, grid, block, sh, D, KS1, WMB, st);
+  if (!ok) dlap_throw_hip(hipErrorInvalidValue, "mlp_fwd: unsupported (KS1, WMB)", __FILE__, __LINE__);
 }
 
 void launch_mlp_fwd_zx(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int WMB, hipStream_t st,
@@ -1302,22 +1336,44 @@ void launch_mlp_fwd_zx(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, 
   dlap_throw_hip(hipErrorInvalidValue, "mlp_fwd_zx: unsupported moment width", __FILE__, __LINE__);
 }
 
+template <class P>
+static bool launch_bwd_sdf_p(const MlpJob* jobs, dim3 grid, dim3 block, size_t sh, int tps, const MlpDims& D,
+                             int KS1, int slab_stride, hipStream_t st) {
+#define S_CASE(K, N, T) if (KS1 == K && D.nl_sdf == N && tps == T) { hipLaunchKernelGGL((k_mlp_bwd_sdf<P, K, N, T, false>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return true; }
+  S_CASE(2, 1, 1) S_CASE(2, 2, 1) S_CASE(2, 3, 1) S_CASE(2, 4, 1)
+  S_CASE(2, 2, 2)
+  S_CASE(4, 1, 1) S_CASE(4, 2, 1) S_CASE(4, 3, 1) S_CASE(4, 4, 1)
+#undef S_CASE
+  return false;
+}
+
 void launch_mlp_bwd_sdf(const MlpJob* jobs, int njobs, int gx, int nslice, int tps, const MlpDims& D,
                         int KS1, int slab_stride, hipStream_t st) {
   dim3 grid(gx, njobs, nslice), block(256);
   size_t sh = bwd_lds_bytes(D, slab_stride);
   if (D.wide) {
-#define SZ_CASE(N, T) if (D.nl_sdf == N && tps == T) { hipLaunchKernelGGL((k_mlp_bwd_sdf<2, N, T, true>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
+    if (D.fp32) dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_sdf: fp32 towers need the fused path", __FILE__, __LINE__);
+#define SZ_CASE(N, T) if (D.nl_sdf == N && tps == T) { hipLaunchKernelGGL((k_mlp_bwd_sdf<PrecBF16, 2, N, T, true>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
     SZ_CASE(1, 1) SZ_CASE(2, 1) SZ_CASE(3, 1) SZ_CASE(4, 1) SZ_CASE(2, 2)
 #undef SZ_CASE
     dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_sdf: unsupported depth (wide)", __FILE__, __LINE__);
   }
-#define S_CASE(K, N, T) if (KS1 == K && D.nl_sdf == N && tps == T) { hipLaunchKernelGGL((k_mlp_bwd_sdf<K, N, T, false>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
-  S_CASE(2, 1, 1) S_CASE(2, 2, 1) S_CASE(2, 3, 1) S_CASE(2, 4, 1)
-  S_CASE(2, 2, 2)
-  S_CASE(4, 1, 1) S_CASE(4, 2, 1) S_CASE(4, 3, 1) S_CASE(4, 4, 1)
-#undef S_CASE
-  dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_sdf: unsupported depth/tiling", __FILE__, __LINE__);
+  const bool ok = D.fp32 ? launch_bwd_sdf_p<PrecF32>(jobs, grid, block, sh, tps, D, KS1, slab_stride, st)
+                         : launch_bwd_sdf_p<PrecBF16>(jobs, grid, block, sh, tps, D, KS1, slab_stride, st);
+  if (!ok) dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_sdf: unsupported depth/tiling", __FILE__, __LINE__);
+}
+
+template <class P>
+static bool launch_bwd_mom_p(const MlpJob* jobs, dim3 grid, dim3 block, size_t sh, int tps, const MlpDims& D,
+                             int KS1, int WMB, int slab_stride, hipStream_t st) {
+#define M_CASE(K, W, N) if (KS1 == K && WMB == W && D.nl_mom == N && tps == 1) { hipLaunchKernelGGL((k_mlp_bwd_mom<P, K, W, N, 1, false>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return true; }
+  M_CASE(2, 1, 1) M_CASE(2, 2, 1) M_CASE(2, 4, 1)
+  M_CASE(2, 1, 2) M_CASE(2, 2, 2) M_CASE(2, 4, 2)
+  M_CASE(2, 1, 3) M_CASE(2, 2, 3) M_CASE(2, 4, 3)
+  M_CASE(4, 1, 1) M_CASE(4, 2, 1) M_CASE(4, 4, 1)
+  M_CASE(4, 1, 2) M_CASE(4, 2, 2) M_CASE(4, 4, 2)
+#undef M_CASE
+  return false;
 }
 
 void launch_mlp_bwd_mom(const MlpJob* jobs, int njobs, int gx, int nslice, int tps, const MlpDims& D,
@@ -1325,21 +1381,17 @@ void launch_mlp_bwd_mom(const MlpJob* jobs, int njobs, int gx, int nslice, int t
   dim3 grid(gx, njobs, nslice), block(256);
   size_t sh = bwd_lds_bytes(D, slab_stride);
   if (D.wide) {
-#define MZ_CASE(W, N) if (WMB == W && D.nl_mom == N && tps == 1) { hipLaunchKernelGGL((k_mlp_bwd_mom<2, W, N, 1, true>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
+    if (D.fp32) dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_mom: fp32 towers need the fused path", __FILE__, __LINE__);
+#define MZ_CASE(W, N) if (WMB == W && D.nl_mom == N && tps == 1) { hipLaunchKernelGGL((k_mlp_bwd_mom<PrecBF16, 2, W, N, 1, true>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
     MZ_CASE(1, 1) MZ_CASE(2, 1) MZ_CASE(4, 1)
     MZ_CASE(1, 2) MZ_CASE(2, 2) MZ_CASE(4, 2)
     MZ_CASE(1, 3) MZ_CASE(2, 3) MZ_CASE(4, 3)
 #undef MZ_CASE
     dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_mom: unsupported depth/width (wide)", __FILE__, __LINE__);
   }
-#define M_CASE(K, W, N) if (KS1 == K && WMB == W && D.nl_mom == N && tps == 1) { hipLaunchKernelGGL((k_mlp_bwd_mom<K, W, N, 1, false>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
-  M_CASE(2, 1, 1) M_CASE(2, 2, 1) M_CASE(2, 4, 1)
-  M_CASE(2, 1, 2) M_CASE(2, 2, 2) M_CASE(2, 4, 2)
-  M_CASE(2, 1, 3) M_CASE(2, 2, 3) M_CASE(2, 4, 3)
-  M_CASE(4, 1, 1) M_CASE(4, 2, 1) M_CASE(4, 4, 1)
-  M_CASE(4, 1, 2) M_CASE(4, 2, 2) M_CASE(4, 4, 2)
-#undef M_CASE
-  dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_mom: unsupported depth/width", __FILE__, __LINE__);
+  const bool ok = D.fp32 ? launch_bwd_mom_p<PrecF32>(jobs, grid, block, sh, tps, D, KS1, WMB, slab_stride, st)
+                         : launch_bwd_mom_p<PrecBF16>(jobs, grid, block, sh, tps, D, KS1, WMB, slab_stride, st);
+  if (!ok) dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_mom: unsupported depth/width", __FILE__, __LINE__);
 }
 
 std::vector<long long> mlp_timestamps() {

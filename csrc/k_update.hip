@@ -220,7 +220,11 @@ __global__ __launch_bounds__(256) void k_pack(const UpdJob* __restrict__ jobs,
   const int total = nproj + md->md.b0_frags * 512;
   const int e = blockIdx.x * 256 + threadIdx.x;
   const auto src = gp(static_cast<const float*>(J.params));
-  if (e < nel) ((DLAP_GLOBAL __bf16*)(J.blob))[e] = (__bf16)pack_blob_elem(md, src, e);
+  if (e < nel) {
+    const float v = pack_blob_elem(md, src, e);
+    if (md->md.fp32) ((DLAP_GLOBAL float*)(J.blob))[e] = v;         // reference-precision towers
+    else ((DLAP_GLOBAL __bf16*)(J.blob))[e] = (__bf16)v;
+  }
   else if (e < naux) gp(J.aux)[e - nel] = pack_aux_elem(md, src, e - nel);
   else if (e < nproj) gp(J.wproj)[e - naux] = pack_proj_elem(md, src, e - naux);
   else if (e < total) ((DLAP_GLOBAL __bf16*)(J.blob0))[e - nproj] = (__bf16)pack_blob0_elem(md, src, e - nproj);

@@ -4,11 +4,12 @@
 #include "common.h"
 
 struct MlpJob {
-  const bf16x8* X;        // [R][KP/8] bf16 panel rows (cols [F, F+Dm) reserved, zero)
+  const bf16x8* X;        // [R][KP/8] bf16 panel rows (cols [F, F+Dm) reserved, zero); fp32
+                          // mode: [R][KP] fp32 rows behind the same pointer
   const int2* rowti;      // [R] (t, i) of each compact row
   const float* pp;        // [T][Dm] per-period SDF inputs (LSTM output or raw macro)
   const float* abias;     // [T][64] moment layer-0 per-period bias (W_macro . m_t + b)
-  const bf16x8* blob;     // packed weight fragments of this job's model
+  const bf16x8* blob;     // packed weight fragments of this job's model (fp32 mode: f32x8 frags)
   const bf16x8* blob0;    // wide path: layer-0 x-column fragments (k_mlp_fwd_zx / k_proj0)
   const float* aux;       // fp32 biases / output row of this job's model
   float* w_out;           // fwd: compact [R] raw SDF weights
@@ -57,6 +58,8 @@ struct MlpDims {
   int KX, KSX;                   // panel row width (multiple of 32) and its 32-column k-steps
   int zc;                        // f32x4 chunks per tile in z: SDF (4 b + u), moment 8 + WMB b + u
   int b0_frags;                  // layer-0 x-column fragments: SDF [4][KSX], moment [WMB][KSX]
+  int fp32;                      // 1: reference-precision towers (fp32 panel rows / blob /
+                                 //    operands, PrecF32 in common.h); 0: bf16 (PrecBF16)
 };
 
 // One model x split of the wide layer-0 kernels.

@@ -5,7 +5,9 @@ every epoch (`/root/reference/src/train.py:69-75`). Here a split is uploaded onc
 HBM in a compacted layout:
 
   X         [R, KP] bf16   valid rows only, in (t, i) order; columns [F, F+Dm) are left zero
-                           (the kernels insert the per-period LSTM / macro inputs there)
+                           (the kernels insert the per-period LSTM / macro inputs there);
+                           fp32 [R, KP] (viewed as uint16 [R, 2 KP]) for the reference-precision
+                           towers (``fp32=True``)
   rowti     [R, 2]  int32  (t, i) of each compact row
   row_ptr   [T+1]   int32  first compact row of each period
   Rm, mask  [T*N]   fp32   dense returns (zero-filled) and 0/1 mask
@@ -54,8 +56,9 @@ def _np(a) -> np.ndarray:
     return np.asarray(a)
 
 
-def prepare_split(batch: Dict, KP: int) -> PanelSplit:
-    """Compact a ``get_full_batch()``-style dict (torch or numpy) for the engine."""
+def prepare_split(batch: Dict, KP: int, fp32: bool = False) -> PanelSplit:
+    """Compact a ``get_full_batch()``-style dict (torch or numpy) for the engine (``fp32``: keep
+    the features in fp32, as uint16 pairs, for the reference-precision towers)."""
     feats = _np(batch["individual_features"]).astype(np.float32, copy=False)
     ret = _np(batch["returns"]).astype(np.float32, copy=False)
     mask = _np(batch["mask"]).astype(bool, copy=False)
@@ -64,9 +67,15 @@ def prepare_split(batch: Dict, KP: int) -> PanelSplit:
         raise ValueError(f"feature dim {F} exceeds engine row width {KP}")
     tt, ii = np.nonzero(mask)                      # row-major: sorted by t then i
     R = len(tt)
-    X = np.zeros((R, KP), dtype=np.uint16)
-    if R:
-        X[:, :F] = f32_to_bf16_bits(feats[tt, ii])
+    if fp32:
+        Xf = np.zeros((R, KP), dtype=np.float32)
+        if R:
+            Xf[:, :F] = feats[tt, ii]
+        X = Xf.view(np.uint16)                      # [R, 2 KP]
+    else:
+        X = np.zeros((R, KP), dtype=np.uint16)
+        if R:
+            X[:, :F] = f32_to_bf16_bits(feats[tt, ii])
     rowti = np.ascontiguousarray(np.stack([tt, ii], axis=1).astype(np.int32))
     counts = mask.sum(axis=1)
     row_ptr = np.zeros(T + 1, dtype=np.int32)
@@ -94,7 +103,7 @@ class DevicePanelSplit:
     macro: np.ndarray
 
 
-def prepare_split_device(batch: Dict, KP: int, chunk_rows: int = 1 << 20) -> DevicePanelSplit:
+def prepare_split_device(batch: Dict, KP: int, chunk_rows: int = 1 << 20, fp32: bool = False) -> DevicePanelSplit:
     """Compact a split whose tensors live on the GPU without a host round trip of the features
     (the scaled 600x30000x512 panel is 37 GB in fp32). The bf16 rounding is torch's
     round-to-nearest-even, identical to ``f32_to_bf16_bits``."""
@@ -106,11 +115,12 @@ def prepare_split_device(batch: Dict, KP: int, chunk_rows: int = 1 << 20) -> Dev
         raise ValueError(f"feature dim {F} exceeds engine row width {KP}")
     idx = mask.reshape(-1).nonzero().squeeze(1)          # row-major: sorted by t then i
     R = int(idx.numel())
-    X = torch.zeros((R, KP), dtype=torch.bfloat16, device=feats.device)
+    xdt = torch.float32 if fp32 else torch.bfloat16
+    X = torch.zeros((R, KP), dtype=xdt, device=feats.device)
     flat = feats.reshape(-1, F)
     for a in range(0, R, chunk_rows):                     # bounded temporaries
         b = min(R, a + chunk_rows)
-        X[a:b, :F] = flat.index_select(0, idx[a:b]).to(torch.bfloat16)
+        X[a:b, :F] = flat.index_select(0, idx[a:b]).to(xdt)
     rowti = torch.stack([idx // N, idx % N], dim=1).to(torch.int32).cpu().numpy()
     row_ptr = np.zeros(T + 1, dtype=np.int32)
     np.cumsum(mask.sum(dim=1).cpu().numpy(), out=row_ptr[1:])

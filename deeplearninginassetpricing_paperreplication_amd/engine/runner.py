@@ -55,21 +55,21 @@ _PREP_CACHE: "OrderedDict[tuple, object]" = OrderedDict()
 _PREP_LOCK = threading.Lock()
 
 
-def _prepared(batch: Dict, KP: int):
+def _prepared(batch: Dict, KP: int, fp32: bool = False):
     """Host compaction of a split, memoised on the identity/version of its input tensors: the
     ensemble and sweep drivers build one engine per architecture bucket over the same panel."""
     def tk(t):
         return (id(t), t.data_ptr(), t._version) if isinstance(t, torch.Tensor) else (id(t),)
-    key = (KP,) + tuple(tk(batch.get(k)) for k in ("individual_features", "returns", "mask", "macro_features"))
+    key = (KP, fp32) + tuple(tk(batch.get(k)) for k in ("individual_features", "returns", "mask", "macro_features"))
     with _PREP_LOCK:       # drivers may build engines from several threads
-        return _prepared_locked(batch, KP, key)
+        return _prepared_locked(batch, KP, key, fp32)
 
 
-def _prepared_locked(batch: Dict, KP: int, key):
+def _prepared_locked(batch: Dict, KP: int, key, fp32: bool = False):
     hit = _PREP_CACHE.get(key)
     if hit is None:
         # the entry keeps the inputs alive, so their ids cannot be reused while it exists
-        hit = (prepare_split(batch, KP), [batch.get(k) for k in ("individual_features", "returns", "mask",
+        hit = (prepare_split(batch, KP, fp32), [batch.get(k) for k in ("individual_features", "returns", "mask",
                                                                    "macro_features")])
         _PREP_CACHE[key] = hit
         while len(_PREP_CACHE) > 6:
@@ -78,18 +78,25 @@ def _prepared_locked(batch: Dict, KP: int, key):
 
 
 class GANEngine:
-    """Native multi-model trainer for one architecture (``spec``) on the current GPU."""
+    """Native multi-model trainer for one architecture (``spec``) on the current GPU.
 
-    def __init__(self, spec: ModelSpec, n_models: int = 1, max_epochs: int = 4096):
+    ``precision``: "bf16" (production: bf16 tower GEMM operands, fp32 accumulation / master
+    weights / losses) or "fp32" (the reference's precision end to end: fp32 panel rows and
+    weight fragments through fp32 MFMA tiles; fused layer-0 path only)."""
+
+    def __init__(self, spec: ModelSpec, n_models: int = 1, max_epochs: int = 4096, precision: str = "bf16"):
+        if precision not in ("bf16", "fp32"):
+            raise ValueError(f"precision must be 'bf16' or 'fp32', not {precision!r}")
         nat = load_native()
         self.spec = spec
         self.G = n_models
+        self.fp32 = precision == "fp32"
         self.eng = nat.Engine(
             F=spec.individual_dim, M=spec.macro_dim, nrnn=spec.rnn_layers, H=spec.rnn_hidden,
             raw_macro_sdf=(spec.rnn_layers == 0 and spec.macro_dim > 0),
             hidden=list(spec.hidden), mom_hidden=list(spec.moment_hidden), K=spec.num_moments,
             dropout=spec.dropout, normalize_w=spec.normalize_w, weighted=spec.weighted_loss,
-            residual=spec.residual_loss_factor, G=n_models, max_epochs=max_epochs)
+            residual=spec.residual_loss_factor, G=n_models, max_epochs=max_epochs, fp32=self.fp32)
         self.desc = self.eng.describe()
         self.KP = int(self.desc["KP"])
         self.splits: Dict[int, object] = {}
@@ -102,12 +109,13 @@ class GANEngine:
             x = b["individual_features"]
             if isinstance(x, torch.Tensor) and x.is_cuda:
                 # compact on the GPU, hand the engine a device pointer (no host copy of X)
-                ps = prepare_split_device(b, self.KP)
-                self.eng.set_split_dev(s, ps.X.data_ptr(), ps.X.numel(), ps.rowti.reshape(-1), ps.row_ptr,
+                ps = prepare_split_device(b, self.KP, fp32=self.fp32)
+                self.eng.set_split_dev(s, ps.X.data_ptr(), ps.X.numel() * (2 if self.fp32 else 1),
+                                       ps.rowti.reshape(-1), ps.row_ptr,
                                        ps.Rm, ps.mask, ps.macro.reshape(-1), ps.T, ps.N)
                 ps.X = None                                  # the engine keeps its own copy
             else:
-                ps = _prepared(b, self.KP)
+                ps = _prepared(b, self.KP, self.fp32)
                 self.eng.set_split(s, ps.X.reshape(-1), ps.rowti.reshape(-1), ps.row_ptr, ps.Rm, ps.mask,
                                    ps.macro.reshape(-1), ps.T, ps.N)
             self.splits[s] = ps
@@ -202,9 +210,6 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
     from ..utils import checkpoint as ckpt
     from ..utils.guards import NonFiniteMonitor
     from ..utils.tracing import Timers, trace_range
-    if precision != "bf16":
-        raise NotImplementedError("the native engine currently computes the tower GEMMs in bf16 "
-                                  "(fp32 accumulation / master weights); use the CPU path for fp32")
     say = print if verbose else (lambda *a, **k: None)
     dev = torch.device(device) if device is not None else torch.device("cuda")
     if dev.index is not None:
@@ -224,7 +229,7 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
     say(f"  SDF network: {n_sdf:,}")
     say(f"  Moment network: {n_mom:,}")
     total = num_epochs_unc + num_epochs_moment + num_epochs
-    eng = GANEngine(spec, n_models, max_epochs=max(total, 1))
+    eng = GANEngine(spec, n_models, max_epochs=max(total, 1), precision=precision)
     eng.set_data(train_data, valid_data, test_data)
     for g, m in enumerate(models):
         eng.set_model(g, m, seeds[g])

@@ -85,19 +85,37 @@ def barrier(d: Dist):
         tdist.barrier()
 
 
-def all_gather_rows(d: Dist, local: np.ndarray, n_total: int, owner_index: Sequence[int]) -> np.ndarray:
+def assign_lpt(costs: Sequence[float], world: int) -> List[List[int]]:
+    """Longest-processing-time-first assignment of items with the given costs to ``world``
+    ranks: items in decreasing cost (ties by index) each go to the least-loaded rank (ties by
+    rank). Deterministic, so every rank computes the same table without a collective. Each
+    rank's list is in increasing item order."""
+    load = [0.0] * world
+    out: List[List[int]] = [[] for _ in range(world)]
+    for i in sorted(range(len(costs)), key=lambda k: (-float(costs[k]), k)):
+        r = min(range(world), key=lambda q: (load[q], q))
+        out[r].append(i)
+        load[r] += float(costs[i])
+    return [sorted(x) for x in out]
+
+
+def all_gather_rows(d: Dist, local: np.ndarray, n_total: int, owner_index: Sequence[int],
+                    assignment: Optional[Sequence[Sequence[int]]] = None) -> np.ndarray:
     """Gather per-item rows from all ranks into item order.
 
-    ``local`` is [n_local, ...] for the items ``owner_index`` of this rank (the ``shard``
-    assignment); returns [n_total, ...] on every rank. One padded all-gather of a single
-    stacked tensor (plus nothing else: counts follow from ``shard``).
+    ``local`` is [n_local, ...] for the items ``owner_index`` of this rank; ``assignment``
+    (per rank, the item indices it owns; default the round-robin ``shard``) tells where every
+    rank's rows go. Returns [n_total, ...] on every rank. One padded all-gather of a single
+    stacked tensor (plus nothing else: counts follow from the assignment).
     """
     local = np.ascontiguousarray(local)
     if not d.active:
         out = np.empty((n_total,) + local.shape[1:], local.dtype)
         out[list(owner_index)] = local
         return out
-    per = [len(shard(n_total, r, d.world)) for r in range(d.world)]
+    owners = [list(a) for a in assignment] if assignment is not None else \
+        [shard(n_total, r, d.world) for r in range(d.world)]
+    per = [len(x) for x in owners]
     cap = max(per)
     pad = np.zeros((cap,) + local.shape[1:], local.dtype)
     pad[:len(local)] = local
@@ -108,7 +126,7 @@ def all_gather_rows(d: Dist, local: np.ndarray, n_total: int, owner_index: Seque
     g = bufs.cpu().numpy().reshape((d.world, cap) + local.shape[1:])
     out = np.empty((n_total,) + local.shape[1:], local.dtype)
     for r in range(d.world):
-        idx = shard(n_total, r, d.world)
+        idx = owners[r]
         out[idx] = g[r, :len(idx)]
     return out
 

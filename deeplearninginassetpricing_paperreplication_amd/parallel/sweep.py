@@ -9,14 +9,26 @@ Grid (paper Table A.VIII):
     CHL {0,1}          conditional hidden layers            -> hidden_dim_moment = [] | [CHU]
     CHU {4,8,16,32}    conditional units (moment count)     -> num_condition_moment = CHU
     LR  {1e-3,5e-4,2e-4,1e-4}
-3 * 2 * 2 * 2 * 4 * 4 = 384 configurations.
+3 * 2 * 2 * 2 * 4 * 4 = 384 configurations. The paper does not list the number of moments as a
+separate axis; its CHU (conditional hidden units) sets the moment count here (with CHL = 0 the
+conditional network has no hidden units, so CHU can only be its output width; with CHL = 1 it is
+both the hidden width and the output width). ``--chu hidden`` instead keeps 8 moments and uses
+CHU only for the hidden layer. Which mapping the paper's code used is parity-unpinned.
+
+``--grid baseline`` is BASELINE.json config 4's literal axes instead (hidden_dim x lr x dropout x
+num_moments, with SMV doubling it to 384): HL {2,3,4} x LR {4 values} x dropout {0, 0.05, 0.1,
+0.2} x moments {4, 8, 16, 32} x SMV {4, 8}, no conditional hidden layer.
 
 Execution: configurations that build the same network form a *bucket* (LR and the no-op CSMV
 vary inside it); a bucket is trained as ONE batched native-engine run, one member per config
-(per-member learning rates, ``Engine.set_lr``), so the 384 configs are 48 engine runs. Buckets are dealt round-robin
-over ranks. A bucket that raises marks its configs failed (metrics NaN) without stopping the
-sweep; the per-config metric table is exchanged with one all-gather and every rank ranks the
-configs identically (best = highest validation Sharpe of the paper-sign SDF factor by default).
+(per-member learning rates, ``Engine.set_lr``), so the paper grid's 384 configs are 48 engine
+runs. Buckets are assigned to ranks longest-processing-time first (``comm.assign_lpt``) by
+``bucket_cost``: the measured per-epoch time of that architecture's 8-member engine on the
+600 x 3000 panel (``sweep_costs.json``, written by ``tools/sweep_costs.py`` on an MI355X) or,
+for architectures it does not list, an analytic estimate. A bucket that raises marks its
+configs failed (metrics NaN) without stopping the sweep; the per-config metric table is
+exchanged with one all-gather and every rank ranks the configs identically (best = highest
+validation Sharpe of the paper-sign SDF factor by default). Per-rank wall-clocks are reported.
 """
 from __future__ import annotations
 
@@ -36,20 +48,73 @@ from .ensemble import SPLITS, _init_models, load_batches
 
 GRID = {"HL": (2, 3, 4), "SMV": (4, 8), "CSMV": (16, 32), "CHL": (0, 1), "CHU": (4, 8, 16, 32),
         "LR": (1e-3, 5e-4, 2e-4, 1e-4)}
+BASELINE_GRID = {"HL": (2, 3, 4), "SMV": (4, 8), "DROPOUT": (0.0, 0.05, 0.1, 0.2), "K": (4, 8, 16, 32),
+                 "LR": (1e-3, 5e-4, 2e-4, 1e-4)}
+COSTS_FILE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "sweep_costs.json")
 METRICS = ("ok", "valid_sharpe", "test_sharpe", "train_sharpe", "valid_loss", "test_loss", "wall_s")
 
 
-def paper_grid(M: int, F: int, grid: Dict = GRID, dropout: float = 0.05) -> List[Tuple[Dict, float, Dict]]:
-    """[(model config, lr, grid point)] in a fixed order (384 entries for the paper grid)."""
+def paper_grid(M: int, F: int, grid: Dict = GRID, dropout: float = 0.05,
+               chu: str = "both") -> List[Tuple[Dict, float, Dict]]:
+    """[(model config, lr, grid point)] in a fixed order (384 entries for the paper grid).
+    ``chu``: "both" -- CHU is the moment count and the conditional hidden width; "hidden" --
+    8 moments, CHU only the conditional hidden width."""
+    keys = list(grid)
+    out = []
+    for vals in itertools.product(*(grid[k] for k in keys)):
+        pt = dict(zip(keys, vals))
+        k = pt["CHU"] if chu == "both" else 8
+        cfg = default_cli_config(M, F, hidden_dim=[64] * pt["HL"], rnn_dim=[pt["SMV"]],
+                                 num_moments=k, dropout=dropout,
+                                 hidden_dim_moment=[pt["CHU"]] * pt["CHL"], rnn_dim_moment=[pt["CSMV"]])
+        out.append((cfg, float(pt["LR"]), pt))
+    return out
+
+
+def baseline_grid(M: int, F: int, grid: Dict = BASELINE_GRID) -> List[Tuple[Dict, float, Dict]]:
+    """BASELINE.json config 4's axes (hidden_dim x lr x dropout x num_moments, x SMV): 384."""
     keys = list(grid)
     out = []
     for vals in itertools.product(*(grid[k] for k in keys)):
         pt = dict(zip(keys, vals))
         cfg = default_cli_config(M, F, hidden_dim=[64] * pt["HL"], rnn_dim=[pt["SMV"]],
-                                 num_moments=pt["CHU"], dropout=dropout,
-                                 hidden_dim_moment=[pt["CHU"]] * pt["CHL"], rnn_dim_moment=[pt["CSMV"]])
+                                 num_moments=pt["K"], dropout=pt["DROPOUT"])
         out.append((cfg, float(pt["LR"]), pt))
     return out
+
+
+def arch_key(spec: ModelSpec) -> str:
+    """Cost-table key of an architecture: SDF depth, LSTM width, moment hidden widths, moments."""
+    return f"HL{len(spec.hidden)}-H{spec.rnn_hidden}-CH{'x'.join(map(str, spec.moment_hidden)) or 0}-K{spec.num_moments}"
+
+
+def _load_costs() -> Dict[str, float]:
+    try:
+        with open(COSTS_FILE) as fh:
+            return {k: float(v) for k, v in json.load(fh)["ms_per_epoch"].items()}
+    except (OSError, ValueError, KeyError):
+        return {}
+
+
+def bucket_cost(spec: ModelSpec, members: int = 8, table: Optional[Dict[str, float]] = None) -> float:
+    """Relative cost of training one bucket (``members`` configs batched in one engine).
+
+    The measured per-epoch time of the architecture (``sweep_costs.json``) when listed, else an
+    analytic per-epoch estimate in the same unit (ms at 600 x 3000 x 46, 8 members): a fixed
+    serial part (LSTM recurrence, loss passes, launches), plus tower work that grows with the
+    SDF depth (the HL >= 3 backward kernels run with spilled registers) and with the padded
+    moment-tower width and depth."""
+    table = _load_costs() if table is None else table
+    key = arch_key(spec)
+    if key in table:
+        return table[key] * members / 8.0
+    hl = len(spec.hidden)
+    wm = max([spec.num_moments] + list(spec.moment_hidden))
+    wmb = 1 if wm <= 16 else (2 if wm <= 32 else 4)
+    sdf = 0.45 * hl * (1.6 if hl >= 3 else 1.0)
+    mom = 0.12 * wmb * (1 + len(spec.moment_hidden))
+    serial = 0.5 + (0.1 if spec.rnn_hidden > 4 else 0.0)
+    return (serial + (sdf + mom) * members / 8.0)
 
 
 def buckets(entries: Sequence[Tuple[Dict, float, Dict]]) -> List[List[int]]:
@@ -108,13 +173,26 @@ def run_bucket(entries, idx: List[int], batches: Dict[str, Dict], device: torch.
     return out
 
 
+def plan(entries, world: int, balance: str = "lpt") -> Tuple[List[List[int]], List[List[int]], List[float]]:
+    """(buckets, per-rank bucket lists, per-bucket cost). ``balance``: "lpt" (cost-aware,
+    default) or "round_robin"."""
+    bks = buckets(entries)
+    table = _load_costs()
+    costs = [bucket_cost(ModelSpec.from_config(entries[b[0]][0]), len(b), table) for b in bks]
+    if balance == "lpt":
+        owners = comm.assign_lpt(costs, world)
+    else:
+        owners = [comm.shard(len(bks), r, world) for r in range(world)]
+    return bks, owners, costs
+
+
 def run_sweep(batches: Dict[str, Dict], entries, dist: Optional[comm.Dist] = None, epochs=(256, 64, 1024),
               ignore_epoch: int = 64, seed: int = 42, selection_sign: float = 1.0,
               rank_sign: float = -1.0, fail_buckets: Sequence[int] = (), verbose: bool = False,
-              concurrency: Optional[int] = None) -> Dict:
+              concurrency: Optional[int] = None, balance: str = "lpt") -> Dict:
     d = dist or comm.Dist()
-    bks = buckets(entries)
-    mine = comm.shard(len(bks), d.rank, d.world)
+    bks, owners, costs = plan(entries, d.world, balance)
+    mine = owners[d.rank]
     local = {}
     errors = {}
     t_start = time.time()
@@ -164,7 +242,7 @@ def run_sweep(batches: Dict[str, Dict], entries, dist: Optional[comm.Dist] = Non
     tab = np.full((len(mine), width, len(METRICS)), np.nan)
     for k, b in enumerate(mine):
         tab[k, :len(bks[b])] = local[b]
-    allb = comm.all_gather_rows(d, tab, len(bks), mine)
+    allb = comm.all_gather_rows(d, tab, len(bks), mine, owners)
     table = np.full((len(entries), len(METRICS)), np.nan)
     for b, ids in enumerate(bks):
         table[ids] = allb[b, :len(ids)]
@@ -172,8 +250,12 @@ def run_sweep(batches: Dict[str, Dict], entries, dist: Optional[comm.Dist] = Non
     score = np.where(ok, rank_sign * table[:, 1], -np.inf)
     best = int(np.argmax(score)) if ok.any() else -1
     walls = comm.all_gather_rows(d, np.array([[time.time() - t_start]]), d.world, [d.rank])[:, 0]
+    loads = [float(sum(costs[b] for b in o)) for o in owners]
     return {"n_configs": len(entries), "n_buckets": len(bks), "n_ok": int(ok.sum()),
             "world_size": d.world, "wall_s": float(walls.max()),
+            "wall_s_per_rank": [float(w) for w in walls], "balance": balance,
+            "predicted_load_per_rank": loads,
+            "predicted_imbalance": (max(loads) / min(loads)) if min(loads) > 0 else float("inf"),
             "failed": [int(i) for i in np.where(~ok)[0]], "best_index": best,
             "best_point": entries[best][2] if best >= 0 else None,
             "best_valid_sharpe": float(table[best, 1]) if best >= 0 else None,
@@ -195,6 +277,11 @@ def main(argv=None):
     p.add_argument("--limit", type=int, default=None, help="only the first K grid points")
     p.add_argument("--out", type=str, default=None, help="write the metric table (.npz) here")
     p.add_argument("--cpu", action="store_true")
+    p.add_argument("--grid", choices=["paper", "baseline"], default="paper",
+                   help="paper: Table A.VIII axes; baseline: BASELINE.json config 4 axes")
+    p.add_argument("--chu", choices=["both", "hidden"], default="both",
+                   help="paper grid: CHU sets the moment count and hidden width (both) or the hidden width only")
+    p.add_argument("--balance", choices=["lpt", "round_robin"], default="lpt")
     a = p.parse_args(argv)
     if not a.synthetic and not a.data_dir:
         p.error("--data_dir or --synthetic is required")
@@ -202,11 +289,11 @@ def main(argv=None):
     batches = load_batches(a, d)
     M = batches["train"]["macro_features"].shape[-1] if "macro_features" in batches["train"] else 0
     F = batches["train"]["individual_features"].shape[-1]
-    entries = paper_grid(M, F)
+    entries = paper_grid(M, F, chu=a.chu) if a.grid == "paper" else baseline_grid(M, F)
     if a.limit:
         entries = entries[:a.limit]
     res = run_sweep(batches, entries, d, (a.epochs_unc, a.epochs_moment, a.epochs), a.ignore_epoch, a.seed,
-                    verbose=True)
+                    verbose=True, balance=a.balance)
     if d.is_main:
         if a.out:
             np.savez(a.out, table=res["table"], metrics=np.array(METRICS))

@@ -1,0 +1,223 @@
+"""Reference-precision (fp32) native engine on an MI355X against the CPU trainer, which reproduces
+the reference bit-for-bit on the CPU (tests/test_model_parity.py, tests/test_trainer_cli.py).
+
+SURVEY §7.3 acceptance test: dropout = 0, the default architecture, consecutive optimisation
+steps through phases 1, 2 and 3; every step's training loss and gradient norm, and every
+parameter tensor afterwards, within 1e-5 relative of the CPU trajectory
+(`/root/reference/src/train.py:45-103`). The loss / schedule branches that the bf16 tests do not
+reach (residual loss, unweighted loss, no zero-mean normalisation, raw-macro SDF without LSTM, a
+2-layer LSTM, paper-sign model selection) run through the same comparison, and one short full
+``train_3phase`` compares the history, the selected checkpoints and the final state.
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from deeplearninginassetpricing_paperreplication_amd.config import default_cli_config
+from deeplearninginassetpricing_paperreplication_amd.data.synthetic import generate_panel_fast
+from deeplearninginassetpricing_paperreplication_amd.models.gan import AssetPricingGAN
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from deeplearninginassetpricing_paperreplication_amd.ops import native
+    native.load(required=True)
+
+
+def _splits(T=(36, 12, 18), N=160, F=46, M=8, seed=0):
+    ret, feats, mask, mac = generate_panel_fast(sum(T), N, F, M, seed=seed)
+    mac = (mac - mac[:T[0]].mean(0)) / (mac[:T[0]].std(0, unbiased=False) + 1e-8)
+    cuts = [(0, T[0]), (T[0], T[0] + T[1]), (T[0] + T[1], sum(T))]
+    return [{"returns": ret[a:b].contiguous(), "individual_features": feats[a:b].contiguous(),
+             "mask": mask[a:b].contiguous(), "macro_features": mac[a:b].contiguous()} for a, b in cuts]
+
+
+def _cpu_trajectory(model, b, sched, lr):
+    """Per-step (loss, grad norm) of the reference step function on ``model`` (modified in place)."""
+    from deeplearninginassetpricing_paperreplication_amd.train.trainer import train_epoch
+    opt_s = torch.optim.Adam(model.sdf_net.parameters(), lr=lr)
+    opt_m = torch.optim.Adam(model.moment_net.parameters(), lr=lr)
+    out = []
+    for phase, n in sched:
+        for _ in range(n):
+            if phase == 2:                     # SDF frozen (`src/train.py:309-312`)
+                for p in model.sdf_net.parameters():
+                    p.requires_grad_(False)
+                r = train_epoch(model, opt_m, b, "cpu", "moment", scope="moment")
+                for p in model.sdf_net.parameters():
+                    p.requires_grad_(True)
+            else:
+                r = train_epoch(model, opt_s, b, "cpu", "unconditional" if phase == 1 else "conditional",
+                                scope="sdf")
+            out.append((r["loss"], r["grad_norm"]))
+    return np.array(out, np.float64)
+
+
+def _gpu_trajectory(model, splits, sched, lr):
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import GANEngine, HIST
+    eng = GANEngine(model.spec, 1, max_epochs=64, precision="fp32")
+    eng.set_data(*splits)
+    eng.set_model(0, model, 7)
+    for phase, n in sched:
+        eng.eng.begin_phase(phase)
+        eng.run(phase, n, lr, 0)
+    eng.eng.sync()
+    h = eng.history_rows(0)
+    return eng, np.stack([h[:, HIST["train_loss"]], h[:, HIST["grad_norm"]]], 1).astype(np.float64)
+
+
+# With the per-period zero-mean normalisation (normalize_w, `/root/reference/src/model.py:274-279`)
+# the SDF output bias cancels out of every loss: its exact gradient is 0 and both executors only
+# see rounding noise (~1e-10), which Adam rescales to steps of up to lr. The two trajectories of
+# that one scalar therefore differ by noise-driven steps; it is checked against that bound
+# (steps x lr) instead of the 1e-5 tolerance.
+NOISE_ONLY = "sdf_net.output_proj.bias"
+
+
+def _tensor_errors(sd_gpu, model, steps=None, lr=None):
+    """Per-tensor ||gpu - cpu|| / ||cpu||; the noise-only bias is checked here against its bound."""
+    out = {}
+    for k, v in model.state_dict().items():
+        ref = v.detach().double()
+        if k == NOISE_ONLY and model.spec.normalize_w and steps is not None:
+            assert float((sd_gpu[k].double() - ref).abs().max()) <= 2 * steps * lr * 1.01, k
+            continue
+        out[k] = float((sd_gpu[k].double() - ref).norm() / max(ref.norm(), 1e-30))
+    return out
+
+
+SCHED = ((1, 4), (2, 2), (3, 4))
+
+BRANCHES = {
+    "default": {},
+    "residual_loss": {"residual_loss_factor": 0.5},
+    "unweighted_loss": {"weighted_loss": False},
+    "no_normalisation": {"normalize_w": False},
+    "no_lstm_raw_macro": {"use_rnn": False},
+    "lstm_2_layers": {"num_units_rnn": [3, 4]},
+    "moment_hidden": {"hidden_dim_moment": [16]},
+}
+
+
+def _double(b):
+    return {k: (v.double() if v.is_floating_point() else v) for k, v in b.items()}
+
+
+@pytest.mark.parametrize("branch", list(BRANCHES))
+def test_fp32_trajectory_matches_cpu_trainer(branch):
+    """10 consecutive steps (4 unconditional, 2 moment, 4 conditional) of the default config and of
+    every loss / architecture branch: losses, grad norms and all parameters within 1e-5 of the
+    CPU trainer.
+
+    Where the CPU fp32 trajectory itself drifts from exact (float64) arithmetic by more than
+    that -- ill-conditioned gradients: with the raw macro series as SDF inputs, the per-period
+    column gradients sum dz over each period's stocks, and the zero-mean normalisation makes those
+    sums cancel almost exactly, so Adam turns their rounding noise into lr-sized steps -- the
+    criterion is that the GPU is no further from the float64 trajectory than the reference's own
+    fp32 arithmetic is (x2)."""
+    splits = _splits()
+    cfg = default_cli_config(8, 46, dropout=0.0)
+    cfg.update(BRANCHES[branch])
+    torch.manual_seed(0)
+    model = AssetPricingGAN(cfg)
+    gpu_model = copy.deepcopy(model)
+    m64 = copy.deepcopy(model).double()
+    lr = 1e-3
+    eng, got = _gpu_trajectory(gpu_model, splits, SCHED, lr)
+    ref = _cpu_trajectory(model, splits[0], SCHED, lr)
+    rel = np.abs(got - ref) / np.maximum(np.abs(ref), 1e-30)
+    errs = _tensor_errors(eng.state_dict(0), model, steps=sum(n for _, n in SCHED), lr=lr)
+    worst = max(errs, key=errs.get)
+    if branch == "default" or (rel.max() < TOL and errs[worst] < TOL):
+        assert rel.max() < TOL, (branch, rel.max(axis=0), got[:3], ref[:3])
+        assert errs[worst] < TOL, (branch, worst, errs[worst])
+        return
+    ref64 = _cpu_trajectory(m64, _double(splits[0]), SCHED, lr)
+    e_gpu = np.abs(got - ref64) / np.abs(ref64)
+    e_cpu = np.abs(ref - ref64) / np.abs(ref64)
+    assert e_gpu.max() <= 2 * e_cpu.max() + 1e-6, (branch, e_gpu.max(), e_cpu.max())
+    sd64 = {k: v for k, v in m64.state_dict().items()}
+    sdg = eng.state_dict(0)
+    for k, v in model.state_dict().items():
+        if k == NOISE_ONLY and model.spec.normalize_w:
+            continue
+        d_gpu = float((sdg[k].double() - sd64[k]).norm() / sd64[k].norm())
+        d_cpu = float((v.double() - sd64[k]).norm() / sd64[k].norm())
+        assert d_gpu <= 2 * d_cpu + TOL, (branch, k, d_gpu, d_cpu)
+
+
+@pytest.mark.parametrize("selection_sign", [1.0, -1.0])
+def test_fp32_train_3phase_matches_cpu(selection_sign):
+    """A short full schedule through ``train_3phase`` on both executors (dropout 0): the history
+    (train / valid / test losses and Sharpe ratios, both phases), the best-Sharpe checkpoint the
+    selection picked (reference un-negated Sharpe, or the paper sign) and the final state."""
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import train_3phase_gpu
+    from deeplearninginassetpricing_paperreplication_amd.train.trainer import _train_3phase_cpu
+    tr, va, te = _splits()
+    cfg = default_cli_config(8, 46, dropout=0.0)
+    torch.manual_seed(0)
+    m_cpu = AssetPricingGAN(cfg)
+    m_gpu = copy.deepcopy(m_cpu)
+    kw = dict(num_epochs_unc=6, num_epochs_moment=3, num_epochs=6, lr=1e-3, print_freq=100, ignore_epoch=1)
+    m_gpu, h_gpu = train_3phase_gpu(cfg, tr, va, te, device="cuda", precision="fp32",
+                                    selection_sign=selection_sign, verbose=False, models=[m_gpu], seeds=[7],
+                                    **kw)
+    m_cpu, h_cpu = _train_3phase_cpu(cfg, tr, va, te, torch.device("cpu"), kw["num_epochs_unc"],
+                                     kw["num_epochs_moment"], kw["num_epochs"], kw["lr"], 100, None,
+                                     kw["ignore_epoch"], selection_sign, False, model=m_cpu)
+    assert h_gpu["phase"] == h_cpu["phase"]
+    for k in ("train_loss", "valid_loss", "test_loss"):
+        a, b = np.asarray(h_gpu[k]), np.asarray(h_cpu[k])
+        assert np.abs(a - b).max() <= TOL * np.abs(b).max(), k
+    for k in ("train_sharpe", "valid_sharpe", "test_sharpe"):
+        a, b = np.asarray(h_gpu[k]), np.asarray(h_cpu[k])
+        assert np.abs(a - b).max() < 1e-4, (k, a, b)
+    errs = _tensor_errors({k: v.cpu() for k, v in m_gpu.state_dict().items()}, m_cpu,
+                          steps=kw["num_epochs_unc"] + kw["num_epochs"], lr=kw["lr"])
+    worst = max(errs, key=errs.get)
+    assert errs[worst] < TOL, (worst, errs[worst])
+
+
+def test_fp32_forward_and_gradients_tight():
+    """One forward / backward per phase at reference precision: weights, moments, losses and the
+    full gradient vector of the trained scope within 1e-5 (the bf16 tests allow 3e-2 / 5e-2)."""
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import GANEngine, flatten_state
+    b = _splits()[0]
+    cfg = default_cli_config(8, 46, dropout=0.0)
+    torch.manual_seed(0)
+    model = AssetPricingGAN(cfg)
+    eng = GANEngine(model.spec, 1, max_epochs=8, precision="fp32")
+    eng.set_data(b)
+    eng.set_model(0, model, 7)
+    T, N = b["mask"].shape
+    m = b["mask"].numpy()
+    with torch.no_grad():
+        out = model(b["macro_features"], b["individual_features"], b["returns"], b["mask"], phase="conditional")
+    eng.eng.forward_split(0, False, True)
+    w = eng.eng.read_ws(0, 0, "wn").reshape(T, N)
+    assert np.abs(w - out["weights"].numpy()).max() < TOL * np.abs(out["weights"].numpy()).max()
+    h = eng.eng.read_ws(0, 0, "h").reshape(T, N, -1)
+    assert np.abs(h[m] - out["moments"].permute(1, 2, 0).numpy()[m]).max() < TOL
+    sc = eng.eng.read_ws(0, 0, "scal")
+    assert abs(sc[0] - out["loss_conditional"].item()) < TOL * out["loss_conditional"].item()
+    assert abs(sc[1] - out["loss_unconditional"].item()) < TOL * out["loss_unconditional"].item()
+    P_sdf = model.spec.param_counts()[0]
+    for phase, pname in ((1, "unconditional"), (3, "conditional"), (2, "moment")):
+        model.zero_grad()
+        o = model(b["macro_features"], b["individual_features"], b["returns"], b["mask"], phase=pname)
+        o["loss"].backward()
+        ref = flatten_state({k: (p.grad if p.grad is not None else torch.zeros_like(p))
+                             for k, p in model.named_parameters()}, model.spec)
+        eng.eng.backward_only(phase)
+        got = eng.eng.get_grads(0)
+        sl = slice(0, P_sdf) if phase != 2 else slice(P_sdf, None)
+        err = np.linalg.norm(got[sl] - ref[sl]) / np.linalg.norm(ref[sl])
+        assert err < TOL, (phase, err)
