@@ -130,7 +130,7 @@ class Engine {
     HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_mid_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_a_, hipEventDisableTiming));
-    eval_gx_ = env_int("DLAP_EVAL_GX", 512);
+    eval_gx_ = env_int("DLAP_EVAL_GX", 256);
     b_wait_ = env_int("DLAP_B_WAIT", 0);
     side_metrics_ = env_int("DLAP_SIDE_METRICS", 0) != 0;
     zx_eval_ = env_int("DLAP_ZX_EVAL", 1) != 0;
