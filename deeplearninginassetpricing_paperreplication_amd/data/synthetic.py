@@ -250,12 +250,17 @@ def _row_quantiles(x, qs):
 
 
 def generate_panel_fast(T: int, N: int, F: int, M: int, seed: int = 0, device: str = "cpu",
-                        n_factors: int = 5, chunk: int = 16):
+                        n_factors: int = 5, chunk: int = 16, return_latent: bool = False):
     """Return (returns [T,N] f32, features [T,N,F] f32, mask [T,N] bool, macro [T,M] f32).
 
     Same model as the reference generator; invalid entries are already zero-filled (the
     loader's view of the data).  Runs in ``chunk``-period slices so a 600×30000×512 panel
     needs only one output copy; on a GPU it takes seconds.
+
+    ``return_latent``: also return the generator's hidden truth as a 5th element, a dict with the
+    factor returns ``f`` [T,K], the loadings ``b`` [N,K], the idiosyncratic vols ``idio`` [N],
+    the factor innovation vols ``vols`` [K] and the AR(1) coefficient ``rho`` (for the oracle
+    Sharpe ceiling, ``analysis.oracle``). The draws are identical with and without it.
     """
     import torch
     g = torch.Generator(device=device).manual_seed(seed)
@@ -315,6 +320,9 @@ def generate_panel_fast(T: int, N: int, F: int, M: int, seed: int = 0, device: s
         mask |= extra & low[:, None]
     ret = torch.where(mask, ret, torch.zeros((), device=dev))
     feats.mul_(mask[:, :, None])
+    if return_latent:
+        latent = {"f": f, "b": b, "idio": idio, "vols": vols, "rho": 0.1}
+        return ret.float(), feats, mask, mac.float(), latent
     return ret.float(), feats, mask, mac.float()
 
 
