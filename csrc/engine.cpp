@@ -18,6 +18,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstring>
 #include <map>
@@ -46,9 +47,13 @@ void dlap_throw_hip(hipError_t e, const char* what, const char* file, int line) 
 // another thread is capturing an epoch graph: every such call and every capture takes this lock.
 // Graph replays, the long part of a run, are outside it.
 static std::mutex g_legacy_mu;
+// Host-blocking HIP calls issued by the engine (synchronous copies / allocations, stream syncs):
+// the module-API tests assert that a training step issues none.
+static std::atomic<long long> g_blocking{0};
 #define HIP_LEGACY(expr)                                \
   do {                                                  \
     std::lock_guard<std::mutex> _legacy_guard(g_legacy_mu); \
+    g_blocking.fetch_add(1, std::memory_order_relaxed); \
     HIP_OK(expr);                                       \
   } while (0)
 
@@ -126,6 +131,7 @@ class Engine {
       HIP_OK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
       HIP_OK(hipStreamCreateWithFlags(&st2_, hipStreamNonBlocking));
     }
+    own_st_ = st_;
     HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_mid_, hipEventDisableTiming));
@@ -155,18 +161,31 @@ class Engine {
       S.wproj.alloc((size_t)(md_.proj_mp + 1) * md_.proj_np);
     }
     ws_.resize((size_t)G * 3);
+    {   // per-model re-pack jobs (buffers allocated above, never reallocated)
+      std::vector<UpdJob> pj(G);
+      for (int g = 0; g < G; ++g) {
+        ModelState& S = models_[g];
+        pj[g].params = S.params.p;
+        pj[g].blob = reinterpret_cast<bf16x8*>(S.blob.p);
+        pj[g].blob0 = reinterpret_cast<bf16x8*>(S.blob0.p);
+        pj[g].aux = S.aux.p;
+        pj[g].wproj = S.wproj.p;
+      }
+      upload(j_pack_, pj);
+    }
   }
   ~Engine() {
     // drain both streams before the graphs, events and (member) buffers go away
     if (st2_) (void)hipStreamSynchronize(st2_);
     if (st_) (void)hipStreamSynchronize(st_);
+    if (own_st_ && own_st_ != st_) (void)hipStreamSynchronize(own_st_);
     for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
     if (ev_fork_) (void)hipEventDestroy(ev_fork_);
     if (ev_join_) (void)hipEventDestroy(ev_join_);
     if (ev_mid_) (void)hipEventDestroy(ev_mid_);
     if (ev_a_) (void)hipEventDestroy(ev_a_);
     if (st2_) (void)hipStreamDestroy(st2_);
-    if (st_) (void)hipStreamDestroy(st_);
+    if (own_st_) (void)hipStreamDestroy(own_st_);
   }
 
   // ---------------------------------------------------------------- description ----------
@@ -410,6 +429,7 @@ class Engine {
   // and join before the Adam update:   head | pipe x (n-1) | tail.
   void run_epochs(int phase, int n, float lr, int ignore_epoch, float sel, bool use_graph) {
     if (!splits_[0].set) throw std::runtime_error("train split not set");
+    if (ext_stream_) throw std::runtime_error("run_epochs needs the engine's own streams (set_stream(0))");
     if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
     if (n <= 0) return;
     if (phase == 2) h_valid_ = false;     // the moment net trains: the cached moments go stale
@@ -447,9 +467,9 @@ class Engine {
   void set_pipeline(bool on) { pipeline_ = on; }
 
   // Pieces used by the module-level API / tests (no bookkeeping).
-  void forward_split(int s, bool train_mode, bool do_mom) {
+  void forward_split(int s, bool train_mode, bool do_mom, bool wait = true) {
     if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
-    fwd_only(s, train_mode, do_mom);
+    fwd_only(s, train_mode, do_mom, wait);
   }
   void train_step(int phase, float lr) {
     if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
@@ -457,11 +477,62 @@ class Engine {
     else ensure_moments();
     enqueue_train(phase, lr);
   }
-  void backward_only(int phase) {   // losses + gradients, no optimiser step
+  void backward_only(int phase, bool wait = true) {   // losses + gradients, no optimiser step
     if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
     if (phase != 2) ensure_moments();
     enqueue_train_grads(phase);
-    sync();
+    if (wait) sync();
+  }
+
+  // ---- module API (ops/fused.py): stream-ordered, no host synchronisation ----------------
+  // Run the engine's launches on an external stream (torch's current stream), so module-level
+  // forward / backward calls are ordered with the surrounding torch ops. Epoch graphs need the
+  // engine's own streams (run_epochs refuses an external one).
+  void set_stream(uintptr_t st) {
+    hipStream_t want = st ? reinterpret_cast<hipStream_t>(st) : own_st_;
+    if (want == st_) return;
+    sync();                                   // work queued on the previous stream completes first
+    st_ = want;
+    ext_stream_ = st != 0;
+  }
+  // parameters from device memory (a flat fp32 vector in state_dict order), re-packed in order
+  void set_params_dev(int g, uintptr_t src) {
+    check_g(g);
+    HIP_OK(hipMemcpyAsync(models_[g].params.p, reinterpret_cast<const void*>(src), md_.P * sizeof(float),
+                          hipMemcpyDeviceToDevice, st_));
+    pack(g, false);
+    h_valid_ = false;
+  }
+  // dropout stream position of model g (module API: fresh masks per forward), no host sync
+  void set_drop_step(int g, int step) { launch_set_int(models_[check_g(g)].drop_step.p, step, st_); }
+  // device-to-device copies of engine state into caller-owned device memory (stream-ordered)
+  long copy_ws(int g, int s, const std::string& name, uintptr_t dst) {
+    ModelSplitWS& W = ws(g, s);
+    const std::map<std::string, DevBuf<float>*> m = {
+        {"wn", &W.wn}, {"h", &W.h}, {"P", &W.P}, {"port", &W.port}, {"scal", &W.scal}, {"pp", &W.pp}};
+    auto it = m.find(name);
+    if (it == m.end()) throw std::invalid_argument("copy_ws: unknown buffer " + name);
+    const DevBuf<float>& b = *it->second;
+    if (b.n) HIP_OK(hipMemcpyAsync(reinterpret_cast<void*>(dst), b.p, b.n * sizeof(float), hipMemcpyDeviceToDevice, st_));
+    return (long)b.n;
+  }
+  void copy_grads(int g, uintptr_t dst) {
+    HIP_OK(hipMemcpyAsync(reinterpret_cast<void*>(dst), models_[check_g(g)].grads.p, md_.P * sizeof(float),
+                          hipMemcpyDeviceToDevice, st_));
+  }
+  // final LSTM state (h_n, c_n) [nrnn][H] of the train split after a forward: the last step of
+  // every layer's saved outputs / cells
+  void copy_hidden(int g, uintptr_t dst_h, uintptr_t dst_c) {
+    ModelSplitWS& W = ws(check_g(g), 0);
+    const int T = splits_[0].T, H = md_.H;
+    if (md_.nrnn == 0 || T == 0) return;
+    for (int l = 0; l < md_.nrnn; ++l) {
+      const size_t off = ((size_t)l * T + (T - 1)) * H;
+      HIP_OK(hipMemcpyAsync(reinterpret_cast<float*>(dst_h) + (size_t)l * H, W.sh.p + off, H * sizeof(float),
+                            hipMemcpyDeviceToDevice, st_));
+      HIP_OK(hipMemcpyAsync(reinterpret_cast<float*>(dst_c) + (size_t)l * H, W.sc.p + off, H * sizeof(float),
+                            hipMemcpyDeviceToDevice, st_));
+    }
   }
 
   py::array_t<float> read_ws(int g, int s, const std::string& name) {
@@ -484,12 +555,20 @@ class Engine {
     HIP_LEGACY(hipMemcpy(out.mutable_data(), S.blob.p, S.blob.n * 2, hipMemcpyDeviceToHost));
     return out;
   }
-  void sync() { HIP_OK(hipStreamSynchronize(st_)); }
+  void sync() {
+    g_blocking.fetch_add(1, std::memory_order_relaxed);
+    HIP_OK(hipStreamSynchronize(st_));
+  }
   uintptr_t stream() const { return (uintptr_t)st_; }
 
  private:
   int G_, max_epochs_;
   hipStream_t st_ = nullptr;
+  hipStream_t own_st_ = nullptr;             // the engine's stream (st_ may be an external one)
+  bool ext_stream_ = false;
+  DevBuf<char> j_pack_;                      // per-model re-pack jobs
+  struct FwdTables { DevBuf<char> r, m, l, w; bool built = false; };
+  std::map<int, FwdTables> fwd_tables_;      // module-API forward job tables (per split / mode)
   int unroll_ = 1;                           // pipelined epochs per graph launch (DLAP_UNROLL)
   bool prio_ = false;                        // stream/node priorities (DLAP_PRIO)
   hipStream_t st2_ = nullptr;                // evaluation branch of the pipelined epoch graph
@@ -560,18 +639,9 @@ class Engine {
     return b;
   }
 
-  void pack(int g) {
-    UpdJob J{};
-    J.params = models_[g].params.p;
-    J.blob = reinterpret_cast<bf16x8*>(models_[g].blob.p);
-    J.blob0 = reinterpret_cast<bf16x8*>(models_[g].blob0.p);
-    J.aux = models_[g].aux.p;
-    J.wproj = models_[g].wproj.p;
-    DevBuf<char> tmp;
-    std::vector<UpdJob> v{J};
-    upload(tmp, v);
-    launch_pack(nullptr, reinterpret_cast<const UpdJob*>(tmp.p), 1, reinterpret_cast<const ModelDesc*>(d_desc_.p), md_, st_);
-    sync();
+  void pack(int g, bool wait = true) {
+    launch_pack(nullptr, as<UpdJob>(j_pack_) + g, 1, reinterpret_cast<const ModelDesc*>(d_desc_.p), md_, st_);
+    if (wait) sync();
   }
 
   // ------------------------------------------------------------ model descriptor ------
@@ -776,7 +846,7 @@ class Engine {
   }
 
   // ------------------------------------------------------------ job tables ------------
-  RnnJob rnn_job(int g, int s, bool train) {
+  RnnJob rnn_job(int g, int s, bool train, int save = -1) {
     ModelSplitWS& W = ws(g, s);
     SplitDev& D = splits_[s];
     RnnJob J{};
@@ -785,7 +855,9 @@ class Engine {
     J.macro = D.macro.p;
     J.T = D.T;
     J.out = W.pp.p;
-    if (train && md_.nrnn > 0) { J.sg = W.sg.p; J.sc = W.sc.p; J.sh = W.sh.p; }
+    // save: keep the per-layer gates / cells / outputs (BPTT; module API final state);
+    // default = train. Only the train split (s == 0) has those buffers.
+    if ((save < 0 ? train : save != 0) && md_.nrnn > 0 && s == 0) { J.sg = W.sg.p; J.sc = W.sc.p; J.sh = W.sh.p; }
     J.xg = W.xg.p; J.xin = W.xin.p;
     J.abias = W.abias.p;
     J.step = models_[g].drop_step.p;
@@ -865,6 +937,7 @@ class Engine {
   void rebuild_jobs() {
     for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
     graphs_.clear();
+    fwd_tables_.clear();
     std::vector<RnnJob> rt, re;
     std::vector<LossJob> le;
     std::vector<MlpJob> me;
@@ -1139,23 +1212,33 @@ class Engine {
     graphs_.emplace(key, exec);
     return exec;
   }
-  void fwd_only(int s, bool train_mode, bool do_mom) {
+  void fwd_only(int s, bool train_mode, bool do_mom, bool wait) {
     const SplitDev& D = splits_[s];
     if (!D.set) throw std::runtime_error("split not set");
-    // build ad-hoc jobs for one split of every model
-    std::vector<RnnJob> rj;
-    std::vector<MlpJob> mj;
-    std::vector<LossJob> lj;
-    std::vector<WideJob> wj;
-    for (int g = 0; g < G_; ++g) {
-      rj.push_back(rnn_job(g, s, train_mode));
-      mj.push_back(mlp_job(g, s, train_mode, true, do_mom));
-      lj.push_back(loss_job(g, s, 0));
-      wj.push_back(wide_job(g, s, true, do_mom));
-      if (!do_mom) lj.back().h = nullptr;
+    // job tables of (split, mode) for every model, built once per rebuild (module API calls
+    // issue no host allocation / synchronous copy). The train split keeps its LSTM state
+    // (final (h, c) of every layer for the module API).
+    const int key = s * 4 + (train_mode ? 2 : 0) + (do_mom ? 1 : 0);
+    FwdTables& F = fwd_tables_[key];
+    if (!F.built) {
+      std::vector<RnnJob> rj;
+      std::vector<MlpJob> mj;
+      std::vector<LossJob> lj;
+      std::vector<WideJob> wj;
+      for (int g = 0; g < G_; ++g) {
+        rj.push_back(rnn_job(g, s, train_mode, s == 0 ? 1 : 0));
+        mj.push_back(mlp_job(g, s, train_mode, true, do_mom));
+        lj.push_back(loss_job(g, s, 0));
+        wj.push_back(wide_job(g, s, true, do_mom));
+        if (!do_mom) lj.back().h = nullptr;
+      }
+      upload(F.r, rj); upload(F.m, mj); upload(F.l, lj); upload(F.w, wj);
+      F.built = true;
     }
-    DevBuf<char> a, b, c, w;
-    upload(a, rj); upload(b, mj); upload(c, lj); upload(w, wj);
+    DevBuf<char>& a = F.r;
+    DevBuf<char>& b = F.m;
+    DevBuf<char>& c = F.l;
+    DevBuf<char>& w = F.w;
     const bool zx = md_.md.wide && zx_eval_ && !train_mode;
     if (md_.md.wide && !zx) launch_proj0(as<WideJob>(w), G_, gx_proj_[s], md_.md, md_.WMB, st_);
     launch_prologue(as<RnnJob>(a), G_, D.T, dd(), md_, st_);
@@ -1164,7 +1247,7 @@ class Engine {
     launch_period_fwd(as<LossJob>(c), G_, D.T, st_);
     launch_asset(as<LossJob>(c), G_, D.N, md_.K, st_);
     launch_job_metrics(as<LossJob>(c), G_, st_);
-    sync();
+    if (wait) sync();
   }
 };
 
@@ -1197,12 +1280,20 @@ PYBIND11_MODULE(_dlap_hip, m) {
       .def("run_epochs", &Engine::run_epochs, py::call_guard<py::gil_scoped_release>())
       .def("set_pipeline", &Engine::set_pipeline)
       .def("set_lr", &Engine::set_lr)
+      .def_static("blocking_calls", []() { return (long long)g_blocking.load(); })
       .def_static("rnn_timestamps", []() { return rnn_timestamps(); })
       .def_static("loss_timestamps", []() { return loss_timestamps(); })
       .def_static("mlp_timestamps", []() { return mlp_timestamps(); })
-      .def("forward_split", &Engine::forward_split)
+      .def("forward_split", &Engine::forward_split, py::arg("s"), py::arg("train_mode"), py::arg("do_mom"),
+           py::arg("wait") = true)
       .def("train_step", &Engine::train_step)
-      .def("backward_only", &Engine::backward_only)
+      .def("backward_only", &Engine::backward_only, py::arg("phase"), py::arg("wait") = true)
+      .def("set_stream", &Engine::set_stream)
+      .def("set_params_dev", &Engine::set_params_dev)
+      .def("set_drop_step", &Engine::set_drop_step)
+      .def("copy_ws", &Engine::copy_ws)
+      .def("copy_grads", &Engine::copy_grads)
+      .def("copy_hidden", &Engine::copy_hidden)
       .def("read_ws", &Engine::read_ws)
       .def("read_aux", &Engine::read_aux)
       .def("read_blob", &Engine::read_blob)

@@ -234,6 +234,18 @@ __global__ __launch_bounds__(256) void k_pack(const UpdJob* __restrict__ jobs,
   }
 }
 
+// One int written on the stream (module API: the dropout stream position of a model), so the
+// host never touches device memory synchronously between calls. The store sits under a lane
+// test (a vector store, not a scalar one).
+__global__ __launch_bounds__(64) void k_set_int(int* p, int v) {
+  if (threadIdx.x == 0) gp(p)[0] = v;
+}
+
+void launch_set_int(int* p, int v, hipStream_t st) {
+  hipLaunchKernelGGL(k_set_int, dim3(1), dim3(64), 0, st, p, v);
+  HIP_OK(hipGetLastError());
+}
+
 static int pack_blocks_of(const ModelDesc& mh) {
   return (mh.md.blob_frags * 512 + mh.md.aux_floats + (mh.proj_mp + 1) * mh.proj_np + mh.md.b0_frags * 512 +
           255) / 256;

@@ -209,17 +209,24 @@ class AssetPricingGAN(nn.Module):
 
 class SimpleSDF(nn.Module):
     """Non-adversarial baseline: FFN on [macro ; x], zero-mean weights, unconditional loss
-    (`model.py:620-694`)."""
+    (`model.py:620-694`). On CUDA tensors it runs the native engine's SDF tower (see
+    ``ops.fused.simple_forward``)."""
 
     def __init__(self, macro_dim: int, individual_dim: int, hidden_dims: List[int] = (64, 64),
                  dropout: float = 0.05):
         super().__init__()
         hidden_dims = list(hidden_dims)
+        self.macro_dim, self.individual_dim = int(macro_dim), int(individual_dim)
         mods = _mlp(macro_dim + individual_dim, hidden_dims, dropout)
         mods.append(nn.Linear(hidden_dims[-1] if hidden_dims else macro_dim + individual_dim, 1))
         self.net = nn.Sequential(*mods)
 
     def forward(self, macro_features, individual_features, returns, mask):
+        if individual_features.is_cuda:          # native engine (ops.fused.simple_forward)
+            if not any(isinstance(m, nn.ReLU) for m in self.net):
+                raise NotImplementedError("SimpleSDF on the GPU engine needs at least one hidden layer")
+            from ..ops.fused import simple_forward
+            return simple_forward(self, macro_features, individual_features, returns, mask)
         T, N, _ = individual_features.shape
         if macro_features is not None:
             x = torch.cat([macro_features[:, None, :].expand(T, N, macro_features.shape[-1]),

@@ -38,9 +38,18 @@ def _to(data: Dict, device):
             data["returns"].to(device), data["mask"].to(device))
 
 
+def _sharpe_dev(p: torch.Tensor) -> torch.Tensor:
+    """``compute_sharpe`` on the device (0 when the unbiased std < 1e-8), no host sync."""
+    sd = p.std()
+    return torch.where(sd < 1e-8, torch.zeros_like(sd), p.mean() / sd)
+
+
 def train_epoch(model, optimizer, data: dict, device, phase: str = "conditional",
                 grad_clip: float = 1.0, scope: str = "all") -> dict:
-    """One full-batch optimisation step (`/root/reference/src/train.py:45-103`)."""
+    """One full-batch optimisation step (`/root/reference/src/train.py:45-103`).
+
+    The six returned scalars are gathered on the device and read back with ONE host
+    synchronisation (the reference calls ``.item()`` six times); values are identical."""
     model.train()
     macro, x, r, m = _to(data, device)
     optimizer.zero_grad()
@@ -51,14 +60,17 @@ def train_epoch(model, optimizer, data: dict, device, phase: str = "conditional"
         scope, model.parameters)()
     gn = torch.nn.utils.clip_grad_norm_(params, max_norm=grad_clip)
     optimizer.step()
-    return {
-        "loss": loss.item(),
-        "loss_unc": out.get("loss_unconditional", torch.tensor(0)).item(),
-        "loss_cond": out.get("loss_conditional", torch.tensor(0)).item(),
-        "loss_residual": out.get("loss_residual", torch.tensor(0)).item(),
-        "sharpe": compute_sharpe(out["portfolio_returns"].detach()),
-        "grad_norm": gn.item() if isinstance(gn, torch.Tensor) else gn,
-    }
+    dev = loss.device
+    z = torch.zeros((), device=dev)
+    vals = torch.stack([loss.detach().reshape(()).float(),
+                        out.get("loss_unconditional", z).detach().reshape(()).float().to(dev),
+                        out.get("loss_conditional", z).detach().reshape(()).float().to(dev),
+                        out.get("loss_residual", z).detach().reshape(()).float().to(dev),
+                        _sharpe_dev(out["portfolio_returns"].detach().float()).to(dev),
+                        torch.as_tensor(gn, device=dev).detach().reshape(()).float()])
+    v = vals.tolist()                                              # the one host sync
+    return {"loss": v[0], "loss_unc": v[1], "loss_cond": v[2], "loss_residual": v[3],
+            "sharpe": v[4], "grad_norm": v[5]}
 
 
 @torch.no_grad()

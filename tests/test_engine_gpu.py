@@ -199,6 +199,77 @@ def test_module_forward_and_backward_run_the_engine():
         assert cos > 0.995, (phase, cos)
 
 
+def test_module_train_epoch_one_host_sync_and_engine_hidden():
+    """``train_epoch(model, opt, data, 'cuda')``: after the first call (panel upload) a step issues
+    no host-blocking engine call and exactly one torch synchronisation (the metrics read-back);
+    the module's ``hidden`` is the engine LSTM's final (h_n, c_n), equal to nn.LSTM's."""
+    import warnings
+    from deeplearninginassetpricing_paperreplication_amd.ops import native
+    from deeplearninginassetpricing_paperreplication_amd.train.trainer import train_epoch
+    cfg = default_cli_config(8, 46, dropout=0.0, rnn_dim=[3, 4])
+    b = _batch()
+    torch.manual_seed(0)
+    cpu = AssetPricingGAN(cfg)
+    gpu = AssetPricingGAN(cfg)
+    gpu.load_state_dict(cpu.state_dict())
+    gpu.cuda()
+    dev = {k: v.cuda() for k, v in b.items()}
+    opt_c = torch.optim.Adam(cpu.sdf_net.parameters(), lr=1e-3)
+    opt_g = torch.optim.Adam(gpu.sdf_net.parameters(), lr=1e-3)
+    rc = [train_epoch(cpu, opt_c, b, "cpu", "conditional", scope="sdf")]
+    rg = [train_epoch(gpu, opt_g, dev, "cuda", "conditional", scope="sdf")]
+    n0 = native.load().Engine.blocking_calls()
+    torch.cuda.set_sync_debug_mode("warn")
+    try:
+        with warnings.catch_warnings(record=True) as w:
+            warnings.simplefilter("always")
+            rg.append(train_epoch(gpu, opt_g, dev, "cuda", "conditional", scope="sdf"))
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    syncs = [x for x in w if "synchroniz" in str(x.message).lower()]
+    assert len(syncs) == 1, [str(x.message) for x in syncs]
+    assert native.load().Engine.blocking_calls() == n0
+    rc.append(train_epoch(cpu, opt_c, b, "cpu", "conditional", scope="sdf"))
+    for a, c in zip(rg, rc):
+        assert _rel(a["loss"], c["loss"]) < 3e-2 and _rel(a["grad_norm"], c["grad_norm"]) < 5e-2
+    with torch.no_grad():
+        o = gpu(dev["macro_features"], dev["individual_features"], dev["returns"], dev["mask"])
+        _, (h_ref, c_ref) = gpu.sdf_net.macro_lstm.cpu()(b["macro_features"])
+        gpu.sdf_net.macro_lstm.cuda()
+    h_n, c_n = o["hidden"]
+    assert h_n.is_cuda and h_n.shape == h_ref.shape == (2, 1, 4)
+    assert _rel(h_n.cpu().numpy(), h_ref.numpy()) < 1e-4 and _rel(c_n.cpu().numpy(), c_ref.numpy()) < 1e-4
+
+
+def test_simple_sdf_runs_the_engine():
+    """SimpleSDF (`/root/reference/src/model.py:620-694`) on CUDA tensors: the engine's SDF tower
+    with the [macro ; x] column order, unweighted unconditional loss; forward and gradients vs the
+    CPU module."""
+    from deeplearninginassetpricing_paperreplication_amd.models.gan import SimpleSDF
+    from deeplearninginassetpricing_paperreplication_amd.ops import native
+    b = _batch()
+    torch.manual_seed(0)
+    cpu = SimpleSDF(8, 46, [64, 64], dropout=0.0)
+    gpu = SimpleSDF(8, 46, [64, 64], dropout=0.0)
+    gpu.load_state_dict(cpu.state_dict())
+    gpu.cuda()
+    dev = {k: v.cuda() for k, v in b.items()}
+    oc = cpu(b["macro_features"], b["individual_features"], b["returns"], b["mask"])
+    og = gpu(dev["macro_features"], dev["individual_features"], dev["returns"], dev["mask"])
+    assert og["weights"].is_cuda
+    assert _rel(og["weights"].detach().cpu().numpy(), oc["weights"].detach().numpy()) < 3e-2
+    assert _rel(og["loss"].item(), oc["loss"].item()) < 3e-2
+    assert _rel(og["sharpe"].item(), oc["sharpe"].item()) < 5e-2
+    oc["loss"].backward()
+    og["loss"].backward()
+    for pc, pg in zip(cpu.parameters(), gpu.parameters()):
+        a, c = pg.grad.cpu().reshape(-1), pc.grad.reshape(-1)
+        if c.norm() > 0:
+            cos = float(torch.dot(a, c) / (a.norm() * c.norm() + 1e-30))
+            assert cos > 0.99, cos
+    assert native.load() is not None
+
+
 def test_per_model_learning_rates_batch_exactly():
     cfg = default_cli_config(8, 46)
     data = _batch()
