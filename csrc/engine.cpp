@@ -429,7 +429,7 @@ class Engine {
   // and join before the Adam update:   head | pipe x (n-1) | tail.
   void run_epochs(int phase, int n, float lr, int ignore_epoch, float sel, bool use_graph) {
     if (!splits_[0].set) throw std::runtime_error("train split not set");
-    if (ext_stream_) throw std::runtime_error("run_epochs needs the engine's own streams (set_stream(0))");
+    if (ext_stream_) throw std::runtime_error("run_epochs needs the engine's own streams (set_stream(0, False))");
     if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
     if (n <= 0) return;
     if (phase == 2) h_valid_ = false;     // the moment net trains: the cached moments go stale
@@ -488,12 +488,14 @@ class Engine {
   // Run the engine's launches on an external stream (torch's current stream), so module-level
   // forward / backward calls are ordered with the surrounding torch ops. Epoch graphs need the
   // engine's own streams (run_epochs refuses an external one).
-  void set_stream(uintptr_t st) {
-    hipStream_t want = st ? reinterpret_cast<hipStream_t>(st) : own_st_;
-    if (want == st_) return;
+  // (external: run on the stream handle ``st`` -- 0 is the legacy NULL stream, torch's default;
+  //  not external: back to the engine's own stream)
+  void set_stream(uintptr_t st, bool external) {
+    hipStream_t want = external ? reinterpret_cast<hipStream_t>(st) : own_st_;
+    if (want == st_ && external == ext_stream_) return;
     sync();                                   // work queued on the previous stream completes first
     st_ = want;
-    ext_stream_ = st != 0;
+    ext_stream_ = external;
   }
   // parameters from device memory (a flat fp32 vector in state_dict order), re-packed in order
   void set_params_dev(int g, uintptr_t src) {
@@ -1288,7 +1290,7 @@ PYBIND11_MODULE(_dlap_hip, m) {
            py::arg("wait") = true)
       .def("train_step", &Engine::train_step)
       .def("backward_only", &Engine::backward_only, py::arg("phase"), py::arg("wait") = true)
-      .def("set_stream", &Engine::set_stream)
+      .def("set_stream", &Engine::set_stream, py::arg("stream"), py::arg("external") = true)
       .def("set_params_dev", &Engine::set_params_dev)
       .def("set_drop_step", &Engine::set_drop_step)
       .def("copy_ws", &Engine::copy_ws)
