@@ -1301,6 +1301,14 @@ PYBIND11_MODULE(_dlap_hip, m) {
       .def("read_blob", &Engine::read_blob)
       .def("sync", &Engine::sync, py::call_guard<py::gil_scoped_release>())
       .def("stream", &Engine::stream);
+  m.def("ensemble_portfolios",
+        [](uintptr_t W, int G, int T, int N, uintptr_t R, uintptr_t mask, uintptr_t port, uintptr_t port_ind,
+           uintptr_t stream) {
+          launch_ensemble(reinterpret_cast<const float*>(W), G, T, N, reinterpret_cast<const float*>(R),
+                          reinterpret_cast<const float*>(mask), reinterpret_cast<float*>(port),
+                          reinterpret_cast<float*>(port_ind), reinterpret_cast<hipStream_t>(stream));
+        },
+        "K11: ensemble portfolio [T] and individual portfolios [G][T] from gathered weights (device pointers)");
   m.attr("HIST_W") = (int)HIST_W;
   m.attr("SC_NSCAL") = (int)SC_NSCAL;
 }

@@ -509,3 +509,64 @@ void launch_job_metrics(const LossJob* jobs, int njobs, hipStream_t st) {
   hipLaunchKernelGGL(k_job_metrics, dim3(njobs), dim3(256), 0, st, jobs);
   HIP_OK(hipGetLastError());
 }
+
+// ---------------------------------------------------------------- ensemble (K11) --------
+// Post-all-gather ensemble portfolio of `/root/reference/src/evaluate_ensemble.py:137-166` on the
+// device: one workgroup per period t over G models' L1-normalised weights W [G][T][N]:
+//   a_i = mean_g W[g,t,i];  s = sum_i |a_i| m_i (fp64);  q_i = s > 1e-8 ? a_i / s : a_i;
+//   port[t] = sum_i q_i R_i m_i,  port_ind[g][t] = sum_i W[g,t,i] R_i m_i   (fp64 sums)
+// The (tiny) Sharpe ratios of these [T] series are taken on the host.
+template <int NT>
+DLAP_DEV double block_sum_d(double v, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) s += red[i];
+  return s;
+}
+
+__global__ __launch_bounds__(256) void k_ensemble(const float* __restrict__ W, int G, int T, int N,
+                                                  const float* __restrict__ R, const float* __restrict__ mask,
+                                                  float* __restrict__ port, float* __restrict__ port_ind) {
+  __shared__ double red[4];
+  const int t = blockIdx.x;
+  if (t >= T) return;
+  const size_t tn = (size_t)t * N;
+  const float invG = 1.f / (float)G;
+  double sa = 0.0;
+  for (int i = threadIdx.x; i < N; i += 256) {
+    float a = 0.f;
+    for (int g = 0; g < G; ++g) a += gp(W)[(size_t)g * T * N + tn + i];
+    a *= invG;
+    sa += fabs((double)a) * (double)gp(mask)[tn + i];
+  }
+  const double s = block_sum_d<256>(sa, red);
+  double pr = 0.0;
+  for (int i = threadIdx.x; i < N; i += 256) {
+    float a = 0.f;
+    for (int g = 0; g < G; ++g) a += gp(W)[(size_t)g * T * N + tn + i];
+    a *= invG;
+    const float q = s > 1e-8 ? (float)((double)a / s) : a;
+    pr += (double)q * (double)gp(R)[tn + i] * (double)gp(mask)[tn + i];
+  }
+  pr = block_sum_d<256>(pr, red);
+  if (threadIdx.x == 0) gp(port)[t] = (float)pr;
+  for (int g = 0; g < G; ++g) {
+    double pg = 0.0;
+    for (int i = threadIdx.x; i < N; i += 256)
+      pg += (double)gp(W)[(size_t)g * T * N + tn + i] * (double)gp(R)[tn + i] * (double)gp(mask)[tn + i];
+    pg = block_sum_d<256>(pg, red);
+    if (threadIdx.x == 0) gp(port_ind)[(size_t)g * T + t] = (float)pg;
+  }
+}
+
+void launch_ensemble(const float* W, int G, int T, int N, const float* R, const float* mask, float* port,
+                     float* port_ind, hipStream_t st) {
+  if (T <= 0 || G <= 0) return;
+  hipLaunchKernelGGL(k_ensemble, dim3(T), dim3(256), 0, st, W, G, T, N, R, mask, port, port_ind);
+  HIP_OK(hipGetLastError());
+}

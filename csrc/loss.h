@@ -57,3 +57,6 @@ void launch_asset(const LossJob* jobs, int njobs, int nmax, int kmax, hipStream_
 void launch_period_bwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st);
 void launch_job_metrics(const LossJob* jobs, int njobs, hipStream_t st);
 std::vector<long long> loss_timestamps();
+// ensemble averaging + re-normalisation + portfolio returns (K11), device pointers
+void launch_ensemble(const float* W, int G, int T, int N, const float* R, const float* mask, float* port,
+                     float* port_ind, hipStream_t st);

@@ -76,6 +76,36 @@ def ensemble_sharpes(weights_by_model: Sequence[Dict[str, np.ndarray]], batches:
     return out
 
 
+def ensemble_sharpes_device(wstack: Dict, batches: Dict[str, Dict]) -> Dict:
+    """``ensemble_sharpes`` with the averaging, re-normalisation and portfolio returns in the
+    native K11 kernel (``k_ensemble``) on the GPU. ``wstack[split]`` is a CUDA tensor [G, T, N]
+    of the models' L1-normalised weights (e.g. straight out of an RCCL all-gather); ``batches``
+    holds the splits' returns / mask (torch or numpy). Only the [T] and [G, T] portfolio series
+    come back to the host."""
+    import torch
+    from ..ops.native import load
+    nat = load(required=True)
+    out = {}
+    ind = None
+    for split, b in batches.items():
+        W = wstack[split].float().contiguous()
+        G, T, N = W.shape
+        dev = W.device
+        R = torch.as_tensor(b["returns"]).to(dev, torch.float32).contiguous()
+        m = torch.as_tensor(b["mask"]).to(dev, torch.float32).contiguous()
+        port = torch.empty(T, dtype=torch.float32, device=dev)
+        pind = torch.empty(G, T, dtype=torch.float32, device=dev)
+        nat.ensemble_portfolios(W.data_ptr(), G, T, N, R.data_ptr(), m.data_ptr(), port.data_ptr(), pind.data_ptr(),
+                                torch.cuda.current_stream(dev).cuda_stream)
+        pr = port.cpu().numpy().astype(np.float64)
+        out[f"{split}_sharpe"] = sharpe_ddof0(-pr)
+        if split == "test":
+            ind = pind.cpu().numpy().astype(np.float64)
+    if ind is not None:
+        out["individual_sharpes"] = [-sharpe_ddof0(ind[g]) for g in range(ind.shape[0])]
+    return out
+
+
 # ------------------------------------------------------------------------------------------
 # Paper metrics the reference does not implement (SURVEY §5.5: EV and XS-R² of Table I,
 # turnover of Table A.VII, max 1-month loss of Table A.VI). The paper's loadings come from a

@@ -131,6 +131,31 @@ def all_gather_rows(d: Dist, local: np.ndarray, n_total: int, owner_index: Seque
     return out
 
 
+def all_gather_rows_tensor(d: Dist, local: torch.Tensor, n_total: int, owner_index: Sequence[int],
+                           assignment: Optional[Sequence[Sequence[int]]] = None) -> torch.Tensor:
+    """``all_gather_rows`` for a torch tensor that stays on the collective device (the rank's
+    GPU under RCCL): the result [n_total, ...] is not copied to the host."""
+    dev = d.comm_device() if d.active else local.device
+    local = local.to(dev).contiguous()
+    if not d.active:
+        out = torch.empty((n_total,) + tuple(local.shape[1:]), dtype=local.dtype, device=dev)
+        out[list(owner_index)] = local
+        return out
+    owners = [list(a) for a in assignment] if assignment is not None else \
+        [shard(n_total, r, d.world) for r in range(d.world)]
+    cap = max(len(x) for x in owners)
+    pad = torch.zeros((cap,) + tuple(local.shape[1:]), dtype=local.dtype, device=dev)
+    pad[:len(local)] = local
+    bufs = torch.empty((d.world * cap,) + tuple(local.shape[1:]), dtype=local.dtype, device=dev)
+    tdist.all_gather_into_tensor(bufs, pad)
+    g = bufs.reshape((d.world, cap) + tuple(local.shape[1:]))
+    out = torch.empty((n_total,) + tuple(local.shape[1:]), dtype=local.dtype, device=dev)
+    for r in range(d.world):
+        if owners[r]:
+            out[owners[r]] = g[r, :len(owners[r])]
+    return out
+
+
 def broadcast_arrays(d: Dist, arrays: Optional[dict], src: int = 0, as_tensors: bool = False) -> dict:
     """Broadcast a dict of numpy arrays from ``src`` (e.g. a panel read once from disk): one
     metadata object broadcast, then one tensor broadcast per array. ``as_tensors`` returns the

@@ -28,7 +28,7 @@ from typing import Dict, List, Optional, Sequence
 import numpy as np
 import torch
 
-from ..analysis.portfolio import ensemble_sharpes
+from ..analysis.portfolio import ensemble_sharpes, ensemble_sharpes_device
 from ..config import default_cli_config
 from ..models.gan import AssetPricingGAN
 from . import comm
@@ -123,13 +123,21 @@ def run_ensemble(config: Dict, batches: Dict[str, Dict], seeds: Sequence[int] = 
     ok_local = np.array([r["ok"] for r in recs], dtype=np.float32).reshape(-1, 1)
     ok = comm.all_gather_rows(d, ok_local, len(seeds), mine)[:, 0] > 0.5
     weights: List[Dict[str, np.ndarray]] = [dict() for _ in seeds]
+    on_gpu = d.device.type == "cuda"
+    wdev = {}
     for sp in SPLITS:
         T, N = batches[sp]["mask"].shape
         loc = np.full((len(recs), T, N), np.nan, np.float32)
         for k, r in enumerate(recs):
             if r["ok"]:
                 loc[k] = r["weights"][sp]
-        allw = comm.all_gather_rows(d, loc, len(seeds), mine)       # one collective per split
+        if on_gpu:
+            # RCCL all-gather into the rank's GPU, the ensemble math stays there (K11 kernel)
+            allt = comm.all_gather_rows_tensor(d, torch.from_numpy(loc).to(d.device), len(seeds), mine)
+            wdev[sp] = allt
+            allw = allt.cpu().numpy()
+        else:
+            allw = comm.all_gather_rows(d, loc, len(seeds), mine)   # one collective per split
         for i in range(len(seeds)):
             weights[i][sp] = allw[i]
     walls = comm.all_gather_rows(d, np.array([[t_train]], np.float64), d.world, [d.rank])[:, 0]
@@ -140,7 +148,10 @@ def run_ensemble(config: Dict, batches: Dict[str, Dict], seeds: Sequence[int] = 
            "world_size": d.world, "train_wall_s_per_rank": walls.tolist(),
            "train_wall_s": float(walls.max())}
     if good:
-        res = ensemble_sharpes([weights[i] for i in good], np_b)
+        if on_gpu:       # K11 on the device, on the all-gathered tensors
+            res = ensemble_sharpes_device({sp: wdev[sp][good] for sp in SPLITS}, np_b)
+        else:
+            res = ensemble_sharpes([weights[i] for i in good], np_b)
         out.update({k: res[k] for k in ("train_sharpe", "valid_sharpe", "test_sharpe")})
         ind = np.full(len(seeds), np.nan)
         ind[good] = res["individual_sharpes"]

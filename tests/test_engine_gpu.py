@@ -309,6 +309,67 @@ def test_batched_ensemble_weights_match_cpu():
         assert _rel(w["test"], ref) < 3e-2
 
 
+def test_device_ensemble_portfolios_match_numpy():
+    """K11 on the device (k_ensemble: average, L1 re-normalisation, portfolio returns) against the
+    numpy post-processing of `/root/reference/src/evaluate_ensemble.py:137-171`."""
+    from deeplearninginassetpricing_paperreplication_amd.analysis.portfolio import (
+        ensemble_sharpes, ensemble_sharpes_device)
+    rng = np.random.default_rng(0)
+    G, T, N = 5, 30, 257
+    batches, ws, wd = {}, [dict() for _ in range(G)], {}
+    for sp in ("train", "valid", "test"):
+        m = rng.random((T, N)) < 0.6
+        m[3] = False                                       # an all-masked period
+        R = (rng.standard_normal((T, N)) * 0.05 * m).astype(np.float32)
+        W = rng.standard_normal((G, T, N)).astype(np.float32) * m
+        W /= np.maximum(np.abs(W).sum(2, keepdims=True), 1e-8)
+        batches[sp] = {"returns": R, "mask": m}
+        for g in range(G):
+            ws[g][sp] = W[g]
+        wd[sp] = torch.from_numpy(W).cuda()
+    ref = ensemble_sharpes(ws, batches)
+    got = ensemble_sharpes_device(wd, batches)
+    for k in ("train_sharpe", "valid_sharpe", "test_sharpe"):
+        assert abs(got[k] - ref[k]) < 1e-5 * max(1.0, abs(ref[k])), (k, got[k], ref[k])
+    np.testing.assert_allclose(got["individual_sharpes"], ref["individual_sharpes"], rtol=1e-5, atol=1e-6)
+
+
+def _rccl_worker(rank, world, port, out):
+    import os
+    os.environ.update(WORLD_SIZE=str(world), RANK=str(rank), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from deeplearninginassetpricing_paperreplication_amd.parallel import comm
+    d = comm.init(backend="nccl", use_gpu=True, timeout_s=120)
+    mine = comm.shard(9, d.rank, d.world)
+    loc = torch.stack([torch.full((4, 5), float(i), device=d.device) for i in mine])
+    g = comm.all_gather_rows_tensor(d, loc, 9, mine)
+    assert g.is_cuda and torch.equal(g[:, 0, 0].cpu(), torch.arange(9, dtype=torch.float32))
+    h = comm.all_gather_rows(d, loc.cpu().numpy(), 9, mine)
+    assert (h[:, 0, 0] == np.arange(9)).all()
+    comm.shutdown(d)
+    out.put(rank)
+
+
+@pytest.mark.skipif(not torch.cuda.is_available() or torch.cuda.device_count() < 2,
+                    reason="needs 2 GPUs (one RCCL rank per GPU)")
+def test_rccl_two_rank_ensemble_all_gather():
+    """The ensemble's weight all-gather over RCCL with one rank per GPU (9 seeds over 2 ranks)."""
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_rccl_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in ps:
+        p.start()
+    for p in ps:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in ps)
+    assert sorted(q.get(timeout=5) for _ in range(2)) == [0, 1]
+
+
 def test_cli_and_ensemble_driver_on_gpu(tmp_path):
     from deeplearninginassetpricing_paperreplication_amd.data.synthetic import generate_all_splits
     from deeplearninginassetpricing_paperreplication_amd.parallel.ensemble import run_ensemble
