@@ -384,21 +384,11 @@ class Engine {
 
   // ---------------------------------------------------------------- phase control -------
   // Reset the per-phase trackers (reference: fresh best values per phase).
+  // Stream-ordered (k_begin_phase after the queued epochs): no host synchronisation.
   void begin_phase(int phase) {
-    sync();   // all queued epochs are done before the trackers are reset (synchronous copies)
-    for (int g = 0; g < G_; ++g) {
-      ModelState& S = models_[g];
-      const float inf = INFINITY;
-      float best[3] = {inf, -inf, -inf};
-      HIP_LEGACY(hipMemcpy(S.best.p, best, sizeof(best), hipMemcpyHostToDevice));
-      HIP_LEGACY(hipMemset(S.snap_flags.p, 0, 2 * sizeof(int)));
-      int ep[2];
-      HIP_LEGACY(hipMemcpy(ep, S.ep.p, sizeof(ep), hipMemcpyDeviceToHost));
-      ep[1] = 0;
-      HIP_LEGACY(hipMemcpy(S.ep.p, ep, sizeof(ep), hipMemcpyHostToDevice));
-    }
-    sync();
-    (void)phase;
+    if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
+    const int p = (phase >= 1 && phase <= 3) ? phase : 1;   // any phase's table names the trackers
+    launch_begin_phase(as<EpochJob>(j_epoch_[p]), G_, st_);
   }
   py::array_t<int> snap_flags(int g) {
     ModelState& S = models_[check_g(g)];

@@ -404,6 +404,26 @@ __global__ __launch_bounds__(256) void k_epoch_end(const EpochJob* __restrict__ 
     for (int i = threadIdx.x; i < P; i += 256) gp(J.snap_sharpe)[i] = gp(J.params)[i];
 }
 
+// Phase start (reference: fresh best trackers per phase, `src/train.py:221-224`): best values
+// (+inf loss, -inf Sharpe, -inf moment loss), snapshot flags and the in-phase epoch counter are
+// reset on the stream, so a phase change needs no host synchronisation. One lane per model.
+__global__ __launch_bounds__(64) void k_begin_phase(const EpochJob* __restrict__ jobs, int njobs) {
+  const int g = blockIdx.x * 64 + threadIdx.x;
+  if (g >= njobs) return;
+  const EpochJob& J = jobs[g];
+  gp(J.best)[0] = INFINITY;
+  gp(J.best)[1] = -INFINITY;
+  gp(J.best)[2] = -INFINITY;
+  gp(J.snap_flags)[0] = 0;
+  gp(J.snap_flags)[1] = 0;
+  gp(J.ep)[1] = 0;
+}
+
+void launch_begin_phase(const EpochJob* jobs, int njobs, hipStream_t st) {
+  hipLaunchKernelGGL(k_begin_phase, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs);
+  HIP_OK(hipGetLastError());
+}
+
 void launch_epoch_end(const EpochJob* jobs, int njobs, int phase, int ignore_epoch, float sel,
                       float res_factor, int P, hipStream_t st) {
   hipLaunchKernelGGL(k_epoch_end, dim3(njobs), dim3(256), 0, st, jobs, phase, ignore_epoch, sel,

@@ -76,5 +76,6 @@ void launch_lstm_bwd(const UpdJob* jobs, int njobs, const ModelDesc* md, const M
 void launch_pack(float* const* params_unused, const UpdJob* jobs, int njobs, const ModelDesc* md,
                  const ModelDesc& mh, hipStream_t st);
 void launch_set_int(int* p, int v, hipStream_t st);
+void launch_begin_phase(const EpochJob* jobs, int njobs, hipStream_t st);
 void launch_epoch_end(const EpochJob* jobs, int njobs, int phase, int ignore_epoch, float sel,
                       float res_factor, int P, hipStream_t st);
