@@ -34,10 +34,22 @@
 #include "mlp.h"
 
 DLAP_DEV int lane_id() { return threadIdx.x & 63; }
+// A wave-uniform zero the compiler cannot see through (an empty asm statement defines it):
+// added to a loop-invariant LDS address, it makes the loads in that loop iteration-local.
+DLAP_DEV int opaque_zero() {
+  int z = 0;
+  asm volatile("" : "+s"(z));
+  return z;
+}
 
 // Waves per SIMD the forward tower kernel is compiled for (its VGPR budget = 512 / this).
 #ifndef DLAP_FWD_WPS
 #define DLAP_FWD_WPS 2
+#endif
+
+// Waves per SIMD of the one-tile-per-slice SDF backward (TPS = 1): 2 halves its register budget.
+#ifndef DLAP_BWD1_WPS
+#define DLAP_BWD1_WPS 1
 #endif
 
 // In-kernel timestamps (wall clock, 100 MHz) of k_mlp_fwd's first / last workgroup, wave 0:
@@ -570,6 +582,9 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __r
   if (keep && tile < ntiles) issue_kw(tile, kw_cur);
   bool first = true;
   for (; tile < ntiles; tile += stride) {
+    const int oz = opaque_zero();             // see bwd_sdf_body: no hoisted weight copies
+    const Frag* ldt = lds + oz;
+    const float* auxt = aux + oz;
     if (tile + stride < ntiles) {
       if constexpr (ZIN) issue_ztile<WMB, false>(J, D, tile + stride, znxt, J.do_sdf, mom);
       else issue_tile<P, KS1, false>(J, tile + stride, nxt);
@@ -588,13 +603,13 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __r
       DLAP_GLOBAL uint32_t* gout = J.gbits ? gbase + (size_t)tile * D.nl_sdf * 64 + lane : nullptr;
       auto l0 = [&](f32x4 (&a)[2][4]) {
         if constexpr (ZIN) {
-          if (D.pp_lds_floats > 0) zin_sdf0(zcur.zs, ri, spp, aux, D, a);
-          else zin_sdf0(zcur.zs, ri, gp(J.pp), aux, D, a);
+          if (D.pp_lds_floats > 0) zin_sdf0(zcur.zs, ri, spp, auxt, D, a);
+          else zin_sdf0(zcur.zs, ri, gp(J.pp), auxt, D, a);
         } else {
-          layer0<P, KS1, 4>(lds, D.s_fwd0, xf, a);
+          layer0<P, KS1, 4>(ldt, D.s_fwd0, xf, a);
         }
       };
-      sdf_forward_tile<P>(lds, aux, D, dc, ri, l0, gout, keep ? kw_cur : nullptr, w);
+      sdf_forward_tile<P>(ldt, auxt, D, dc, ri, l0, gout, keep ? kw_cur : nullptr, w);
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         const int r = tile * 32 + 16 * b + (lane & 15);
@@ -611,10 +626,10 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __r
 #pragma unroll
             for (int u = 0; u < WMB; ++u) a[b][u] = zcur.zm[b][u];
         } else {
-          layer0<P, KS1, WMB>(lds, D.m_fwd0, xf, a);
+          layer0<P, KS1, WMB>(ldt, D.m_fwd0, xf, a);
         }
       };
-      mom_forward_tile<P, WMB>(lds, aux, D, J, dc, ri, l0, gout, ab_cur);
+      mom_forward_tile<P, WMB>(ldt, auxt, D, J, dc, ri, l0, gout, ab_cur);
     }
     if constexpr (ZIN) zcur = znxt;
     else cur = nxt;
@@ -810,21 +825,20 @@ DLAP_DEV void wg_slab_store(const MlpJob& J, const float* red, int slab_stride) 
 // SDF backward. NL = number of hidden (MFMA) layers, all 64 wide.
 // ZIN (wide path): layer 0 is recomputed from z, its weight gradient is left to k_wgrad0: the
 // kernel stores the layer-0 dz as rows-as-k fragments instead (J.dz_out [tile][4][64]).
-template <class P, int KS1, int NL, int TPS, bool ZIN>
-__global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict__ jobs, MlpDims D,
-                                                        int slab_stride) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+// TLC: the layer of this slice's gradient tile when it is known at compile time (TPS = 1, one
+// instantiation per layer, selected from blockIdx.z), else -1. A slice of layer TLC > 0 stops
+// its backward chain at that layer and leaves the bias / output-layer / per-period input
+// gradients to slice 0, so its live state (and register budget) is that of its own role.
+template <class P, int KS1, int NL, int TPS, bool ZIN, int TLC>
+DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, char* smem, int slice, int C0) {
   using Frag = typename P::Frag;
-  const MlpJob& J = jobs[blockIdx.y];
   Frag* lds = reinterpret_cast<Frag*>(smem);
   float* aux = aux_lds_ptr(smem, D);
   float* spp = pp_lds_ptr(smem, D);
   const int lane = lane_id(), q = lane >> 4, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   const int ntiles = (J.R + 31) >> 5;
-  const int slice = blockIdx.z;
-  // 64-column chunks of layer 0 with a gradient tile: the X chunks (fused) or, on the wide
-  // path, only the per-period input columns (the X columns are k_wgrad0's)
-  const int C0 = ZIN ? (D.Dm + 63) / 64 : KS1 / 2;
+  const bool s0 = TLC <= 0 && slice == 0;      // the slice that owns the extra gradients
+  constexpr int JLO = TLC > 0 ? TLC : 0;        // lowest layer the backward chain reaches
   const Frag selP0 = make_sel<P>(true, 0), selP1 = make_sel<P>(true, 1);
   const Frag selN0 = make_sel<P>(false, 0), selN1 = make_sel<P>(false, 1);
 
@@ -843,8 +857,8 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
 #pragma unroll
   for (int t = 0; t < TPS; ++t) {
     const int tid = slice * TPS + t;
-    tl[t] = tid < C0 ? 0 : tid - C0 + 1;
-    tc[t] = tid < C0 ? tid : 0;
+    tl[t] = TLC >= 0 ? TLC : (tid < C0 ? 0 : tid - C0 + 1);
+    tc[t] = TLC > 0 ? 0 : (tid < C0 ? tid : 0);
   }
 
   const int stride = gridDim.x * nwaves;
@@ -863,6 +877,11 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
   stage_weights<P>(J, D, lds, aux, spp);       // first tile's loads are already in flight
   const DropCtx dc = drop_ctx(J, D);
   for (; tile < ntiles; tile += stride) {
+    // LDS base laundered per tile: keeps the compiler from hoisting every weight fragment and
+    // bias of the staged blob out of the loop into registers (~150 VGPRs at this depth)
+    const int oz = opaque_zero();
+    const Frag* ldt = lds + oz;
+    const float* auxt = aux + oz;
     if (tile + stride < ntiles) {
       if constexpr (ZIN) issue_ztile<1, true>(J, D, tile + stride, znxt, true, false);
       else issue_tile<P, KS1, true>(J, tile + stride, nxt);
@@ -878,17 +897,17 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
     uint32_t gates[NL][2];
     f32x4 a[2][4];
     if constexpr (ZIN) {
-      if (D.pp_lds_floats > 0) zin_sdf0(zcur.zs, ri, spp, aux, D, a);
-      else zin_sdf0(zcur.zs, ri, gp(J.pp), aux, D, a);
+      if (D.pp_lds_floats > 0) zin_sdf0(zcur.zs, ri, spp, auxt, D, a);
+      else zin_sdf0(zcur.zs, ri, gp(J.pp), auxt, D, a);
     } else {
-      layer0<P, KS1, 4>(lds, D.s_fwd0, xf, a);
+      layer0<P, KS1, 4>(ldt, D.s_fwd0, xf, a);
     }
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
-      if (j > 0) layer_chain<P, 4, 2>(lds, D.s_fwd + (j - 1) * 8, act[j - 1], a);
+      if (j > 0) layer_chain<P, 4, 2>(ldt, D.s_fwd + (j - 1) * 8, act[j - 1], a);
       gates[j][0] = gw_cur[j] & 0xFFFFu;
       gates[j][1] = gw_cur[j] >> 16;
-      relu_gates<4>(a, aux + D.a_sb + 64 * j, aux + D.a_sb + 64 * j, dc.scale, gates[j]);
+      relu_gates<4>(a, auxt + D.a_sb + 64 * j, auxt + D.a_sb + 64 * j, dc.scale, gates[j]);
       pack_blocks<P, 4>(a, act[j]);
     }
     // ---- output layer: w = wo . a_last + bo ----
@@ -896,13 +915,13 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
     if constexpr (ZIN) { dwr[0] = zcur.dw[0]; dwr[1] = zcur.dw[1]; }
     else { dwr[0] = cur.dw[0]; dwr[1] = cur.dw[1]; }
     f32x4 dz[2][4];
-    const float* wo = aux + D.a_wo;
+    const float* wo = auxt + D.a_wo;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const f32x4 ww = *reinterpret_cast<const f32x4*>(wo + 16 * u + 4 * q);
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
-        gwo[u] += dwr[b] * a[b][u];
+        if (s0) gwo[u] += dwr[b] * a[b][u];
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const bool on = (gates[NL - 1][b] >> (u * 4 + r)) & 1u;
@@ -910,22 +929,23 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
         }
       }
     }
-    if (q == 0) gbo += dwr[0] + dwr[1];
+    if (s0 && q == 0) gbo += dwr[0] + dwr[1];
     // ---- backward chain ----
 #pragma unroll
     for (int j = NL - 1; j >= 0; --j) {
+      if (j < JLO) break;
       Frag dzf[2][2];
       pack_blocks<P, 4>(dz, dzf);
       Frag dzN[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) to_rows_k<P, 4>(dzf, u, selP0, selP1, dzN[u]);
-      if (slice == 0) {
+      if (s0) {
         const Frag oh = make_onehot<P>(j);
 #pragma unroll
         for (int u = 0; u < 4; ++u) gbias[u] = P::mma(dzN[u], oh, gbias[u]);
       }
       if constexpr (ZIN) {
-        if (j == 0 && slice == 0) {                 // layer-0 dz for k_wgrad0
+        if (j == 0 && s0) {                         // layer-0 dz for k_wgrad0
           const auto dzo = gp(J.dz_out) + (size_t)tile * 4 * 64 + lane;
 #pragma unroll
           for (int u = 0; u < 4; ++u) dzo[u * 64] = dzN[u];
@@ -963,9 +983,9 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
           }
         }
       }
-      if (j > 0) {
+      if (j > JLO) {
         f32x4 da[2][4];
-        layer_chain<P, 4, 2>(lds, D.s_bwd + (j - 1) * 8, dzf, da);
+        layer_chain<P, 4, 2>(ldt, D.s_bwd + (j - 1) * 8, dzf, da);
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
@@ -975,14 +995,14 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
               const bool on = (gates[j > 0 ? j - 1 : 0][b] >> (u * 4 + r)) & 1u;
               dz[b][u][r] = on ? da[b][u][r] * dc.scale : 0.f;
             }
-      } else if (D.nrnn > 0 && slice == 0) {
+      } else if (j == 0 && D.nrnn > 0 && s0) {
         // dL/d(per-period input d) per row = sum_out W0[out][F + d] * dz0[out][row]: one MFMA
         // chain per 16 inputs with the packed W0[:, F:F+Dm]^T fragments
         for (int ub = 0; ub < D.ubpp; ++ub) {
           f32x4 c0 = zero4(), c1 = zero4();
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
-            const Frag w = ldsf(lds, D.s_upp + 2 * ub + s);
+            const Frag w = ldsf(ldt, D.s_upp + 2 * ub + s);
             c0 = P::mma(w, dzf[0][s], c0);
             c1 = P::mma(w, dzf[1][s], c1);
           }
@@ -1017,7 +1037,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
 #pragma unroll
             for (int r = 0; r < 4; ++r)
               red[t * 4096 + (16 * u + 4 * q + r) * 64 + 16 * v + (lane & 15)] += dW[t][u][v][r];
-      if (slice == 0) {
+      if (s0) {
         float* ex = red + TPS * 4096;
 #pragma unroll
         for (int u = 0; u < 4; ++u)
@@ -1037,6 +1057,27 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_sdf(const MlpJob* __restrict
   }
   wg_slab_store(J, red, slab_stride);
 }
+
+template <class P, int KS1, int NL, int TPS, bool ZIN>
+__global__ __launch_bounds__(256, TPS == 1 ? DLAP_BWD1_WPS : 1) void k_mlp_bwd_sdf(const MlpJob* __restrict__ jobs, MlpDims D,
+                                                        int slab_stride) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const MlpJob& J = jobs[blockIdx.y];
+  const int slice = blockIdx.z;
+  // 64-column chunks of layer 0 with a gradient tile: the X chunks (fused) or, on the wide
+  // path, only the per-period input columns (the X columns are k_wgrad0's)
+  const int C0 = ZIN ? (D.Dm + 63) / 64 : KS1 / 2;
+  if constexpr (TPS == 1) {
+    const int tl = slice < C0 ? 0 : slice - C0 + 1;     // block-uniform: one role per slice
+    if (tl == 0) bwd_sdf_body<P, KS1, NL, 1, ZIN, 0>(J, D, slab_stride, smem, slice, C0);
+    if constexpr (NL > 1) if (tl == 1) bwd_sdf_body<P, KS1, NL, 1, ZIN, 1>(J, D, slab_stride, smem, slice, C0);
+    if constexpr (NL > 2) if (tl == 2) bwd_sdf_body<P, KS1, NL, 1, ZIN, 2>(J, D, slab_stride, smem, slice, C0);
+    if constexpr (NL > 3) if (tl == 3) bwd_sdf_body<P, KS1, NL, 1, ZIN, 3>(J, D, slab_stride, smem, slice, C0);
+  } else {
+    bwd_sdf_body<P, KS1, NL, TPS, ZIN, -1>(J, D, slab_stride, smem, slice, C0);
+  }
+}
+
 
 // Moment backward (phase 2). NLM MFMA layers of WM = 16*WMB units; tanh on the last.
 // ZIN: as k_mlp_bwd_sdf (layer 0 from z, layer-0 dz stored as J.dz_out [tile][WMB][64]).
@@ -1089,6 +1130,9 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
   stage_weights<P>(J, D, lds, aux);
   const DropCtx dc = drop_ctx(J, D);
   for (; tile < ntiles; tile += stride) {
+    const int oz = opaque_zero();             // see bwd_sdf_body: no hoisted weight copies
+    const Frag* ldt = lds + oz;
+    const float* auxt = aux + oz;
     if (tile + stride < ntiles) {
       if constexpr (ZIN) issue_ztile<WMB, false>(J, D, tile + stride, znxt, false, true);
       else issue_tile<P, KS1, false>(J, tile + stride, nxt);
@@ -1109,11 +1153,11 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
 #pragma unroll
         for (int u = 0; u < WMB; ++u) a[b][u] = zcur.zm[b][u];
     } else {
-      layer0<P, KS1, WMB>(lds, D.m_fwd0, xf, a);
+      layer0<P, KS1, WMB>(ldt, D.m_fwd0, xf, a);
     }
 #pragma unroll
     for (int j = 0; j < NLM; ++j) {
-      if (j > 0) layer_chain<P, WMB, KSM>(lds, D.m_fwd + (j - 1) * WMB * KSM, act[j - 1], a);
+      if (j > 0) layer_chain<P, WMB, KSM>(ldt, D.m_fwd + (j - 1) * WMB * KSM, act[j - 1], a);
       auto body = [&](auto b0, auto b1) {
         if (j + 1 < NLM) {
           gates[j][0] = gw_cur[j < NH ? j : 0] & 0xFFFFu;
@@ -1142,7 +1186,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
       };
       // layer-0 bias is per period (global), later biases are staged (LDS)
       if (j == 0) body(gp(J.abias) + ri.t[0] * 64, gp(J.abias) + ri.t[1] * 64);
-      else body(aux + D.a_mb + 64 * j, aux + D.a_mb + 64 * j);
+      else body(auxt + D.a_mb + 64 * j, auxt + D.a_mb + 64 * j);
     }
     f32x4 dz[2][WMB];
 #pragma unroll
@@ -1194,7 +1238,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
       }
       if (j > 0) {
         f32x4 da[2][WMB];
-        layer_chain<P, WMB, KSM>(lds, D.m_bwd + (j - 1) * WMB * KSM, dzf, da);
+        layer_chain<P, WMB, KSM>(ldt, D.m_bwd + (j - 1) * WMB * KSM, dzf, da);
 #pragma unroll
         for (int b = 0; b < 2; ++b)
 #pragma unroll
