@@ -99,6 +99,7 @@ struct PrecBF16 {
   DLAP_DEV static Frag pack(const f32x4& lo, const f32x4& hi) { return pack8(lo, hi); }
   DLAP_DEV static Frag zero() { return zero8(); }
   DLAP_DEV static void set(Frag& f, int j, float v) { f[j] = (__bf16)v; }
+  DLAP_DEV static void set_if(Frag& f, int j, bool c, float v) { f[j] = c ? (__bf16)v : f[j]; }
 };
 
 struct PrecF32 {
@@ -114,6 +115,7 @@ struct PrecF32 {
   }
   DLAP_DEV static Frag zero() { return Frag{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}; }
   DLAP_DEV static void set(Frag& f, int j, float v) { f[j] = v; }
+  DLAP_DEV static void set_if(Frag& f, int j, bool c, float v) { f[j] = c ? v : f[j]; }
 };
 
 // ---- counter-based RNG for dropout (murmur3 finaliser on a mixed counter) -------------

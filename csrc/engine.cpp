@@ -579,6 +579,9 @@ class Engine {
   bool h_cache_ = true;                      // DLAP_H_CACHE
   bool h_valid_ = false;                     // cached h matches the current moment parameters
   bool cache_train_h() const { return h_cache_ && (md_.nl_m == 1 || md_.dropout == 0.f); }
+  // whether the training towers of a phase run the moment network (and so need its
+  // per-period bias table from the prologue)
+  bool train_mom(int phase) const { return phase == 2 || (phase == 3 && !cache_train_h()); }
   ModelDesc md_{};
   DevBuf<char> d_desc_;
   SplitDev splits_[3];
@@ -992,12 +995,12 @@ class Engine {
       std::vector<EpochJob> ej;
       std::vector<WideJob> wt, wb;
       for (int g = 0; g < G_; ++g) {
-        mt.push_back(mlp_job(g, 0, true, true, phase == 2 || (phase == 3 && !cache_train_h())));
+        mt.push_back(mlp_job(g, 0, true, true, train_mom(phase)));
         mb.push_back(mlp_job(g, 0, true, true, true));
         mb.back().dz_out = reinterpret_cast<bf16x8*>(phase == 2 ? ws(g, 0).dzm.p : ws(g, 0).dzs.p);
         mt.back().z_out = reinterpret_cast<f32x4*>(ws(g, 0).z.p);
         mt.back().store_mz = phase == 2;
-        wt.push_back(wide_job(g, 0, true, phase == 2 || (phase == 3 && !cache_train_h())));
+        wt.push_back(wide_job(g, 0, true, train_mom(phase)));
         wb.push_back(wide_job(g, 0, phase != 2, phase == 2));
         // the training forward stores the gate words its backward reuses
         if (phase == 2) {
@@ -1072,7 +1075,7 @@ class Engine {
     const SplitDev& D = splits_[0];
     if (!premasked) enqueue_dropmask(phase, 0, st_);
     // the latency-bound LSTM first, before the streaming projection loads the memory system
-    launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_);
+    launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_, train_mom(phase));
     const bool zx_train = md_.md.wide && zx_train_;
     if (md_.md.wide && !zx_train)
       launch_proj0(as<WideJob>(j_wide_train_[phase]), G_, gx_proj_[0], md_.md, md_.WMB, st_);
@@ -1121,7 +1124,7 @@ class Engine {
   }
   void enqueue_eval_prologue(hipStream_t st) {
     if (n_eval_jobs_ == 0) return;
-    launch_prologue(as<RnnJob>(j_rnn_eval_), n_eval_jobs_, tmax_eval_, dd(), md_, st);
+    launch_prologue(as<RnnJob>(j_rnn_eval_), n_eval_jobs_, tmax_eval_, dd(), md_, st, !h_cache_);
   }
   void enqueue_eval_towers(hipStream_t st) {
     if (n_eval_jobs_ == 0) return;
@@ -1233,7 +1236,7 @@ class Engine {
     DevBuf<char>& w = F.w;
     const bool zx = md_.md.wide && zx_eval_ && !train_mode;
     if (md_.md.wide && !zx) launch_proj0(as<WideJob>(w), G_, gx_proj_[s], md_.md, md_.WMB, st_);
-    launch_prologue(as<RnnJob>(a), G_, D.T, dd(), md_, st_);
+    launch_prologue(as<RnnJob>(a), G_, D.T, dd(), md_, st_, do_mom);
     if (zx) launch_mlp_fwd_zx(as<MlpJob>(b), G_, std::max(1, zx_gx_ / G_), md_.md, md_.WMB, st_);
     else launch_mlp_fwd(as<MlpJob>(b), G_, gx_fwd_[s], md_.md, md_.KS1, md_.WMB, st_);
     launch_period_fwd(as<LossJob>(c), G_, D.T, st_);

@@ -41,6 +41,18 @@ DLAP_DEV int opaque_zero() {
   asm volatile("" : "+s"(z));
   return z;
 }
+// v if bit k of the gate word g is set, else +0: a one-bit sign extension (v_bfe_i32) and an
+// AND, no compare, so no lane mask lives in SGPRs.
+DLAP_DEV float gate_and(float v, uint32_t g, int k) {
+  const int m = (int)(g << (31 - k)) >> 31;
+  return __int_as_float(__float_as_int(v) & m);
+}
+// Hide a gate word's value from the optimiser: the backward's masks are then rebuilt from it
+// instead of the forward's compare results being kept alive (as SGPR lane masks) across the tile.
+DLAP_DEV uint32_t opaque_gate(uint32_t g) {
+  asm volatile("" : "+v"(g));
+  return g;
+}
 
 // Waves per SIMD the forward tower kernel is compiled for (its VGPR budget = 512 / this).
 #ifndef DLAP_FWD_WPS
@@ -206,16 +218,19 @@ DLAP_DEV RowInfo finish_tile(const MlpJob& J, const MlpDims& D, int tile, TileIn
 #pragma unroll
     for (int s = 0; s < KS1; ++s) xf[b][s] = ok ? in.x[b][s] : P::zero();
     if (INS && D.Dm > 0) {
+      // branch-free: every lane loads (clamped index) and selects. The column offset goes through
+      // an opaque zero so the 8 x KS1 lane-range tests are made here, per tile, instead of being
+      // hoisted out of the tile loop as lane masks that pin (and spill) SGPR pairs.
+      const int cbase = 8 * q - D.F + opaque_zero();
       auto insert = [&](auto pp) {
 #pragma unroll
         for (int s = 0; s < KS1; ++s) {
           if (s >= s_lo && s <= s_hi) {                          // wave-uniform
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-              const int col = 32 * s + 8 * q + j - D.F;
-              const bool in_rng = (unsigned)col < (unsigned)D.Dm;
+              const int col = cbase + 32 * s + j;
               const float v = pp[min(max(col, 0), D.Dm - 1)];
-              if (in_rng && ok) P::set(xf[b][s], j, v);
+              P::set_if(xf[b][s], j, ((unsigned)col < (unsigned)D.Dm) & ok, v);
             }
           }
         }
@@ -392,10 +407,7 @@ DLAP_DEV void relu_gates(f32x4 (&a)[2][UB], BP bias0, BP bias1, float scale,
     for (int u = 0; u < UB; ++u) {
       const f32x4 bb = ld4(bp + 16 * u + 4 * q);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float z = a[b][u][r] + bb[r];
-        a[b][u][r] = ((gate[b] >> (u * 4 + r)) & 1u) ? z * scale : 0.f;
-      }
+      for (int r = 0; r < 4; ++r) a[b][u][r] = gate_and((a[b][u][r] + bb[r]) * scale, gate[b], u * 4 + r);
     }
   }
 }
@@ -574,21 +586,26 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __r
   const auto gbase = J.gbits ? gp(J.gbits) + (size_t)(dc.step & 1u) * J.gb_half : nullptr;
   constexpr int KWM = 4;                           // max SDF hidden layers (engine limit)
   uint32_t kw_cur[KWM], kw_nxt[KWM];
-  auto issue_kw = [&](int t, uint32_t (&kw)[KWM]) {
+  auto issue_kw = [&](int t, uint32_t (&kw)[KWM], int nls) {
 #pragma unroll
     for (int j = 0; j < KWM; ++j)
-      kw[j] = j < D.nl_sdf ? gbase[((size_t)t * D.nl_sdf + j) * 64 + lane] : 0xFFFFFFFFu;
+      kw[j] = j < nls ? gbase[((size_t)t * nls + j) * 64 + lane] : 0xFFFFFFFFu;
   };
-  if (keep && tile < ntiles) issue_kw(tile, kw_cur);
+  if (keep && tile < ntiles) issue_kw(tile, kw_cur, D.nl_sdf);
   bool first = true;
   for (; tile < ntiles; tile += stride) {
     const int oz = opaque_zero();             // see bwd_sdf_body: no hoisted weight copies
     const Frag* ldt = lds + oz;
     const float* auxt = aux + oz;
+    // depth tests made per tile from laundered copies: hoisted out of the loop they become
+    // 64-bit lane masks that pin (and spill) SGPR pairs for the whole kernel
+    MlpDims Dt = D;
+    Dt.nl_sdf += oz;
+    Dt.nl_mom += oz;
     if (tile + stride < ntiles) {
       if constexpr (ZIN) issue_ztile<WMB, false>(J, D, tile + stride, znxt, J.do_sdf, mom);
       else issue_tile<P, KS1, false>(J, tile + stride, nxt);
-      if (keep) issue_kw(tile + stride, kw_nxt);
+      if (keep) issue_kw(tile + stride, kw_nxt, Dt.nl_sdf);
       if (mom) {
         issue_abias<WMB>(J, ti_ahead, ab_nxt);             // periods known since last iteration
         if (tile + 2 * stride < ntiles) issue_rowti(J, tile + 2 * stride, ti_ahead);
@@ -609,7 +626,7 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __r
           layer0<P, KS1, 4>(ldt, D.s_fwd0, xf, a);
         }
       };
-      sdf_forward_tile<P>(ldt, auxt, D, dc, ri, l0, gout, keep ? kw_cur : nullptr, w);
+      sdf_forward_tile<P>(ldt, auxt, Dt, dc, ri, l0, gout, keep ? kw_cur : nullptr, w);
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         const int r = tile * 32 + 16 * b + (lane & 15);
@@ -629,7 +646,7 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __r
           layer0<P, KS1, WMB>(ldt, D.m_fwd0, xf, a);
         }
       };
-      mom_forward_tile<P, WMB>(ldt, auxt, D, J, dc, ri, l0, gout, ab_cur);
+      mom_forward_tile<P, WMB>(ldt, auxt, Dt, J, dc, ri, l0, gout, ab_cur);
     }
     if constexpr (ZIN) zcur = znxt;
     else cur = nxt;
@@ -826,7 +843,9 @@ DLAP_DEV void wg_slab_store(const MlpJob& J, const float* red, int slab_stride) 
 // ZIN (wide path): layer 0 is recomputed from z, its weight gradient is left to k_wgrad0: the
 // kernel stores the layer-0 dz as rows-as-k fragments instead (J.dz_out [tile][4][64]).
 // TLC: the layer of this slice's gradient tile when it is known at compile time (TPS = 1, one
-// instantiation per layer, selected from blockIdx.z), else -1. A slice of layer TLC > 0 stops
+// instantiation per layer, selected from blockIdx.z); -2: TPS = 2 on a two-tile tower (tile t
+// is layer t, one slice), so every gradient MFMA is unconditional and the accumulators stay
+// in place across the tile loop; else -1 (runtime tile map). A slice of layer TLC > 0 stops
 // its backward chain at that layer and leaves the bias / output-layer / per-period input
 // gradients to slice 0, so its live state (and register budget) is that of its own role.
 template <class P, int KS1, int NL, int TPS, bool ZIN, int TLC>
@@ -837,7 +856,7 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
   float* spp = pp_lds_ptr(smem, D);
   const int lane = lane_id(), q = lane >> 4, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   const int ntiles = (J.R + 31) >> 5;
-  const bool s0 = TLC <= 0 && slice == 0;      // the slice that owns the extra gradients
+  const bool s0 = TLC <= 0 && slice == 0;      // the slice that owns the extra gradients (-2: slice 0)
   constexpr int JLO = TLC > 0 ? TLC : 0;        // lowest layer the backward chain reaches
   const Frag selP0 = make_sel<P>(true, 0), selP1 = make_sel<P>(true, 1);
   const Frag selN0 = make_sel<P>(false, 0), selN1 = make_sel<P>(false, 1);
@@ -857,8 +876,8 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
 #pragma unroll
   for (int t = 0; t < TPS; ++t) {
     const int tid = slice * TPS + t;
-    tl[t] = TLC >= 0 ? TLC : (tid < C0 ? 0 : tid - C0 + 1);
-    tc[t] = TLC > 0 ? 0 : (tid < C0 ? tid : 0);
+    tl[t] = TLC == -2 ? t : TLC >= 0 ? TLC : (tid < C0 ? 0 : tid - C0 + 1);
+    tc[t] = (TLC == -2 || TLC > 0) ? 0 : (tid < C0 ? tid : 0);
   }
 
   const int stride = gridDim.x * nwaves;
@@ -910,6 +929,8 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
       relu_gates<4>(a, auxt + D.a_sb + 64 * j, auxt + D.a_sb + 64 * j, dc.scale, gates[j]);
       pack_blocks<P, 4>(a, act[j]);
     }
+#pragma unroll
+    for (int j = 0; j < NL; ++j) { gates[j][0] = opaque_gate(gates[j][0]); gates[j][1] = opaque_gate(gates[j][1]); }
     // ---- output layer: w = wo . a_last + bo ----
     float dwr[2];
     if constexpr (ZIN) { dwr[0] = zcur.dw[0]; dwr[1] = zcur.dw[1]; }
@@ -923,10 +944,7 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
       for (int b = 0; b < 2; ++b) {
         if (s0) gwo[u] += dwr[b] * a[b][u];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool on = (gates[NL - 1][b] >> (u * 4 + r)) & 1u;
-          dz[b][u][r] = on ? dwr[b] * ww[r] * dc.scale : 0.f;
-        }
+        for (int r = 0; r < 4; ++r) dz[b][u][r] = gate_and(dwr[b] * ww[r] * dc.scale, gates[NL - 1][b], u * 4 + r);
       }
     }
     if (s0 && q == 0) gbo += dwr[0] + dwr[1];
@@ -991,10 +1009,8 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
 #pragma unroll
           for (int u = 0; u < 4; ++u)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const bool on = (gates[j > 0 ? j - 1 : 0][b] >> (u * 4 + r)) & 1u;
-              dz[b][u][r] = on ? da[b][u][r] * dc.scale : 0.f;
-            }
+            for (int r = 0; r < 4; ++r)
+              dz[b][u][r] = gate_and(da[b][u][r] * dc.scale, gates[j > 0 ? j - 1 : 0][b], u * 4 + r);
       } else if (j == 0 && D.nrnn > 0 && s0) {
         // dL/d(per-period input d) per row = sum_out W0[out][F + d] * dz0[out][row]: one MFMA
         // chain per 16 inputs with the packed W0[:, F:F+Dm]^T fragments
@@ -1073,6 +1089,8 @@ __global__ __launch_bounds__(256, TPS == 1 ? DLAP_BWD1_WPS : 1) void k_mlp_bwd_s
     if constexpr (NL > 1) if (tl == 1) bwd_sdf_body<P, KS1, NL, 1, ZIN, 1>(J, D, slab_stride, smem, slice, C0);
     if constexpr (NL > 2) if (tl == 2) bwd_sdf_body<P, KS1, NL, 1, ZIN, 2>(J, D, slab_stride, smem, slice, C0);
     if constexpr (NL > 3) if (tl == 3) bwd_sdf_body<P, KS1, NL, 1, ZIN, 3>(J, D, slab_stride, smem, slice, C0);
+  } else if (TPS == 2 && C0 == 1) {     // the engine's TPS = 2 case: tiles (layer 0, layer 1)
+    bwd_sdf_body<P, KS1, NL, TPS, ZIN, -2>(J, D, slab_stride, smem, slice, C0);
   } else {
     bwd_sdf_body<P, KS1, NL, TPS, ZIN, -1>(J, D, slab_stride, smem, slice, C0);
   }
@@ -1188,6 +1206,8 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
       if (j == 0) body(gp(J.abias) + ri.t[0] * 64, gp(J.abias) + ri.t[1] * 64);
       else body(auxt + D.a_mb + 64 * j, auxt + D.a_mb + 64 * j);
     }
+#pragma unroll
+    for (int j = 0; j < NLM; ++j) { gates[j][0] = opaque_gate(gates[j][0]); gates[j][1] = opaque_gate(gates[j][1]); }
     f32x4 dz[2][WMB];
 #pragma unroll
     for (int b = 0; b < 2; ++b)
@@ -1244,10 +1264,8 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
 #pragma unroll
           for (int u = 0; u < WMB; ++u)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const bool on = (gates[j > 0 ? j - 1 : 0][b] >> (u * 4 + r)) & 1u;
-              dz[b][u][r] = on ? da[b][u][r] * dc.scale : 0.f;
-            }
+            for (int r = 0; r < 4; ++r)
+              dz[b][u][r] = gate_and(da[b][u][r] * dc.scale, gates[j > 0 ? j - 1 : 0][b], u * 4 + r);
       } else if (slice == 0) {
 #pragma unroll
         for (int b = 0; b < 2; ++b) {

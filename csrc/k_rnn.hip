@@ -51,17 +51,11 @@ DLAP_DEV float ftanh(float x) {
 // the biases): all loads of a tile are independent, so the tile costs ~one memory round trip.
 //   A (16x4): lane l -> A[t = l&15][k = l>>4];  B (4x16): lane l -> B[k = l>>4][o = l&15]
 //   C (16x16): lane l -> C[t = 4*(l>>4) + r][o = l&15]
-__global__ __launch_bounds__(64) void k_proj(const RnnJob* __restrict__ jobs,
-                                             const ModelDesc* __restrict__ md) {
-  const RnnJob& J = jobs[blockIdx.z];
+// One 16 (periods) x 16 (outputs) tile of the projection on one wave: returns lane l's
+// accumulator C[t0 + 4*(l>>4) + r][o0 + (l&15)] with the bias added.
+DLAP_DEV f32x4 proj_tile(const RnnJob& J, const ModelDesc* md, int t0, int o0) {
   const int T = J.T, M = md->M, MP = md->proj_mp, NP = md->proj_np;
-  const int t0 = blockIdx.x * 16, o0 = blockIdx.y * 16;
-  const int G4 = md->nrnn > 0 ? 4 * md->H : 0;
-  if (t0 >= T) return;
-  if (o0 >= G4 && !J.abias) return;
-  const bool tsm = blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0;
-  RNN_TS(12, tsm);
-  const int l = threadIdx.x, n = l & 15, kq = l >> 4;
+  const int l = threadIdx.x & 63, n = l & 15, kq = l >> 4;
   const int ta = min(t0 + n, T - 1);
   const auto xrow = gp(J.macro) + (size_t)ta * M;
   const auto wcol = gp(J.wproj) + o0 + n;
@@ -83,12 +77,29 @@ __global__ __launch_bounds__(64) void k_proj(const RnnJob* __restrict__ jobs,
     for (int s = 0; s < PROJ_KC; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
   }
   const float bias = wcol[(size_t)MP * NP];
+  return acc + bias;
+}
+
+// grid (ceil(T/16), column tiles, jobs); blockIdx.y counts from column tile y0 (y0 = G4/16 when
+// the LSTM projects its own inputs: only the moment table is left here).
+__global__ __launch_bounds__(64) void k_proj(const RnnJob* __restrict__ jobs,
+                                             const ModelDesc* __restrict__ md, int y0) {
+  const RnnJob& J = jobs[blockIdx.z];
+  const int T = J.T;
+  const int t0 = blockIdx.x * 16, o0 = (blockIdx.y + y0) * 16;
+  const int G4 = md->nrnn > 0 ? 4 * md->H : 0;
+  if (t0 >= T) return;
+  if (o0 >= G4 && !J.abias) return;
+  const bool tsm = blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0;
+  RNN_TS(12, tsm);
+  const f32x4 acc = proj_tile(J, md, t0, o0);
+  const int l = threadIdx.x, n = l & 15, kq = l >> 4;
   const int o = o0 + n;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int t = t0 + 4 * kq + r;
     if (t >= T) break;
-    const float v = acc[r] + bias;
+    const float v = acc[r];
     if (o < G4) gp(J.xg)[(size_t)t * G4 + o] = v;
     else if (o - G4 < 64) gp(J.abias)[t * 64 + (o - G4)] = v;
   }
@@ -383,14 +394,35 @@ __global__ __launch_bounds__(64) void k_lstm_gl(const RnnJob* __restrict__ jobs,
 // LDS (floats): xg [T][4H] | gates [T][4H] | cells [T][H] | outputs 2 x [T][H] | junk [64].
 static inline size_t gls_lds_floats(int T, int H) { return (size_t)T * (8 * H + 3 * H) + 64; }
 
-template <int HM, bool DPPG>
-__global__ __launch_bounds__(64) void k_lstm_gls(const RnnJob* __restrict__ jobs,
-                                                 const ModelDesc* __restrict__ md) {
+// FUSE: the workgroup (LSTM_FUSE_THREADS) first computes the layer-0 input projections of its
+// job straight into the LDS staging area with all its waves (k_proj + the staging copy in one
+// launch), then waves 1.. exit and wave 0 runs the recurrence (see launch_prologue).
+#define LSTM_FUSE_THREADS 1024
+template <int HM, bool DPPG, bool FUSE>
+__global__ __launch_bounds__(FUSE ? LSTM_FUSE_THREADS : 64) void k_lstm_gls(const RnnJob* __restrict__ jobs,
+                                                                            const ModelDesc* __restrict__ md) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const RnnJob& J = jobs[blockIdx.x];
   const int nrnn = md->nrnn;
   if (nrnn == 0) return;
   const int T = J.T, H = DPPG ? HM : md->H, G4 = 4 * H;
+  if constexpr (FUSE) {
+    RNN_TS((J.sc != nullptr ? 0 : 4) + 0, J.sc != nullptr || blockIdx.x == gridDim.x - 1);
+    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6, l = threadIdx.x & 63;
+    const int nto = (G4 + 15) >> 4, ntiles = ((T + 15) >> 4) * nto;
+    for (int tile = w; tile < ntiles; tile += nw) {
+      const int t0 = (tile / nto) * 16, o0 = (tile % nto) * 16;
+      const f32x4 acc = proj_tile(J, md, t0, o0);
+      const int o = o0 + (l & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = t0 + 4 * (l >> 4) + r;
+        if (t < T && o < G4) sm[t * G4 + o] = acc[r];
+      }
+    }
+    __syncthreads();
+    if (w > 0) return;
+  }
   const int L = threadIdx.x;
   const bool gl = L < G4, ul = L < H;
   const int row = gl ? L : 0;
@@ -412,17 +444,17 @@ __global__ __launch_bounds__(64) void k_lstm_gls(const RnnJob* __restrict__ jobs
   const bool save = J.sc != nullptr;
   const int tsb = save ? 0 : 4;
   const bool tsm = save || blockIdx.x == gridDim.x - 1;
-  RNN_TS(tsb + 0, tsm);
+  if (!FUSE) RNN_TS(tsb + 0, tsm);
   float* sx = sm;
   float* sgb = sx + (size_t)T * G4;
   float* scb = sgb + (size_t)T * G4;
   float* shb0 = scb + (size_t)T * H;
   float* junk = shb0 + (size_t)2 * T * H;
-  {
+  if constexpr (!FUSE) {
     const auto xg = gp(J.xg);
     for (int i = L; i < T * G4; i += 64) sx[i] = xg[i];
+    __syncthreads();
   }
-  __syncthreads();
   for (int l = 0; l < nrnn; ++l) {
     float whh[HM], wih[HM];
 #pragma unroll
@@ -502,9 +534,25 @@ __global__ __launch_bounds__(64) void k_lstm_gls(const RnnJob* __restrict__ jobs
 }
 
 void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* md, const ModelDesc& mh,
-                     hipStream_t st) {
-  {
-    hipLaunchKernelGGL(k_proj, dim3((tmax + 15) / 16, mh.proj_np / 16, njobs), dim3(64), 0, st, jobs, md);
+                     hipStream_t st, bool abias) {
+  // DLAP_LSTM_FUSE_PROJ=1: the LSTM workgroup projects its own inputs (k_lstm_gls<.., FUSE>) and
+  // k_proj only builds the moment network's per-period bias table. Off by default: one
+  // workgroup streams the whole macro panel through one CU (15 us at T = 240, M = 178, against
+  // 6 us for k_proj's T/16 workgroups plus the 3.5 us staging copy). The bias table is built
+  // only when a tower launched after this prologue reads it.
+  const char* fz_env = std::getenv("DLAP_LSTM_FUSE_PROJ");
+  const char* ul_env0 = std::getenv("DLAP_LSTM_UNIT_LANES");
+  const char* gls_env0 = std::getenv("DLAP_LSTM_GLS");
+  const bool fuse = mh.nrnn > 0 && (fz_env && std::atoi(fz_env) == 1) && !(ul_env0 && std::atoi(ul_env0) == 1) &&
+                    !(gls_env0 && std::atoi(gls_env0) == 0) && mh.H <= 16 &&
+                    gls_lds_floats(tmax, mh.H) * sizeof(float) <= 64 * 1024;
+  const int G4 = mh.nrnn > 0 ? 4 * mh.H : 0;
+  // column tiles for k_proj: all (abias, unfused), the moment ones only (abias, fused; a tile
+  // shared by the last gates and the first moment columns stays), the gates only, or none
+  const int y0 = abias && fuse ? G4 / 16 : 0;
+  const int ny = abias ? mh.proj_np / 16 - y0 : (fuse ? 0 : (G4 + 15) / 16);
+  if (ny > 0) {
+    hipLaunchKernelGGL(k_proj, dim3((tmax + 15) / 16, ny, njobs), dim3(64), 0, st, jobs, md, y0);
     HIP_OK(hipGetLastError());
   }
   if (mh.nrnn > 0) {
@@ -521,7 +569,9 @@ void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* m
     const bool gls = !(gls_env && std::atoi(gls_env) == 0) && mh.H <= 16 &&
                      gls_lds_floats(tmax, mh.H) * sizeof(float) <= 64 * 1024;
     const size_t shg = gls_lds_floats(tmax, mh.H) * sizeof(float);
-#define S_CASE(HM, DP) hipLaunchKernelGGL((k_lstm_gls<HM, DP>), dim3(njobs), dim3(64), shg, st, jobs, md);
+#define S_CASE(HM, DP) \
+    if (fuse) hipLaunchKernelGGL((k_lstm_gls<HM, DP, true>), dim3(njobs), dim3(LSTM_FUSE_THREADS), shg, st, jobs, md); \
+    else hipLaunchKernelGGL((k_lstm_gls<HM, DP, false>), dim3(njobs), dim3(64), shg, st, jobs, md);
     if (ul_env && std::atoi(ul_env) == 1) {       // unit-per-lane form (reference for tests)
       if (mh.H <= 4) { L_CASE(4) } else if (mh.H <= 8) { L_CASE(8) } else if (mh.H <= 16) { L_CASE(16) } else { L_CASE(32) }
     } else if (gls) {

@@ -335,7 +335,8 @@ void launch_update(const UpdJob* jobs, int njobs, const ModelDesc* md, const Mod
 }
 
 // ============================================================ epoch bookkeeping =========
-__global__ __launch_bounds__(256) void k_epoch_end(const EpochJob* __restrict__ jobs, int phase,
+#define EPOCH_END_THREADS 1024
+__global__ __launch_bounds__(EPOCH_END_THREADS) void k_epoch_end(const EpochJob* __restrict__ jobs, int phase,
                                                    int ignore_epoch, float sel, float res_factor, int P) {
   const EpochJob& J = jobs[blockIdx.x];
   __shared__ int dec[2];
@@ -398,10 +399,30 @@ __global__ __launch_bounds__(256) void k_epoch_end(const EpochJob* __restrict__ 
     dec[1] = up_sr;
   }
   __syncthreads();
-  if (dec[0])
-    for (int i = threadIdx.x; i < P; i += 256) gp(J.snap_loss)[i] = gp(J.params)[i];
-  if (dec[1])
-    for (int i = threadIdx.x; i < P; i += 256) gp(J.snap_sharpe)[i] = gp(J.params)[i];
+  // snapshot copies: 16-byte accesses, every load of a thread issued before its stores (one
+  // memory round trip for the whole vector instead of one per 256 floats)
+  auto copy = [&](float* dst) {
+    const auto src = gp(J.params);
+    const auto d = gp(dst);
+    const int P4 = ((reinterpret_cast<uintptr_t>(J.params) | reinterpret_cast<uintptr_t>(dst)) & 15) ? 0 : P >> 2;
+    constexpr int U = 8;
+    for (int i0 = threadIdx.x; i0 < P4; i0 += U * EPOCH_END_THREADS) {
+      f32x4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * EPOCH_END_THREADS;
+        v[u] = i < P4 ? ld4(src + 4 * i) : zero4();
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * EPOCH_END_THREADS;
+        if (i < P4) *(DLAP_GLOBAL f32x4*)(d + 4 * i) = v[u];
+      }
+    }
+    for (int i = 4 * P4 + threadIdx.x; i < P; i += EPOCH_END_THREADS) d[i] = src[i];
+  };
+  if (dec[0]) copy(J.snap_loss);
+  if (dec[1]) copy(J.snap_sharpe);
 }
 
 // Phase start (reference: fresh best trackers per phase, `src/train.py:221-224`): best values
@@ -426,7 +447,7 @@ void launch_begin_phase(const EpochJob* jobs, int njobs, hipStream_t st) {
 
 void launch_epoch_end(const EpochJob* jobs, int njobs, int phase, int ignore_epoch, float sel,
                       float res_factor, int P, hipStream_t st) {
-  hipLaunchKernelGGL(k_epoch_end, dim3(njobs), dim3(256), 0, st, jobs, phase, ignore_epoch, sel,
+  hipLaunchKernelGGL(k_epoch_end, dim3(njobs), dim3(EPOCH_END_THREADS), 0, st, jobs, phase, ignore_epoch, sel,
                      res_factor, P);
   HIP_OK(hipGetLastError());
 }

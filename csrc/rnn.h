@@ -22,7 +22,9 @@ struct RnnJob {
   int train;
 };
 
+// abias: also build the moment network's per-period layer-0 bias table (a tower launched after
+// this prologue runs the moment network).
 void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* md, const ModelDesc& mh,
-                     hipStream_t st);
+                     hipStream_t st, bool abias = true);
 
 std::vector<long long> rnn_timestamps();

@@ -68,19 +68,29 @@ def variant_path(variant: str) -> Path:
     return PKG / variant / ext_path().name
 
 
+# Per-source extra flags of the production build (none). Measured alternative, kept for A/B
+# runs: k_mlp.hip with "-mllvm -amdgpu-mfma-vgpr-form" (MFMA results in VGPRs instead of the
+# accumulator file: half the v_accvgpr_read moves in the tower backward) ran within noise of
+# the default (3954/3999 vs 3990/3972 model-epochs/s, profiles/README.md).
+FILE_FLAGS: dict = {}
+
+
 def build(force: bool = False, jobs: int = 8, verbose: bool = True, ubsan: bool = False,
-          debug: bool = False) -> Path:
+          debug: bool = False, variant: str | None = None, file_flags: dict | None = None) -> Path:
+    """Build the extension; ``variant`` + ``file_flags`` build a named side artefact (loaded with
+    ``DLAP_NATIVE=<variant>``) whose per-file flags replace FILE_FLAGS, for A/B measurements."""
     srcs = sorted(CSRC.glob("*.hip")) + [CSRC / "engine.cpp"]
     headers = sorted(CSRC.glob("*.h"))
     out = ext_path()
     build_dir = BUILD
-    variant = "ubsan" if ubsan else ("debug" if debug else None)
+    ff = FILE_FLAGS if file_flags is None else file_flags
+    variant = "ubsan" if ubsan else ("debug" if debug else variant)
     if variant:     # a separate artefact next to the production one (selected by DLAP_NATIVE)
         out = variant_path(variant)
         out.parent.mkdir(exist_ok=True)
         build_dir = BUILD / variant
     stamp = build_dir / "stamp"
-    key = _hash(srcs + headers)
+    key = _hash(srcs + headers) + repr(sorted(ff.items()))
     if not force and out.exists() and stamp.exists() and stamp.read_text() == key:
         if verbose:
             print(f"[dlap] native extension up to date: {out.name}")
@@ -89,7 +99,7 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True, ubsan: bool 
     flags = _includes() + ["-Wno-unused-result"] + (UBSAN_FLAGS if ubsan else []) + (DEBUG_FLAGS if debug else [])
     objs = []
     with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(srcs)))) as ex:
-        futs = {ex.submit(_compile, s, build_dir / (s.stem + ".o"), flags): s for s in srcs}
+        futs = {ex.submit(_compile, s, build_dir / (s.stem + ".o"), flags + ff.get(s.name, [])): s for s in srcs}
         for f in cf.as_completed(futs):
             objs.append(f.result())
             if verbose:
@@ -106,4 +116,14 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True, ubsan: bool 
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv, ubsan="--ubsan" in sys.argv, debug="--debug" in sys.argv)
+    # --variant NAME [--file-flags FILE=FLAG,FLAG ...]: a named side build for A/B runs
+    argv = sys.argv[1:]
+    var, ffl = None, None
+    if "--variant" in argv:
+        var = argv[argv.index("--variant") + 1]
+        ffl = {}
+        for a in argv:
+            if "=" in a and a.split("=", 1)[0].endswith((".hip", ".cpp")):
+                f, fl = a.split("=", 1)
+                ffl[f] = [x for x in fl.split(",") if x]
+    build(force="--force" in argv, ubsan="--ubsan" in argv, debug="--debug" in argv, variant=var, file_flags=ffl)
