@@ -131,14 +131,22 @@ class Engine {
       HIP_OK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
       HIP_OK(hipStreamCreateWithFlags(&st2_, hipStreamNonBlocking));
     }
+    HIP_OK(hipStreamCreateWithFlags(&st3_, hipStreamNonBlocking));
     own_st_ = st_;
     HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_mid_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_a_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_m3_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_b3_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_f3_, hipEventDisableTiming));
     eval_gx_ = env_int("DLAP_EVAL_GX", 256);
     b_wait_ = env_int("DLAP_B_WAIT", 0);
+    // both off: a third graph branch changes how the runtime maps the graph onto its hardware
+    // queues -- the evaluation branch then shared a queue with the training backward and ran
+    // after it (2718 vs 3978 model-epochs/s, profiles/r2_knobs_third_stream.log)
     side_metrics_ = env_int("DLAP_SIDE_METRICS", 0) != 0;
+    split_tail_ = env_int("DLAP_SPLIT_TAIL", 0) != 0;
     zx_eval_ = env_int("DLAP_ZX_EVAL", 1) != 0;
     zx_train_ = env_int("DLAP_ZX_TRAIN", 1) != 0;
     zx_gx_ = std::max(1, env_int("DLAP_ZX_GX", 256));
@@ -177,6 +185,7 @@ class Engine {
   ~Engine() {
     // drain both streams before the graphs, events and (member) buffers go away
     if (st2_) (void)hipStreamSynchronize(st2_);
+    if (st3_) (void)hipStreamSynchronize(st3_);
     if (st_) (void)hipStreamSynchronize(st_);
     if (own_st_ && own_st_ != st_) (void)hipStreamSynchronize(own_st_);
     for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
@@ -184,7 +193,9 @@ class Engine {
     if (ev_join_) (void)hipEventDestroy(ev_join_);
     if (ev_mid_) (void)hipEventDestroy(ev_mid_);
     if (ev_a_) (void)hipEventDestroy(ev_a_);
+    for (hipEvent_t e : {ev_m3_, ev_b3_, ev_f3_}) if (e) (void)hipEventDestroy(e);
     if (st2_) (void)hipStreamDestroy(st2_);
+    if (st3_) (void)hipStreamDestroy(st3_);
     if (own_st_) (void)hipStreamDestroy(own_st_);
   }
 
@@ -565,12 +576,18 @@ class Engine {
   bool prio_ = false;                        // stream/node priorities (DLAP_PRIO)
   hipStream_t st2_ = nullptr;                // evaluation branch of the pipelined epoch graph
   hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr, ev_mid_ = nullptr, ev_a_ = nullptr;
+  // third stream: side work of the training chain that nothing on it waits for soon -- the
+  // train split's metrics (read by the epoch bookkeeping) and the weight-gradient slab sums
+  // (read by Adam) -- forked with ev_m3_/ev_b3_ and joined back through ev_f3_
+  hipStream_t st3_ = nullptr;
+  hipEvent_t ev_m3_ = nullptr, ev_b3_ = nullptr, ev_f3_ = nullptr;
+  bool split_tail_ = false;                  // DLAP_SPLIT_TAIL
   int eval_gx_ = 0;                          // cap on the evaluation tower grid (DLAP_EVAL_GX)
   int b_wait_ = 0;                           // evaluation towers after train towers (DLAP_B_WAIT)
   bool zx_eval_ = true;                      // wide path: fused layer-0 evaluation towers (DLAP_ZX_EVAL)
   bool zx_train_ = true;                     // ... and training forward (DLAP_ZX_TRAIN)
   int zx_gx_ = 256;                          // their workgroups over all evaluation jobs (DLAP_ZX_GX)
-  bool side_metrics_ = false;                // train Sharpe monitor on a graph side branch (DLAP_SIDE_METRICS)
+  bool side_metrics_ = false;                // train metrics on the side stream st3_ (DLAP_SIDE_METRICS)
   bool train_first_ = true;                  // capture the training chain before the evaluation branch
   // Moment cache: the moment net only changes in phase 2, so outside it the moments h of every
   // split are constant (eval mode has no dropout; the train split's only if the moment tower has
@@ -1092,6 +1109,8 @@ class Engine {
       HIP_OK(hipEventRecord(ev_mid_, st_));
       HIP_OK(hipStreamWaitEvent(side, ev_mid_, 0));
       launch_job_metrics(as<LossJob>(j_loss_train_[phase]), G_, side);
+      HIP_OK(hipEventRecord(ev_m3_, side));
+      side_open_ = true;
     } else {
       launch_job_metrics(as<LossJob>(j_loss_train_[phase]), G_, st_);
     }
@@ -1111,8 +1130,28 @@ class Engine {
   }
   void enqueue_train_tail(int phase) {
     const SplitDev& D = splits_[0];
-    launch_finalize(as<FinJob>(j_fin_), G_, dd(), md_, phase, slab_stride(), D.T, st_);
-    launch_lstm_bwd(as<UpdJob>(j_upd_), G_, dd(), md_, D.T, phase, st_);
+    if (split_tail_) {
+      // slab sums beside the LSTM backward (which reads only the per-period sums)
+      HIP_OK(hipEventRecord(ev_b3_, st_));
+      HIP_OK(hipStreamWaitEvent(st3_, ev_b3_, 0));
+      launch_finalize(as<FinJob>(j_fin_), G_, dd(), md_, phase, slab_stride(), D.T, st3_, 1);
+      launch_finalize(as<FinJob>(j_fin_), G_, dd(), md_, phase, slab_stride(), D.T, st_, 2);
+      launch_lstm_bwd(as<UpdJob>(j_upd_), G_, dd(), md_, D.T, phase, st_);
+      side_open_ = true;
+      join_side();
+    } else {
+      launch_finalize(as<FinJob>(j_fin_), G_, dd(), md_, phase, slab_stride(), D.T, st_);
+      launch_lstm_bwd(as<UpdJob>(j_upd_), G_, dd(), md_, D.T, phase, st_);
+      join_side();
+    }
+  }
+  // join whatever was forked onto st3_ back into st_ (required before a graph capture ends)
+  bool side_open_ = false;
+  void join_side() {
+    if (!side_open_) return;
+    HIP_OK(hipEventRecord(ev_f3_, st3_));
+    HIP_OK(hipStreamWaitEvent(st_, ev_f3_, 0));
+    side_open_ = false;
   }
   void enqueue_train(int phase, float lr) {
     enqueue_train_grads(phase);
@@ -1162,22 +1201,25 @@ class Engine {
     HIP_OK(hipStreamWaitEvent(st2_, ev_fork_, 0));
     if (b_wait_ == 0 && train_first_) {
       // same graph topology, training-chain nodes first (they land on the graph's first queue)
-      enqueue_train_grads(phase, side_metrics_ ? st2_ : nullptr, true);   // this epoch's fwd/bwd
+      enqueue_train_grads(phase, side_metrics_ ? st3_ : nullptr, true);   // this epoch's fwd/bwd
       enqueue_eval(st2_);                                 // previous epoch's evaluation
+      if (side_metrics_) HIP_OK(hipStreamWaitEvent(st2_, ev_m3_, 0));   // train metrics
       enqueue_epoch_end(phase, ignore_epoch, sel, st2_);  // ... and its bookkeeping
       enqueue_dropmask(phase, 1, st2_);                   // next epoch's dropout masks
     } else if (b_wait_ == 0) {
+      // (the bookkeeping is enqueued before the training chain here: train metrics stay on st_)
       enqueue_eval(st2_);                                 // previous epoch's evaluation
       enqueue_epoch_end(phase, ignore_epoch, sel, st2_);  // ... and its bookkeeping
       enqueue_dropmask(phase, 1, st2_);                   // next epoch's dropout masks
-      enqueue_train_grads(phase, side_metrics_ ? st2_ : nullptr, true);   // this epoch's fwd/bwd
+      enqueue_train_grads(phase, nullptr, true);          // this epoch's fwd/bwd
     } else {
       // the evaluation towers start once the training towers (b_wait_ 1: backward, 2:
       // forward) are done, so the wide kernels of the two branches do not contend
       enqueue_eval_prologue(st2_);
-      enqueue_train_grads(phase, side_metrics_ ? st2_ : nullptr, true, b_wait_, true);
+      enqueue_train_grads(phase, side_metrics_ ? st3_ : nullptr, true, b_wait_, true);
       HIP_OK(hipStreamWaitEvent(st2_, ev_a_, 0));
       enqueue_eval_towers(st2_);
+      if (side_metrics_) HIP_OK(hipStreamWaitEvent(st2_, ev_m3_, 0));
       enqueue_epoch_end(phase, ignore_epoch, sel, st2_);
       enqueue_dropmask(phase, 1, st2_);
       enqueue_train_tail(phase);

@@ -18,7 +18,7 @@
 // per-row LSTM / moment-bias gradients into per-period sums. grid (nblocks, models).
 __global__ __launch_bounds__(256) void k_finalize(const FinJob* __restrict__ jobs,
                                                   const ModelDesc* __restrict__ md, int phase,
-                                                  int slab_stride) {
+                                                  int slab_stride, int b0) {
   const FinJob& J = jobs[blockIdx.y];
   const bool mom = phase == 2;
   const int ntile = mom ? md->ntile_m : md->ntile_s;
@@ -27,7 +27,7 @@ __global__ __launch_bounds__(256) void k_finalize(const FinJob* __restrict__ job
   const int nb_extra = (SLAB_EXTRA + 63) / 64;
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int b = blockIdx.x;
+  int b = blockIdx.x + b0;       // b0: first block of a partial launch (see launch_finalize)
   // slab sums: lane = element, the 4 waves split the slabs (each sums its quarter in order,
   // 16 independent loads in flight), then a fixed-order LDS combine
   auto slab_sum = [&](const float* src) {
@@ -84,12 +84,17 @@ __global__ __launch_bounds__(256) void k_finalize(const FinJob* __restrict__ job
 }
 
 void launch_finalize(const FinJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
-                     int phase, int slab_stride, int tmax, hipStream_t st) {
+                     int phase, int slab_stride, int tmax, hipStream_t st, int part) {
   const bool mom = phase == 2;
   const int ntile = mom ? mh.ntile_m : mh.ntile_s;
   const int D = mom ? 64 : (mh.nrnn > 0 ? mh.Dm : 0);
-  const int nb = ntile * 64 + (SLAB_EXTRA + 63) / 64 + (D > 0 ? tmax : 0);
-  hipLaunchKernelGGL(k_finalize, dim3(nb, njobs), dim3(256), 0, st, jobs, md, phase, slab_stride);
+  const int nslab = ntile * 64 + (SLAB_EXTRA + 63) / 64, nper = D > 0 ? tmax : 0;
+  // part 0: everything; 1: the weight / bias slab sums; 2: the per-period segment sums (what
+  // the LSTM backward reads), so part 1 can run beside the LSTM backward on another stream
+  const int b0 = part == 2 ? nslab : 0;
+  const int nb = part == 1 ? nslab : part == 2 ? nper : nslab + nper;
+  if (nb == 0) return;
+  hipLaunchKernelGGL(k_finalize, dim3(nb, njobs), dim3(256), 0, st, jobs, md, phase, slab_stride, b0);
   HIP_OK(hipGetLastError());
 }
 

@@ -68,7 +68,7 @@ struct EpochJob {          // one model
 };
 
 void launch_finalize(const FinJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
-                     int phase, int slab_stride, int tmax, hipStream_t st);
+                     int phase, int slab_stride, int tmax, hipStream_t st, int part = 0);
 void launch_update(const UpdJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh, int phase,
                    float lr, hipStream_t st);
 void launch_lstm_bwd(const UpdJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
