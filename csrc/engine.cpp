@@ -18,6 +18,10 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <execinfo.h>
+#include <signal.h>
+#include <unistd.h>
+
 #include <atomic>
 #include <cmath>
 #include <cstring>
@@ -50,6 +54,8 @@ static std::mutex g_legacy_mu;
 // Host-blocking HIP calls issued by the engine (synchronous copies / allocations, stream syncs):
 // the module-API tests assert that a training step issues none.
 static std::atomic<long long> g_blocking{0};
+// Engines alive in the process (leak checks in the GPU tests)
+static std::atomic<int> g_live_engines{0};
 #define HIP_LEGACY(expr)                                \
   do {                                                  \
     std::lock_guard<std::mutex> _legacy_guard(g_legacy_mu); \
@@ -114,12 +120,19 @@ static int env_int(const char* name, int dflt) {
   return v && *v ? std::atoi(v) : dflt;
 }
 
+static void install_crash_handler();
+// DLAP_TRACE_HOST=1: one stderr line per host-side engine step (crash localisation on boxes
+// where a native backtrace is not available)
+static const bool g_htrace = [] { const char* v = std::getenv("DLAP_TRACE_HOST"); return v && *v == '1'; }();
+#define HTRACE(...) do { if (g_htrace) { fprintf(stderr, "[dlap-trace] " __VA_ARGS__); fputc('\n', stderr); fflush(stderr); } } while (0)
+
 class Engine {
  public:
   Engine(int F, int M, int nrnn, int H, bool raw_macro_sdf, std::vector<int> hidden,
          std::vector<int> mom_hidden, int K, float dropout, bool normalize_w, bool weighted,
          float residual, int G, int max_epochs, bool fp32)
       : G_(G), max_epochs_(max_epochs) {
+    g_live_engines.fetch_add(1);
     unroll_ = std::max(1, env_int("DLAP_UNROLL", 1));
     prio_ = env_int("DLAP_PRIO", 0) != 0;
     if (prio_) {   // the training chain (critical path) ahead of the evaluation branch
@@ -183,6 +196,7 @@ class Engine {
     }
   }
   ~Engine() {
+    g_live_engines.fetch_sub(1);
     // drain both streams before the graphs, events and (member) buffers go away
     if (st2_) (void)hipStreamSynchronize(st2_);
     if (st3_) (void)hipStreamSynchronize(st3_);
@@ -429,6 +443,8 @@ class Engine {
   // epoch e read the same parameters, so they run as two concurrent branches of one hipGraph
   // and join before the Adam update:   head | pipe x (n-1) | tail.
   void run_epochs(int phase, int n, float lr, int ignore_epoch, float sel, bool use_graph) {
+    install_crash_handler();
+    HTRACE("run_epochs phase=%d n=%d graph=%d dirty=%d", phase, n, (int)use_graph, (int)graphs_dirty_);
     if (!splits_[0].set) throw std::runtime_error("train split not set");
     if (ext_stream_) throw std::runtime_error("run_epochs needs the engine's own streams (set_stream(0, False))");
     if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
@@ -458,12 +474,15 @@ class Engine {
       bodyU = graph_for(graph_key(phase, lr, ignore_epoch, sel, 100 + U), [&] {
         for (int u = 0; u < U; ++u) enqueue_pipe(phase, lr, ignore_epoch, sel);
       });
+    HTRACE("launch head");
     HIP_OK(hipGraphLaunch(head, st_));
     int e = 1;
     if (bodyU)
       for (; e + U <= n; e += U) HIP_OK(hipGraphLaunch(bodyU, st_));
     for (; e < n; ++e) HIP_OK(hipGraphLaunch(body, st_));
+    HTRACE("launch tail");
     HIP_OK(hipGraphLaunch(tail, st_));
+    HTRACE("run_epochs done");
   }
   void set_pipeline(bool on) { pipeline_ = on; }
 
@@ -947,6 +966,7 @@ class Engine {
   }
 
   void rebuild_jobs() {
+    HTRACE("rebuild_jobs");
     for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
     graphs_.clear();
     fwd_tables_.clear();
@@ -1065,12 +1085,16 @@ class Engine {
   // read them) if the moment parameters may have changed since they were computed.
   void ensure_moments() {
     if (!h_cache_ || h_valid_ || n_mom_jobs_ == 0) return;
+    HTRACE("ensure_moments jobs=%d tmax=%d gx=%d", n_mom_jobs_, tmax_all_, gx_mom_);
+    HTRACE("launch_prologue");
     launch_prologue(as<RnnJob>(j_rnn_mom_), n_mom_jobs_, tmax_all_, dd(), md_, st_);
     if (md_.md.wide && zx_eval_) {
+      HTRACE("launch_mlp_fwd_zx");
       launch_mlp_fwd_zx(as<MlpJob>(j_mlp_mom_), n_mom_jobs_, std::max(1, zx_gx_ / n_mom_jobs_), md_.md, md_.WMB, st_);
     } else {
       if (md_.md.wide) launch_proj0(as<WideJob>(j_wide_mom_), n_mom_jobs_, std::max({gx_proj_[0], gx_proj_[1], gx_proj_[2]}),
                                     md_.md, md_.WMB, st_);
+      HTRACE("launch_mlp_fwd");
       launch_mlp_fwd(as<MlpJob>(j_mlp_mom_), n_mom_jobs_, gx_mom_, md_.md, md_.KS1, md_.WMB, st_);
     }
     h_valid_ = true;
@@ -1079,6 +1103,7 @@ class Engine {
   // keep masks of the step *drop_step + offset* (phases 1/3: the SDF tower's dropout)
   void enqueue_dropmask(int phase, int offset, hipStream_t st) {
     if (!dropmask_on(phase)) return;
+    HTRACE("launch_dropmask");
     launch_dropmask(as<MlpJob>(j_mlp_train_[phase]), G_, (splits_[0].R + 31) / 32, md_.md, offset, st);
   }
   // side: if non-null, the train split's Sharpe monitor (not needed by the backward) runs
@@ -1092,6 +1117,7 @@ class Engine {
     const SplitDev& D = splits_[0];
     if (!premasked) enqueue_dropmask(phase, 0, st_);
     // the latency-bound LSTM first, before the streaming projection loads the memory system
+    HTRACE("launch_prologue");
     launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_, train_mom(phase));
     const bool zx_train = md_.md.wide && zx_train_;
     if (md_.md.wide && !zx_train)
@@ -1103,22 +1129,29 @@ class Engine {
       launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, phase == 2 ? gx_fwd_[0] : gx_fwd13_, md_.md, md_.KS1,
                      md_.WMB, st_);
     if (mark == 2) HIP_OK(hipEventRecord(ev_a_, st_));
+    HTRACE("launch_period_fwd");
     launch_period_fwd(as<LossJob>(j_loss_train_[phase]), G_, D.T, st_);
+    HTRACE("launch_asset");
     launch_asset(as<LossJob>(j_loss_train_[phase]), G_, D.N, md_.K, st_);
     if (side) {
       HIP_OK(hipEventRecord(ev_mid_, st_));
       HIP_OK(hipStreamWaitEvent(side, ev_mid_, 0));
+      HTRACE("launch_job_metrics");
       launch_job_metrics(as<LossJob>(j_loss_train_[phase]), G_, side);
       HIP_OK(hipEventRecord(ev_m3_, side));
       side_open_ = true;
     } else {
+      HTRACE("launch_job_metrics");
       launch_job_metrics(as<LossJob>(j_loss_train_[phase]), G_, st_);
     }
     if (phase == 2) {
+      HTRACE("launch_mlp_bwd_mom");
       launch_mlp_bwd_mom(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_m, 1, md_.md, md_.KS1,
                          md_.WMB, slab_stride(), st_);
     } else {
+      HTRACE("launch_period_bwd");
       launch_period_bwd(as<LossJob>(j_loss_train_[phase]), G_, D.T, st_);
+      HTRACE("launch_mlp_bwd_sdf");
       launch_mlp_bwd_sdf(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_s, md_.tps_s, md_.md, md_.KS1,
                          slab_stride(), st_);
     }
@@ -1134,13 +1167,18 @@ class Engine {
       // slab sums beside the LSTM backward (which reads only the per-period sums)
       HIP_OK(hipEventRecord(ev_b3_, st_));
       HIP_OK(hipStreamWaitEvent(st3_, ev_b3_, 0));
+      HTRACE("launch_finalize");
       launch_finalize(as<FinJob>(j_fin_), G_, dd(), md_, phase, slab_stride(), D.T, st3_, 1);
+      HTRACE("launch_finalize");
       launch_finalize(as<FinJob>(j_fin_), G_, dd(), md_, phase, slab_stride(), D.T, st_, 2);
+      HTRACE("launch_lstm_bwd");
       launch_lstm_bwd(as<UpdJob>(j_upd_), G_, dd(), md_, D.T, phase, st_);
       side_open_ = true;
       join_side();
     } else {
+      HTRACE("launch_finalize");
       launch_finalize(as<FinJob>(j_fin_), G_, dd(), md_, phase, slab_stride(), D.T, st_);
+      HTRACE("launch_lstm_bwd");
       launch_lstm_bwd(as<UpdJob>(j_upd_), G_, dd(), md_, D.T, phase, st_);
       join_side();
     }
@@ -1155,6 +1193,7 @@ class Engine {
   }
   void enqueue_train(int phase, float lr) {
     enqueue_train_grads(phase);
+    HTRACE("launch_update");
     launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);
   }
   void enqueue_eval(hipStream_t st) {
@@ -1163,6 +1202,7 @@ class Engine {
   }
   void enqueue_eval_prologue(hipStream_t st) {
     if (n_eval_jobs_ == 0) return;
+    HTRACE("launch_prologue");
     launch_prologue(as<RnnJob>(j_rnn_eval_), n_eval_jobs_, tmax_eval_, dd(), md_, st, !h_cache_);
   }
   void enqueue_eval_towers(hipStream_t st) {
@@ -1170,23 +1210,30 @@ class Engine {
     int gx = std::max(gx_fwd_[1], gx_fwd_[2]);
     if (eval_gx_ > 0) gx = std::min(gx, eval_gx_);
     if (md_.md.wide && zx_eval_) {     // layer 0 streamed inside the evaluation towers
+      HTRACE("launch_mlp_fwd_zx");
       launch_mlp_fwd_zx(as<MlpJob>(j_mlp_eval_), n_eval_jobs_, std::max(1, zx_gx_ / n_eval_jobs_), md_.md, md_.WMB, st);
     } else {
       if (md_.md.wide)
         launch_proj0(as<WideJob>(j_wide_eval_), n_eval_jobs_, std::max(gx_proj_[1], gx_proj_[2]), md_.md, md_.WMB, st);
+      HTRACE("launch_mlp_fwd");
       launch_mlp_fwd(as<MlpJob>(j_mlp_eval_), n_eval_jobs_, gx, md_.md, md_.KS1, md_.WMB, st);
     }
+    HTRACE("launch_period_fwd");
     launch_period_fwd(as<LossJob>(j_loss_eval_), n_eval_jobs_, tmax_eval_, st);
+    HTRACE("launch_asset");
     launch_asset(as<LossJob>(j_loss_eval_), n_eval_jobs_, nmax_eval_, md_.K, st);
+    HTRACE("launch_job_metrics");
     launch_job_metrics(as<LossJob>(j_loss_eval_), n_eval_jobs_, st);
   }
   void enqueue_epoch_end(int phase, int ignore_epoch, float sel, hipStream_t st) {
+    HTRACE("launch_epoch_end");
     launch_epoch_end(as<EpochJob>(j_epoch_[phase]), G_, phase, ignore_epoch, sel, md_.residual_factor,
                      md_.P, st);
   }
   // sequential epoch: train step, evaluation, bookkeeping
   void enqueue_epoch(int phase, float lr, int ignore_epoch, float sel) {
     enqueue_train_grads(phase);
+    HTRACE("launch_update");
     launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);
     if (phase != 2) enqueue_eval(st_);
     enqueue_epoch_end(phase, ignore_epoch, sel, st_);
@@ -1194,6 +1241,7 @@ class Engine {
   void enqueue_head(int phase, float lr) {
     enqueue_train_grads(phase);
     enqueue_dropmask(phase, 1, st_);                     // masks of the first pipelined epoch
+    HTRACE("launch_update");
     launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);
   }
   void enqueue_pipe(int phase, float lr, int ignore_epoch, float sel) {
@@ -1226,6 +1274,7 @@ class Engine {
     }
     HIP_OK(hipEventRecord(ev_join_, st2_));               // (train monitor ran on st2_ too)
     HIP_OK(hipStreamWaitEvent(st_, ev_join_, 0));
+    HTRACE("launch_update");
     launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);
   }
   void enqueue_tail(int phase, int ignore_epoch, float sel) {
@@ -1239,10 +1288,13 @@ class Engine {
     hipGraph_t graph;
     {
       std::lock_guard<std::mutex> g(g_legacy_mu);
+      HTRACE("capture %s", key.c_str());
       HIP_OK(hipStreamBeginCapture(st_, hipStreamCaptureModeThreadLocal));
       enqueue();
+      HTRACE("end capture");
       HIP_OK(hipStreamEndCapture(st_, &graph));
     }
+    HTRACE("instantiate");
     hipGraphExec_t exec;
     HIP_OK(hipGraphInstantiateWithFlags(&exec, graph, prio_ ? hipGraphInstantiateFlagUseNodePriority : 0));
     HIP_OK(hipGraphDestroy(graph));
@@ -1288,7 +1340,35 @@ class Engine {
   }
 };
 
+// Native-frame backtrace on a host crash (failure detection): Python's faulthandler
+// only names the Python frame; this prints the native frames (file-relative offsets, resolvable
+// with addr2line against the in-tree .so) and then chains to the previous handler.
+static struct sigaction g_prev_segv, g_prev_bus;
+static void dlap_crash_handler(int sig, siginfo_t*, void*) {
+  void* fr[64];
+  const int n = backtrace(fr, 64);
+  static const char msg[] = "[dlap] native backtrace:\n";
+  (void)!write(2, msg, sizeof msg - 1);
+  backtrace_symbols_fd(fr, n, 2);
+  sigaction(sig, sig == SIGBUS ? &g_prev_bus : &g_prev_segv, nullptr);
+  raise(sig);
+}
+static void install_crash_handler() {
+  if (env_int("DLAP_CRASH_TRACE", 1) == 0) return;
+  struct sigaction cur {};
+  if (sigaction(SIGSEGV, nullptr, &cur) == 0 && (cur.sa_flags & SA_SIGINFO) &&
+      cur.sa_sigaction == dlap_crash_handler)
+    return;                                    // (re-installed on entry points: others may replace it)
+  struct sigaction sa {};
+  sa.sa_sigaction = dlap_crash_handler;
+  sa.sa_flags = SA_SIGINFO | SA_ONSTACK;
+  sigemptyset(&sa.sa_mask);
+  sigaction(SIGSEGV, &sa, &g_prev_segv);
+  sigaction(SIGBUS, &sa, &g_prev_bus);
+}
+
 PYBIND11_MODULE(_dlap_hip, m) {
+  install_crash_handler();
   m.doc() = "DLAP MI355X native engine (HIP kernels for gfx950 + hipGraph epoch executor)";
   py::class_<Engine>(m, "Engine")
       .def(py::init<int, int, int, int, bool, std::vector<int>, std::vector<int>, int, float, bool, bool,
@@ -1318,6 +1398,7 @@ PYBIND11_MODULE(_dlap_hip, m) {
       .def("set_pipeline", &Engine::set_pipeline)
       .def("set_lr", &Engine::set_lr)
       .def_static("blocking_calls", []() { return (long long)g_blocking.load(); })
+      .def_static("live_engines", []() { return g_live_engines.load(); })
       .def_static("rnn_timestamps", []() { return rnn_timestamps(); })
       .def_static("loss_timestamps", []() { return loss_timestamps(); })
       .def_static("mlp_timestamps", []() { return mlp_timestamps(); })

@@ -533,6 +533,9 @@ __global__ __launch_bounds__(FUSE ? LSTM_FUSE_THREADS : 64) void k_lstm_gls(cons
   RNN_TS(tsb + 3, tsm);
 }
 
+static const bool g_rtrace = [] { const char* v = std::getenv("DLAP_TRACE_HOST"); return v && *v == '1'; }();
+#define RTRACE(...) do { if (g_rtrace) { fprintf(stderr, "[dlap-trace] " __VA_ARGS__); fputc('\n', stderr); fflush(stderr); } } while (0)
+
 void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* md, const ModelDesc& mh,
                      hipStream_t st, bool abias) {
   // DLAP_LSTM_FUSE_PROJ=1: the LSTM workgroup projects its own inputs (k_lstm_gls<.., FUSE>) and
@@ -551,10 +554,13 @@ void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* m
   // shared by the last gates and the first moment columns stays), the gates only, or none
   const int y0 = abias && fuse ? G4 / 16 : 0;
   const int ny = abias ? mh.proj_np / 16 - y0 : (fuse ? 0 : (G4 + 15) / 16);
+  RTRACE("prologue jobs=%p njobs=%d tmax=%d H=%d nrnn=%d proj_np=%d y0=%d ny=%d fuse=%d st=%p", (const void*)jobs,
+         njobs, tmax, mh.H, mh.nrnn, mh.proj_np, y0, ny, (int)fuse, (void*)st);
   if (ny > 0) {
     hipLaunchKernelGGL(k_proj, dim3((tmax + 15) / 16, ny, njobs), dim3(64), 0, st, jobs, md, y0);
     HIP_OK(hipGetLastError());
   }
+  RTRACE("prologue proj launched");
   if (mh.nrnn > 0) {
     const bool stage = tmax * 4 * mh.H <= 12288;     // 48 KiB of LDS
     const size_t sh = stage ? (size_t)tmax * 4 * mh.H * sizeof(float) : 0;
@@ -586,6 +592,7 @@ void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* m
 #undef G_CASE
 #undef S_CASE
     HIP_OK(hipGetLastError());
+    RTRACE("prologue lstm launched (gls=%d shg=%zu)", (int)gls, shg);
   }
 }
 

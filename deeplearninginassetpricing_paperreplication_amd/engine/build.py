@@ -98,12 +98,24 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True, ubsan: bool 
     build_dir.mkdir(parents=True, exist_ok=True)
     flags = _includes() + ["-Wno-unused-result"] + (UBSAN_FLAGS if ubsan else []) + (DEBUG_FLAGS if debug else [])
     objs = []
-    with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(srcs)))) as ex:
-        futs = {ex.submit(_compile, s, build_dir / (s.stem + ".o"), flags + ff.get(s.name, [])): s for s in srcs}
+    hkey = _hash(headers)
+    todo = []
+    for s in srcs:      # per-object cache: source + every header + its flags
+        obj = build_dir / (s.stem + ".o")
+        okey = build_dir / (s.stem + ".key")
+        k = _hash([s]) + hkey + repr(flags + ff.get(s.name, []))
+        if not force and obj.exists() and okey.exists() and okey.read_text() == k:
+            objs.append(obj)
+        else:
+            todo.append((s, obj, okey, k))
+    with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(todo) or 1))) as ex:
+        futs = {ex.submit(_compile, s, obj, flags + ff.get(s.name, [])): (s, okey, k) for s, obj, okey, k in todo}
         for f in cf.as_completed(futs):
             objs.append(f.result())
+            s, okey, k = futs[f]
+            okey.write_text(k)
             if verbose:
-                print(f"[dlap] compiled {futs[f].name}")
+                print(f"[dlap] compiled {s.name}")
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *(UBSAN_FLAGS if ubsan else []),
            *map(str, sorted(objs)), "-o", str(out)]
     r = subprocess.run(cmd, capture_output=True, text=True)

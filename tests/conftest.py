@@ -46,3 +46,14 @@ def shipped_data():
     if not os.path.isdir(os.path.join(SHIPPED_DATA, "char")):
         pytest.skip("reference synthetic data not available")
     return SHIPPED_DATA
+
+
+@pytest.fixture(autouse=True)
+def _trace_live_engines(request):
+    """DLAP_TRACE_LIVE=1: print the number of native engines alive after each test (leaks)."""
+    yield
+    if os.environ.get("DLAP_TRACE_LIVE") == "1" and "deeplearninginassetpricing_paperreplication_amd._dlap_hip" in sys.modules:
+        import gc
+        gc.collect()
+        mod = sys.modules["deeplearninginassetpricing_paperreplication_amd._dlap_hip"]
+        print(f"\n[live-engines] {request.node.name}: {mod.Engine.live_engines()}", flush=True)
