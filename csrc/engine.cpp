@@ -20,6 +20,7 @@
 
 #include <execinfo.h>
 #include <signal.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include <atomic>
@@ -62,6 +63,25 @@ static std::atomic<int> g_live_engines{0};
     g_blocking.fetch_add(1, std::memory_order_relaxed); \
     HIP_OK(expr);                                       \
   } while (0)
+
+// Retired epoch-graph executors. The runtime completes a graph launch through a handler on
+// its own thread that still touches the executor after the launching stream has been
+// synchronised; destroying the executor right away and having the allocator hand its memory
+// to the next executor crashed the next hipGraphLaunch inside the runtime (measured: the
+// pipelined body graph of a fresh engine, created right after the previous engine died, got the
+// address of the freshly destroyed one and segfaulted at its first launch). Executors are
+// therefore destroyed only after many later retirements (their handlers long finished); a few
+// hundred stay alive at most (a few KiB each).
+static std::mutex g_retired_mu;
+static std::vector<hipGraphExec_t> g_retired;
+static void retire_graph_exec(hipGraphExec_t e) {
+  std::lock_guard<std::mutex> g(g_retired_mu);
+  g_retired.push_back(e);
+  if (g_retired.size() >= 512) {
+    for (size_t i = 0; i < 256; ++i) (void)hipGraphExecDestroy(g_retired[i]);
+    g_retired.erase(g_retired.begin(), g_retired.begin() + 256);
+  }
+}
 
 namespace {
 
@@ -153,6 +173,8 @@ class Engine {
     HIP_OK(hipEventCreateWithFlags(&ev_m3_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_b3_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_f3_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
     eval_gx_ = env_int("DLAP_EVAL_GX", 256);
     b_wait_ = env_int("DLAP_B_WAIT", 0);
     // both off: a third graph branch changes how the runtime maps the graph onto its hardware
@@ -197,17 +219,18 @@ class Engine {
   }
   ~Engine() {
     g_live_engines.fetch_sub(1);
+    HTRACE("~Engine tid=%ld", (long)syscall(SYS_gettid));
     // drain both streams before the graphs, events and (member) buffers go away
     if (st2_) (void)hipStreamSynchronize(st2_);
     if (st3_) (void)hipStreamSynchronize(st3_);
     if (st_) (void)hipStreamSynchronize(st_);
     if (own_st_ && own_st_ != st_) (void)hipStreamSynchronize(own_st_);
-    for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
+    for (auto& kv : graphs_) retire_graph_exec(kv.second);
     if (ev_fork_) (void)hipEventDestroy(ev_fork_);
     if (ev_join_) (void)hipEventDestroy(ev_join_);
     if (ev_mid_) (void)hipEventDestroy(ev_mid_);
     if (ev_a_) (void)hipEventDestroy(ev_a_);
-    for (hipEvent_t e : {ev_m3_, ev_b3_, ev_f3_}) if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {ev_m3_, ev_b3_, ev_f3_, ev_in_, ev_out_}) if (e) (void)hipEventDestroy(e);
     if (st2_) (void)hipStreamDestroy(st2_);
     if (st3_) (void)hipStreamDestroy(st3_);
     if (own_st_) (void)hipStreamDestroy(own_st_);
@@ -498,6 +521,7 @@ class Engine {
     enqueue_train(phase, lr);
   }
   void backward_only(int phase, bool wait = true) {   // losses + gradients, no optimiser step
+    HTRACE("backward_only phase=%d tid=%ld", phase, (long)syscall(SYS_gettid));
     if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
     if (phase != 2) ensure_moments();
     enqueue_train_grads(phase);
@@ -511,11 +535,25 @@ class Engine {
   // (external: run on the stream handle ``st`` -- 0 is the legacy NULL stream, torch's default;
   //  not external: back to the engine's own stream)
   void set_stream(uintptr_t st, bool external) {
+    HTRACE("set_stream %p ext=%d tid=%ld", (void*)st, (int)external, (long)syscall(SYS_gettid));
     hipStream_t want = external ? reinterpret_cast<hipStream_t>(st) : own_st_;
     if (want == st_ && external == ext_stream_) return;
     sync();                                   // work queued on the previous stream completes first
     st_ = want;
     ext_stream_ = external;
+  }
+  // Event handoff with a caller's stream (torch's current stream; 0 = the legacy NULL stream):
+  // join_from: the engine's stream waits for the work queued so far on `ext`; join_to: `ext`
+  // waits for the work queued so far on the engine's stream. The module API brackets its
+  // engine calls with these, so the engine never runs on the caller's (possibly legacy) stream
+  // and no host synchronisation is needed.
+  void join_from(uintptr_t ext) {
+    HIP_OK(hipEventRecord(ev_in_, reinterpret_cast<hipStream_t>(ext)));
+    HIP_OK(hipStreamWaitEvent(st_, ev_in_, 0));
+  }
+  void join_to(uintptr_t ext) {
+    HIP_OK(hipEventRecord(ev_out_, st_));
+    HIP_OK(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(ext), ev_out_, 0));
   }
   // parameters from device memory (a flat fp32 vector in state_dict order), re-packed in order
   void set_params_dev(int g, uintptr_t src) {
@@ -600,6 +638,7 @@ class Engine {
   // (read by Adam) -- forked with ev_m3_/ev_b3_ and joined back through ev_f3_
   hipStream_t st3_ = nullptr;
   hipEvent_t ev_m3_ = nullptr, ev_b3_ = nullptr, ev_f3_ = nullptr;
+  hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;   // join_from / join_to
   bool split_tail_ = false;                  // DLAP_SPLIT_TAIL
   int eval_gx_ = 0;                          // cap on the evaluation tower grid (DLAP_EVAL_GX)
   int b_wait_ = 0;                           // evaluation towers after train towers (DLAP_B_WAIT)
@@ -967,7 +1006,7 @@ class Engine {
 
   void rebuild_jobs() {
     HTRACE("rebuild_jobs");
-    for (auto& kv : graphs_) (void)hipGraphExecDestroy(kv.second);
+    for (auto& kv : graphs_) retire_graph_exec(kv.second);
     graphs_.clear();
     fwd_tables_.clear();
     std::vector<RnnJob> rt, re;
@@ -1288,7 +1327,7 @@ class Engine {
     hipGraph_t graph;
     {
       std::lock_guard<std::mutex> g(g_legacy_mu);
-      HTRACE("capture %s", key.c_str());
+      HTRACE("capture %s tid=%ld", key.c_str(), (long)syscall(SYS_gettid));
       HIP_OK(hipStreamBeginCapture(st_, hipStreamCaptureModeThreadLocal));
       enqueue();
       HTRACE("end capture");
@@ -1408,6 +1447,8 @@ PYBIND11_MODULE(_dlap_hip, m) {
       .def("backward_only", &Engine::backward_only, py::arg("phase"), py::arg("wait") = true)
       .def("set_stream", &Engine::set_stream, py::arg("stream"), py::arg("external") = true)
       .def("set_params_dev", &Engine::set_params_dev)
+      .def("join_from", &Engine::join_from)
+      .def("join_to", &Engine::join_to)
       .def("set_drop_step", &Engine::set_drop_step)
       .def("copy_ws", &Engine::copy_ws)
       .def("copy_grads", &Engine::copy_grads)

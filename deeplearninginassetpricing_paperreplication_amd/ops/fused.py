@@ -5,7 +5,9 @@ persistent LSTM), not eager PyTorch ops.
 Reference semantics: `/root/reference/src/model.py:485-594` (forward dict, get_weights) and
 `:620-694` (SimpleSDF).
 
-Everything is stream-ordered on torch's current stream (``Engine.set_stream``): parameters go
+Everything is stream-ordered with torch's current stream: the engine runs on its own stream and
+joins torch's stream with events on entry and exit (``Engine.join_from`` / ``join_to``; it never
+queues work on torch's, possibly legacy NULL, stream). Parameters go
 to the engine as one device-to-device copy of the flat fp32 vector (skipped when no parameter
 changed since the last call), results come back as device-to-device copies into torch tensors,
 and the dropout stream advances with a one-int kernel -- a forward / backward pair issues no
@@ -80,9 +82,18 @@ def _flat_params(params: List[torch.Tensor], device) -> torch.Tensor:
     return torch.cat([p.detach().reshape(-1).to(device=device, dtype=torch.float32) for p in params])
 
 
-def _bind(s: _Slot, device):
+def _bind(s: _Slot, device) -> int:
+    """Order the engine's stream after torch's current stream; returns that stream's handle
+    for the matching ``_release``."""
     torch.cuda.set_device(device)
-    s.eng.eng.set_stream(torch.cuda.current_stream(device).cuda_stream)
+    ts = torch.cuda.current_stream(device).cuda_stream
+    s.eng.eng.join_from(ts)
+    return ts
+
+
+def _release(s: _Slot, ts: int):
+    """Order torch's stream ``ts`` after everything queued on the engine so far."""
+    s.eng.eng.join_to(ts)
 
 
 def _prepare(model, spec: ModelSpec, params: List[torch.Tensor], flat_fn, macro, individual, returns, mask,
@@ -92,7 +103,7 @@ def _prepare(model, spec: ModelSpec, params: List[torch.Tensor], flat_fn, macro,
     sp = spec if training else dataclasses.replace(spec, dropout=0.0)
     s = _slot(sp)
     dev = individual.device
-    _bind(s, dev)
+    torch.cuda.set_device(dev)
     key = (_tkey(macro), _tkey(individual), _tkey(returns), _tkey(mask))
     if key != s.data_key:
         batch = {"individual_features": individual.detach(), "returns": returns.detach(),
@@ -105,6 +116,8 @@ def _prepare(model, spec: ModelSpec, params: List[torch.Tensor], flat_fn, macro,
     pkey = tuple((p.data_ptr(), p._version) for p in params)
     if pkey != s.param_key:
         s._flat = flat_fn(dev).contiguous()            # kept alive until the next call
+    s.ts = _bind(s, dev)               # the engine waits for torch's queued work (panel, params)
+    if pkey != s.param_key:
         s.eng.eng.set_params_dev(0, s._flat.data_ptr())
         s.param_key = pkey
     if training:
@@ -116,6 +129,7 @@ def _prepare(model, spec: ModelSpec, params: List[torch.Tensor], flat_fn, macro,
 
 def _copy(s: _Slot, name: str, n: int, dev) -> torch.Tensor:
     out = torch.empty(n, dtype=torch.float32, device=dev)
+    s.eng.eng.join_from(s.ts)          # (out may reuse memory torch's stream still reads)
     got = s.eng.eng.copy_ws(0, 0, name, out.data_ptr())
     assert got == n, (name, got, n)
     return out
@@ -132,14 +146,16 @@ class _EngineLoss(torch.autograd.Function):
         s = ctx.slot
         eng = s.eng.eng
         dev = g.device
-        _bind(s, dev)
+        ts = _bind(s, dev)
         P = sum(int(n) for n in ctx.spec.param_counts())
         P_sdf = ctx.spec.param_counts()[0]
 
         def grads(phase):
-            eng.backward_only(phase, False)
             out = torch.empty(P, dtype=torch.float32, device=dev)
+            eng.join_from(ts)          # (out may reuse memory torch's stream still reads)
+            eng.backward_only(phase, False)
             eng.copy_grads(0, out.data_ptr())
+            _release(s, ts)
             return out
 
         flat = torch.zeros(P, dtype=torch.float32, device=dev)
@@ -178,6 +194,14 @@ def gan_forward(model, macro, individual, returns, mask, phase: str = "condition
     wn = _copy(s, "wn", T * N, dev).reshape(T, N)
     h = _copy(s, "h", T * N * K, dev).reshape(T, N, K).permute(2, 0, 1)
     p = _copy(s, "P", T, dev)
+    hidden = None
+    if model.spec.rnn_layers > 0 and macro is not None:
+        Lr, H = model.spec.rnn_layers, model.spec.rnn_hidden
+        h_n = torch.empty(Lr, 1, H, device=dev)
+        c_n = torch.empty(Lr, 1, H, device=dev)
+        eng.copy_hidden(0, h_n.data_ptr(), c_n.data_ptr())
+        hidden = (h_n, c_n)
+    _release(s, s.ts)                  # torch's stream waits for the engine's results
     l_cond, l_unc, l_res = sc[SC["loss_cond"]], sc[SC["loss_unc"]], sc[SC["loss_res"]]
     res_f = float(model.spec.residual_loss_factor)
     zero = torch.zeros((), device=dev)
@@ -193,13 +217,6 @@ def gan_forward(model, macro, individual, returns, mask, phase: str = "condition
     if torch.is_grad_enabled() and any(q.requires_grad for q in params):
         loss = _EngineLoss.apply(loss, s, model.spec, _PHASE[phase], res_f, _split_flat(model.spec, params),
                                  *params)
-    hidden = None
-    if model.spec.rnn_layers > 0 and macro is not None:
-        Lr, H = model.spec.rnn_layers, model.spec.rnn_hidden
-        h_n = torch.empty(Lr, 1, H, device=dev)
-        c_n = torch.empty(Lr, 1, H, device=dev)
-        eng.copy_hidden(0, h_n.data_ptr(), c_n.data_ptr())
-        hidden = (h_n, c_n)
     return {
         "weights": wn, "loss": loss, "loss_unconditional": l_unc_out, "loss_conditional": l_cond_out,
         "loss_residual": l_res if res_f > 0 else zero,
@@ -226,6 +243,7 @@ def gan_weights(model, macro, individual, mask, normalized: bool = False) -> tor
                  _zeros_like_mask(mask), mask, bool(model.training))
     s.eng.eng.forward_split(0, bool(model.training), False, False)
     w = _copy(s, "wn", s.T * s.N, individual.device).reshape(s.T, s.N)
+    _release(s, s.ts)
     if normalized:
         w = L.l1_normalize(w, mask)
     return w
@@ -294,6 +312,7 @@ def simple_forward(model, macro, individual, returns, mask) -> Dict:
     sc = _copy(s, "scal", 8, dev)
     w = _copy(s, "wn", T * N, dev).reshape(T, N)
     p = _copy(s, "P", T, dev)
+    _release(s, s.ts)
     loss = sc[SC["loss_unc"]].clone()
     if torch.is_grad_enabled() and any(q.requires_grad for q in params):
         loss = _EngineLoss.apply(loss, s, s.spec, 1, 0.0, _simple_to_params(model, spec), *params)
