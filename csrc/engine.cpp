@@ -854,7 +854,7 @@ class Engine {
       W.w.alloc((size_t)std::max(R, 1)); W.wn.alloc((size_t)T * N); W.h.alloc((size_t)T * N * K);
       W.P.alloc(T); W.port.alloc(T); W.sdf.alloc(T); W.mu.alloc(T);
       W.E.alloc((size_t)N * K); W.Eu.alloc(N); W.dE.alloc((size_t)N * K); W.dEu.alloc(N);
-      W.part.alloc(2 * (((size_t)N * (K + 1) + 255) / 256));
+      W.part.alloc(2 * std::max(((size_t)N * (K + 1) + 255) / 256, ((size_t)N + 15) / 16));
       W.pe.alloc((size_t)DLAP_TCH * N * K); W.pu.alloc((size_t)DLAP_TCH * N);
       W.scal.alloc(SC_NSCAL);
       if (s == 0) W.scal_prev.alloc(SC_NSCAL);
@@ -992,6 +992,7 @@ class Engine {
     J.row_ptr = D.row_ptr.p; J.rowti = reinterpret_cast<const int2*>(D.rowti.p); J.Rc = D.Rc.p; J.mu = W.mu.p;
     J.normalize = md_.normalize_w; J.weighted = md_.weighted_loss; J.phase = phase;
     J.res_factor = md_.residual_factor;
+    J.asset_full = (phase > 0 && asset_full_default()) ? 1 : 0;   // training jobs only
     const float kn = (float)md_.K * (float)D.N;
     J.coef_c = phase == 3 ? 2.f / kn : (phase == 2 ? -2.f / kn : 0.f);
     J.coef_u = phase == 1 ? 2.f / (float)D.N : 0.f;
@@ -1171,7 +1172,7 @@ class Engine {
     HTRACE("launch_period_fwd");
     launch_period_fwd(as<LossJob>(j_loss_train_[phase]), G_, D.T, st_);
     HTRACE("launch_asset");
-    launch_asset(as<LossJob>(j_loss_train_[phase]), G_, D.N, md_.K, st_);
+    launch_asset(as<LossJob>(j_loss_train_[phase]), G_, D.N, md_.K, st_, asset_full_default());
     if (side) {
       HIP_OK(hipEventRecord(ev_mid_, st_));
       HIP_OK(hipStreamWaitEvent(side, ev_mid_, 0));
@@ -1179,17 +1180,17 @@ class Engine {
       launch_job_metrics(as<LossJob>(j_loss_train_[phase]), G_, side);
       HIP_OK(hipEventRecord(ev_m3_, side));
       side_open_ = true;
-    } else {
+    } else if (phase == 2) {
       HTRACE("launch_job_metrics");
       launch_job_metrics(as<LossJob>(j_loss_train_[phase]), G_, st_);
-    }
+    }   // (phases 1 / 3: the metrics run as an extra workgroup of the period backward)
     if (phase == 2) {
       HTRACE("launch_mlp_bwd_mom");
       launch_mlp_bwd_mom(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_m, 1, md_.md, md_.KS1,
                          md_.WMB, slab_stride(), st_);
     } else {
       HTRACE("launch_period_bwd");
-      launch_period_bwd(as<LossJob>(j_loss_train_[phase]), G_, D.T, st_);
+      launch_period_bwd(as<LossJob>(j_loss_train_[phase]), G_, D.T, st_, side == nullptr);
       HTRACE("launch_mlp_bwd_sdf");
       launch_mlp_bwd_sdf(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_s, md_.tps_s, md_.md, md_.KS1,
                          slab_stride(), st_);

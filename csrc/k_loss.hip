@@ -16,6 +16,8 @@
 //                 the zero-mean normalisation, dL/dw_raw = m c_t (R - mean_t R) (+ residual)
 //   k_job_metrics one workgroup per job: scalar losses, Sharpe (unbiased std, 1e-8 guard),
 //                 max drawdown (cumprod scan), mean/std of the evaluation returns
+#include <cstdlib>
+
 #include "common.h"
 #include "loss.h"
 
@@ -217,7 +219,11 @@ __global__ __launch_bounds__(256) void k_asset_part(const LossJob* __restrict__ 
 // all requested before they are summed (in chunk order), so the pass is one memory round trip.
 // Writes E, E_unc, dL/dE and the block's loss partial sums. Without moments (h == nullptr: the
 // unconditional training loss) only the E_unc outputs exist.
-DLAP_DEV int asset_red_blocks(const LossJob& J) { return (J.N * (J.h ? J.K + 1 : 1) + 255) >> 8; }
+// number of loss partials the asset pass leaves in J.part (read by final_losses)
+#define AF_S 16            // k_asset_full: stocks per workgroup (x 16 time lanes)
+DLAP_DEV int asset_red_blocks(const LossJob& J) {
+  return J.asset_full ? (J.N + AF_S - 1) / AF_S : (J.N * (J.h ? J.K + 1 : 1) + 255) >> 8;
+}
 
 __global__ __launch_bounds__(256) void k_asset_red(const LossJob* __restrict__ jobs) {
   const LossJob& J = jobs[blockIdx.y];
@@ -256,25 +262,133 @@ __global__ __launch_bounds__(256) void k_asset_red(const LossJob* __restrict__ j
   }
 }
 
+// One-pass asset reduction, grid (ceil(N / AF_S), jobs), 256 threads = AF_S stocks x 16 time
+// lanes: each thread sums E over its time lane's periods (blocks of AF_U periods, every operand
+// requested before use), the 16 lanes are summed in LDS in a fixed order, and the first lane of
+// each stock writes E, E_unc, dL/dE and the block's loss partials -- the whole time axis of a
+// stock stays in one workgroup, so no second reduction launch (k_asset_red) is needed.
+#define AF_U 4
+__global__ __launch_bounds__(256) void k_asset_full(const LossJob* __restrict__ jobs) {
+  const LossJob& J = jobs[blockIdx.y];
+  const int N = J.N, K = J.K, T = J.T;
+  if ((int)blockIdx.x * AF_S >= N) return;                      // block-uniform
+  __shared__ float red[16][AF_S][9];
+  __shared__ float lred[4];
+  const int s = threadIdx.x % AF_S, tl = threadIdx.x / AF_S;
+  const int i = blockIdx.x * AF_S + s;
+  const bool ok = i < N;
+  const int ic = ok ? i : N - 1;
+  const int kmax = J.h ? K : 0;
+  const float invT = gp(J.invT)[ic];
+  float lc = 0.f, lu = 0.f;
+  for (int k0 = 0; k0 < max(kmax, 1); k0 += 8) {
+    const int kn = J.h ? min(8, K - k0) : 0;
+    float e[8], eu = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) e[k] = 0.f;
+    if (kn == 8 && (K & 3) == 0) {
+      for (int tb = tl; tb < T; tb += 16 * AF_U) {
+        float q[AF_U];
+        f32x4 ha[AF_U], hb[AF_U];
+#pragma unroll
+        for (int u = 0; u < AF_U; ++u) {
+          const int t = tb + 16 * u;
+          const int tc = t < T ? t : T - 1;
+          const size_t d = (size_t)tc * N + ic;
+          q[u] = t < T ? gp(J.Rm)[d] * gp(J.sdfv)[tc] : 0.f;
+          const auto hp = gp(J.h) + d * K + k0;
+          ha[u] = ld4(hp);
+          hb[u] = ld4(hp + 4);
+        }
+#pragma unroll
+        for (int u = 0; u < AF_U; ++u) {
+          eu += q[u];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) { e[k] += ha[u][k] * q[u]; e[4 + k] += hb[u][k] * q[u]; }
+        }
+      }
+    } else {
+      for (int tb = tl; tb < T; tb += 16 * AF_U) {
+        float q[AF_U];
+#pragma unroll
+        for (int u = 0; u < AF_U; ++u) {
+          const int t = tb + 16 * u;
+          const int tc = t < T ? t : T - 1;
+          q[u] = t < T ? gp(J.Rm)[(size_t)tc * N + ic] * gp(J.sdfv)[tc] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < AF_U; ++u) {
+          const int t = tb + 16 * u;
+          eu += q[u];
+          if (t < T)
+            for (int k = 0; k < kn; ++k) e[k] += gp(J.h)[((size_t)t * N + ic) * K + k0 + k] * q[u];
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 8; ++k) red[tl][s][k] = e[k];
+    red[tl][s][8] = eu;
+    __syncthreads();
+    if (tl == 0 && ok) {
+      for (int k = 0; k < kn; ++k) {
+        float v = 0.f;
+#pragma unroll
+        for (int l = 0; l < 16; ++l) v += red[l][s][k];
+        v *= invT;
+        gp(J.E)[(size_t)i * K + k0 + k] = v;
+        if (gp(J.dE)) gp(J.dE)[(size_t)i * K + k0 + k] = J.coef_c * v;
+        lc += v * v;
+      }
+      if (k0 == 0) {
+        float v = 0.f;
+#pragma unroll
+        for (int l = 0; l < 16; ++l) v += red[l][s][8];
+        v *= invT;
+        gp(J.Eu)[i] = v;
+        if (gp(J.dEu)) gp(J.dEu)[i] = J.coef_u * v;
+        lu = v * v;
+      }
+    }
+  }
+  lc = block_sum<256>(lc, lred);
+  lu = block_sum<256>(lu, lred);
+  if (threadIdx.x == 0) {
+    gp(J.part)[2 * blockIdx.x + 0] = lc;
+    gp(J.part)[2 * blockIdx.x + 1] = lu;
+  }
+}
+
 // Block-wide (256 threads) fixed-order sum of the asset blocks' loss partials: every thread
 // takes a strided share (all loads in flight at once, instead of 2 * nblk dependent round trips
 // on one thread), then the fixed-order block reduction.
+template <int NT>
 DLAP_DEV void final_losses(const LossJob& J, float& lc, float& lu, float* red) {
   const int nblk = asset_red_blocks(J);
   float a = 0.f, b = 0.f;
-  for (int k = threadIdx.x; k < nblk; k += 256) { a += gp(J.part)[2 * k]; b += gp(J.part)[2 * k + 1]; }
-  a = block_sum<256>(a, red);
-  b = block_sum<256>(b, red);
+  for (int k = threadIdx.x; k < nblk; k += NT) { a += gp(J.part)[2 * k]; b += gp(J.part)[2 * k + 1]; }
+  a = block_sum<NT>(a, red);
+  b = block_sum<NT>(b, red);
   lc = J.h ? a / ((float)J.K * (float)J.N) : 0.f;
   lu = b / (float)J.N;
 }
 
 // ---------------------------------------------------------------- period backward ------
+template <int NT> DLAP_DEV void job_metrics_body(const LossJob& J, float* red, float* ret);
+
+// METRICS: one extra workgroup (the last, blockIdx.x == gridDim.x - 1) computes the job's
+// scalar metrics (k_job_metrics) beside the period workgroups: one launch less on the
+// training chain.
+template <bool METRICS>
 __global__ __launch_bounds__(PER_NT) void k_period_bwd(const LossJob* __restrict__ jobs) {
   const LossJob& J = jobs[blockIdx.y];
   const int t = blockIdx.x;
-  if (t >= J.T) return;
   __shared__ float red[PER_NT / 64];
+  if constexpr (METRICS) {
+    __shared__ float ret[DLAP_MAX_T];
+    if (t == (int)gridDim.x - 1) { job_metrics_body<PER_NT>(J, red, ret); return; }
+  }
+  if (t >= J.T) return;
   const int N = J.N, K = J.K;
   const size_t base = (size_t)t * N;
   const int r0 = gp(J.row_ptr)[t], r1 = gp(J.row_ptr)[t + 1];
@@ -403,14 +517,12 @@ __device__ long long g_loss_ts[4];
 
 // ---------------------------------------------------------------- per-job scalars -------
 // scal layout: see loss.h (SC_*).
-__global__ __launch_bounds__(256) void k_job_metrics(const LossJob* __restrict__ jobs) {
-  const LossJob& J = jobs[blockIdx.x];
-  __shared__ float red[4];
-  __shared__ float ret[DLAP_MAX_T];
+template <int NT>
+DLAP_DEV void job_metrics_body(const LossJob& J, float* red, float* ret) {
   const int T = J.T;
   MET_TS(0);
   float lc, lu;
-  final_losses(J, lc, lu, red);
+  final_losses<NT>(J, lc, lu, red);
   MET_TS(1);
   if (threadIdx.x == 0) {
     float lres = 0.f, inv_b, n1;
@@ -423,15 +535,15 @@ __global__ __launch_bounds__(256) void k_job_metrics(const LossJob* __restrict__
   for (int pass = 0; pass < 2; ++pass) {
     const float* src = pass == 0 ? gp(J.P) : gp(J.port);
     if (!src) continue;
-    for (int t = threadIdx.x; t < T; t += 256) ret[t] = src[t];
+    for (int t = threadIdx.x; t < T; t += NT) ret[t] = src[t];
     __syncthreads();
     float s = 0.f;
-    for (int t = threadIdx.x; t < T; t += 256) s += ret[t];
-    s = block_sum<256>(s, red);
+    for (int t = threadIdx.x; t < T; t += NT) s += ret[t];
+    s = block_sum<NT>(s, red);
     const float mean = s / (float)T;
     float v = 0.f;
-    for (int t = threadIdx.x; t < T; t += 256) { const float x = ret[t] - mean; v += x * x; }
-    v = block_sum<256>(v, red);
+    for (int t = threadIdx.x; t < T; t += NT) { const float x = ret[t] - mean; v += x * x; }
+    v = block_sum<NT>(v, red);
     if (threadIdx.x == 0) {
       const float sd_u = T > 1 ? sqrtf(v / (float)(T - 1)) : __builtin_nanf("");
       const float sharpe = (sd_u < 1e-8f) ? 0.f : mean / sd_u;
@@ -484,6 +596,12 @@ __global__ __launch_bounds__(256) void k_job_metrics(const LossJob* __restrict__
   }
 }
 
+__global__ __launch_bounds__(256) void k_job_metrics(const LossJob* __restrict__ jobs) {
+  __shared__ float red[4];
+  __shared__ float ret[DLAP_MAX_T];
+  job_metrics_body<256>(jobs[blockIdx.x], red, ret);
+}
+
 std::vector<long long> loss_timestamps() {
   std::vector<long long> v(4);
   HIP_OK(hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(g_loss_ts), sizeof(long long) * 4));
@@ -495,14 +613,24 @@ void launch_period_fwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st)
   hipLaunchKernelGGL(k_period_fwd, dim3(tmax, njobs), dim3(PER_NT), 0, st, jobs);
   HIP_OK(hipGetLastError());
 }
-void launch_asset(const LossJob* jobs, int njobs, int nmax, int kmax, hipStream_t st) {
+bool asset_full_default() {
+  static const bool on = [] { const char* v = std::getenv("DLAP_ASSET_FULL"); return !(v && *v == '0'); }();
+  return on;
+}
+void launch_asset(const LossJob* jobs, int njobs, int nmax, int kmax, hipStream_t st, bool full) {
+  if (full) {                     // (the job tables were built with asset_full = 1)
+    hipLaunchKernelGGL(k_asset_full, dim3((nmax + AF_S - 1) / AF_S, njobs), dim3(256), 0, st, jobs);
+    HIP_OK(hipGetLastError());
+    return;
+  }
   hipLaunchKernelGGL(k_asset_part, dim3((nmax + 63) / 64, DLAP_TCH, njobs), dim3(256), 0, st, jobs);
   HIP_OK(hipGetLastError());
   hipLaunchKernelGGL(k_asset_red, dim3((nmax * (kmax + 1) + 255) / 256, njobs), dim3(256), 0, st, jobs);
   HIP_OK(hipGetLastError());
 }
-void launch_period_bwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st) {
-  hipLaunchKernelGGL(k_period_bwd, dim3(tmax, njobs), dim3(PER_NT), 0, st, jobs);
+void launch_period_bwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st, bool metrics) {
+  if (metrics) hipLaunchKernelGGL(k_period_bwd<true>, dim3(tmax + 1, njobs), dim3(PER_NT), 0, st, jobs);
+  else hipLaunchKernelGGL(k_period_bwd<false>, dim3(tmax, njobs), dim3(PER_NT), 0, st, jobs);
   HIP_OK(hipGetLastError());
 }
 void launch_job_metrics(const LossJob* jobs, int njobs, hipStream_t st) {

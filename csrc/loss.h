@@ -32,6 +32,7 @@ struct LossJob {
   int phase;             // 1: unconditional, 2: moment, 3: conditional, 0: evaluation
   float res_factor;      // residual_loss_factor (gradient only in training jobs)
   float coef_c, coef_u;  // dL/dE = coef * E (0 disables the write)
+  int asset_full;        // 1: one-pass asset reduction (k_asset_full), else k_asset_part + k_asset_red
   // per (model, split) workspace
   const float* w;        // [R] raw SDF output (compact rows)
   float* wn;             // [T*N] normalised weights w' (dense, zero at invalid entries)
@@ -53,8 +54,13 @@ struct LossJob {
 
 void launch_period_fwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st);
 // kmax: the moment count K of the jobs (sizes the output grid of the reduction pass)
-void launch_asset(const LossJob* jobs, int njobs, int nmax, int kmax, hipStream_t st);
-void launch_period_bwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st);
+// full: the one-pass k_asset_full (training jobs: fewer launches on the critical chain; the
+// jobs must have been built with asset_full = 1), else k_asset_part + k_asset_red (evaluation
+// jobs: more parallel over the long test split, off the critical chain)
+void launch_asset(const LossJob* jobs, int njobs, int nmax, int kmax, hipStream_t st, bool full = false);
+// metrics: also compute the job metrics (k_job_metrics) in one extra workgroup
+void launch_period_bwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st, bool metrics = false);
+bool asset_full_default();   // DLAP_ASSET_FULL (default 1): one-pass asset reduction for training jobs
 void launch_job_metrics(const LossJob* jobs, int njobs, hipStream_t st);
 std::vector<long long> loss_timestamps();
 // ensemble averaging + re-normalisation + portfolio returns (K11), device pointers
