@@ -528,6 +528,55 @@ class Engine {
     if (wait) sync();
   }
 
+  // ---- cross-sectional sharding (parallel/xsection.py) ------------------------------------
+  // Tower backward of the train split from EXTERNAL loss gradients: the caller evaluates the
+  // cross-sectional parts of the loss (sums over all ranks' stocks) itself and hands back
+  //   phase 1 / 3: dw   -- dL/d(raw SDF weight) of every compact row [R] (device pointer);
+  //   phase 2:     dE   -- dL/dE [N][K] and sdf -- the global SDF_t = 1 + P_t [T].
+  // The train forward is recomputed (same dropout step), the loss passes are skipped, and the
+  // tower backward + gradient finalisation + LSTM BPTT leave the phase's gradients in `grads`
+  // (copy_grads). Stream-ordered on the engine stream, no host synchronisation.
+  void xs_backward(int phase, uintptr_t dw, uintptr_t dE, uintptr_t sdf) {
+    if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
+    if (phase < 1 || phase > 3) throw std::invalid_argument("phase must be 1, 2 or 3");
+    if (phase != 2) ensure_moments();
+    const SplitDev& D = splits_[0];
+    enqueue_dropmask(phase, 0, st_);
+    launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_, train_mom(phase));
+    const bool zx_train = md_.md.wide && zx_train_;
+    if (md_.md.wide && !zx_train)
+      launch_proj0(as<WideJob>(j_wide_train_[phase]), G_, gx_proj_[0], md_.md, md_.WMB, st_);
+    if (zx_train)
+      launch_mlp_fwd_zx(as<MlpJob>(j_mlp_train_[phase]), G_, std::max(1, zx_gx_ / G_), md_.md, md_.WMB, st_, true);
+    else
+      launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, phase == 2 ? gx_fwd_[0] : gx_fwd13_, md_.md, md_.KS1,
+                     md_.WMB, st_);
+    for (int g = 0; g < G_; ++g) {
+      ModelSplitWS& W = ws(g, 0);
+      if (phase == 2) {
+        if (!dE || !sdf) throw std::invalid_argument("phase 2 needs dE and sdf");
+        HIP_OK(hipMemcpyAsync(W.dE.p, reinterpret_cast<const void*>(dE), W.dE.n * sizeof(float),
+                              hipMemcpyDeviceToDevice, st_));
+        HIP_OK(hipMemcpyAsync(W.sdf.p, reinterpret_cast<const void*>(sdf), W.sdf.n * sizeof(float),
+                              hipMemcpyDeviceToDevice, st_));
+      } else {
+        if (!dw) throw std::invalid_argument("phases 1 / 3 need dw");
+        if (D.R) HIP_OK(hipMemcpyAsync(W.dw.p, reinterpret_cast<const void*>(dw), (size_t)D.R * sizeof(float),
+                                       hipMemcpyDeviceToDevice, st_));
+      }
+    }
+    if (phase == 2)
+      launch_mlp_bwd_mom(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_m, 1, md_.md, md_.KS1,
+                         md_.WMB, slab_stride(), st_);
+    else
+      launch_mlp_bwd_sdf(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_s, md_.tps_s, md_.md, md_.KS1,
+                         slab_stride(), st_);
+    if (md_.md.wide)
+      launch_wgrad0(as<WideJob>(j_wide_bwd_[phase]), G_, dd(), md_.md, phase == 2, md_.WMB, nsplit_, st_);
+    enqueue_train_tail(phase);
+  }
+  long split_rows(int s) const { return splits_[s].R; }
+
   // ---- module API (ops/fused.py): stream-ordered, no host synchronisation ----------------
   // Run the engine's launches on an external stream (torch's current stream), so module-level
   // forward / backward calls are ordered with the surrounding torch ops. Epoch graphs need the
@@ -569,7 +618,8 @@ class Engine {
   long copy_ws(int g, int s, const std::string& name, uintptr_t dst) {
     ModelSplitWS& W = ws(g, s);
     const std::map<std::string, DevBuf<float>*> m = {
-        {"wn", &W.wn}, {"h", &W.h}, {"P", &W.P}, {"port", &W.port}, {"scal", &W.scal}, {"pp", &W.pp}};
+        {"wn", &W.wn}, {"h", &W.h}, {"P", &W.P}, {"port", &W.port}, {"scal", &W.scal}, {"pp", &W.pp},
+        {"w", &W.w}};
     auto it = m.find(name);
     if (it == m.end()) throw std::invalid_argument("copy_ws: unknown buffer " + name);
     const DevBuf<float>& b = *it->second;
@@ -1449,6 +1499,8 @@ PYBIND11_MODULE(_dlap_hip, m) {
       .def("set_stream", &Engine::set_stream, py::arg("stream"), py::arg("external") = true)
       .def("set_params_dev", &Engine::set_params_dev)
       .def("join_from", &Engine::join_from)
+      .def("xs_backward", &Engine::xs_backward)
+      .def("split_rows", &Engine::split_rows)
       .def("join_to", &Engine::join_to)
       .def("set_drop_step", &Engine::set_drop_step)
       .def("copy_ws", &Engine::copy_ws)

@@ -20,9 +20,16 @@ gets dL/d(its local partial sums), and one flat all-reduce of the parameter grad
 dL/dθ = Σ_r (local paths). The replicated clip + Adam then keep the replicas bit-identical.
 
 Collectives per training step: 3 forward ([2,T], [2,T], [K]; +[4,T] with a residual loss), their 3 backward mirrors and one
-flat gradient all-reduce (~12k floats) — all latency-bound, a few µs each over xGMI. The local
-towers run as PyTorch ops on the rank's device (hipBLASLt GEMMs on a GPU): this mode trades the
-fused single-GPU engine for capacity.
+flat gradient all-reduce (~12k floats) — all latency-bound, a few µs each over xGMI.
+
+Local towers on a GPU run on the native engine (``EngineTowers``; one engine per rank holding
+the rank's three split shards): the LSTM, the SDF tower and the moment network are the engine's
+fused MFMA kernels, and the cross-sectional remainder (zero mean, P_t, E, losses: [T]- and
+[N_r, K]-sized tensors) stays in torch around the all-reduces. Autograd enters the engine at
+two points -- the raw SDF weights w[t, i] and the moment sums E[k, i] = Σ_t h q / T_i (the only
+way the moments reach any loss) -- and leaves through ``Engine.xs_backward``, which recomputes
+the rank's forward and runs the engine's tower backward from the external dL/dw or
+(dL/dE, global SDF_t). On CPU (or ``engine=False``) the towers are PyTorch ops.
 """
 from __future__ import annotations
 
@@ -83,6 +90,166 @@ def shard_batch(batch: Dict, rank: int, world: int) -> Dict:
     return out
 
 
+def _mkey(t: torch.Tensor):
+    return (t.data_ptr(), tuple(t.shape), t._version)
+
+
+class EngineTowers:
+    """The rank's local towers on the native engine (one model, the rank's shards of the
+    train / valid / test splits). Reference modules: `SDFNetwork` / `MomentNetwork` /
+    `MacroLSTM` (`/root/reference/src/model.py:21-279`)."""
+
+    def __init__(self, model: AssetPricingGAN, shards: Sequence[Optional[Dict]], device,
+                 seed: int = 0, precision: str = "bf16"):
+        from ..engine.runner import GANEngine
+        self.device = torch.device(device)
+        self.spec = model.spec
+        self.eng = GANEngine(model.spec, 1, max_epochs=8, precision=precision)
+        dev = [None if b is None else {k: (v.to(self.device) if isinstance(v, torch.Tensor) else v)
+                                       for k, v in b.items() if k != "n_total"} for b in shards]
+        self.eng.set_data(*dev)
+        # the same seed on every rank: the replicated LSTM draws identical inter-layer masks
+        self.eng.eng.set_seed(0, int(seed) & 0xFFFFFFFF)
+        self.masks = {}
+        for s, b in enumerate(dev):
+            if b is not None:
+                m = b["mask"].bool()
+                self.masks[s] = m
+        self.keys = {}
+        self.param_key = None
+        self.step = 0
+        self._flat = None
+        self._h = {}
+
+    def register(self, s: int, mask: torch.Tensor):
+        self.keys[_mkey(mask)] = s
+
+    def split_of(self, mask: torch.Tensor) -> int:
+        s = self.keys.get(_mkey(mask))
+        if s is None:
+            for k, m in self.masks.items():      # same tensor values as a registered split
+                if m.shape == mask.shape and bool(torch.equal(m, mask.bool())):
+                    self.keys[_mkey(mask)] = s = k
+                    break
+        if s is None:
+            raise KeyError("EngineTowers: this shard is not one of the engine's splits")
+        return s
+
+    def _ts(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def sync_params(self, params: Sequence[torch.Tensor], training: bool):
+        from ..ops.fused import _flat_params
+        key = tuple((p.data_ptr(), p._version) for p in params)
+        if key != self.param_key:
+            self._flat = _flat_params(list(params), self.device).contiguous()
+        ts = self._ts()
+        self.eng.eng.join_from(ts)
+        if key != self.param_key:
+            self.eng.eng.set_params_dev(0, self._flat.data_ptr())
+            self.param_key = key
+        if training:
+            self.step += 1
+            self.eng.eng.set_drop_step(0, self.step)
+        return ts
+
+    def forward(self, s: int, training: bool, do_mom: bool):
+        """Raw SDF weights [T, N_r] (zero where masked) and moments [K, T, N_r] of split s."""
+        ts = self._ts()
+        self.eng.eng.forward_split(s, bool(training), bool(do_mom), False)
+        m = self.masks[s]
+        R = int(self.eng.eng.split_rows(s))
+        wc = torch.empty(max(R, 1), dtype=torch.float32, device=self.device)
+        self.eng.eng.copy_ws(0, s, "w", wc.data_ptr())
+        h = None
+        if do_mom:
+            T, N = m.shape
+            h = torch.empty(T * N * self.spec.num_moments, dtype=torch.float32, device=self.device)
+            self.eng.eng.copy_ws(0, s, "h", h.data_ptr())
+        self.eng.eng.join_to(ts)
+        w = torch.zeros(m.shape, dtype=torch.float32, device=self.device)
+        w[m] = wc[:R]
+        if h is not None:
+            h = h.reshape(m.shape[0], m.shape[1], -1).permute(2, 0, 1)
+        return w, h
+
+    def backward(self, phase: int, dw: Optional[torch.Tensor] = None, dE: Optional[torch.Tensor] = None,
+                 sdf: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Flat parameter gradient of the train split from external dL/dw [T, N_r] (phases 1 / 3)
+        or dL/dE [K, N_r] with the global SDF_t (phase 2)."""
+        P = sum(int(n) for n in self.spec.param_counts())
+        out = torch.empty(P, dtype=torch.float32, device=self.device)
+        ts = self._ts()
+        if phase == 2:
+            dEc = dE.detach().t().contiguous().float()          # engine layout [N][K]
+            sdfc = sdf.detach().contiguous().float()
+            self.eng.eng.join_from(ts)
+            self.eng.eng.xs_backward(2, 0, dEc.data_ptr(), sdfc.data_ptr())
+        else:
+            dwc = dw.detach()[self.masks[0]].contiguous().float()
+            if dwc.numel() == 0:
+                dwc = torch.zeros(1, device=self.device)
+            self.eng.eng.join_from(ts)
+            self.eng.eng.xs_backward(phase, dwc.data_ptr(), 0, 0)
+        self.eng.eng.copy_grads(0, out.data_ptr())
+        self.eng.eng.join_to(ts)
+        return out
+
+
+class _TowerSDF(torch.autograd.Function):
+    """w_raw [T, N_r] (computed by the engine, passed in as ``w``) as a function of the SDF-side
+    parameters (``params``, flat-layout order); backward: ``Engine.xs_backward`` phase 1."""
+
+    @staticmethod
+    def forward(ctx, et, s, w, *params):
+        ctx.et, ctx.s = et, s
+        ctx.shapes = [p.shape for p in params]
+        return w.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        if ctx.s != 0:
+            raise RuntimeError("engine towers: gradients only for the train split")
+        flat = ctx.et.backward(1, dw=g)
+        P_sdf = ctx.et.spec.param_counts()[0]
+        return (None, None, None, *_split_like(flat[:P_sdf], ctx.shapes))
+
+
+class _TowerE(torch.autograd.Function):
+    """E [K, N_r] = Σ_t h q / T_i with q = R m SDF_t and h the engine's moments (``h``, computed
+    outside); differentiable w.r.t. SDF_t (in torch) and the moment parameters (``params``,
+    through ``Engine.xs_backward`` phase 2 when ``want`` is set)."""
+
+    @staticmethod
+    def forward(ctx, et, want, h, r, m, t_i, sdf, *params):
+        ctx.et, ctx.want = et, want
+        ctx.shapes = [p.shape for p in params]
+        ctx.save_for_backward(h, r, m, t_i, sdf)
+        q = r * m * sdf[:, None]
+        return (h * q[None]).sum(1) / t_i
+
+    @staticmethod
+    def backward(ctx, de):
+        h, r, m, t_i, sdf = ctx.saved_tensors
+        g = de / t_i                                            # [K, N_r]
+        dsdf = (torch.einsum("ki,kti->ti", g, h) * r * m).sum(1)
+        grads = [None] * len(ctx.shapes)
+        if ctx.want:
+            flat = ctx.et.backward(2, dE=de, sdf=sdf)
+            P_sdf = ctx.et.spec.param_counts()[0]
+            grads = _split_like(flat[P_sdf:], ctx.shapes)
+        return (None, None, None, None, None, None, dsdf, *grads)
+
+
+def _split_like(flat: torch.Tensor, shapes):
+    out, off = [], 0
+    for shp in shapes:
+        n = int(np.prod(shp)) if len(shp) else 1
+        out.append(flat[off:off + n].reshape(shp))
+        off += n
+    return out
+
+
 class XSectionGAN(AssetPricingGAN):
     """``AssetPricingGAN`` whose forward / get_weights take the rank's stock shard and return
     the GLOBAL losses, portfolio returns and Sharpe (weights and moments stay local).
@@ -93,6 +260,34 @@ class XSectionGAN(AssetPricingGAN):
         self.dist = dist
         self.lstm_seed = int(lstm_seed)
         self._lstm_calls = 0
+        self.et: Optional[EngineTowers] = None
+
+    def attach_engine(self, shards: Sequence[Optional[Dict]], device, precision: str = "bf16") -> "XSectionGAN":
+        """Run the local towers on the native engine (``shards``: this rank's train / valid /
+        test dicts, as passed to train_epoch / evaluate)."""
+        self.et = EngineTowers(self, shards, device, seed=self.lstm_seed, precision=precision)
+        return self
+
+    def _engine_pass(self, mask, want_mom: bool):
+        from ..ops.fused import _ordered_params
+        et = self.et
+        s = et.split_of(mask)
+        params = _ordered_params(self)
+        n_sdf = sum(1 for k, _ in self.spec.param_layout() if k.startswith("sdf_net."))
+        et.sync_params(params, self.training)
+        w, h = et.forward(s, self.training, want_mom)
+        if torch.is_grad_enabled() and s == 0:
+            w = _TowerSDF.apply(et, s, w, *params[:n_sdf])
+        return s, w, h, params[n_sdf:]
+
+    def _normalize(self, w_raw, mask):
+        m = mask.float()
+        w = w_raw * m
+        if not self.sdf_net.normalize_weights:
+            return w
+        s = all_reduce_sum(torch.stack([(w * m).sum(1), m.sum(1)]), self.dist)
+        mu = s[0] / s[1].clamp(min=1)
+        return (w - mu[:, None]) * m
 
     # -- local pieces --------------------------------------------------------------------------
     def _macro_state(self, macro):
@@ -116,13 +311,9 @@ class XSectionGAN(AssetPricingGAN):
 
     def shard_weights(self, macro, x, mask):
         """Zero-mean (over ALL ranks' valid stocks) weights of the local stocks."""
-        m = mask.float()
-        w = self.raw_weights(macro, x) * m
-        if not self.sdf_net.normalize_weights:
-            return w
-        s = all_reduce_sum(torch.stack([(w * m).sum(1), m.sum(1)]), self.dist)
-        mu = s[0] / s[1].clamp(min=1)
-        return (w - mu[:, None]) * m
+        if self.et is not None:
+            return self._normalize(self._engine_pass(mask, False)[1], mask)
+        return self._normalize(self.raw_weights(macro, x), mask)
 
     # -- global losses -------------------------------------------------------------------------
     def _portfolio(self, w, r, m):
@@ -132,10 +323,14 @@ class XSectionGAN(AssetPricingGAN):
         n_t = s[1].clamp(min=1)
         return s[0] / n_t * n_t.mean()
 
-    def _moment_loss(self, h, r, m, sdf, n_total):
+    def _moment_loss(self, h, r, m, sdf, n_total, engine=None):
         t_i = m.sum(0).clamp(min=1)
-        q = r * m * sdf[:, None]
-        e = (q.sum(0) / t_i)[None] if h is None else (h * q[None]).sum(1) / t_i     # [K, N_r]
+        if engine is not None:        # (et, want moment-parameter gradients, moment params)
+            et, want, mparams = engine
+            e = _TowerE.apply(et, want, h, r, m, t_i, sdf, *mparams)
+        else:
+            q = r * m * sdf[:, None]
+            e = (q.sum(0) / t_i)[None] if h is None else (h * q[None]).sum(1) / t_i     # [K, N_r]
         return all_reduce_sum((e ** 2).sum(1), self.dist).mean() / n_total
 
     def _residual(self, w, r, m):
@@ -162,18 +357,26 @@ class XSectionGAN(AssetPricingGAN):
             n_total = int(all_reduce_sum(torch.tensor([float(returns.shape[1])], device=returns.device),
                                          self.dist).item()) if self.dist.active else returns.shape[1]
         m = mask.float()
-        w = self.shard_weights(macro_features, individual_features, mask)
-        moments = self.moment_net(self._moment_input(macro_features, individual_features))
+        eng = None
+        if self.et is not None:
+            # engine towers; the moment network's output only enters the losses through E
+            s_, w_raw, moments, mparams = self._engine_pass(mask, phase != "unconditional")
+            w = self._normalize(w_raw, mask)
+            if moments is not None:
+                eng = (self.et, torch.is_grad_enabled() and s_ == 0 and phase == "moment", mparams)
+        else:
+            w = self.shard_weights(macro_features, individual_features, mask)
+            moments = self.moment_net(self._moment_input(macro_features, individual_features))
         p = self._portfolio(w, returns, m)
         zero = torch.zeros((), device=w.device)
         if phase == "unconditional":
             loss_unc = self._moment_loss(None, returns, m, p + 1.0, n_total)
             loss_cond, total = zero, loss_unc
         elif phase == "moment":
-            loss_cond = self._moment_loss(moments, returns, m, p + 1.0, n_total)
+            loss_cond = self._moment_loss(moments, returns, m, p + 1.0, n_total, eng)
             loss_unc, total = zero, -loss_cond
         else:
-            loss_cond = self._moment_loss(moments, returns, m, p + 1.0, n_total)
+            loss_cond = self._moment_loss(moments, returns, m, p + 1.0, n_total, eng)
             loss_unc = self._moment_loss(None, returns, m, p + 1.0, n_total)
             total = loss_cond
         loss_res = zero
@@ -248,16 +451,26 @@ def train_3phase_xsection(config: Dict, train_data: Dict, valid_data: Dict, test
                           num_epochs_moment: int = 64, num_epochs: int = 1024, lr: float = 1e-3,
                           print_freq: int = 128, save_dir: Optional[str] = None, ignore_epoch: int = 64,
                           seed: int = 42, selection_sign: float = 1.0, verbose: bool = True,
-                          nan_policy: str = "warn"):
+                          nan_policy: str = "warn", engine: Optional[bool] = None, precision: str = "bf16"):
     """``train_3phase`` over stock shards (``*_data``: FULL split dicts or already-sharded ones
     carrying ``n_total``). Same schedule, trackers and checkpoints as the CPU trainer; rank 0
-    writes the checkpoints. Returns ``(model, history)`` on every rank."""
+    writes the checkpoints. Returns ``(model, history)`` on every rank.
+    ``engine`` (default: on a GPU) runs the local towers on the native engine."""
     from ..train.trainer import _train_3phase_cpu
     device = torch.device(device or dist.device)
     sh = [None if b is None else (b if "n_total" in b else shard_batch(b, dist.rank, dist.world))
           for b in (train_data, valid_data, test_data)]
+    use_engine = device.type == "cuda" if engine is None else bool(engine)
+    if use_engine:       # shards resident on the device once (the engine keys its splits by them)
+        sh = [None if b is None else {k: (v.to(device) if isinstance(v, torch.Tensor) else v) for k, v in b.items()}
+              for b in sh]
     torch.manual_seed(seed)                      # identical initial parameters on every rank
     model = XSectionGAN(config, dist, lstm_seed=seed).to(device)
+    if use_engine:
+        model.attach_engine(sh, device, precision=precision)
+        for s_, b in enumerate(sh):
+            if b is not None:
+                model.et.register(s_, b["mask"])
     torch.manual_seed(seed + 7919 * (dist.rank + 1))   # per-rank dropout streams of the local rows
     main = dist.rank == 0
     # every rank runs the same (collective) evaluations, including the verbose final report;
@@ -291,6 +504,7 @@ def main(argv: Optional[Sequence[str]] = None):
     ap.add_argument("--print_freq", type=int, default=128)
     ap.add_argument("--save_dir", default=None)
     ap.add_argument("--cpu", action="store_true")
+    ap.add_argument("--torch_towers", action="store_true", help="local towers as PyTorch ops instead of the engine")
     ap.add_argument("--out", default=None)
     args = ap.parse_args(argv)
     d = comm.init(use_gpu=False if args.cpu else None)
@@ -302,7 +516,8 @@ def main(argv: Optional[Sequence[str]] = None):
     model, hist = train_3phase_xsection(cfg, b["train"], b["valid"], b["test"], d, num_epochs_unc=args.epochs[0],
                                         num_epochs_moment=args.epochs[1], num_epochs=args.epochs[2], lr=args.lr,
                                         print_freq=args.print_freq, save_dir=args.save_dir,
-                                        ignore_epoch=args.ignore_epoch, seed=args.seed)
+                                        ignore_epoch=args.ignore_epoch, seed=args.seed,
+                                        engine=False if args.torch_towers else None)
     ev = {k: evaluate(model, b[k], d.device) for k in SPLITS}
     res = {"world_size": d.world, "n_stocks": tr["n_total"], "wall_s": time.time() - t0,
            **{f"{k}_sharpe": float(ev[k]["sharpe"]) for k in SPLITS}}
