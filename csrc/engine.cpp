@@ -175,13 +175,16 @@ class Engine {
     HIP_OK(hipEventCreateWithFlags(&ev_f3_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
-    eval_gx_ = env_int("DLAP_EVAL_GX", 256);
+    // evaluation tower grid cap: the evaluation branch is within a few us of the training chain,
+    // so it gets as many workgroups as the training forward (profiles/r2_knobs_grids.log)
+    eval_gx_ = env_int("DLAP_EVAL_GX", 512);
     b_wait_ = env_int("DLAP_B_WAIT", 0);
     // both off: a third graph branch changes how the runtime maps the graph onto its hardware
     // queues -- the evaluation branch then shared a queue with the training backward and ran
     // after it (2718 vs 3978 model-epochs/s, profiles/r2_knobs_third_stream.log)
     side_metrics_ = env_int("DLAP_SIDE_METRICS", 0) != 0;
     split_tail_ = env_int("DLAP_SPLIT_TAIL", 0) != 0;
+    defer_metrics_ = env_int("DLAP_DEFER_METRICS", 1) != 0;
     zx_eval_ = env_int("DLAP_ZX_EVAL", 1) != 0;
     zx_train_ = env_int("DLAP_ZX_TRAIN", 1) != 0;
     zx_gx_ = std::max(1, env_int("DLAP_ZX_GX", 256));
@@ -696,6 +699,7 @@ class Engine {
   bool zx_train_ = true;                     // ... and training forward (DLAP_ZX_TRAIN)
   int zx_gx_ = 256;                          // their workgroups over all evaluation jobs (DLAP_ZX_GX)
   bool side_metrics_ = false;                // train metrics on the side stream st3_ (DLAP_SIDE_METRICS)
+  bool defer_metrics_ = true;                // pipelined epochs: train metrics on the evaluation branch
   bool train_first_ = true;                  // capture the training chain before the evaluation branch
   // Moment cache: the moment net only changes in phase 2, so outside it the moments h of every
   // split are constant (eval mode has no dropout; the train split's only if the moment tower has
@@ -938,7 +942,7 @@ class Engine {
     // workgroup per CU (256); phase 2 (moment tower, no evaluation branch) with 1024
     gx_fwd_[s] = std::max(1, std::min(((R + 31) / 32 + 3) / 4, env_int("DLAP_GX_FWD", 1024)));
     if (s == 0) {
-      gx_fwd13_ = std::max(1, std::min(((R + 31) / 32 + 3) / 4, env_int("DLAP_GX_FWD13", 256)));
+      gx_fwd13_ = std::max(1, std::min(((R + 31) / 32 + 3) / 4, env_int("DLAP_GX_FWD13", 384)));
     }
     if (md_.md.wide) {
       const size_t ntl = (size_t)(R + 31) / 32;
@@ -1202,8 +1206,10 @@ class Engine {
   // mark: record ev_a_ after the tower backward (1), the tower forward (2) or the wide
   // layer-0 projection (3);
   // part1_only: stop before the gradient finalisation (the caller enqueues the tail).
+  // defer_metrics: the train split's metrics are left to the caller (it records ev_mid_ after the
+  // asset pass; the pipelined epoch runs them on the evaluation branch, off the critical chain).
   void enqueue_train_grads(int phase, hipStream_t side = nullptr, bool premasked = false, int mark = 0,
-                           bool part1_only = false) {
+                           bool part1_only = false, bool defer_metrics = false) {
     const SplitDev& D = splits_[0];
     if (!premasked) enqueue_dropmask(phase, 0, st_);
     // the latency-bound LSTM first, before the streaming projection loads the memory system
@@ -1223,24 +1229,28 @@ class Engine {
     launch_period_fwd(as<LossJob>(j_loss_train_[phase]), G_, D.T, st_);
     HTRACE("launch_asset");
     launch_asset(as<LossJob>(j_loss_train_[phase]), G_, D.N, md_.K, st_, asset_full_default());
-    if (side) {
+    if (defer_metrics && phase != 2) {
+      HIP_OK(hipEventRecord(ev_mid_, st_));
+    } else if (side) {
       HIP_OK(hipEventRecord(ev_mid_, st_));
       HIP_OK(hipStreamWaitEvent(side, ev_mid_, 0));
       HTRACE("launch_job_metrics");
       launch_job_metrics(as<LossJob>(j_loss_train_[phase]), G_, side);
       HIP_OK(hipEventRecord(ev_m3_, side));
       side_open_ = true;
-    } else if (phase == 2) {
+    } else {
+      // (k_job_metrics, not the metrics workgroup of k_period_bwd<true>: the same reduction
+      // order as the deferred launch of the pipelined epochs, so both schedules are bitwise equal)
       HTRACE("launch_job_metrics");
       launch_job_metrics(as<LossJob>(j_loss_train_[phase]), G_, st_);
-    }   // (phases 1 / 3: the metrics run as an extra workgroup of the period backward)
+    }
     if (phase == 2) {
       HTRACE("launch_mlp_bwd_mom");
       launch_mlp_bwd_mom(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_m, 1, md_.md, md_.KS1,
                          md_.WMB, slab_stride(), st_);
     } else {
       HTRACE("launch_period_bwd");
-      launch_period_bwd(as<LossJob>(j_loss_train_[phase]), G_, D.T, st_, side == nullptr);
+      launch_period_bwd(as<LossJob>(j_loss_train_[phase]), G_, D.T, st_);
       HTRACE("launch_mlp_bwd_sdf");
       launch_mlp_bwd_sdf(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_s, md_.tps_s, md_.md, md_.KS1,
                          slab_stride(), st_);
@@ -1339,9 +1349,14 @@ class Engine {
     HIP_OK(hipStreamWaitEvent(st2_, ev_fork_, 0));
     if (b_wait_ == 0 && train_first_) {
       // same graph topology, training-chain nodes first (they land on the graph's first queue)
-      enqueue_train_grads(phase, side_metrics_ ? st3_ : nullptr, true);   // this epoch's fwd/bwd
+      const bool defer = !side_metrics_ && defer_metrics_;
+      enqueue_train_grads(phase, side_metrics_ ? st3_ : nullptr, true, 0, false, defer);   // this epoch's fwd/bwd
       enqueue_eval(st2_);                                 // previous epoch's evaluation
       if (side_metrics_) HIP_OK(hipStreamWaitEvent(st2_, ev_m3_, 0));   // train metrics
+      if (defer && phase != 2) {                          // this epoch's train metrics, after its
+        HIP_OK(hipStreamWaitEvent(st2_, ev_mid_, 0));     // asset pass (read by the next bookkeeping)
+        launch_job_metrics(as<LossJob>(j_loss_train_[phase]), G_, st2_);
+      }
       enqueue_epoch_end(phase, ignore_epoch, sel, st2_);  // ... and its bookkeeping
       enqueue_dropmask(phase, 1, st2_);                   // next epoch's dropout masks
     } else if (b_wait_ == 0) {

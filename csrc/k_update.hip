@@ -346,56 +346,69 @@ __global__ __launch_bounds__(EPOCH_END_THREADS) void k_epoch_end(const EpochJob*
   const EpochJob& J = jobs[blockIdx.x];
   __shared__ int dec[2];
   if (threadIdx.x == 0) {
+    // every input is loaded before the first store: the stores below may alias them, so
+    // loads left after a store would each pay a full memory round trip in sequence
+    const bool hv = phase != 2 && J.sc_valid, ht = hv && J.sc_test;
+    float tr[SC_NSCAL], va[SC_NSCAL], te[SC_NSCAL];
+#pragma unroll
+    for (int c = 0; c < SC_NSCAL; ++c) {
+      tr[c] = gp(J.sc_train)[c];
+      va[c] = hv ? gp(J.sc_valid)[c] : 0.f;
+      te[c] = ht ? gp(J.sc_test)[c] : 0.f;
+    }
     const int ep = gp(J.ep)[0], ep_ph = gp(J.ep)[1];
+    const float gn = gp(J.gnorm)[0];
+    const float best0 = gp(J.best)[0], best1 = gp(J.best)[1], best2 = gp(J.best)[2];
     // past the history capacity the row goes to a per-block scratch instead of out of bounds
     __shared__ float spill[HIST_W];
     float* row = ep < J.max_ep ? gp(J.hist) + (size_t)ep * HIST_W : spill;
-    const float* tr = gp(J.sc_train);
     const float lres = tr[SC_LRES] * res_factor;
     float tloss;
     if (phase == 1) tloss = tr[SC_LUNC] + lres;
     else if (phase == 2) tloss = -tr[SC_LCOND] + lres;
     else tloss = tr[SC_LCOND] + lres;
-    for (int c = 0; c < HIST_W; ++c) row[c] = __builtin_nanf("");
-    row[H_PHASE] = (float)phase;
-    row[H_TRAIN_LOSS] = tloss;
-    row[H_TRAIN_SHARPE] = tr[SC_TRAIN_SHARPE];
-    row[H_TRAIN_LUNC] = phase == 2 ? 0.f : tr[SC_LUNC];
-    row[H_TRAIN_LCOND] = phase == 1 ? 0.f : tr[SC_LCOND];
-    row[H_TRAIN_LRES] = tr[SC_LRES];
-    row[H_GNORM] = gp(J.gnorm)[0];
+    float r[HIST_W];
+#pragma unroll
+    for (int c = 0; c < HIST_W; ++c) r[c] = __builtin_nanf("");
+    r[H_PHASE] = (float)phase;
+    r[H_TRAIN_LOSS] = tloss;
+    r[H_TRAIN_SHARPE] = tr[SC_TRAIN_SHARPE];
+    r[H_TRAIN_LUNC] = phase == 2 ? 0.f : tr[SC_LUNC];
+    r[H_TRAIN_LCOND] = phase == 1 ? 0.f : tr[SC_LCOND];
+    r[H_TRAIN_LRES] = tr[SC_LRES];
+    r[H_GNORM] = gn;
     int up_loss = 0, up_sr = 0;
-    if (phase != 2) {
-      const float* va = gp(J.sc_valid);
+    if (hv) {
       const float vloss = phase == 1 ? va[SC_LUNC] : va[SC_LCOND];
-      row[H_VALID_LOSS] = vloss;
-      row[H_VALID_SHARPE] = va[SC_SHARPE];
-      row[H_VALID_LUNC] = va[SC_LUNC];
-      row[H_VALID_LCOND] = va[SC_LCOND];
-      row[H_VALID_MDD] = va[SC_MDD];
-      row[H_VALID_MEAN] = va[SC_MEAN];
-      row[H_VALID_STD] = va[SC_STD];
-      if (gp(J.sc_test)) {
-        const float* te = gp(J.sc_test);
-        row[H_TEST_LOSS] = phase == 1 ? te[SC_LUNC] : te[SC_LCOND];
-        row[H_TEST_SHARPE] = te[SC_SHARPE];
-        row[H_TEST_LUNC] = te[SC_LUNC];
-        row[H_TEST_LCOND] = te[SC_LCOND];
-        row[H_TEST_MDD] = te[SC_MDD];
-        row[H_TEST_MEAN] = te[SC_MEAN];
-        row[H_TEST_STD] = te[SC_STD];
+      r[H_VALID_LOSS] = vloss;
+      r[H_VALID_SHARPE] = va[SC_SHARPE];
+      r[H_VALID_LUNC] = va[SC_LUNC];
+      r[H_VALID_LCOND] = va[SC_LCOND];
+      r[H_VALID_MDD] = va[SC_MDD];
+      r[H_VALID_MEAN] = va[SC_MEAN];
+      r[H_VALID_STD] = va[SC_STD];
+      if (ht) {
+        r[H_TEST_LOSS] = phase == 1 ? te[SC_LUNC] : te[SC_LCOND];
+        r[H_TEST_SHARPE] = te[SC_SHARPE];
+        r[H_TEST_LUNC] = te[SC_LUNC];
+        r[H_TEST_LCOND] = te[SC_LCOND];
+        r[H_TEST_MDD] = te[SC_MDD];
+        r[H_TEST_MEAN] = te[SC_MEAN];
+        r[H_TEST_STD] = te[SC_STD];
       }
       if (ep_ph > ignore_epoch) {
-        if (vloss < gp(J.best)[0]) { gp(J.best)[0] = vloss; up_loss = 1; }
+        if (vloss < best0) { gp(J.best)[0] = vloss; up_loss = 1; }
         const float s = sel * va[SC_SHARPE];
-        if (s > gp(J.best)[1]) { gp(J.best)[1] = s; up_sr = 1; }
+        if (s > best1) { gp(J.best)[1] = s; up_sr = 1; }
       }
-    } else {
+    } else if (phase == 2) {
       const float lc = tr[SC_LCOND];
-      if (lc > gp(J.best)[2]) { gp(J.best)[2] = lc; up_loss = 1; }
+      if (lc > best2) { gp(J.best)[2] = lc; up_loss = 1; }
     }
-    row[H_BEST_LOSS] = (float)up_loss;
-    row[H_BEST_SR] = (float)up_sr;
+    r[H_BEST_LOSS] = (float)up_loss;
+    r[H_BEST_SR] = (float)up_sr;
+#pragma unroll
+    for (int c = 0; c < HIST_W; ++c) row[c] = r[c];
     if (up_loss) gp(J.snap_flags)[0] = 1;
     if (up_sr) gp(J.snap_flags)[1] = 1;
     gp(J.ep)[0] = ep + 1;
