@@ -1472,7 +1472,14 @@ static void install_crash_handler() {
   sigaction(SIGBUS, &sa, &g_prev_bus);
 }
 
+// DLAP_EMBED: the host-ASan harness (csrc/host/asan_main.cpp) links the engine into an
+// executable that embeds Python; the module is then a built-in one.
+#ifdef DLAP_EMBED
+#include <pybind11/embed.h>
+PYBIND11_EMBEDDED_MODULE(_dlap_hip, m) {
+#else
 PYBIND11_MODULE(_dlap_hip, m) {
+#endif
   install_crash_handler();
   m.doc() = "DLAP MI355X native engine (HIP kernels for gfx950 + hipGraph epoch executor)";
   py::class_<Engine>(m, "Engine")

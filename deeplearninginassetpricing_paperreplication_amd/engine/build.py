@@ -127,6 +127,51 @@ def build(force: bool = False, jobs: int = 8, verbose: bool = True, ubsan: bool 
     return out
 
 
+# Host AddressSanitizer harness: the runtime + the host side of every kernel file,
+# instrumented, linked into an executable that embeds Python (csrc/host/asan_main.cpp). The ASan
+# runtime is part of the executable, so nothing has to be preloaded into a Python process.
+# Device code is not instrumented (GPU sanitizers are not available on the MI355X pool).
+ASAN_FLAGS = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fno-omit-frame-pointer"]
+
+
+def asan_harness_path() -> Path:
+    # in-tree next to the package (travels to the GPU box with the snapshot; git-ignored)
+    return PKG / "asan" / "dlap_asan_python"
+
+
+def build_asan_harness(force: bool = False, jobs: int = 8, verbose: bool = True) -> Path:
+    srcs = sorted(CSRC.glob("*.hip")) + [CSRC / "engine.cpp", CSRC / "host" / "asan_main.cpp"]
+    headers = sorted(CSRC.glob("*.h"))
+    bdir = BUILD / "asan"
+    out = asan_harness_path()
+    stamp = bdir / "stamp"
+    key = _hash(srcs + headers) + "asan"
+    if not force and out.exists() and stamp.exists() and stamp.read_text() == key:
+        return out
+    bdir.mkdir(parents=True, exist_ok=True)
+    out.parent.mkdir(exist_ok=True)
+    flags = _includes() + ["-Wno-unused-result", "-DDLAP_EMBED=1"] + ASAN_FLAGS
+    with cf.ThreadPoolExecutor(max_workers=max(1, min(jobs, len(srcs)))) as ex:
+        futs = {ex.submit(_compile, s, bdir / (s.stem + ".o"), flags): s for s in srcs}
+        objs = [f.result() for f in cf.as_completed(futs)]
+    libdir = sysconfig.get_config_var("LIBDIR")
+    pyver = sysconfig.get_config_var("LDVERSION") or sysconfig.get_python_version()
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    # torch dlopens some of its own libraries by bare name (e.g. libcaffe2_nvrtc): the harness
+    # executable carries torch/lib in its rpath, as the python binary's loader setup does
+    rp = [f"-Wl,-rpath,{libdir}"] + ([f"-Wl,-rpath,{Path(spec.origin).parent / 'lib'}"] if spec else [])
+    cmd = [HIPCC, f"--offload-arch={ARCH}", *ASAN_FLAGS, *map(str, sorted(objs)), f"-L{libdir}",
+           f"-lpython{pyver}", *rp, "-o", str(out)]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"asan harness link failed:\n{r.stderr[-4000:]}")
+    stamp.write_text(key)
+    if verbose:
+        print(f"[dlap] built {out}")
+    return out
+
+
 if __name__ == "__main__":
     # --variant NAME [--file-flags FILE=FLAG,FLAG ...]: a named side build for A/B runs
     argv = sys.argv[1:]
@@ -138,4 +183,7 @@ if __name__ == "__main__":
             if "=" in a and a.split("=", 1)[0].endswith((".hip", ".cpp")):
                 f, fl = a.split("=", 1)
                 ffl[f] = [x for x in fl.split(",") if x]
-    build(force="--force" in argv, ubsan="--ubsan" in argv, debug="--debug" in argv, variant=var, file_flags=ffl)
+    if "--asan-harness" in argv:
+        build_asan_harness(force="--force" in argv)
+    else:
+        build(force="--force" in argv, ubsan="--ubsan" in argv, debug="--debug" in argv, variant=var, file_flags=ffl)
