@@ -162,7 +162,21 @@ class Engine {
       HIP_OK(hipStreamCreateWithPriority(&st2_, hipStreamNonBlocking, lo));
     } else {
       HIP_OK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
-      HIP_OK(hipStreamCreateWithFlags(&st2_, hipStreamNonBlocking));
+      const int ncu = env_int("DLAP_EVAL_CUS", 0);     // >0: evaluation branch on a CU subset
+      if (ncu > 0) {
+        hipDeviceProp_t prop;
+        int dev = 0;
+        HIP_OK(hipGetDevice(&dev));
+        HIP_OK(hipGetDeviceProperties(&prop, dev));
+        const int total = prop.multiProcessorCount;
+        std::vector<uint32_t> mask((total + 31) / 32, 0u);
+        // every XCD keeps the same share of its CUs (logical CU ids interleave the XCDs)
+        for (int cu = 0; cu < total; ++cu)
+          if ((long)(cu % 32) * total < (long)ncu * 32) mask[cu / 32] |= 1u << (cu % 32);
+        HIP_OK(hipExtStreamCreateWithCUMask(&st2_, (uint32_t)mask.size(), mask.data()));
+      } else {
+        HIP_OK(hipStreamCreateWithFlags(&st2_, hipStreamNonBlocking));
+      }
     }
     HIP_OK(hipStreamCreateWithFlags(&st3_, hipStreamNonBlocking));
     own_st_ = st_;
