@@ -88,7 +88,10 @@ def ensemble_sharpes_device(wstack: Dict, batches: Dict[str, Dict]) -> Dict:
     out = {}
     ind = None
     for split, b in batches.items():
-        W = wstack[split].float().contiguous()
+        W = wstack[split].float()
+        if not W.is_cuda:
+            W = W.to(torch.device("cuda", torch.cuda.current_device()))
+        W = W.contiguous()
         G, T, N = W.shape
         dev = W.device
         R = torch.as_tensor(b["returns"]).to(dev, torch.float32).contiguous()

@@ -134,7 +134,7 @@ def run_ensemble(config: Dict, batches: Dict[str, Dict], seeds: Sequence[int] = 
         if on_gpu:
             # RCCL all-gather into the rank's GPU, the ensemble math stays there (K11 kernel)
             allt = comm.all_gather_rows_tensor(d, torch.from_numpy(loc).to(d.device), len(seeds), mine)
-            wdev[sp] = allt
+            wdev[sp] = allt.to(d.device)    # (a gloo rehearsal gathers on the host)
             allw = allt.cpu().numpy()
         else:
             allw = comm.all_gather_rows(d, loc, len(seeds), mine)   # one collective per split
