@@ -7,9 +7,12 @@
 // the process without any preloading, and every host allocation of the runtime, the launchers
 // and the pybind11 bindings is checked. Usage:
 //     dlap_asan_python SCRIPT.py [args...]       (runs SCRIPT as __main__)
+//     dlap_asan_python -c CODE [args...]         (python -c; multiprocessing's spawned children
+//                                                  re-run sys.executable this way)
 #include <pybind11/embed.h>
 
 #include <cstdio>
+#include <string>
 
 namespace py = pybind11;
 
@@ -22,13 +25,16 @@ int main(int argc, char** argv) {
   int rc = 0;
   try {
     py::module_ sys = py::module_::import("sys");
+    const bool code = std::string(argv[1]) == "-c" && argc >= 3;
     py::list av;
-    for (int i = 1; i < argc; ++i) av.append(argv[i]);
+    if (code) av.append("-c");
+    for (int i = code ? 3 : 1; i < argc; ++i) av.append(argv[i]);
     sys.attr("argv") = av;
     // the package's loader finds the instrumented engine under its usual module name
     py::module_ eng = py::module_::import("_dlap_hip");
     sys.attr("modules")["deeplearninginassetpricing_paperreplication_amd._dlap_hip"] = eng;
-    py::module_::import("runpy").attr("run_path")(argv[1], py::arg("run_name") = "__main__");
+    if (code) py::exec(argv[2], py::module_::import("__main__").attr("__dict__"));
+    else py::module_::import("runpy").attr("run_path")(argv[1], py::arg("run_name") = "__main__");
   } catch (py::error_already_set& e) {
     if (e.matches(PyExc_SystemExit)) {
       py::object code = e.value().attr("code");
