@@ -11,8 +11,9 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-import pytest  # noqa: E402
+if __name__ == "__main__":     # (multiprocessing's spawned children re-import this file)
+    import pytest
 
-mod = sys.modules.get("deeplearninginassetpricing_paperreplication_amd._dlap_hip")
-print(f"[asan] engine module: {getattr(mod, '__file__', 'built-in (instrumented)')}", flush=True)
-sys.exit(pytest.main(sys.argv[1:]))
+    mod = sys.modules.get("deeplearninginassetpricing_paperreplication_amd._dlap_hip")
+    print(f"[asan] engine module: {getattr(mod, '__file__', 'built-in (instrumented)')}", flush=True)
+    sys.exit(pytest.main(sys.argv[1:]))
