@@ -80,6 +80,46 @@ DLAP_DEV bf16x8 zero8() {
   return r;
 }
 
+// ---- packed bf16 element ops (the tower activations) ----------------------------------
+// Two bf16 values per dword. The keep words of the dropout masks use a "split" layout: for row
+// block b and element e of a lane's 16 (e = 4u + r, unit 16u + 4q + r), the keep bit sits at
+// (e & 1) * 16 + 8 b + (e >> 1), so the two elements of a packed dword have their bits at the
+// same position of the two 16-bit halves and one v_pk_lshlrev_b16 + v_pk_ashrrev_i16 turns them
+// into a 0x0000 / 0xFFFF mask per half (hipcc rewrites the plain C form into compares and
+// selects, hence the asm).
+typedef short s16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+DLAP_DEV uint32_t cvt_pk(float a, float b) {           // v_cvt_pk_bf16_f32 (RNE)
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector((f32x2){a, b}, bf16x2));
+}
+// halves of the keep word at bit `sh` (and 16 + sh) -> 0xFFFF / 0x0000 per half
+template <int SH>
+DLAP_DEV uint32_t keep_mask(uint32_t kw) {
+  // (op_sel_hi:[0,1]: the high half also takes its shift from the low 16 bits of the inline
+  // constant -- by default it would read the constant's high half, 0)
+  uint32_t k;
+  asm("v_pk_lshlrev_b16 %0, %1, %2 op_sel_hi:[0,1]" : "=v"(k) : "i"(15 - SH), "v"(kw));
+  asm("v_pk_ashrrev_i16 %0, 15, %1 op_sel_hi:[0,1]" : "=v"(k) : "v"(k));
+  return k;
+}
+// ReLU on a packed bf16 pair: as int16 a negative bf16 is negative, so max(x, 0) zeroes it
+DLAP_DEV uint32_t relu_pk(uint32_t v) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s16x2, v), (s16x2){0, 0}));
+}
+// 0xFFFF per half where the (non-negative) packed bf16 activation is non-zero
+DLAP_DEV uint32_t nz_mask(uint32_t a) {
+  const u16x2 x = __builtin_bit_cast(u16x2, a) + (u16x2){0x7FFF, 0x7FFF};
+  uint32_t m;
+  asm("v_pk_ashrrev_i16 %0, 15, %1 op_sel_hi:[0,1]" : "=v"(m) : "v"(__builtin_bit_cast(uint32_t, x)));
+  return m;
+}
+DLAP_DEV float bf16_lo(uint32_t v) { return __uint_as_float(v << 16); }
+DLAP_DEV float bf16_hi(uint32_t v) { return __uint_as_float(v & 0xFFFF0000u); }
+
 // ---- tower precision policies ------------------------------------------------------------
 // The tower kernels are written once over an operand "fragment" of 8 k-values per lane (the
 // 16x16x32 MFMA operand map above) and instantiated for two precisions:
@@ -92,14 +132,44 @@ DLAP_DEV bf16x8 zero8() {
 //             HBM bytes per fragment.
 typedef float f32x8 __attribute__((ext_vector_type(8)));
 
+// Activation ops of both policies (fragment element j of a pack of C blocks lo / hi is
+// lo[j] (j < 4) or hi[j - 4]; its dword d = j >> 1 has keep bit BS + d in both halves, with
+// BS = 8 b + 4 s for row block b, k-step s -- see the split keep-word layout above):
+//   act<BS, DROP>(lo, hi, kw)  ReLU (and the keep mask) of the pre-activations, packed;
+//   gate(dlo, dhi, a)          d masked by (a != 0), packed: the ReLU'/dropout gate of a
+//                              recomputed activation fragment a (backward);
+//   unpack(f, lo, hi)          the fragment's values as two fp32 C blocks.
 struct PrecBF16 {
   using Frag = bf16x8;
   static constexpr bool kF32 = false;
   DLAP_DEV static f32x4 mma(const Frag& a, const Frag& b, const f32x4& c) { return mfma16(a, b, c); }
-  DLAP_DEV static Frag pack(const f32x4& lo, const f32x4& hi) { return pack8(lo, hi); }
+  DLAP_DEV static Frag pack(const f32x4& lo, const f32x4& hi) {
+    return __builtin_bit_cast(Frag, u32x4{cvt_pk(lo[0], lo[1]), cvt_pk(lo[2], lo[3]), cvt_pk(hi[0], hi[1]),
+                                          cvt_pk(hi[2], hi[3])});
+  }
   DLAP_DEV static Frag zero() { return zero8(); }
   DLAP_DEV static void set(Frag& f, int j, float v) { f[j] = (__bf16)v; }
   DLAP_DEV static void set_if(Frag& f, int j, bool c, float v) { f[j] = c ? (__bf16)v : f[j]; }
+  template <int BS, bool DROP>
+  DLAP_DEV static Frag act(const f32x4& lo, const f32x4& hi, uint32_t kw) {
+    u32x4 v{relu_pk(cvt_pk(lo[0], lo[1])), relu_pk(cvt_pk(lo[2], lo[3])), relu_pk(cvt_pk(hi[0], hi[1])),
+            relu_pk(cvt_pk(hi[2], hi[3]))};
+    if constexpr (DROP) {
+      v[0] &= keep_mask<BS + 0>(kw); v[1] &= keep_mask<BS + 1>(kw);
+      v[2] &= keep_mask<BS + 2>(kw); v[3] &= keep_mask<BS + 3>(kw);
+    }
+    return __builtin_bit_cast(Frag, v);
+  }
+  DLAP_DEV static Frag gate(const f32x4& lo, const f32x4& hi, const Frag& a) {
+    const u32x4 av = __builtin_bit_cast(u32x4, a);
+    return __builtin_bit_cast(Frag, u32x4{cvt_pk(lo[0], lo[1]) & nz_mask(av[0]), cvt_pk(lo[2], lo[3]) & nz_mask(av[1]),
+                                          cvt_pk(hi[0], hi[1]) & nz_mask(av[2]), cvt_pk(hi[2], hi[3]) & nz_mask(av[3])});
+  }
+  DLAP_DEV static void unpack(const Frag& f, f32x4& lo, f32x4& hi) {
+    const u32x4 v = __builtin_bit_cast(u32x4, f);
+    lo = f32x4{bf16_lo(v[0]), bf16_hi(v[0]), bf16_lo(v[1]), bf16_hi(v[1])};
+    hi = f32x4{bf16_lo(v[2]), bf16_hi(v[2]), bf16_lo(v[3]), bf16_hi(v[3])};
+  }
 };
 
 struct PrecF32 {
@@ -116,6 +186,27 @@ struct PrecF32 {
   DLAP_DEV static Frag zero() { return Frag{0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}; }
   DLAP_DEV static void set(Frag& f, int j, float v) { f[j] = v; }
   DLAP_DEV static void set_if(Frag& f, int j, bool c, float v) { f[j] = c ? v : f[j]; }
+  template <int BS, bool DROP>
+  DLAP_DEV static Frag act(const f32x4& lo, const f32x4& hi, uint32_t kw) {
+    Frag f = pack(lo, hi);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      float v = fmaxf(f[j], 0.f);
+      if constexpr (DROP) v = ((kw >> ((j & 1) * 16 + BS + (j >> 1))) & 1u) ? v : 0.f;
+      f[j] = v;
+    }
+    return f;
+  }
+  DLAP_DEV static Frag gate(const f32x4& lo, const f32x4& hi, const Frag& a) {
+    Frag d = pack(lo, hi);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) d[j] = a[j] != 0.f ? d[j] : 0.f;
+    return d;
+  }
+  DLAP_DEV static void unpack(const Frag& f, f32x4& lo, f32x4& hi) {
+    lo = f32x4{f[0], f[1], f[2], f[3]};
+    hi = f32x4{f[4], f[5], f[6], f[7]};
+  }
 };
 
 // ---- counter-based RNG for dropout (murmur3 finaliser on a mixed counter) -------------
@@ -143,6 +234,28 @@ DLAP_DEV bool dropout_keep(uint32_t key, uint32_t row, uint32_t unit, uint32_t t
 // is hoisted per row by the caller. Branch-free: evaluated for every element.
 DLAP_DEV uint32_t dropout_pair(uint32_t key, uint32_t rowmix, uint32_t pair) {
   return fmix32(key ^ rowmix ^ (pair * 0x27d4eb2fu));
+}
+DLAP_DEV uint32_t row_mix(uint32_t row) { return row * 0xcc9e2d51u ^ (row >> 16); }
+// Keep word of lane group q (split layout, see "packed bf16 element ops" below) for UB unit
+// blocks of the two row blocks: unit 16u + 4q + r of row block b keeps iff its 16-bit hash half
+// is >= thr16; one hash per unit pair (16u + 4q + 2h, +1).
+template <int UB>
+DLAP_DEV uint32_t keep_word(uint32_t key, const uint32_t (&rowmix)[2], uint32_t thr16, int q) {
+  uint32_t w = 0;
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const uint32_t pair0 = (uint32_t)(8 * u + 2 * q);
+      const uint32_t h0 = dropout_pair(key, rowmix[b], pair0);
+      const uint32_t h1 = dropout_pair(key, rowmix[b], pair0 + 1);
+      const int p = 8 * b + 2 * u;          // element e = 4u + r -> bit (r & 1) * 16 + 8b + (e >> 1)
+      w |= ((h0 & 0xFFFFu) >= thr16 ? 1u : 0u) << p;
+      w |= ((h0 >> 16) >= thr16 ? 1u : 0u) << (16 + p);
+      w |= ((h1 & 0xFFFFu) >= thr16 ? 1u : 0u) << (p + 1);
+      w |= ((h1 >> 16) >= thr16 ? 1u : 0u) << (16 + p + 1);
+    }
+  return w;
 }
 
 // ---- wave / block reductions (fixed order) --------------------------------------------

@@ -118,11 +118,16 @@ struct ModelSplitWS {   // per (model, split)
   DevBuf<float> pp, abias, xg, xin, sg, sc, sh;
   DevBuf<float> w, wn, h, P, port, sdf, mu, E, Eu, dE, dEu, part, pe, pu, dw, rstat, scal;
   DevBuf<float> u, v, dpp, dab, dg, dx;
-  DevBuf<uint32_t> gb, mgb;   // forward gate words of the train split (SDF / moment hidden)
+  DevBuf<uint32_t> gb;        // SDF dropout keep words of the train split (two parity halves)
   DevBuf<float> scal_prev;    // train split: metrics of the last finished step (bookkeeping)
   DevBuf<float> z;            // wide path: layer-0 pre-activations [ntiles][zc][64][4]
   DevBuf<uint16_t> dzs, dzm;  // wide path, train: layer-0 dz fragments (SDF / moment)
   DevBuf<float> wpart;        // wide path, train: layer-0 weight-gradient partials
+  DevBuf<float> h0, c0;       // [nrnn][H] initial LSTM state of the split (zero unless set_hidden)
+  DevBuf<float> dh0, dc0;     // train split: dL/d(initial state) from the last LSTM backward
+  DevBuf<float> dhx;          // train split, module API: external dL/dh [T*N][K] (lazy)
+  DevBuf<double> gram;        // Gram mode: [2][T][T] Gc, Gu of the frozen moments (k_gram.hip)
+  DevBuf<double> gpart;       // Gram mode: [T][2] per-period quadratic-form terms
 };
 
 struct ModelState {
@@ -204,6 +209,7 @@ class Engine {
     zx_gx_ = std::max(1, env_int("DLAP_ZX_GX", 256));
     train_first_ = env_int("DLAP_TRAIN_FIRST", 1) != 0;
     h_cache_ = env_int("DLAP_H_CACHE", 1) != 0;
+    gram_on_ = env_int("DLAP_GRAM", 1) != 0;
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
                residual, fp32);
     d_desc_.alloc(sizeof(ModelDesc));
@@ -213,10 +219,11 @@ class Engine {
       ModelState& S = models_[g];
       S.params.alloc(md_.P); S.grads.alloc(md_.P); S.m.alloc(md_.P); S.v.alloc(md_.P);
       S.snap_loss.alloc(md_.P); S.snap_sharpe.alloc(md_.P);
-      S.gnorm.alloc(1); S.best.alloc(3); S.aux.alloc(md_.md.aux_floats);
+      // packed weights: evaluation copy, then the training copy (dropout scale folded in)
+      S.gnorm.alloc(1); S.best.alloc(3); S.aux.alloc((size_t)2 * md_.md.aux_floats);
       S.hist.alloc((size_t)max_epochs_ * HIST_W);
       S.adam_step.alloc(2); S.drop_step.alloc(1); S.snap_flags.alloc(2); S.ep.alloc(2);
-      S.blob.alloc((size_t)md_.md.blob_frags * 512 * xw());       // bf16 (or fp32: 2 u16 each)
+      S.blob.alloc((size_t)2 * md_.md.blob_frags * 512 * xw());   // bf16 (or fp32: 2 u16 each)
       S.blob0.alloc((size_t)std::max(1, md_.md.b0_frags) * 512);
       S.wproj.alloc((size_t)(md_.proj_mp + 1) * md_.proj_np);
     }
@@ -490,7 +497,12 @@ class Engine {
     if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
     if (n <= 0) return;
     if (phase == 2) h_valid_ = false;     // the moment net trains: the cached moments go stale
-    else ensure_moments();
+    else ensure_moments(true);
+    struct GramScope {                    // epoch graphs run the loss in Gram mode
+      bool& f;
+      explicit GramScope(bool& x) : f(x) { f = true; }
+      ~GramScope() { f = false; }
+    } gram_scope(gram_run_);
     const bool pipe = phase != 2 && n_eval_jobs_ > 0 && pipeline_;
     if (!use_graph) {
       for (int e = 0; e < n; ++e) enqueue_epoch(phase, lr, ignore_epoch, sel);
@@ -553,9 +565,29 @@ class Engine {
   // The train forward is recomputed (same dropout step), the loss passes are skipped, and the
   // tower backward + gradient finalisation + LSTM BPTT leave the phase's gradients in `grads`
   // (copy_grads). Stream-ordered on the engine stream, no host synchronisation.
-  void xs_backward(int phase, uintptr_t dw, uintptr_t dE, uintptr_t sdf) {
+  // dh (phase 2, module API): an external dL/dh [T*N][K] (dense, the moments of the train split)
+  // instead of dE / sdf -- a caller's loss of the moments.
+  void xs_backward(int phase, uintptr_t dw, uintptr_t dE, uintptr_t sdf, uintptr_t dh = 0) {
     if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
     if (phase < 1 || phase > 3) throw std::invalid_argument("phase must be 1, 2 or 3");
+    if (dh) {
+      if (phase != 2) throw std::invalid_argument("an external dL/dh needs phase 2 (the moment tower)");
+      const SplitDev& D = splits_[0];
+      const size_t n = (size_t)D.T * D.N * md_.K;
+      if (!j_mlp_bwd_dh_.p) {                     // first use: buffers + job table
+        std::vector<MlpJob> mb;
+        for (int g = 0; g < G_; ++g) {
+          ws(g, 0).dhx.alloc(std::max<size_t>(n, 1), false);
+          mb.push_back(mlp_job(g, 0, true, true, true));
+          mb.back().dz_out = reinterpret_cast<bf16x8*>(ws(g, 0).dzm.p);
+          mb.back().dh_ext = ws(g, 0).dhx.p;
+        }
+        upload(j_mlp_bwd_dh_, mb);
+      }
+      for (int g = 0; g < G_; ++g)
+        if (n) HIP_OK(hipMemcpyAsync(ws(g, 0).dhx.p, reinterpret_cast<const void*>(dh), n * sizeof(float),
+                                     hipMemcpyDeviceToDevice, st_));
+    }
     if (phase != 2) ensure_moments();
     const SplitDev& D = splits_[0];
     enqueue_dropmask(phase, 0, st_);
@@ -570,7 +602,9 @@ class Engine {
                      md_.WMB, st_);
     for (int g = 0; g < G_; ++g) {
       ModelSplitWS& W = ws(g, 0);
-      if (phase == 2) {
+      if (phase == 2 && dh) {
+        // (the moment tower backward reads dL/dh directly)
+      } else if (phase == 2) {
         if (!dE || !sdf) throw std::invalid_argument("phase 2 needs dE and sdf");
         HIP_OK(hipMemcpyAsync(W.dE.p, reinterpret_cast<const void*>(dE), W.dE.n * sizeof(float),
                               hipMemcpyDeviceToDevice, st_));
@@ -583,8 +617,8 @@ class Engine {
       }
     }
     if (phase == 2)
-      launch_mlp_bwd_mom(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_m, 1, md_.md, md_.KS1,
-                         md_.WMB, slab_stride(), st_);
+      launch_mlp_bwd_mom(as<MlpJob>(dh ? j_mlp_bwd_dh_ : j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_m, 1, md_.md,
+                         md_.KS1, md_.WMB, slab_stride(), st_);
     else
       launch_mlp_bwd_sdf(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_s, md_.tps_s, md_.md, md_.KS1,
                          slab_stride(), st_);
@@ -647,6 +681,25 @@ class Engine {
     HIP_OK(hipMemcpyAsync(reinterpret_cast<void*>(dst), models_[check_g(g)].grads.p, md_.P * sizeof(float),
                           hipMemcpyDeviceToDevice, st_));
   }
+  // initial LSTM state (h0, c0) [nrnn][H] of split s (device pointers; 0 = back to the zero
+  // state). Stream-ordered, no host synchronisation.
+  void set_hidden(int g, int s, uintptr_t h, uintptr_t c) {
+    ModelSplitWS& W = ws(check_g(g), s);
+    const size_t n = (size_t)md_.nrnn * md_.H;
+    if (n == 0) return;
+    if (h) HIP_OK(hipMemcpyAsync(W.h0.p, reinterpret_cast<const void*>(h), n * 4, hipMemcpyDeviceToDevice, st_));
+    else HIP_OK(hipMemsetAsync(W.h0.p, 0, n * 4, st_));
+    if (c) HIP_OK(hipMemcpyAsync(W.c0.p, reinterpret_cast<const void*>(c), n * 4, hipMemcpyDeviceToDevice, st_));
+    else HIP_OK(hipMemsetAsync(W.c0.p, 0, n * 4, st_));
+  }
+  // dL/d(h0, c0) [nrnn][H] of the last LSTM backward of the train split (device pointers)
+  void copy_hidden_grad(int g, uintptr_t dh, uintptr_t dc) {
+    ModelSplitWS& W = ws(check_g(g), 0);
+    const size_t n = (size_t)md_.nrnn * md_.H;
+    if (n == 0) return;
+    HIP_OK(hipMemcpyAsync(reinterpret_cast<void*>(dh), W.dh0.p, n * 4, hipMemcpyDeviceToDevice, st_));
+    HIP_OK(hipMemcpyAsync(reinterpret_cast<void*>(dc), W.dc0.p, n * 4, hipMemcpyDeviceToDevice, st_));
+  }
   // final LSTM state (h_n, c_n) [nrnn][H] of the train split after a forward: the last step of
   // every layer's saved outputs / cells
   void copy_hidden(int g, uintptr_t dst_h, uintptr_t dst_c) {
@@ -675,6 +728,20 @@ class Engine {
     return down(*it->second);
   }
   py::array_t<float> read_aux(int g) { sync(); return down(models_[check_g(g)].aux); }
+  // Gram matrices [2][T][T] (Gc, Gu) of (model g, split s) as last built (tests)
+  py::array_t<double> read_gram(int g, int s) {
+    ModelSplitWS& W = ws(check_g(g), s);
+    sync();
+    py::array_t<double> out(W.gram.n);
+    if (W.gram.n) HIP_LEGACY(hipMemcpy(out.mutable_data(), W.gram.p, W.gram.n * sizeof(double), hipMemcpyDeviceToHost));
+    return out;
+  }
+  // (re)build the Gram matrices from the current moments now (tests; run_epochs does it itself)
+  void refresh_gram() {
+    if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
+    ensure_moments(true);
+  }
+  bool gram_enabled(int phase) const { return phase == 0 ? gram_eval() : gram_train(phase); }
   py::array_t<uint16_t> read_blob(int g) {
     sync();  // (already synchronous)
     ModelState& S = models_[check_g(g)];
@@ -722,6 +789,24 @@ class Engine {
   bool h_cache_ = true;                      // DLAP_H_CACHE
   bool h_valid_ = false;                     // cached h matches the current moment parameters
   bool cache_train_h() const { return h_cache_ && (md_.nl_m == 1 || md_.dropout == 0.f); }
+  // Gram mode (k_gram.hip): while the moments are frozen the losses are quadratic forms in the
+  // SDF vector, built once per moment refresh (ensure_moments). Needs the moment cache and, for
+  // the conditional form, K % 4 == 0 (16-byte rows of the per-stock moment vectors).
+  bool gram_on_ = true;                      // DLAP_GRAM
+  bool gram_cond_ok() const { return gram_on_ && h_cache_ && md_.K % 4 == 0; }
+  bool gram_train(int phase) const {
+    return gram_on_ && h_cache_ && (phase == 1 || (phase == 3 && cache_train_h() && gram_cond_ok()));
+  }
+  bool gram_eval() const { return gram_cond_ok(); }
+  DevBuf<double> gram_scratch_;              // split-K partials of the Gram build
+  DevBuf<char> j_gram_[3];                   // Gram build jobs per split (every model)
+  DevBuf<char> j_loss_gram_[4];              // phase training loss jobs in Gram mode (epoch graphs)
+  bool gram_valid_ = false;                  // G matches the cached moments (build_gram ran)
+  bool gram_run_ = false;                    // inside run_epochs (epoch graphs use Gram mode)
+  bool use_gram(int phase) const { return gram_run_ && gram_train(phase); }
+  const LossJob* loss_tab(int phase, bool gram) const {
+    return gram ? as<LossJob>(j_loss_gram_[phase]) : as<LossJob>(j_loss_train_[phase]);
+  }
   // whether the training towers of a phase run the moment network (and so need its
   // per-period bias table from the prologue)
   bool train_mom(int phase) const { return phase == 2 || (phase == 3 && !cache_train_h()); }
@@ -741,6 +826,7 @@ class Engine {
       j_loss_eval_, j_fin_, j_upd_, j_epoch_[4];
   DevBuf<char> j_wide_train_[4], j_wide_eval_, j_wide_bwd_[4];   // wide path (k_wide.hip)
   DevBuf<char> j_rnn_mom_, j_mlp_mom_, j_wide_mom_;             // moment refresh (every split)
+  DevBuf<char> j_mlp_bwd_dh_;                                   // moment backward from an external dL/dh
   int n_mom_jobs_ = 0, tmax_all_ = 0, gx_mom_ = 1;
   int n_eval_jobs_ = 0;
   int tmax_eval_ = 0, nmax_eval_ = 0;
@@ -797,7 +883,10 @@ class Engine {
     d.F = F; d.M = M; d.nrnn = nrnn; d.H = nrnn > 0 ? H : 0; d.K = K;
     d.Dm = nrnn > 0 ? H : (raw_macro_sdf ? M : 0);
     d.KIN = F + d.Dm;
-    const int ks = (d.KIN + 31) / 32;
+    // fused path: the per-period inputs are written into the last 8*ceil(Dm/8) columns of the
+    // panel row by the tower kernels (k_mlp.hip finish_tile), after the F characteristics
+    const int ppw = (d.Dm + 7) / 8 * 8;
+    const int ks = (F + ppw + 31) / 32;
     // wide path: layer-0 inputs beyond the 128 columns a fused tower tile holds in registers
     // (or DLAP_WIDE=1) -> layer 0 runs as the streaming k_proj0 / k_wgrad0 GEMMs
     const bool wide = ks > 4 || env_int("DLAP_WIDE", 0) != 0;
@@ -810,6 +899,8 @@ class Engine {
       d.KSB = d.KS1;
       d.KP = 32 * d.KS1;
     }
+    d.md.ppc = wide ? 0 : d.KP - ppw;
+    d.md.ppst = (d.Dm + 3) / 4 * 4;
     d.dropout = dropout; d.normalize_w = normalize_w; d.weighted_loss = weighted; d.residual_factor = residual;
     int off = 0;
     for (int l = 0; l < nrnn; ++l) {
@@ -854,7 +945,8 @@ class Engine {
     D.m_bwd = D.m_fwd + (d.nl_m - 1) * d.WMB * KSM;
     D.s_upp = D.m_bwd + (d.nl_m - 1) * d.WMB * KSM;
     D.ubpp = nrnn > 0 ? (d.Dm + 15) / 16 : 0;
-    D.blob_frags = D.s_upp + 2 * D.ubpp;
+    D.s_wo = D.s_upp + 2 * D.ubpp;
+    D.blob_frags = D.s_wo + 2;
     D.a_sb = 0; D.a_wo = 64 * d.nl_s; D.a_bo = D.a_wo + 64; D.a_pp = D.a_bo + 4;
     D.a_mb = D.a_pp + 64 * d.Dm; D.aux_floats = D.a_mb + 64 * d.nl_m;
     D.wide = wide ? 1 : 0;
@@ -875,10 +967,10 @@ class Engine {
     const int C0 = wide ? (d.Dm + 63) / 64 : d.KS1 / 2;
     int t = 0;
     for (int c = 0; c < C0; ++c, ++t)
-      d.tile_s[t] = wide ? GradTile{d.s[0].w_off, d.s[0].ld, F, d.s[0].out, d.Dm, c, t}
-                         : GradTile{d.s[0].w_off, d.s[0].ld, 0, d.s[0].out, d.s[0].in, c, t};
+      d.tile_s[t] = wide ? GradTile{d.s[0].w_off, d.s[0].ld, F, d.s[0].out, d.Dm, c, t, 0, 0}
+                         : GradTile{d.s[0].w_off, d.s[0].ld, 0, d.s[0].out, d.KP, c, t, 0, 1};
     for (int j = 1; j < d.nl_s; ++j, ++t)
-      d.tile_s[t] = GradTile{d.s[j].w_off, d.s[j].ld, 0, d.s[j].out, d.s[j].in, 0, t};
+      d.tile_s[t] = GradTile{d.s[j].w_off, d.s[j].ld, 0, d.s[j].out, d.s[j].in, 0, t, j, 0};
     d.ntile_s = t;
     // two gradient tiles per slice share one forward recompute (fits the 512-register
     // budget of a single wave per SIMD); DLAP_TPS=1 forces one tile per slice
@@ -891,9 +983,9 @@ class Engine {
     t = 0;
     const int C0m = wide ? 0 : d.KS1 / 2;
     for (int c = 0; c < C0m; ++c, ++t)
-      d.tile_m[t] = GradTile{d.m[0].w_off, d.m[0].ld, d.m[0].col0, d.m[0].out, d.m[0].in, c, t};
+      d.tile_m[t] = GradTile{d.m[0].w_off, d.m[0].ld, d.m[0].col0, d.m[0].out, d.m[0].in, c, t, 0, 0};
     for (int j = 1; j < d.nl_m; ++j, ++t)
-      d.tile_m[t] = GradTile{d.m[j].w_off, d.m[j].ld, 0, d.m[j].out, d.m[j].in, 0, t};
+      d.tile_m[t] = GradTile{d.m[j].w_off, d.m[j].ld, 0, d.m[j].out, d.m[j].in, 0, t, j, 0};
     d.ntile_m = t;
     d.nslice_m = std::max(1, t);
     d.tps_m = 1;
@@ -925,6 +1017,9 @@ class Engine {
       W.part.alloc(2 * std::max(((size_t)N * (K + 1) + 255) / 256, ((size_t)N + 15) / 16));
       W.pe.alloc((size_t)DLAP_TCH * N * K); W.pu.alloc((size_t)DLAP_TCH * N);
       W.scal.alloc(SC_NSCAL);
+      W.gram.alloc((size_t)2 * T * T); W.gpart.alloc((size_t)2 * std::max(T, 1));
+      W.h0.alloc((size_t)std::max(md_.nrnn * H, 1)); W.c0.alloc((size_t)std::max(md_.nrnn * H, 1));
+      if (s == 0) { W.dh0.alloc((size_t)std::max(md_.nrnn * H, 1)); W.dc0.alloc((size_t)std::max(md_.nrnn * H, 1)); }
       if (s == 0) W.scal_prev.alloc(SC_NSCAL);
       if (md_.residual_factor > 0.f) W.rstat.alloc((size_t)T * 4);
       if (s == 0) {
@@ -935,7 +1030,6 @@ class Engine {
         W.dab.alloc((size_t)T * 64);
         const size_t ntl = (size_t)(R + 31) / 32;
         W.gb.alloc(std::max<size_t>(2 * ntl * md_.nl_s * 64, 1), false);   // two parity halves
-        W.mgb.alloc(std::max<size_t>(ntl * std::max(md_.nl_m - 1, 0) * 64, 1), false);
         if (md_.nrnn > 0) {
           W.sg.alloc((size_t)md_.nrnn * T * 4 * H);
           W.sc.alloc((size_t)md_.nrnn * T * H);
@@ -979,7 +1073,7 @@ class Engine {
     int tmax = 0;
     for (int k = 0; k < 3; ++k)
       if (splits_[k].set || k == s) tmax = std::max(tmax, splits_[k].T);
-    const int ppf = tmax * md_.Dm;
+    const int ppf = tmax * md_.md.ppst;
     md_.md.pp_lds_floats = (md_.Dm > 0 && ppf <= 8192 && !env_int("DLAP_PP_GLOBAL", 0)) ? ppf : 0;
   }
 
@@ -999,6 +1093,7 @@ class Engine {
     J.xg = W.xg.p; J.xin = W.xin.p;
     J.abias = W.abias.p;
     J.step = models_[g].drop_step.p;
+    J.h0 = W.h0.p; J.c0 = W.c0.p;
     J.seed = models_[g].seed;
     J.train = train;
     return J;
@@ -1016,9 +1111,10 @@ class Engine {
     J.rowti = reinterpret_cast<const int2*>(D.rowti.p);
     J.pp = pp_ptr(g, s);
     J.abias = W.abias.p;
-    J.blob = reinterpret_cast<const bf16x8*>(models_[g].blob.p);
+    // train-mode towers read the training copy of the packed weights (k_pack)
+    J.blob = reinterpret_cast<const bf16x8*>(models_[g].blob.p + (train ? (size_t)md_.md.blob_frags * 512 * xw() : 0));
     J.blob0 = reinterpret_cast<const bf16x8*>(models_[g].blob0.p);
-    J.aux = models_[g].aux.p;
+    J.aux = models_[g].aux.p + (train ? md_.md.aux_floats : 0);
     J.w_out = W.w.p; J.h_out = W.h.p;
     J.dw = W.dw.p; J.dE = W.dE.p; J.Rm = D.Rm.p; J.sdfv = W.sdf.p; J.invT = D.invT.p;
     J.slab = slab_.p;
@@ -1051,7 +1147,7 @@ class Engine {
     J.do_sdf = do_sdf; J.do_mom = do_mom;
     return J;
   }
-  LossJob loss_job(int g, int s, int phase) {
+  LossJob loss_job(int g, int s, int phase, bool gram = false) {
     ModelSplitWS& W = ws(g, s);
     SplitDev& D = splits_[s];
     LossJob J{};
@@ -1070,7 +1166,50 @@ class Engine {
     J.dE = (phase == 2 || phase == 3) ? W.dE.p : nullptr;
     J.dEu = phase == 1 ? W.dEu.p : nullptr;
     J.part = W.part.p; J.pe = W.pe.p; J.pu = W.pu.p; J.dw = W.dw.p; J.rstat = W.rstat.p; J.scal = W.scal.p;
+    if (gram) {
+      J.gram = 1; J.G = W.gram.p; J.gpart = W.gpart.p;
+      J.asset_full = 0;
+    }
     return J;
+  }
+  GramJob gram_job(int g, int s, bool cond) {
+    ModelSplitWS& W = ws(g, s);
+    SplitDev& D = splits_[s];
+    GramJob J{};
+    J.h = cond ? W.h.p : nullptr;
+    J.Rm = D.Rm.p; J.invT = D.invT.p; J.G = W.gram.p;
+    J.T = D.T; J.N = D.N; J.K = md_.K;
+    return J;
+  }
+  // Gram build job tables of every split (rebuild_jobs): the train split's conditional matrix
+  // only if its moments are cacheable. One scratch area, reused split after split.
+  void build_gram_jobs() {
+    size_t need = 0;
+    for (int s = 0; s < 3; ++s)
+      if (splits_[s].set) need = std::max(need, gram_part_doubles(splits_[s].T, G_));
+    gram_scratch_.alloc(std::max<size_t>(need, 1), false);
+    for (int s = 0; s < 3; ++s) {
+      const SplitDev& D = splits_[s];
+      if (!D.set || D.T == 0) continue;
+      const bool cond = gram_cond_ok() && (s != 0 || cache_train_h());
+      const size_t per = (size_t)gram_slices(D.T, G_) * 2 * D.T * D.T;
+      std::vector<GramJob> jobs;
+      for (int g = 0; g < G_; ++g) {
+        jobs.push_back(gram_job(g, s, cond));
+        jobs.back().part = gram_scratch_.p + per * g;
+      }
+      upload(j_gram_[s], jobs);
+    }
+  }
+  // Build the Gram matrices of every (model, split) from the current cached moments.
+  // Stream-ordered on st_ (no host synchronisation).
+  void build_gram() {
+    for (int s = 0; s < 3; ++s) {
+      const SplitDev& D = splits_[s];
+      if (!D.set || D.T == 0) continue;
+      HTRACE("launch_gram split=%d", s);
+      launch_gram(as<GramJob>(j_gram_[s]), G_, D.T, gram_slices(D.T, G_), st_);
+    }
   }
 
   void rebuild_jobs() {
@@ -1078,6 +1217,7 @@ class Engine {
     for (auto& kv : graphs_) retire_graph_exec(kv.second);
     graphs_.clear();
     fwd_tables_.clear();
+    j_mlp_bwd_dh_.free();
     std::vector<RnnJob> rt, re;
     std::vector<LossJob> le;
     std::vector<MlpJob> me;
@@ -1092,7 +1232,7 @@ class Engine {
         re.push_back(rnn_job(g, s, false));
         me.push_back(mlp_job(g, s, false, true, !h_cache_));
         we.push_back(wide_job(g, s, true, !h_cache_));
-        le.push_back(loss_job(g, s, 0));
+        le.push_back(loss_job(g, s, 0, gram_eval()));
         tmax_eval_ = std::max(tmax_eval_, splits_[s].T);
         nmax_eval_ = std::max(nmax_eval_, splits_[s].N);
       }
@@ -1111,10 +1251,13 @@ class Engine {
       U.blob0 = reinterpret_cast<bf16x8*>(S.blob0.p);
       U.dpp = W.dpp.p; U.macro = splits_[0].macro.p; U.sg = W.sg.p; U.sc = W.sc.p; U.sh = W.sh.p;
       U.dg = W.dg.p; U.dx = W.dx.p; U.dab = W.dab.p; U.scal = W.scal.p; U.scal_prev = W.scal_prev.p;
+      U.h0 = W.h0.p; U.c0 = W.c0.p; U.dh0 = W.dh0.p; U.dc0 = W.dc0.p;
       U.T = splits_[0].T; U.seed = S.seed; U.lr = S.lr;
       uj.push_back(U);
     }
     n_eval_jobs_ = (int)le.size();
+    if (gram_on_) build_gram_jobs();
+    gram_valid_ = false;
     upload(j_rnn_train_, rt); upload(j_rnn_eval_, re); upload(j_mlp_eval_, me); upload(j_loss_eval_, le);
     upload(j_fin_, fj); upload(j_upd_, uj); upload(j_wide_eval_, we);
     {   // moment refresh: eval-mode moment tower (and its per-period bias) of every split
@@ -1136,7 +1279,7 @@ class Engine {
     }
     for (int phase = 1; phase <= 3; ++phase) {
       std::vector<MlpJob> mt, mb;
-      std::vector<LossJob> lt;
+      std::vector<LossJob> lt, lg;
       std::vector<EpochJob> ej;
       std::vector<WideJob> wt, wb;
       for (int g = 0; g < G_; ++g) {
@@ -1147,14 +1290,13 @@ class Engine {
         mt.back().store_mz = phase == 2;
         wt.push_back(wide_job(g, 0, true, train_mom(phase)));
         wb.push_back(wide_job(g, 0, phase != 2, phase == 2));
-        // the training forward stores the gate words its backward reuses
-        if (phase == 2) {
-          if (md_.nl_m > 1) mt.back().mgbits = mb.back().mgbits = ws(g, 0).mgb.p;
-        } else {
+        // the SDF keep words of the step (k_dropmask), read by its forward and backward
+        if (phase != 2) {
           mt.back().gbits = mb.back().gbits = ws(g, 0).gb.p;
           mt.back().gb_half = mb.back().gb_half = ((splits_[0].R + 31) / 32) * md_.nl_s * 64;
         }
         lt.push_back(loss_job(g, 0, phase));
+        lg.push_back(loss_job(g, 0, phase, gram_train(phase)));
         ModelState& S = models_[g];
         EpochJob E{};
         E.sc_train = ws(g, 0).scal_prev.p;
@@ -1167,6 +1309,7 @@ class Engine {
         ej.push_back(E);
       }
       upload(j_mlp_train_[phase], mt); upload(j_mlp_bwd_[phase], mb); upload(j_loss_train_[phase], lt);
+      upload(j_loss_gram_[phase], lg);
       upload(j_epoch_[phase], ej); upload(j_wide_train_[phase], wt); upload(j_wide_bwd_[phase], wb);
     }
     // evaluation-only jobs of the train split (module API / final evaluation)
@@ -1191,8 +1334,14 @@ class Engine {
 
   // Recompute the cached moments of every split (enqueued on st_, ahead of the epochs that
   // read them) if the moment parameters may have changed since they were computed.
-  void ensure_moments() {
-    if (!h_cache_ || h_valid_ || n_mom_jobs_ == 0) return;
+  // with_gram: also (re)build the Gram matrices (epoch graphs: run_epochs); the module-API
+  // steps use the dense loss passes and skip it.
+  void ensure_moments(bool with_gram = false) {
+    if (!h_cache_ || n_mom_jobs_ == 0) return;
+    if (h_valid_) {
+      if (with_gram && gram_on_ && !gram_valid_) { build_gram(); gram_valid_ = true; }
+      return;
+    }
     HTRACE("ensure_moments jobs=%d tmax=%d gx=%d", n_mom_jobs_, tmax_all_, gx_mom_);
     HTRACE("launch_prologue");
     launch_prologue(as<RnnJob>(j_rnn_mom_), n_mom_jobs_, tmax_all_, dd(), md_, st_);
@@ -1206,6 +1355,8 @@ class Engine {
       launch_mlp_fwd(as<MlpJob>(j_mlp_mom_), n_mom_jobs_, gx_mom_, md_.md, md_.KS1, md_.WMB, st_);
     }
     h_valid_ = true;
+    gram_valid_ = false;
+    if (with_gram && gram_on_) { build_gram(); gram_valid_ = true; }
   }
   bool dropmask_on(int phase) const { return md_.dropout > 0.f && phase != 2; }
   // keep masks of the step *drop_step + offset* (phases 1/3: the SDF tower's dropout)
@@ -1225,6 +1376,8 @@ class Engine {
   void enqueue_train_grads(int phase, hipStream_t side = nullptr, bool premasked = false, int mark = 0,
                            bool part1_only = false, bool defer_metrics = false) {
     const SplitDev& D = splits_[0];
+    const bool gram = use_gram(phase);
+    const LossJob* lj = loss_tab(phase, gram);
     if (!premasked) enqueue_dropmask(phase, 0, st_);
     // the latency-bound LSTM first, before the streaming projection loads the memory system
     HTRACE("launch_prologue");
@@ -1240,31 +1393,40 @@ class Engine {
                      md_.WMB, st_);
     if (mark == 2) HIP_OK(hipEventRecord(ev_a_, st_));
     HTRACE("launch_period_fwd");
-    launch_period_fwd(as<LossJob>(j_loss_train_[phase]), G_, D.T, st_);
-    HTRACE("launch_asset");
-    launch_asset(as<LossJob>(j_loss_train_[phase]), G_, D.N, md_.K, st_, asset_full_default());
+    launch_period_fwd(lj, G_, D.T, st_);
+    if (!gram) {
+      HTRACE("launch_asset");
+      launch_asset(lj, G_, D.N, md_.K, st_, asset_full_default());
+    } else {
+      // Gram mode: the quadratic-form loss terms and dL/dw come from one per-period pass, which
+      // the job metrics (the loss values) then read
+      HTRACE("launch_period_bwd(gram)");
+      launch_period_bwd(lj, G_, D.T, st_);
+    }
     if (defer_metrics && phase != 2) {
       HIP_OK(hipEventRecord(ev_mid_, st_));
     } else if (side) {
       HIP_OK(hipEventRecord(ev_mid_, st_));
       HIP_OK(hipStreamWaitEvent(side, ev_mid_, 0));
       HTRACE("launch_job_metrics");
-      launch_job_metrics(as<LossJob>(j_loss_train_[phase]), G_, side);
+      launch_job_metrics(lj, G_, side);
       HIP_OK(hipEventRecord(ev_m3_, side));
       side_open_ = true;
     } else {
       // (k_job_metrics, not the metrics workgroup of k_period_bwd<true>: the same reduction
       // order as the deferred launch of the pipelined epochs, so both schedules are bitwise equal)
       HTRACE("launch_job_metrics");
-      launch_job_metrics(as<LossJob>(j_loss_train_[phase]), G_, st_);
+      launch_job_metrics(lj, G_, st_);
     }
     if (phase == 2) {
       HTRACE("launch_mlp_bwd_mom");
       launch_mlp_bwd_mom(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_m, 1, md_.md, md_.KS1,
                          md_.WMB, slab_stride(), st_);
     } else {
-      HTRACE("launch_period_bwd");
-      launch_period_bwd(as<LossJob>(j_loss_train_[phase]), G_, D.T, st_);
+      if (!gram) {
+        HTRACE("launch_period_bwd");
+        launch_period_bwd(lj, G_, D.T, st_);
+      }
       HTRACE("launch_mlp_bwd_sdf");
       launch_mlp_bwd_sdf(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_s, md_.tps_s, md_.md, md_.KS1,
                          slab_stride(), st_);
@@ -1334,8 +1496,13 @@ class Engine {
     }
     HTRACE("launch_period_fwd");
     launch_period_fwd(as<LossJob>(j_loss_eval_), n_eval_jobs_, tmax_eval_, st);
-    HTRACE("launch_asset");
-    launch_asset(as<LossJob>(j_loss_eval_), n_eval_jobs_, nmax_eval_, md_.K, st);
+    if (gram_run_ && gram_eval()) {  // quadratic-form terms per period (no asset passes)
+      HTRACE("launch_period_bwd(eval)");
+      launch_period_bwd(as<LossJob>(j_loss_eval_), n_eval_jobs_, tmax_eval_, st);
+    } else {
+      HTRACE("launch_asset");
+      launch_asset(as<LossJob>(j_loss_eval_), n_eval_jobs_, nmax_eval_, md_.K, st);
+    }
     HTRACE("launch_job_metrics");
     launch_job_metrics(as<LossJob>(j_loss_eval_), n_eval_jobs_, st);
   }
@@ -1369,7 +1536,7 @@ class Engine {
       if (side_metrics_) HIP_OK(hipStreamWaitEvent(st2_, ev_m3_, 0));   // train metrics
       if (defer && phase != 2) {                          // this epoch's train metrics, after its
         HIP_OK(hipStreamWaitEvent(st2_, ev_mid_, 0));     // asset pass (read by the next bookkeeping)
-        launch_job_metrics(as<LossJob>(j_loss_train_[phase]), G_, st2_);
+        launch_job_metrics(loss_tab(phase, use_gram(phase)), G_, st2_);
       }
       enqueue_epoch_end(phase, ignore_epoch, sel, st2_);  // ... and its bookkeeping
       enqueue_dropmask(phase, 1, st2_);                   // next epoch's dropout masks
@@ -1417,6 +1584,9 @@ class Engine {
     hipGraphExec_t exec;
     HIP_OK(hipGraphInstantiateWithFlags(&exec, graph, prio_ ? hipGraphInstantiateFlagUseNodePriority : 0));
     HIP_OK(hipGraphDestroy(graph));
+    // device-side upload now, not at the first launch (that launch may sit inside a timed or
+    // latency-critical region)
+    HIP_OK(hipGraphUpload(exec, st_));
     graphs_.emplace(key, exec);
     return exec;
   }
@@ -1535,7 +1705,10 @@ PYBIND11_MODULE(_dlap_hip, m) {
       .def("set_stream", &Engine::set_stream, py::arg("stream"), py::arg("external") = true)
       .def("set_params_dev", &Engine::set_params_dev)
       .def("join_from", &Engine::join_from)
-      .def("xs_backward", &Engine::xs_backward)
+      .def("xs_backward", &Engine::xs_backward, py::arg("phase"), py::arg("dw"), py::arg("dE"), py::arg("sdf"),
+           py::arg("dh") = 0)
+      .def("set_hidden", &Engine::set_hidden)
+      .def("copy_hidden_grad", &Engine::copy_hidden_grad)
       .def("split_rows", &Engine::split_rows)
       .def("join_to", &Engine::join_to)
       .def("set_drop_step", &Engine::set_drop_step)
@@ -1544,6 +1717,9 @@ PYBIND11_MODULE(_dlap_hip, m) {
       .def("copy_hidden", &Engine::copy_hidden)
       .def("read_ws", &Engine::read_ws)
       .def("read_aux", &Engine::read_aux)
+      .def("read_gram", &Engine::read_gram)
+      .def("refresh_gram", &Engine::refresh_gram)
+      .def("gram_enabled", &Engine::gram_enabled)
       .def("read_blob", &Engine::read_blob)
       .def("sync", &Engine::sync, py::call_guard<py::gil_scoped_release>())
       .def("stream", &Engine::stream);

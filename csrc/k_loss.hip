@@ -363,7 +363,20 @@ __global__ __launch_bounds__(256) void k_asset_full(const LossJob* __restrict__ 
 // takes a strided share (all loads in flight at once, instead of 2 * nblk dependent round trips
 // on one thread), then the fixed-order block reduction.
 template <int NT>
+DLAP_DEV double block_sum_d(double v, double* red);
+
+template <int NT>
 DLAP_DEV void final_losses(const LossJob& J, float& lc, float& lu, float* red) {
+  if (J.gram) {        // fixed-order fp64 sum of the per-period quadratic-form terms
+    __shared__ double redd[NT / 64];
+    double a = 0.0, b = 0.0;
+    for (int t = threadIdx.x; t < J.T; t += NT) { a += gp(J.gpart)[2 * t]; b += gp(J.gpart)[2 * t + 1]; }
+    a = block_sum_d<NT>(a, redd);
+    b = block_sum_d<NT>(b, redd);
+    lc = J.h ? (float)(a / ((double)J.K * (double)J.N)) : 0.f;
+    lu = (float)(b / (double)J.N);
+    return;
+  }
   const int nblk = asset_red_blocks(J);
   float a = 0.f, b = 0.f;
   for (int k = threadIdx.x; k < nblk; k += NT) { a += gp(J.part)[2 * k]; b += gp(J.part)[2 * k + 1]; }
@@ -375,6 +388,46 @@ DLAP_DEV void final_losses(const LossJob& J, float& lc, float& lu, float* red) {
 
 // ---------------------------------------------------------------- period backward ------
 template <int NT> DLAP_DEV void job_metrics_body(const LossJob& J, float* red, float* ret);
+
+template <int NT>
+DLAP_DEV double block_sum_d(double v, double* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) s += red[i];
+  return s;
+}
+
+// Gram mode: (Gc s)_t and (Gu s)_t for period t in fp64, their loss terms s_t (G s)_t into
+// gpart, and dL/dSDF_t of the job's training loss (phase 1: L_unc, 3: L_cond; 0: none).
+DLAP_DEV float gram_period(const LossJob& J, int t, double* redd) {
+  const int T = J.T;
+  const size_t T2 = (size_t)T * T;
+  const auto G = gp(J.G) + (size_t)t * T;
+  const auto sv = gp(J.sdfv);
+  const bool cond = J.h != nullptr;
+  double vc = 0.0, vu = 0.0;
+  for (int u = threadIdx.x; u < T; u += PER_NT) {
+    const double s = (double)sv[u];
+    if (cond) vc += G[u] * s;
+    vu += G[T2 + u] * s;
+  }
+  if (cond) vc = block_sum_d<PER_NT>(vc, redd);
+  vu = block_sum_d<PER_NT>(vu, redd);
+  if (threadIdx.x == 0) {
+    const double st = (double)sv[t];
+    gp(J.gpart)[2 * t + 0] = cond ? st * vc : 0.0;
+    gp(J.gpart)[2 * t + 1] = st * vu;
+  }
+  // coef_c = +-2/(KN), coef_u = 2/N (see Engine::loss_job); dL/dSDF = coef (G s)
+  if (J.phase == 1) return (float)((double)J.coef_u * vu);
+  if (J.phase == 2 || J.phase == 3) return (float)((double)J.coef_c * vc);
+  return 0.f;
+}
 
 // METRICS: one extra workgroup (the last, blockIdx.x == gridDim.x - 1) computes the job's
 // scalar metrics (k_job_metrics) beside the period workgroups: one launch less on the
@@ -393,6 +446,12 @@ __global__ __launch_bounds__(PER_NT) void k_period_bwd(const LossJob* __restrict
   const size_t base = (size_t)t * N;
   const int r0 = gp(J.row_ptr)[t], r1 = gp(J.row_ptr)[t + 1];
   DLAP_ASSERT(0 <= r0 && r0 <= r1 && r1 <= J.R);
+  float sg = 0.f;                  // Gram mode: dL/dSDF_t
+  if (J.gram) {
+    __shared__ double redd[PER_NT / 64];
+    sg = gram_period(J, t, redd);
+    if (J.phase == 0) return;      // evaluation: loss terms only
+  }
   // no compact rows in this period (all stocks masked): no dL/dw to write, and the clamped
   // row index of the loads below would point past the end of the arrays when r0 == R
   if (r1 == r0) return;            // block-uniform, before any barrier
@@ -450,15 +509,26 @@ __global__ __launch_bounds__(PER_NT) void k_period_bwd(const LossJob* __restrict
   };
   float rv[RB];
   float s = 0.f;
-  if (fast) {
-    s = chunk_sum(r0, rv);
-  } else {
-    for (int c0 = r0; c0 < r1; c0 += PER_NT * RB) {
-      float rt[RB];
-      s += chunk_sum(c0, rt);
+  if (J.gram) {
+    s = sg;
+    if (fast) {
+#pragma unroll
+      for (int k = 0; k < RB; ++k) {
+        const int r = r0 + threadIdx.x + PER_NT * k;
+        rv[k] = Rc[r < r1 ? r : r0];
+      }
     }
+  } else {
+    if (fast) {
+      s = chunk_sum(r0, rv);
+    } else {
+      for (int c0 = r0; c0 < r1; c0 += PER_NT * RB) {
+        float rt[RB];
+        s += chunk_sum(c0, rt);
+      }
+    }
+    s = block_sum<PER_NT>(s, red);
   }
-  s = block_sum<PER_NT>(s, red);
   const float c = J.weighted ? s * J.Nbar * gp(J.invNt)[t] : s;   // dL/dS_t with S_t = sum w' R m
   // optional residual-loss gradient wrt w' (valid stocks of period t)
   float rcoef = 0.f, beta = 0.f;
@@ -644,18 +714,6 @@ void launch_job_metrics(const LossJob* jobs, int njobs, hipStream_t st) {
 //   a_i = mean_g W[g,t,i];  s = sum_i |a_i| m_i (fp64);  q_i = s > 1e-8 ? a_i / s : a_i;
 //   port[t] = sum_i q_i R_i m_i,  port_ind[g][t] = sum_i W[g,t,i] R_i m_i   (fp64 sums)
 // The (tiny) Sharpe ratios of these [T] series are taken on the host.
-template <int NT>
-DLAP_DEV double block_sum_d(double v, double* red) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-  __syncthreads();
-  double s = 0.0;
-#pragma unroll
-  for (int i = 0; i < NT / 64; ++i) s += red[i];
-  return s;
-}
 
 __global__ __launch_bounds__(256) void k_ensemble(const float* __restrict__ W, int G, int T, int N,
                                                   const float* __restrict__ R, const float* __restrict__ mask,

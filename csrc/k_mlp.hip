@@ -41,18 +41,6 @@ DLAP_DEV int opaque_zero() {
   asm volatile("" : "+s"(z));
   return z;
 }
-// v if bit k of the gate word g is set, else +0: a one-bit sign extension (v_bfe_i32) and an
-// AND, no compare, so no lane mask lives in SGPRs.
-DLAP_DEV float gate_and(float v, uint32_t g, int k) {
-  const int m = (int)(g << (31 - k)) >> 31;
-  return __int_as_float(__float_as_int(v) & m);
-}
-// Hide a gate word's value from the optimiser: the backward's masks are then rebuilt from it
-// instead of the forward's compare results being kept alive (as SGPR lane masks) across the tile.
-DLAP_DEV uint32_t opaque_gate(uint32_t g) {
-  asm volatile("" : "+v"(g));
-  return g;
-}
 
 // Waves per SIMD the forward tower kernel is compiled for (its VGPR budget = 512 / this).
 #ifndef DLAP_FWD_WPS
@@ -107,6 +95,64 @@ struct RowInfo {
   int t[2], i[2];
 };
 
+// ---- dropout keep words --------------------------------------------------------------------
+// k_dropmask pre-generates the SDF tower's words of the phase-1/3 training steps (parity
+// halves of J.gbits); every other train-mode tower (phase-2 SDF, moment hidden layers, module
+// API) hashes the same words in-kernel. Layer ids: SDF hidden layer j -> j, moment hidden
+// layer j -> 16 + j (`dropout_key`).
+struct DropCtx {
+  bool on; uint32_t thr16, seed, step;
+};
+// (the dropout step counter is loaded by the caller at kernel start, ahead of the staging)
+DLAP_DEV uint32_t load_step(const MlpJob& J) { return J.step ? (uint32_t)*gp(J.step) : 0u; }
+DLAP_DEV DropCtx drop_ctx(const MlpJob& J, const MlpDims& D, uint32_t step) {
+  DropCtx dc;
+  dc.on = J.train && D.dropout > 0.f;
+  dc.thr16 = (uint32_t)(D.dropout * 65536.f + 0.5f);
+  dc.seed = J.seed;
+  dc.step = step;
+  return dc;
+}
+template <int UB>
+DLAP_DEV uint32_t hash_keep(const DropCtx& dc, int layer_id, const RowInfo& ri) {
+  const uint32_t rm[2] = {row_mix((uint32_t)ri.dense[0]), row_mix((uint32_t)ri.dense[1])};
+  return keep_word<UB>(dropout_key(dc.seed, dc.step, layer_id), rm, dc.thr16, lane_id() >> 4);
+}
+
+// ---- activations ---------------------------------------------------------------------------
+// ReLU (+ keep mask) of a layer's pre-activations straight into the packed operand fragments of
+// the next MFMA. The dropout scale 1/(1-p) is folded into the next layer's packed weights (the
+// train blob, k_pack), so the activations are ReLU(z) * keep exactly.
+template <class P, int UB, bool DROP>
+DLAP_DEV void act_tile(const f32x4 (&a)[2][UB], uint32_t kw, typename P::Frag (&pf)[2][(UB + 1) / 2]) {
+  if constexpr (UB == 1) {
+    pf[0][0] = P::template act<0, DROP>(a[0][0], zero4(), kw);
+    pf[1][0] = P::template act<8, DROP>(a[1][0], zero4(), kw);
+  } else {
+    pf[0][0] = P::template act<0, DROP>(a[0][0], a[0][1], kw);
+    pf[1][0] = P::template act<8, DROP>(a[1][0], a[1][1], kw);
+    if constexpr (UB == 4) {
+      pf[0][1] = P::template act<4, DROP>(a[0][2], a[0][3], kw);
+      pf[1][1] = P::template act<12, DROP>(a[1][2], a[1][3], kw);
+    }
+  }
+}
+template <class P, int UB>
+DLAP_DEV void act_tile_rt(const f32x4 (&a)[2][UB], bool drop, uint32_t kw, typename P::Frag (&pf)[2][(UB + 1) / 2]) {
+  if (drop) act_tile<P, UB, true>(a, kw, pf);
+  else act_tile<P, UB, false>(a, kw, pf);
+}
+// d (fp32 C blocks) gated by the recomputed activations act (ReLU' * keep), packed
+template <class P, int UB>
+DLAP_DEV void gate_tile(const f32x4 (&d)[2][UB], const typename P::Frag (&act)[2][(UB + 1) / 2],
+                        typename P::Frag (&out)[2][(UB + 1) / 2]) {
+#pragma unroll
+  for (int b = 0; b < 2; ++b)
+#pragma unroll
+    for (int s = 0; s < (UB + 1) / 2; ++s)
+      out[b][s] = P::gate(d[b][2 * s], (2 * s + 1 < UB) ? d[b][(2 * s + 1) % UB] : zero4(), act[b][s]);
+}
+
 // ---- wide path (ZIN instantiations): layer 0 comes from k_proj0 (k_wide.hip) ----------
 // z chunk (tile, c) of lane l is exactly the layer-0 accumulator a[b][u] of that lane, so a
 // tile is 8 + 2*WMB lane-linear 16-byte loads instead of the X row fragments.
@@ -155,18 +201,18 @@ DLAP_DEV RowInfo finish_ztile(const MlpJob& J, int tile, ZTile<WMB>& in) {
   return ri;
 }
 
-// SDF layer 0 of the wide path: a = z + W0[:, F:F+Dm] . pp_t in fp32 (the bias is added by the
-// ReLU step, as in the fused path). W0's per-period columns are the aux block a_pp [Dm][64].
+// SDF layer 0 of the wide path: a = z + W0[:, F:F+Dm] . pp_t + b0 in fp32. W0's per-period
+// columns are the aux block a_pp [Dm][64]; pp rows have stride `pst`.
 template <typename PP>
-DLAP_DEV void zin_sdf0(const f32x4 (&zs)[2][4], const RowInfo& ri, PP pp, const float* aux,
+DLAP_DEV void zin_sdf0(const f32x4 (&zs)[2][4], const RowInfo& ri, PP pp, int pst, const float* aux,
                        const MlpDims& D, f32x4 (&a)[2][4]) {
   const int q = lane_id() >> 4;
 #pragma unroll
   for (int b = 0; b < 2; ++b)
 #pragma unroll
-    for (int u = 0; u < 4; ++u) a[b][u] = zs[b][u];
+    for (int u = 0; u < 4; ++u) a[b][u] = zs[b][u] + ld4(aux + D.a_sb + 16 * u + 4 * q);
   for (int d = 0; d < D.Dm; ++d) {
-    const float p0 = pp[ri.t[0] * D.Dm + d], p1 = pp[ri.t[1] * D.Dm + d];
+    const float p0 = pp[ri.t[0] * pst + d], p1 = pp[ri.t[1] * pst + d];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const f32x4 w = ld4(aux + D.a_pp + 64 * d + 16 * u + 4 * q);
@@ -199,14 +245,15 @@ DLAP_DEV void issue_tile(const MlpJob& J, int tile, TileIn<P, KS1>& in) {
   }
 }
 
-// Finish a prefetched tile: row info, zero rows beyond R, insert the per-period columns
-// (INS; from the LDS copy staged with the weights when it fits, else from global memory).
+// Finish a prefetched tile: row info, zero rows beyond R, and (INS) the per-period SDF inputs
+// of each row's period written into the panel row's last columns [ppc, ppc + Dm) (zero in
+// HBM): the lane groups whose 8 columns fall there take pp[t][col - ppc .. +7] -- from the LDS
+// copy (row stride ppst, zero-padded) with two 16-byte reads, else from global memory.
 template <class P, int KS1, bool INS = true>
 DLAP_DEV RowInfo finish_tile(const MlpJob& J, const MlpDims& D, int tile, TileIn<P, KS1>& in,
                              typename P::Frag (&xf)[2][KS1], const float* spp = nullptr) {
   RowInfo ri;
   const int l = lane_id(), q = l >> 4;
-  const int s_lo = D.F >> 5, s_hi = (D.F + D.Dm - 1) >> 5;
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
     const int r = tile * 32 + 16 * b + (l & 15);
@@ -218,38 +265,37 @@ DLAP_DEV RowInfo finish_tile(const MlpJob& J, const MlpDims& D, int tile, TileIn
 #pragma unroll
     for (int s = 0; s < KS1; ++s) xf[b][s] = ok ? in.x[b][s] : P::zero();
     if (INS && D.Dm > 0) {
-      // branch-free: every lane loads (clamped index) and selects. The column offset goes through
-      // an opaque zero so the 8 x KS1 lane-range tests are made here, per tile, instead of being
-      // hoisted out of the tile loop as lane masks that pin (and spill) SGPR pairs.
-      const int cbase = 8 * q - D.F + opaque_zero();
-      auto insert = [&](auto pp) {
 #pragma unroll
-        for (int s = 0; s < KS1; ++s) {
-          if (s >= s_lo && s <= s_hi) {                          // wave-uniform
+      for (int s = 0; s < KS1; ++s) {
+        if (32 * s + 32 <= D.ppc) continue;                     // wave-uniform
+        const int c0 = 32 * s + 8 * q - D.ppc;                   // pp column of element 0
+        typename P::Frag f;
+        if (D.pp_lds_floats > 0) {
+          const float* row = spp + ri.t[b] * D.ppst;
+          const int ca = min(max(c0, 0), D.ppst - 4), cb = min(max(c0 + 4, 0), D.ppst - 4);
+          const f32x4 v0 = ld4(row + ca), v1 = ld4(row + cb);
+          f = P::pack(v0, c0 + 4 < D.ppst ? v1 : zero4());
+        } else {
+          const auto row = gp(J.pp) + ri.t[b] * D.Dm;
+          f = P::zero();
 #pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const int col = cbase + 32 * s + j;
-              const float v = pp[min(max(col, 0), D.Dm - 1)];
-              P::set_if(xf[b][s], j, ((unsigned)col < (unsigned)D.Dm) & ok, v);
-            }
-          }
+          for (int j = 0; j < 8; ++j) P::set(f, j, c0 + j < D.Dm ? row[min(max(c0 + j, 0), D.Dm - 1)] : 0.f);
         }
-      };
-      if (D.pp_lds_floats > 0) insert(spp + ri.t[b] * D.Dm);      // LDS: ~100-cycle lookups
-      else insert(gp(J.pp) + ri.t[b] * D.Dm);
+        xf[b][s] = (c0 >= 0 && ok) ? f : xf[b][s];
+      }
     }
     if (!ok) in.dw[b] = 0.f;
   }
   return ri;
 }
 
-// acc[b][u] = W0 . X^T  (UB output blocks)
+// acc[b][u] = W0 . X^T + init[b][u]  (UB output blocks)
 template <class P, int KS1, int UB>
 DLAP_DEV void layer0(const typename P::Frag* lds, int off, const typename P::Frag (&xf)[2][KS1],
-                     f32x4 (&acc)[2][UB]) {
+                     const f32x4 (&init)[2][UB], f32x4 (&acc)[2][UB]) {
 #pragma unroll
   for (int u = 0; u < UB; ++u) {
-    f32x4 c0 = zero4(), c1 = zero4();
+    f32x4 c0 = init[0][u], c1 = init[1][u];
 #pragma unroll
     for (int s = 0; s < KS1; ++s) {
       const typename P::Frag w = ldsf(lds, off + u * KS1 + s);
@@ -260,13 +306,15 @@ DLAP_DEV void layer0(const typename P::Frag* lds, int off, const typename P::Fra
   }
 }
 
-// acc = W . prev^T, prev as KS packed fragments per row block, UB output blocks.
+// acc = W . prev^T (+ the bias row `bias` of the layer, if given: the accumulators start from
+// it), prev as KS packed fragments per row block, UB output blocks.
 template <class P, int UB, int KS>
 DLAP_DEV void layer_chain(const typename P::Frag* lds, int off, const typename P::Frag (&pf)[2][KS],
-                          f32x4 (&acc)[2][UB]) {
+                          f32x4 (&acc)[2][UB], const float* bias = nullptr) {
+  const int q = lane_id() >> 4;
 #pragma unroll
   for (int u = 0; u < UB; ++u) {
-    f32x4 c0 = zero4(), c1 = zero4();
+    f32x4 c0 = bias ? ld4(bias + 16 * u + 4 * q) : zero4(), c1 = c0;
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const typename P::Frag w = ldsf(lds, off + u * KS + s);
@@ -277,99 +325,36 @@ DLAP_DEV void layer_chain(const typename P::Frag* lds, int off, const typename P
   }
 }
 
+template <int UB>
+DLAP_DEV void bias_init(const float* bias, f32x4 (&init)[2][UB]) {
+  const int q = lane_id() >> 4;
+#pragma unroll
+  for (int u = 0; u < UB; ++u) init[0][u] = init[1][u] = ld4(bias + 16 * u + 4 * q);
+}
+
 template <class P, int UB>
 DLAP_DEV void pack_blocks(const f32x4 (&a)[2][UB], typename P::Frag (&pf)[2][(UB + 1) / 2]) {
 #pragma unroll
   for (int b = 0; b < 2; ++b)
 #pragma unroll
     for (int s = 0; s < (UB + 1) / 2; ++s)
-      pf[b][s] = P::pack(a[b][2 * s], (2 * s + 1 < UB) ? a[b][2 * s + 1] : zero4());
+      pf[b][s] = P::pack(a[b][2 * s], (2 * s + 1 < UB) ? a[b][(2 * s + 1) % UB] : zero4());
 }
 
 // Natural-k fragment of the per-period SDF inputs of k-step s for a row of period t (lane:
-// columns 32 s + 8 q + j of pp[t], zero beyond Dm), bf16 as the fused path inserts them: the
-// wide path's operand for the W0[:, F:F+Dm] weight-gradient tile (transposed by x_rows_k).
+// columns 32 s + 8 q + j of pp[t], zero beyond Dm; row stride pst), bf16 as the fused path
+// inserts them: the wide path's operand for the W0[:, F:F+Dm] weight-gradient tile
+// (transposed by x_rows_k).
 template <class P, typename PP>
-DLAP_DEV typename P::Frag pp_xfrag(PP pp, int t, int s, const MlpDims& D) {
+DLAP_DEV typename P::Frag pp_xfrag(PP pp, int pst, int t, int s, const MlpDims& D) {
   const int q = lane_id() >> 4;
   typename P::Frag f = P::zero();
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     const int col = 32 * s + 8 * q + j;
-    P::set(f, j, col < D.Dm ? pp[t * D.Dm + col] : 0.f);
+    P::set(f, j, col < D.Dm ? pp[t * pst + col] : 0.f);
   }
   return f;
-}
-
-struct DropCtx {
-  bool on; uint32_t thr16; float scale; uint32_t seed, step;
-};
-
-// bias + ReLU + dropout in place; gate bit (u*4+r) per row block. Branch-free: one hash
-// per unit pair gives both keep decisions (see dropout_pair). ``getb(b, u)`` returns the
-// f32x4 bias of units 16u + 4q .. +3 for row block b.
-template <int UB, typename GetB>
-DLAP_DEV void relu_dropout_g(f32x4 (&a)[2][UB], GetB getb, const DropCtx& dc, int layer_id,
-                             const RowInfo& ri, uint32_t (&gate)[2]) {
-  const int q = lane_id() >> 4;
-  const uint32_t key = dropout_key(dc.seed, dc.step, layer_id);
-#pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    const uint32_t row = (uint32_t)ri.dense[b];
-    const uint32_t rowmix = row * 0xcc9e2d51u ^ (row >> 16);
-    uint32_t g = 0;
-#pragma unroll
-    for (int u = 0; u < UB; ++u) {
-      const f32x4 bb = getb(b, u);
-      uint32_t keep = 0xFu;
-      if (dc.on) {   // wave-uniform
-        const uint32_t pair0 = (uint32_t)(8 * u + 2 * q);
-        const uint32_t h0 = dropout_pair(key, rowmix, pair0);
-        const uint32_t h1 = dropout_pair(key, rowmix, pair0 + 1);
-        keep = ((h0 & 0xFFFFu) >= dc.thr16 ? 1u : 0u) | ((h0 >> 16) >= dc.thr16 ? 2u : 0u) |
-               ((h1 & 0xFFFFu) >= dc.thr16 ? 4u : 0u) | ((h1 >> 16) >= dc.thr16 ? 8u : 0u);
-      }
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float z = a[b][u][r] + bb[r];
-        const bool on = (z > 0.f) & (((keep >> r) & 1u) != 0u);
-        a[b][u][r] = on ? z * dc.scale : 0.f;
-        g |= (on ? 1u : 0u) << (u * 4 + r);
-      }
-    }
-    gate[b] = g;
-  }
-}
-
-template <int UB, typename BP>
-DLAP_DEV void relu_dropout(f32x4 (&a)[2][UB], BP bias0, BP bias1,
-                           const DropCtx& dc, int layer_id, const RowInfo& ri, uint32_t (&gate)[2]) {
-  const int q = lane_id() >> 4;
-  relu_dropout_g<UB>(a, [&](int b, int u) { return ld4((b ? bias1 : bias0) + 16 * u + 4 * q); },
-                     dc, layer_id, ri, gate);
-}
-
-// bias + ReLU + dropout from pre-generated keep bits (k_dropmask): gate = (z > 0) & keep.
-template <int UB, typename BP>
-DLAP_DEV void relu_keep(f32x4 (&a)[2][UB], BP bias, float scale, uint32_t kw, uint32_t (&gate)[2]) {
-  const int q = lane_id() >> 4;
-#pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    const uint32_t keep = b ? (kw >> 16) : (kw & 0xFFFFu);
-    uint32_t g = 0;
-#pragma unroll
-    for (int u = 0; u < UB; ++u) {
-      const f32x4 bb = ld4(bias + 16 * u + 4 * q);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float z = a[b][u][r] + bb[r];
-        const bool on = (z > 0.f) & (((keep >> (u * 4 + r)) & 1u) != 0u);
-        a[b][u][r] = on ? z * scale : 0.f;
-        g |= (on ? 1u : 0u) << (u * 4 + r);
-      }
-    }
-    gate[b] = g;
-  }
 }
 
 // Per-period moment layer-0 bias of a tile's rows (abias[t][16u + 4q .. +3]), loaded one tile
@@ -394,40 +379,10 @@ DLAP_DEV void issue_rowti(const MlpJob& J, int tile, int2 (&ti)[2]) {
   for (int b = 0; b < 2; ++b) ti[b] = gp(J.rowti)[min(tile * 32 + 16 * b + (l & 15), J.R - 1)];
 }
 
-// bias + ReLU + dropout from gate bits stored by the training forward (bit u*4+r per row
-// block): bitwise the same activations as relu_dropout, without re-hashing the mask.
-template <int UB, typename BP>
-DLAP_DEV void relu_gates(f32x4 (&a)[2][UB], BP bias0, BP bias1, float scale,
-                         const uint32_t (&gate)[2]) {
-  const int q = lane_id() >> 4;
-#pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    const BP bp = b ? bias1 : bias0;
-#pragma unroll
-    for (int u = 0; u < UB; ++u) {
-      const f32x4 bb = ld4(bp + 16 * u + 4 * q);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) a[b][u][r] = gate_and((a[b][u][r] + bb[r]) * scale, gate[b], u * 4 + r);
-    }
-  }
-}
-
-DLAP_DEV uint32_t gate_word(const uint32_t (&g)[2]) { return g[0] | (g[1] << 16); }
-
 DLAP_DEV float reduce_q(float v) {  // sum over the 4 lane groups that share l & 15
   v += __shfl_xor(v, 16, 64);
   v += __shfl_xor(v, 32, 64);
   return v;
-}
-
-DLAP_DEV DropCtx drop_ctx(const MlpJob& J, const MlpDims& D) {
-  DropCtx dc;
-  dc.on = J.train && D.dropout > 0.f;
-  dc.thr16 = (uint32_t)(D.dropout * 65536.f + 0.5f);
-  dc.scale = dc.on ? 1.f / (1.f - D.dropout) : 1.f;
-  dc.seed = J.seed;
-  dc.step = J.step ? (uint32_t)*gp(J.step) : 0u;
-  return dc;
 }
 
 // LDS image of the tower kernels: blob fragments (1 KiB bf16 / 2 KiB fp32 each), aux floats,
@@ -444,112 +399,131 @@ DLAP_DEV float* aux_lds_ptr(char* smem, const MlpDims& D) {
 DLAP_DEV float* pp_lds_ptr(char* smem, const MlpDims& D) {
   return reinterpret_cast<float*>(smem + blob_bytes_of(D) + (size_t)((D.aux_floats + 3) & ~3) * 4);
 }
+// Stage the blob + aux of the job (its train or evaluation copy) and the per-period inputs
+// (zero-padded to the row stride ppst, so a lane reads its 4 / 8 columns with 16-byte loads).
+// The blob (lane-linear 1 / 2 KiB fragments) goes global -> LDS by LDS-DMA
+// (global_load_lds_dwordx4: no VGPRs, every piece in flight at once); aux and pp by plain loads
+// issued in batches before their LDS stores. One memory round trip for the whole prologue
+// instead of one per staging-loop iteration.
 template <class P>
 DLAP_DEV void stage_weights(const MlpJob& J, const MlpDims& D, typename P::Frag* lds, float* aux,
                             float* spp = nullptr) {
-  const auto blob = gp(reinterpret_cast<const typename P::Frag*>(J.blob));
-  for (int i = threadIdx.x; i < D.blob_frags * 64; i += blockDim.x) lds[i] = blob[i];
-  for (int i = threadIdx.x; i < D.aux_floats; i += blockDim.x) aux[i] = gp(J.aux)[i];
-  if (spp && D.pp_lds_floats > 0 && D.Dm > 0)
-    for (int i = threadIdx.x; i < J.T * D.Dm; i += blockDim.x) spp[i] = gp(J.pp)[i];
+  const int n16 = D.blob_frags * 64 * (P::kF32 ? 2 : 1);            // 16-byte pieces
+  const auto src = reinterpret_cast<const DLAP_GLOBAL int4*>(gp(J.blob));
+  int4* l16 = reinterpret_cast<int4*>(lds);
+  const int lane = threadIdx.x & 63;
+  for (int i = threadIdx.x; i < n16; i += blockDim.x)
+    __builtin_amdgcn_global_load_lds(src + i, (__attribute__((address_space(3))) void*)(l16 + (i - lane)), 16, 0, 0);
+  constexpr int B = 8;
+  const auto ga = gp(J.aux);
+  for (int i0 = threadIdx.x; i0 < D.aux_floats; i0 += B * blockDim.x) {
+    float v[B];
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+      const int i = i0 + k * blockDim.x;
+      v[k] = ga[i < D.aux_floats ? i : 0];
+    }
+#pragma unroll
+    for (int k = 0; k < B; ++k) {
+      const int i = i0 + k * blockDim.x;
+      if (i < D.aux_floats) aux[i] = v[k];
+    }
+  }
+  if (spp && D.pp_lds_floats > 0 && D.Dm > 0) {
+    const int n = J.T * D.ppst;
+    const auto gpp = gp(J.pp);
+    for (int i0 = threadIdx.x; i0 < n; i0 += B * blockDim.x) {
+      float v[B];
+#pragma unroll
+      for (int k = 0; k < B; ++k) {
+        const int i = i0 + k * blockDim.x;
+        const int t = i / D.ppst, c = i - t * D.ppst;
+        v[k] = (i < n && c < D.Dm) ? gpp[t * D.Dm + c] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < B; ++k) {
+        const int i = i0 + k * blockDim.x;
+        if (i < n) spp[i] = v[k];
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");     // the LDS-DMA pieces have landed
   __syncthreads();
 }
 
 // SDF tower forward on one tile: the raw (pre-normalisation) weight of each row block.
-// gout: gate words of the tile (train). With keep words (kw, pre-generated by k_dropmask) the
-// dropout decisions are read instead of hashed; the gates overwrite the keep words in place.
-// layer0_fn(a) fills the layer-0 accumulators (fused: MFMA over the X tile; wide: from z).
-template <class P, typename L0>
+// kw[j]: keep word of hidden layer j (ignored unless DROP). layer0_fn(a) fills the layer-0
+// pre-activations including the bias (fused: MFMA over the X tile; wide: from z).
+// Output layer on the matrix cores: the 2 s_wo fragments hold the output row as row 0 of an
+// A operand, so C[0][row] = wo . act + bo lands on the lanes of lane group 0.
+template <class P, bool DROP, typename L0>
 DLAP_DEV void sdf_forward_tile(const typename P::Frag* lds, const float* aux, const MlpDims& D,
-                               const DropCtx& dc, const RowInfo& ri, L0&& layer0_fn,
-                               DLAP_GLOBAL uint32_t* gout, const uint32_t* kw, float (&w)[2]) {
+                               const uint32_t (&kw)[4], L0&& layer0_fn, float (&w)[2]) {
   f32x4 a[2][4];
   typename P::Frag pf[2][2];
-  uint32_t gate[2];
   layer0_fn(a);
-  if (kw) relu_keep<4>(a, aux + D.a_sb, dc.scale, kw[0], gate);
-  else relu_dropout<4>(a, aux + D.a_sb, aux + D.a_sb, dc, 0, ri, gate);
-  if (gout) gout[0] = gate_word(gate);
+  act_tile<P, 4, DROP>(a, kw[0], pf);
   // fully unrolled to the engine's 4-layer limit so kw[j] is a register, not scratch
 #pragma unroll
   for (int j = 1; j < 4; ++j) {
     if (j >= D.nl_sdf) break;
-    pack_blocks<P, 4>(a, pf);
-    layer_chain<P, 4, 2>(lds, D.s_fwd + (j - 1) * 8, pf, a);
-    if (kw) relu_keep<4>(a, aux + D.a_sb + 64 * j, dc.scale, kw[j], gate);
-    else relu_dropout<4>(a, aux + D.a_sb + 64 * j, aux + D.a_sb + 64 * j, dc, j, ri, gate);
-    if (gout) gout[64 * j] = gate_word(gate);
+    layer_chain<P, 4, 2>(lds, D.s_fwd + (j - 1) * 8, pf, a, aux + D.a_sb + 64 * j);
+    act_tile<P, 4, DROP>(a, kw[j], pf);
   }
   const int q = lane_id() >> 4;
-  const float* wo = aux + D.a_wo;
   const float bo = aux[D.a_bo];
+  f32x4 c0 = f32x4{q == 0 ? bo : 0.f, 0.f, 0.f, 0.f}, c1 = c0;
 #pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    float s = 0.f;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const f32x4 ww = *reinterpret_cast<const f32x4*>(wo + 16 * u + 4 * q);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) s += a[b][u][r] * ww[r];
-    }
-    w[b] = reduce_q(s) + bo;
+  for (int s = 0; s < 2; ++s) {
+    const typename P::Frag wf = ldsf(lds, D.s_wo + s);
+    c0 = P::mma(wf, pf[0][s], c0);
+    c1 = P::mma(wf, pf[1][s], c1);
   }
+  w[0] = c0[0];
+  w[1] = c1[0];
 }
 
-// Moment tower forward on one tile: writes the K tanh outputs of every valid row.
+// Moment tower forward on one tile: writes the K tanh outputs of every valid row. layer0_fn
+// fills the layer-0 pre-activations including the per-period bias.
 template <class P, int WMB, typename L0>
 DLAP_DEV void mom_forward_tile(const typename P::Frag* lds, const float* aux, const MlpDims& D,
-                               const MlpJob& J, const DropCtx& dc, const RowInfo& ri,
-                               L0&& layer0_fn, DLAP_GLOBAL uint32_t* gout,
-                               const AbPre<WMB>& ab) {
+                               const MlpJob& J, const DropCtx& dc, const RowInfo& ri, L0&& layer0_fn) {
   constexpr int KSM = (WMB + 1) / 2;
   f32x4 a[2][WMB];
   typename P::Frag pf[2][KSM];
-  uint32_t gate[2];
   const int q = lane_id() >> 4;
   layer0_fn(a);
-  // layer-0 bias is per period (prefetched), later biases are staged (LDS)
   for (int j = 0; j + 1 < D.nl_mom; ++j) {
-    if (j == 0) relu_dropout_g<WMB>(a, [&](int b, int u) { return ab.v[b][u]; }, dc, 16 + j, ri, gate);
-    else relu_dropout<WMB>(a, aux + D.a_mb + 64 * j, aux + D.a_mb + 64 * j, dc, 16 + j, ri, gate);
-    if (gout) gout[64 * j] = gate_word(gate);
-    pack_blocks<P, WMB>(a, pf);
-    layer_chain<P, WMB, KSM>(lds, D.m_fwd + j * WMB * KSM, pf, a);
+    const uint32_t kw = dc.on ? hash_keep<WMB>(dc, 16 + j, ri) : 0xFFFFFFFFu;
+    act_tile_rt<P, WMB>(a, dc.on, kw, pf);
+    layer_chain<P, WMB, KSM>(lds, D.m_fwd + j * WMB * KSM, pf, a, aux + D.a_mb + 64 * (j + 1));
   }
-  auto emit = [&](auto pb0, auto pb1) {
 #pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      if (ri.dense[b] < 0) continue;
-      const auto bp = b ? pb1 : pb0;
-      const auto dst = gp(J.h_out) + (size_t)ri.dense[b] * D.K;
+  for (int b = 0; b < 2; ++b) {
+    if (ri.dense[b] < 0) continue;
+    const auto dst = gp(J.h_out) + (size_t)ri.dense[b] * D.K;
 #pragma unroll
-      for (int u = 0; u < WMB; ++u)
+    for (int u = 0; u < WMB; ++u)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int k = 16 * u + 4 * q + r;
-          if (k < D.K) dst[k] = tanhf(a[b][u][r] + bp[k]);
-        }
-    }
-  };
-  if (D.nl_mom > 1) {
-    emit(aux + D.a_mb + 64 * (D.nl_mom - 1), aux + D.a_mb + 64 * (D.nl_mom - 1));
-  } else {                                   // single layer: its bias is the per-period one
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-      if (ri.dense[b] < 0) continue;
-      const auto dst = gp(J.h_out) + (size_t)ri.dense[b] * D.K;
-#pragma unroll
-      for (int u = 0; u < WMB; ++u)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int k = 16 * u + 4 * q + r;
-          if (k < D.K) dst[k] = tanhf(a[b][u][r] + ab.v[b][u][r]);
-        }
-    }
+      for (int r = 0; r < 4; ++r) {
+        const int k = 16 * u + 4 * q + r;
+        if (k < D.K) dst[k] = tanhf(a[b][u][r]);
+      }
   }
 }
 
 // ============================== forward ==================================================
+// Keep words of the SDF hidden layers for one tile: pre-generated (pre), hashed, or all kept.
+DLAP_DEV void sdf_keep_words(bool pre, const uint32_t (&kw_pre)[4], const DropCtx& dc, const RowInfo& ri,
+                             int nl, uint32_t (&kw)[4]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (pre) kw[j] = kw_pre[j];
+    else if (dc.on && j < nl) kw[j] = hash_keep<4>(dc, j, ri);
+    else kw[j] = 0xFFFFFFFFu;
+  }
+}
+
 template <class P, int KS1, int WMB, bool ZIN>
 __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __restrict__ jobs, MlpDims D) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -569,29 +543,39 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __r
   AbPre<WMB> ab_cur, ab_nxt;
   int2 ti_ahead[2];                      // periods of the tile after next (for the abias prefetch)
   const bool mom = J.do_mom;
+  // prologue: the step counter, the first tile's panel rows and keep words (both parity
+  // halves: the step is not known yet) are all in flight with the weight staging
+  const uint32_t stp = load_step(J);
+  const bool pre = J.gbits && J.train && D.dropout > 0.f;   // keep words pre-generated (k_dropmask)
+  constexpr int KWM = 4;                           // max SDF hidden layers (engine limit)
+  uint32_t kw_cur[KWM], kw_nxt[KWM], kw_alt[KWM];
+  auto issue_kw = [&](const DLAP_GLOBAL uint32_t* base, int t, uint32_t (&kw)[KWM], int nls) {
+#pragma unroll
+    for (int j = 0; j < KWM; ++j)
+      kw[j] = j < nls ? base[((size_t)t * nls + j) * 64 + lane] : 0xFFFFFFFFu;
+  };
   if (tile < ntiles) {
     if constexpr (ZIN) issue_ztile<WMB, false>(J, D, tile, zcur, J.do_sdf, mom);
     else issue_tile<P, KS1, false>(J, tile, cur);            // in flight during the staging
     if (mom && tile + stride < ntiles) issue_rowti(J, tile + stride, ti_ahead);
+    if (pre) {
+      issue_kw(gp(J.gbits), tile, kw_cur, D.nl_sdf);
+      issue_kw(gp(J.gbits) + J.gb_half, tile, kw_alt, D.nl_sdf);
+    }
   }
   stage_weights<P>(J, D, lds, aux, spp);
   MLP_TS(1);
-  const DropCtx dc = drop_ctx(J, D);
+  const DropCtx dc = drop_ctx(J, D, stp);
+  const auto gbase = pre ? gp(J.gbits) + (size_t)(dc.step & 1u) * J.gb_half : nullptr;
+  if (pre && (dc.step & 1u)) {
+#pragma unroll
+    for (int j = 0; j < KWM; ++j) kw_cur[j] = kw_alt[j];
+  }
   if (mom && tile < ntiles) {
     if constexpr (ZIN) issue_abias<WMB>(J, zcur.ti, ab_cur);
     else issue_abias<WMB>(J, cur.ti, ab_cur);
   }
-  // train forward with dropout: keep words of this step's parity half, prefetched with the tile
-  const bool keep = J.gbits && dc.on;
-  const auto gbase = J.gbits ? gp(J.gbits) + (size_t)(dc.step & 1u) * J.gb_half : nullptr;
-  constexpr int KWM = 4;                           // max SDF hidden layers (engine limit)
-  uint32_t kw_cur[KWM], kw_nxt[KWM];
-  auto issue_kw = [&](int t, uint32_t (&kw)[KWM], int nls) {
-#pragma unroll
-    for (int j = 0; j < KWM; ++j)
-      kw[j] = j < nls ? gbase[((size_t)t * nls + j) * 64 + lane] : 0xFFFFFFFFu;
-  };
-  if (keep && tile < ntiles) issue_kw(tile, kw_cur, D.nl_sdf);
+  const int pst = D.pp_lds_floats > 0 ? D.ppst : D.Dm;
   bool first = true;
   for (; tile < ntiles; tile += stride) {
     const int oz = opaque_zero();             // see bwd_sdf_body: no hoisted weight copies
@@ -605,7 +589,7 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __r
     if (tile + stride < ntiles) {
       if constexpr (ZIN) issue_ztile<WMB, false>(J, D, tile + stride, znxt, J.do_sdf, mom);
       else issue_tile<P, KS1, false>(J, tile + stride, nxt);
-      if (keep) issue_kw(tile + stride, kw_nxt, Dt.nl_sdf);
+      if (pre) issue_kw(gbase, tile + stride, kw_nxt, Dt.nl_sdf);
       if (mom) {
         issue_abias<WMB>(J, ti_ahead, ab_nxt);             // periods known since last iteration
         if (tile + 2 * stride < ntiles) issue_rowti(J, tile + 2 * stride, ti_ahead);
@@ -617,16 +601,20 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __r
     else ri = finish_tile<P, KS1>(J, D, tile, cur, xf, spp);
     if (J.do_sdf) {
       float w[2];
-      DLAP_GLOBAL uint32_t* gout = J.gbits ? gbase + (size_t)tile * D.nl_sdf * 64 + lane : nullptr;
+      uint32_t kw[4];
+      sdf_keep_words(pre, kw_cur, dc, ri, Dt.nl_sdf, kw);
       auto l0 = [&](f32x4 (&a)[2][4]) {
         if constexpr (ZIN) {
-          if (D.pp_lds_floats > 0) zin_sdf0(zcur.zs, ri, spp, auxt, D, a);
-          else zin_sdf0(zcur.zs, ri, gp(J.pp), auxt, D, a);
+          if (D.pp_lds_floats > 0) zin_sdf0(zcur.zs, ri, spp, pst, auxt, D, a);
+          else zin_sdf0(zcur.zs, ri, gp(J.pp), pst, auxt, D, a);
         } else {
-          layer0<P, KS1, 4>(ldt, D.s_fwd0, xf, a);
+          f32x4 init[2][4];
+          bias_init<4>(auxt + D.a_sb, init);
+          layer0<P, KS1, 4>(ldt, D.s_fwd0, xf, init, a);
         }
       };
-      sdf_forward_tile<P>(ldt, auxt, Dt, dc, ri, l0, gout, keep ? kw_cur : nullptr, w);
+      if (dc.on) sdf_forward_tile<P, true>(ldt, auxt, Dt, kw, l0, w);
+      else sdf_forward_tile<P, false>(ldt, auxt, Dt, kw, l0, w);
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
         const int r = tile * 32 + 16 * b + (lane & 15);
@@ -634,19 +622,17 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __r
       }
     }
     if (J.do_mom) {
-      DLAP_GLOBAL uint32_t* gout = (J.mgbits && D.nl_mom > 1)
-                           ? gp(J.mgbits) + (size_t)tile * (D.nl_mom - 1) * 64 + lane : nullptr;
       auto l0 = [&](f32x4 (&a)[2][WMB]) {
         if constexpr (ZIN) {
 #pragma unroll
           for (int b = 0; b < 2; ++b)
 #pragma unroll
-            for (int u = 0; u < WMB; ++u) a[b][u] = zcur.zm[b][u];
+            for (int u = 0; u < WMB; ++u) a[b][u] = zcur.zm[b][u] + ab_cur.v[b][u];
         } else {
-          layer0<P, KS1, WMB>(ldt, D.m_fwd0, xf, a);
+          layer0<P, KS1, WMB>(ldt, D.m_fwd0, xf, ab_cur.v, a);
         }
       };
-      mom_forward_tile<P, WMB>(ldt, auxt, Dt, J, dc, ri, l0, gout, ab_cur);
+      mom_forward_tile<P, WMB>(ldt, auxt, Dt, J, dc, ri, l0);
     }
     if constexpr (ZIN) zcur = znxt;
     else cur = nxt;
@@ -666,8 +652,8 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __r
 // one workgroup per CU (the layer-0 fragments take up to (4 + WMB) x KSX KiB of LDS). The
 // next tile's first k-chunk is in flight while the tower runs on the current one.
 // TRAIN: the training forward of the same kind -- dropout from the pre-generated keep words,
-// gate words for the backward, and the layer-0 pre-activations stored to z (SDF blocks; the
-// moment blocks too when J.store_mz, i.e. in phase 2) for the ZIN backward kernels.
+// and the layer-0 pre-activations stored to z (SDF blocks; the moment blocks too when
+// J.store_mz, i.e. in phase 2) for the ZIN backward kernels.
 template <int WMB, bool TRAIN>
 __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict__ jobs, MlpDims D) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -681,15 +667,17 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
   const int KSX = D.KSX, rstride = D.KX >> 3;
   const int u0 = J.do_sdf ? 0 : 4, u1 = J.do_mom ? NU : 4;
   for (int i = threadIdx.x; i < (u1 - u0) * KSX * 64; i += blockDim.x) lds0[i] = gp(J.blob0)[u0 * KSX * 64 + i];
+  const uint32_t stp = load_step(J);
   stage_weights<PrecBF16>(J, D, lds, aux, spp);           // (ends with the barrier)
-  const DropCtx dc = drop_ctx(J, D);
+  const DropCtx dc = drop_ctx(J, D, stp);
   const int ntiles = (J.R + 31) >> 5;
   const int nch = (KSX + 3) >> 2;
   const int stride = gridDim.x * nwaves;
+  const int pst = D.pp_lds_floats > 0 ? D.ppst : D.Dm;
   int tile = blockIdx.x * nwaves + wave;
   if (tile >= ntiles) return;
-  const bool keep = TRAIN && J.gbits && dc.on;
-  const auto gbase = (TRAIN && J.gbits) ? gp(J.gbits) + (size_t)(dc.step & 1u) * J.gb_half : nullptr;
+  const bool pre = TRAIN && J.gbits && dc.on;
+  const auto gbase = pre ? gp(J.gbits) + (size_t)(dc.step & 1u) * J.gb_half : nullptr;
   auto issue = [&](int tl, int ch, bf16x8 (&x)[2][4]) {
 #pragma unroll
     for (int b = 0; b < 2; ++b) {
@@ -743,7 +731,7 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
       }
       int2 tn[2];
       if (more) issue_rowti(J, ntl, tn);
-      uint32_t kw[4];
+      uint32_t kwp[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
       if constexpr (TRAIN) {
         const auto zt = gp(J.z_out) + (size_t)tile * D.zc * 64 + lane;
 #pragma unroll
@@ -755,10 +743,10 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
             for (int u = 0; u < WMB; ++u) zt[(8 + WMB * b + u) * 64] = acc[b][4 + u];
           }
         }
-        if (keep) {
+        if (pre) {
 #pragma unroll
           for (int j = 0; j < 4; ++j)
-            kw[j] = j < D.nl_sdf ? gbase[((size_t)tile * D.nl_sdf + j) * 64 + lane] : 0xFFFFFFFFu;
+            kwp[j] = j < D.nl_sdf ? gbase[((size_t)tile * D.nl_sdf + j) * 64 + lane] : 0xFFFFFFFFu;
         }
       }
       if (J.do_sdf) {
@@ -768,12 +756,14 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
 #pragma unroll
           for (int u = 0; u < 4; ++u) zs[b][u] = acc[b][u];
         auto l0 = [&](f32x4 (&a)[2][4]) {
-          if (D.pp_lds_floats > 0) zin_sdf0(zs, ri, spp, aux, D, a);
-          else zin_sdf0(zs, ri, gp(J.pp), aux, D, a);
+          if (D.pp_lds_floats > 0) zin_sdf0(zs, ri, spp, pst, aux, D, a);
+          else zin_sdf0(zs, ri, gp(J.pp), pst, aux, D, a);
         };
+        uint32_t kw[4];
+        sdf_keep_words(pre, kwp, dc, ri, D.nl_sdf, kw);
         float w[2];
-        DLAP_GLOBAL uint32_t* gout = (TRAIN && J.gbits) ? gbase + (size_t)tile * D.nl_sdf * 64 + lane : nullptr;
-        sdf_forward_tile<PrecBF16>(lds, aux, D, dc, ri, l0, gout, keep ? kw : nullptr, w);
+        if (dc.on) sdf_forward_tile<PrecBF16, true>(lds, aux, D, kw, l0, w);
+        else sdf_forward_tile<PrecBF16, false>(lds, aux, D, kw, l0, w);
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
           const int r = tile * 32 + 16 * b + (lane & 15);
@@ -787,11 +777,9 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
 #pragma unroll
           for (int b = 0; b < 2; ++b)
 #pragma unroll
-            for (int u = 0; u < WMB; ++u) a[b][u] = acc[b][4 + u];
+            for (int u = 0; u < WMB; ++u) a[b][u] = acc[b][4 + u] + ab.v[b][u];
         };
-        DLAP_GLOBAL uint32_t* mgout = (TRAIN && J.mgbits && D.nl_mom > 1)
-                                          ? gp(J.mgbits) + (size_t)tile * (D.nl_mom - 1) * 64 + lane : nullptr;
-        mom_forward_tile<PrecBF16, WMB>(lds, aux, D, J, dc, ri, l0m, mgout, ab);
+        mom_forward_tile<PrecBF16, WMB>(lds, aux, D, J, dc, ri, l0m);
       }
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
@@ -840,6 +828,9 @@ DLAP_DEV void wg_slab_store(const MlpJob& J, const float* red, int slab_stride) 
 }
 
 // SDF backward. NL = number of hidden (MFMA) layers, all 64 wide.
+// The forward of the tile is recomputed from the panel (with this step's keep words, the train
+// blob: dropout scale folded into the weights), the ReLU'/dropout gates come from the recomputed
+// packed activations, and every dz goes straight into packed operand fragments.
 // ZIN (wide path): layer 0 is recomputed from z, its weight gradient is left to k_wgrad0: the
 // kernel stores the layer-0 dz as rows-as-k fragments instead (J.dz_out [tile][4][64]).
 // TLC: the layer of this slice's gradient tile when it is known at compile time (TPS = 1, one
@@ -860,6 +851,7 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
   constexpr int JLO = TLC > 0 ? TLC : 0;        // lowest layer the backward chain reaches
   const Frag selP0 = make_sel<P>(true, 0), selP1 = make_sel<P>(true, 1);
   const Frag selN0 = make_sel<P>(false, 0), selN1 = make_sel<P>(false, 1);
+  const int pst = D.pp_lds_floats > 0 ? D.ppst : D.Dm;
 
   f32x4 dW[TPS][4][4];
 #pragma unroll
@@ -884,17 +876,27 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
   int tile = blockIdx.x * nwaves + wave;
   TileIn<P, KS1> cur, nxt;
   ZTile<1> zcur, znxt;
-  uint32_t gw_cur[NL], gw_nxt[NL];   // gate words of the forward pass, prefetched with the tile
-  const uint32_t stp = J.step ? (uint32_t)*gp(J.step) : 0u;
-  const auto gbase = gp(J.gbits) + (size_t)(stp & 1u) * J.gb_half;
+  // prologue as k_mlp_fwd: step, first tile and its keep words of both parities in flight with
+  // the staging
+  const uint32_t stp = load_step(J);
+  const bool pre = J.gbits && J.train && D.dropout > 0.f;   // keep words of this step (k_dropmask)
+  uint32_t kw_cur[NL], kw_nxt[NL], kw_alt[NL];
   if (tile < ntiles) {
     if constexpr (ZIN) issue_ztile<1, true>(J, D, tile, zcur, true, false);
     else issue_tile<P, KS1, true>(J, tile, cur);
 #pragma unroll
-    for (int j = 0; j < NL; ++j) gw_cur[j] = gbase[((size_t)tile * NL + j) * 64 + lane];
+    for (int j = 0; j < NL; ++j) {
+      kw_cur[j] = pre ? gp(J.gbits)[((size_t)tile * NL + j) * 64 + lane] : 0xFFFFFFFFu;
+      kw_alt[j] = pre ? gp(J.gbits)[J.gb_half + ((size_t)tile * NL + j) * 64 + lane] : 0xFFFFFFFFu;
+    }
   }
   stage_weights<P>(J, D, lds, aux, spp);       // first tile's loads are already in flight
-  const DropCtx dc = drop_ctx(J, D);
+  const DropCtx dc = drop_ctx(J, D, stp);
+  const auto gbase = pre ? gp(J.gbits) + (size_t)(dc.step & 1u) * J.gb_half : nullptr;
+  if (dc.step & 1u) {
+#pragma unroll
+    for (int j = 0; j < NL; ++j) kw_cur[j] = kw_alt[j];
+  }
   for (; tile < ntiles; tile += stride) {
     // LDS base laundered per tile: keeps the compiler from hoisting every weight fragment and
     // bias of the staged blob out of the loop into registers (~150 VGPRs at this depth)
@@ -905,55 +907,64 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
       if constexpr (ZIN) issue_ztile<1, true>(J, D, tile + stride, znxt, true, false);
       else issue_tile<P, KS1, true>(J, tile + stride, nxt);
 #pragma unroll
-      for (int j = 0; j < NL; ++j) gw_nxt[j] = gbase[((size_t)(tile + stride) * NL + j) * 64 + lane];
+      for (int j = 0; j < NL; ++j)
+        kw_nxt[j] = pre ? gbase[((size_t)(tile + stride) * NL + j) * 64 + lane] : 0xFFFFFFFFu;
     }
     Frag xf[2][KS1];
     RowInfo ri;
     if constexpr (ZIN) ri = finish_ztile<1>(J, tile, zcur);
     else ri = finish_tile<P, KS1>(J, D, tile, cur, xf, spp);
-    // ---- forward recompute from the stored gates, keep packed activations ----
+    uint32_t kw[NL];
+#pragma unroll
+    for (int j = 0; j < NL; ++j) kw[j] = (pre || !dc.on) ? kw_cur[j] : hash_keep<4>(dc, j, ri);
+    // ---- forward recompute: packed activations of every hidden layer ----
     Frag act[NL][2][2];
-    uint32_t gates[NL][2];
     f32x4 a[2][4];
     if constexpr (ZIN) {
-      if (D.pp_lds_floats > 0) zin_sdf0(zcur.zs, ri, spp, auxt, D, a);
-      else zin_sdf0(zcur.zs, ri, gp(J.pp), auxt, D, a);
+      if (D.pp_lds_floats > 0) zin_sdf0(zcur.zs, ri, spp, pst, auxt, D, a);
+      else zin_sdf0(zcur.zs, ri, gp(J.pp), pst, auxt, D, a);
     } else {
-      layer0<P, KS1, 4>(ldt, D.s_fwd0, xf, a);
+      f32x4 init[2][4];
+      bias_init<4>(auxt + D.a_sb, init);
+      layer0<P, KS1, 4>(ldt, D.s_fwd0, xf, init, a);
     }
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
-      if (j > 0) layer_chain<P, 4, 2>(ldt, D.s_fwd + (j - 1) * 8, act[j - 1], a);
-      gates[j][0] = gw_cur[j] & 0xFFFFu;
-      gates[j][1] = gw_cur[j] >> 16;
-      relu_gates<4>(a, auxt + D.a_sb + 64 * j, auxt + D.a_sb + 64 * j, dc.scale, gates[j]);
-      pack_blocks<P, 4>(a, act[j]);
+      if (j > 0) layer_chain<P, 4, 2>(ldt, D.s_fwd + (j - 1) * 8, act[j - 1], a, auxt + D.a_sb + 64 * j);
+      act_tile_rt<P, 4>(a, dc.on, kw[j], act[j]);
     }
-#pragma unroll
-    for (int j = 0; j < NL; ++j) { gates[j][0] = opaque_gate(gates[j][0]); gates[j][1] = opaque_gate(gates[j][1]); }
-    // ---- output layer: w = wo . a_last + bo ----
+    // ---- output layer: w = wo' . act + bo (wo' = wo / (1 - p): train aux) ----
     float dwr[2];
     if constexpr (ZIN) { dwr[0] = zcur.dw[0]; dwr[1] = zcur.dw[1]; }
     else { dwr[0] = cur.dw[0]; dwr[1] = cur.dw[1]; }
-    f32x4 dz[2][4];
-    const float* wo = auxt + D.a_wo;
+    Frag dzf[2][2];
+    {
+      const float* wo = auxt + D.a_wo;
+      f32x4 t[2][4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const f32x4 ww = *reinterpret_cast<const f32x4*>(wo + 16 * u + 4 * q);
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        if (s0) gwo[u] += dwr[b] * a[b][u];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dz[b][u][r] = gate_and(dwr[b] * ww[r] * dc.scale, gates[NL - 1][b], u * 4 + r);
+      for (int u = 0; u < 4; ++u) {
+        const f32x4 ww = ld4(wo + 16 * u + 4 * q);
+        t[0][u] = dwr[0] * ww;
+        t[1][u] = dwr[1] * ww;
       }
+      gate_tile<P, 4>(t, act[NL - 1], dzf);
     }
-    if (s0 && q == 0) gbo += dwr[0] + dwr[1];
+    if (s0) {
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          f32x4 lo, hi;
+          P::unpack(act[NL - 1][b][s], lo, hi);
+          gwo[2 * s] += dwr[b] * lo;
+          gwo[2 * s + 1] += dwr[b] * hi;
+        }
+      if (q == 0) gbo += dwr[0] + dwr[1];
+    }
     // ---- backward chain ----
 #pragma unroll
     for (int j = NL - 1; j >= 0; --j) {
       if (j < JLO) break;
-      Frag dzf[2][2];
-      pack_blocks<P, 4>(dz, dzf);
       Frag dzN[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) to_rows_k<P, 4>(dzf, u, selP0, selP1, dzN[u]);
@@ -987,9 +998,9 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
                 if (16 * blk >= D.Dm) continue;             // wave-uniform: no columns here
                 Frag x0, x1;
                 if (D.pp_lds_floats > 0) {
-                  x0 = pp_xfrag<P>(spp, ri.t[0], blk >> 1, D); x1 = pp_xfrag<P>(spp, ri.t[1], blk >> 1, D);
+                  x0 = pp_xfrag<P>(spp, pst, ri.t[0], blk >> 1, D); x1 = pp_xfrag<P>(spp, pst, ri.t[1], blk >> 1, D);
                 } else {
-                  x0 = pp_xfrag<P>(gp(J.pp), ri.t[0], blk >> 1, D); x1 = pp_xfrag<P>(gp(J.pp), ri.t[1], blk >> 1, D);
+                  x0 = pp_xfrag<P>(gp(J.pp), pst, ri.t[0], blk >> 1, D); x1 = pp_xfrag<P>(gp(J.pp), pst, ri.t[1], blk >> 1, D);
                 }
                 x_rows_k<P>(x0, x1, blk, selN0, selN1, aN);
               }
@@ -1004,13 +1015,7 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
       if (j > JLO) {
         f32x4 da[2][4];
         layer_chain<P, 4, 2>(ldt, D.s_bwd + (j - 1) * 8, dzf, da);
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              dz[b][u][r] = gate_and(da[b][u][r] * dc.scale, gates[j > 0 ? j - 1 : 0][b], u * 4 + r);
+        gate_tile<P, 4>(da, act[j > 0 ? j - 1 : 0], dzf);
       } else if (j == 0 && D.nrnn > 0 && s0) {
         // dL/d(per-period input d) per row = sum_out W0[out][F + d] * dz0[out][row]: one MFMA
         // chain per 16 inputs with the packed W0[:, F:F+Dm]^T fragments
@@ -1038,7 +1043,7 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
     if constexpr (ZIN) zcur = znxt;
     else cur = nxt;
 #pragma unroll
-    for (int j = 0; j < NL; ++j) gw_cur[j] = gw_nxt[j];
+    for (int j = 0; j < NL; ++j) kw_cur[j] = kw_nxt[j];
   }
   // ---- workgroup slab: waves add their partials into LDS in a fixed order ----
   float* red = wg_slab_begin(smem, slab_stride);
@@ -1097,7 +1102,8 @@ __global__ __launch_bounds__(256, TPS == 1 ? DLAP_BWD1_WPS : 1) void k_mlp_bwd_s
 }
 
 
-// Moment backward (phase 2). NLM MFMA layers of WM = 16*WMB units; tanh on the last.
+// Moment backward (phase 2). NLM MFMA layers of WM = 16*WMB units; tanh on the last. Hidden
+// layers' keep words are hashed as in the forward; gates from the recomputed activations.
 // ZIN: as k_mlp_bwd_sdf (layer 0 from z, layer-0 dz stored as J.dz_out [tile][WMB][64]).
 template <class P, int KS1, int WMB, int NLM, int TPS, bool ZIN>
 __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict__ jobs, MlpDims D,
@@ -1135,18 +1141,22 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
 
   const int stride = gridDim.x * nwaves;
   int tile = blockIdx.x * nwaves + wave;
-  constexpr int NH = NLM > 1 ? NLM - 1 : 1;   // hidden layers with stored gate words
   TileIn<P, KS1> cur, nxt;
   ZTile<WMB> zcur, znxt;
-  uint32_t gw_cur[NH], gw_nxt[NH];
+  AbPre<WMB> ab_cur, ab_nxt;
+  int2 ti_ahead[2];
   if (tile < ntiles) {
     if constexpr (ZIN) issue_ztile<WMB, false>(J, D, tile, zcur, false, true);
     else issue_tile<P, KS1, false>(J, tile, cur);
-#pragma unroll
-    for (int j = 0; j + 1 < NLM; ++j) gw_cur[j] = gp(J.mgbits)[((size_t)tile * (NLM - 1) + j) * 64 + lane];
+    if (tile + stride < ntiles) issue_rowti(J, tile + stride, ti_ahead);
   }
+  const uint32_t stp = load_step(J);
   stage_weights<P>(J, D, lds, aux);
-  const DropCtx dc = drop_ctx(J, D);
+  const DropCtx dc = drop_ctx(J, D, stp);
+  if (tile < ntiles) {
+    if constexpr (ZIN) issue_abias<WMB>(J, zcur.ti, ab_cur);
+    else issue_abias<WMB>(J, cur.ti, ab_cur);
+  }
   for (; tile < ntiles; tile += stride) {
     const int oz = opaque_zero();             // see bwd_sdf_body: no hoisted weight copies
     const Frag* ldt = lds + oz;
@@ -1154,69 +1164,55 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
     if (tile + stride < ntiles) {
       if constexpr (ZIN) issue_ztile<WMB, false>(J, D, tile + stride, znxt, false, true);
       else issue_tile<P, KS1, false>(J, tile + stride, nxt);
-#pragma unroll
-      for (int j = 0; j + 1 < NLM; ++j)
-        gw_nxt[j] = gp(J.mgbits)[((size_t)(tile + stride) * (NLM - 1) + j) * 64 + lane];
+      issue_abias<WMB>(J, ti_ahead, ab_nxt);
+      if (tile + 2 * stride < ntiles) issue_rowti(J, tile + 2 * stride, ti_ahead);
     }
     Frag xf[2][KS1];
     RowInfo ri;
     if constexpr (ZIN) ri = finish_ztile<WMB>(J, tile, zcur);
     else ri = finish_tile<P, KS1, false>(J, D, tile, cur, xf);   // moment tower: no per-period cols
     Frag act[NLM][2][KSM];
-    uint32_t gates[NLM][2];
     f32x4 a[2][WMB];
     if constexpr (ZIN) {
 #pragma unroll
       for (int b = 0; b < 2; ++b)
 #pragma unroll
-        for (int u = 0; u < WMB; ++u) a[b][u] = zcur.zm[b][u];
+        for (int u = 0; u < WMB; ++u) a[b][u] = zcur.zm[b][u] + ab_cur.v[b][u];
     } else {
-      layer0<P, KS1, WMB>(ldt, D.m_fwd0, xf, a);
+      layer0<P, KS1, WMB>(ldt, D.m_fwd0, xf, ab_cur.v, a);
     }
-#pragma unroll
-    for (int j = 0; j < NLM; ++j) {
-      if (j > 0) layer_chain<P, WMB, KSM>(ldt, D.m_fwd + (j - 1) * WMB * KSM, act[j - 1], a);
-      auto body = [&](auto b0, auto b1) {
-        if (j + 1 < NLM) {
-          gates[j][0] = gw_cur[j < NH ? j : 0] & 0xFFFFu;
-          gates[j][1] = gw_cur[j < NH ? j : 0] >> 16;
-          relu_gates<WMB>(a, b0, b1, dc.scale, gates[j]);
-          pack_blocks<P, WMB>(a, act[j]);
-        } else {
-          // h = tanh(z); dz = dh (1 - h^2), dh = dE[i][k] R SDF_t / T_i
-#pragma unroll
-          for (int b = 0; b < 2; ++b) {
-            const auto bp = b ? b1 : b0;
-            const int d = ri.dense[b];
-            const float cst = d >= 0 ? gp(J.Rm)[d] * gp(J.sdfv)[ri.t[b]] * gp(J.invT)[ri.i[b]] : 0.f;
-            const auto de = gp(J.dE) + (size_t)ri.i[b] * D.K;
-#pragma unroll
-            for (int u = 0; u < WMB; ++u)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                const int k = 16 * u + 4 * q + r;
-                const float h = tanhf(a[b][u][r] + bp[k]);
-                const float g = (d >= 0 && k < D.K) ? de[k] * cst : 0.f;
-                a[b][u][r] = g * (1.f - h * h);
-              }
-          }
-        }
-      };
-      // layer-0 bias is per period (global), later biases are staged (LDS)
-      if (j == 0) body(gp(J.abias) + ri.t[0] * 64, gp(J.abias) + ri.t[1] * 64);
-      else body(auxt + D.a_mb + 64 * j, auxt + D.a_mb + 64 * j);
-    }
-#pragma unroll
-    for (int j = 0; j < NLM; ++j) { gates[j][0] = opaque_gate(gates[j][0]); gates[j][1] = opaque_gate(gates[j][1]); }
     f32x4 dz[2][WMB];
 #pragma unroll
-    for (int b = 0; b < 2; ++b)
+    for (int j = 0; j < NLM; ++j) {
+      if (j > 0) layer_chain<P, WMB, KSM>(ldt, D.m_fwd + (j - 1) * WMB * KSM, act[j - 1], a, auxt + D.a_mb + 64 * j);
+      if (j + 1 < NLM) {
+        const uint32_t kw = dc.on ? hash_keep<WMB>(dc, 16 + j, ri) : 0xFFFFFFFFu;
+        act_tile_rt<P, WMB>(a, dc.on, kw, act[j]);
+      } else {
+        // h = tanh(z); dz = dh (1 - h^2), dh = dE[i][k] R SDF_t / T_i (the moment loss), or an
+        // external dL/dh (module API: a caller's loss of the moments)
+        const bool ext = J.dh_ext != nullptr;
 #pragma unroll
-      for (int u = 0; u < WMB; ++u) dz[b][u] = a[b][u];
+        for (int b = 0; b < 2; ++b) {
+          const int d = ri.dense[b];
+          const float cst = (d >= 0 && !ext) ? gp(J.Rm)[d] * gp(J.sdfv)[ri.t[b]] * gp(J.invT)[ri.i[b]] : 0.f;
+          const auto de = ext ? gp(J.dh_ext) + (size_t)(d >= 0 ? d : 0) * D.K : gp(J.dE) + (size_t)ri.i[b] * D.K;
+#pragma unroll
+          for (int u = 0; u < WMB; ++u)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int k = 16 * u + 4 * q + r;
+              const float h = tanhf(a[b][u][r]);
+              const float g = (d >= 0 && k < D.K) ? (ext ? de[k] : de[k] * cst) : 0.f;
+              dz[b][u][r] = g * (1.f - h * h);
+            }
+        }
+      }
+    }
+    Frag dzf[2][KSM];
+    pack_blocks<P, WMB>(dz, dzf);
 #pragma unroll
     for (int j = NLM - 1; j >= 0; --j) {
-      Frag dzf[2][KSM];
-      pack_blocks<P, WMB>(dz, dzf);
       Frag dzN[WMB];
 #pragma unroll
       for (int u = 0; u < WMB; ++u) to_rows_k<P, WMB>(dzf, u, selP0, selP1, dzN[u]);
@@ -1259,29 +1255,30 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
       if (j > 0) {
         f32x4 da[2][WMB];
         layer_chain<P, WMB, KSM>(ldt, D.m_bwd + (j - 1) * WMB * KSM, dzf, da);
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-          for (int u = 0; u < WMB; ++u)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-              dz[b][u][r] = gate_and(da[b][u][r] * dc.scale, gates[j > 0 ? j - 1 : 0][b], u * 4 + r);
+        gate_tile<P, WMB>(da, act[j > 0 ? j - 1 : 0], dzf);
       } else if (slice == 0) {
+        // dL/d(layer-0 pre-activation) per row for the macro-column / bias gradients: fp32 when
+        // layer 0 is the tanh layer, else the packed dz0 unpacked (the values the weight-gradient
+        // MFMAs used)
 #pragma unroll
         for (int b = 0; b < 2; ++b) {
           const int row = tile * 32 + 16 * b + (lane & 15);
           if (row < J.R) {
 #pragma unroll
-            for (int u = 0; u < WMB; ++u)
-              *reinterpret_cast<f32x4*>(gp(J.v_out) + (size_t)row * 64 + 16 * u + 4 * q) = dz[b][u];
+            for (int s = 0; s < KSM; ++s) {
+              f32x4 lo, hi;
+              if (NLM == 1) { lo = dz[b][2 * s]; hi = dz[b][(2 * s + 1) % WMB]; }
+              else P::unpack(dzf[b][s], lo, hi);
+              *reinterpret_cast<f32x4*>(gp(J.v_out) + (size_t)row * 64 + 32 * s + 4 * q) = lo;
+              if (2 * s + 1 < WMB) *reinterpret_cast<f32x4*>(gp(J.v_out) + (size_t)row * 64 + 32 * s + 16 + 4 * q) = hi;
+            }
           }
         }
       }
     }
     if constexpr (ZIN) zcur = znxt;
     else cur = nxt;
-#pragma unroll
-    for (int j = 0; j < NH; ++j) gw_cur[j] = gw_nxt[j];
+    ab_cur = ab_nxt;
   }
   float* red = wg_slab_begin(smem, slab_stride);
   for (int w = 0; w < nwaves; ++w) {
@@ -1311,9 +1308,9 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
 
 // ============================== dropout keep-mask generator ===========================
 // Keep words of every (tile, SDF layer, lane) for the dropout step *step + step_offset*, in
-// that step's parity half of gbits. The decisions are exactly relu_dropout's (same key, row
-// and unit hashing); generating them here lets the next step's masks be produced on an idle
-// branch of the epoch graph while the serial LSTM kernels run, instead of inside the forward.
+// that step's parity half of gbits (split layout, keep_word). Generating them here lets the
+// next step's masks be produced on an idle branch of the epoch graph while the serial LSTM
+// kernels run; the training forward and the backward of that step both read them.
 __global__ __launch_bounds__(256) void k_dropmask(const MlpJob* __restrict__ jobs, MlpDims D, int step_offset) {
   const MlpJob& J = jobs[blockIdx.y];
   const int ntiles = (J.R + 31) >> 5;
@@ -1325,29 +1322,13 @@ __global__ __launch_bounds__(256) void k_dropmask(const MlpJob* __restrict__ job
   uint32_t rowmix[2];
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
-    const int r = min(tile * 32 + 16 * b + (lane & 15), J.R - 1);
-    const int2 ti = gp(J.rowti)[r];
-    const uint32_t row = (uint32_t)(ti.x * J.N + ti.y);
-    rowmix[b] = row * 0xcc9e2d51u ^ (row >> 16);
+    const int r = tile * 32 + 16 * b + (lane & 15);
+    const int2 ti = gp(J.rowti)[min(r, J.R - 1)];
+    // rows beyond R hash as dense row -1, as the towers do (their words are never used)
+    rowmix[b] = row_mix(r < J.R ? (uint32_t)(ti.x * J.N + ti.y) : 0xFFFFFFFFu);
   }
-  const auto dst = gp(J.gbits) + (size_t)(step & 1u) * J.gb_half + (size_t)tile * D.nl_sdf * 64 + lane;
-  for (int j = 0; j < D.nl_sdf; ++j) {
-    const uint32_t key = dropout_key(J.seed, step, j);
-    uint32_t word = 0;
-#pragma unroll
-    for (int b = 0; b < 2; ++b) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t pair0 = (uint32_t)(8 * u + 2 * q);
-        const uint32_t h0 = dropout_pair(key, rowmix[b], pair0);
-        const uint32_t h1 = dropout_pair(key, rowmix[b], pair0 + 1);
-        const uint32_t keep = ((h0 & 0xFFFFu) >= thr16 ? 1u : 0u) | ((h0 >> 16) >= thr16 ? 2u : 0u) |
-                              ((h1 & 0xFFFFu) >= thr16 ? 4u : 0u) | ((h1 >> 16) >= thr16 ? 8u : 0u);
-        word |= keep << (16 * b + 4 * u);
-      }
-    }
-    dst[64 * j] = word;
-  }
+  const auto dst = gp(const_cast<uint32_t*>(J.gbits)) + (size_t)(step & 1u) * J.gb_half + (size_t)tile * D.nl_sdf * 64 + lane;
+  for (int j = 0; j < D.nl_sdf; ++j) dst[64 * j] = keep_word<4>(dropout_key(J.seed, step, j), rowmix, thr16, q);
 }
 
 void launch_dropmask(const MlpJob* jobs, int njobs, int ntiles, const MlpDims& D, int step_offset,

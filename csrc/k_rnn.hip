@@ -198,7 +198,7 @@ __global__ __launch_bounds__(64) void k_lstm(const RnnJob* __restrict__ jobs,
     const auto hout = save ? gp(J.sh) + (size_t)l * T * H : gp(J.out);
     const auto sg = gp(J.sg) + (size_t)l * T * G4;
     const auto sc = gp(J.sc) + (size_t)l * T * H;
-    float h = 0.f, c = 0.f;
+    float h = act && J.h0 ? gp(J.h0)[l * H + k] : 0.f, c = act && J.c0 ? gp(J.c0)[l * H + k] : 0.f;
     auto cell = [&](int t, const float (&p)[4]) {
       const float gi = sigm(p[0]), gf = sigm(p[1]), gg = ftanh(p[2]), go = sigm(p[3]);
       c = gf * c + gi * gg;
@@ -328,7 +328,7 @@ __global__ __launch_bounds__(64) void k_lstm_gl(const RnnJob* __restrict__ jobs,
     const auto sc = gp(J.sc) + (size_t)l * T * H;
     const auto out = gp(J.out);
     const bool last = l + 1 == nrnn;
-    float h = 0.f, c = 0.f;
+    float h = ul && J.h0 ? gp(J.h0)[l * H + L] : 0.f, c = ul && J.c0 ? gp(J.c0)[l * H + L] : 0.f;
     auto cell = [&](int t, float pre) {
       pre += bcast_dot<HM>(whh, h);
       float y = kb * sigm(ka * pre) + kc;
@@ -478,7 +478,7 @@ __global__ __launch_bounds__(FUSE ? LSTM_FUSE_THREADS : 64) void k_lstm_gls(cons
     const int gstride = gl ? G4 : 0, ustride = ul ? H : 0;
     // h / c on lanes >= H are bounded garbage: the broadcast reads lanes j < HM only, and
     // lanes H <= j < HM carry zero weights
-    float h = 0.f, c = 0.f;
+    float h = ul && J.h0 ? gp(J.h0)[l * H + L] : 0.f, c = ul && J.c0 ? gp(J.c0)[l * H + L] * KC : 0.f;
     auto cell = [&](int t, float pre) {
       if constexpr (DPPG) pre += bcast_dot_row<HM>(whh, h);
       else pre += bcast_dot<HM>(whh, h);
@@ -493,12 +493,25 @@ __global__ __launch_bounds__(FUSE ? LSTM_FUSE_THREADS : 64) void k_lstm_gls(cons
       udst_h[t * ustride] = h;
     };
     if (l == 0) {
-      float nx = sx[row] * kx;
-      for (int t = 0; t < T; ++t) {
-        const float pre = nx;
-        nx = sx[(t + 1 < T ? t + 1 : t) * G4 + row] * kx;   // next step's input, from LDS
-        cell(t, pre);
+      // inputs in chunks of CH steps, the next chunk's LDS reads issued a whole chunk ahead:
+      // inside a chunk the recurrence has no LDS load (and no wait on the per-step LDS stores,
+      // which a one-step-ahead read kept on the chain through the shared LDS counter)
+      constexpr int CH = 8;
+      float xa[CH], xb[CH];
+      auto ldch = [&](int t0, float (&x)[CH]) {
+#pragma unroll
+        for (int k = 0; k < CH; ++k) x[k] = sx[min(t0 + k, T - 1) * G4 + row];
+      };
+      const int tfull = T / CH * CH;
+      ldch(0, xa);
+      for (int t0 = 0; t0 < tfull; t0 += CH) {
+        ldch(t0 + CH, xb);
+#pragma unroll
+        for (int k = 0; k < CH; ++k) cell(t0 + k, xa[k] * kx);
+#pragma unroll
+        for (int k = 0; k < CH; ++k) xa[k] = xb[k];
       }
+      for (int t = tfull; t < T; ++t) cell(t, sx[t * G4 + row] * kx);
     } else {
       const uint32_t key_in = dropout_key(J.seed, step, 32 + (l - 1));
       float nx = ul ? sin[L] : 0.f;
@@ -633,7 +646,7 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
       const int t = i / H, k = i - t * H;
       const float gi = sgg[(size_t)t * G4 + k], gf = sgg[(size_t)t * G4 + H + k];
       const float gg = sgg[(size_t)t * G4 + 2 * H + k], go = sgg[(size_t)t * G4 + 3 * H + k];
-      const float c = scg[i], cp = t > 0 ? scg[i - H] : 0.f;
+      const float c = scg[i], cp = t > 0 ? scg[i - H] : (J.c0 ? gp(J.c0)[l * H + k] : 0.f);
       const float tc = ftanh(c);
       float* q = s_cf + t * LSTM_NCOEF * H + k;
       q[0 * H] = go * (1.f - tc * tc);
@@ -712,6 +725,8 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
           t -= U;
         }
       }
+      // dL/d(initial state) of the layer: the gradients carried past t = 0
+      if (J.dh0 && lane < 4) { gp(J.dh0)[l * 4 + lane] = dh_next; gp(J.dc0)[l * 4 + lane] = dc_next; }
     } else if (wave == 0) {
       const int k = lane < H ? lane : 0;
       const bool act = lane < H;
@@ -775,6 +790,7 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
           t -= U;
         }
       }
+      if (J.dh0 && act) { gp(J.dh0)[l * H + k] = dh_next; gp(J.dc0)[l * H + k] = dc_next; }
     }
     __syncthreads();
     if (l == 0) RNN_TS(10, tsm);
@@ -802,6 +818,7 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
         if (col < H) {
 #pragma unroll 4
           for (int t = max(ta, 1); t < tb; ++t) acc += dgs[t * G4 + g] * s_h[(t - 1) * H + col];
+          if (ta == 0 && J.h0) acc += dgs[g] * gp(J.h0)[l * H + col];     // h_{-1} = initial state
         } else if (col == H) {
 #pragma unroll 4
           for (int t = ta; t < tb; ++t) acc += dgs[t * G4 + g];

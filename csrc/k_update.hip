@@ -39,13 +39,24 @@ __global__ __launch_bounds__(256) void k_finalize(const FinJob* __restrict__ job
     __syncthreads();
     return red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
   };
+  // the packed training weights of layers >= 1 and the SDF output row carry the dropout scale
+  // 1/(1-p) (k_pack), so their slab sums are gradients w.r.t. the scaled weights: scale back
+  const float dscale = md->dropout > 0.f ? 1.f / (1.f - md->dropout) : 1.f;
   if (b < nb_tiles) {
     const int ti = b >> 6, e = ((b & 63) << 6) + lane;
     const GradTile& G = mom ? md->tile_m[ti] : md->tile_s[ti];
     const int o = e >> 6, i = (e & 63) + 64 * G.chunk;
     const int tpos = ti - G.slice * tps;
     const float v = slab_sum(J.slab + (size_t)G.slice * J.nslab * slab_stride + tpos * 4096 + e);
-    if (wave == 0 && o < G.out && i < G.in) gp(J.grads)[G.w_off + o * G.ld + G.col0 + i] = v;
+    bool ok = o < G.out && i < G.in;
+    int col = G.col0 + i;
+    if (G.xmap) {                                   // fused SDF layer 0: panel column -> W0 column
+      const int F = md->F, ppc = md->md.ppc;
+      if (i < F) col = i;
+      else if (i >= ppc && i < ppc + md->Dm) col = F + (i - ppc);
+      else ok = false;
+    }
+    if (wave == 0 && ok) gp(J.grads)[G.w_off + o * G.ld + col] = G.layer > 0 ? v * dscale : v;
     return;
   }
   b -= nb_tiles;
@@ -54,7 +65,8 @@ __global__ __launch_bounds__(256) void k_finalize(const FinJob* __restrict__ job
     const int ec = e < SLAB_EXTRA ? e : SLAB_EXTRA - 1;
     const float v = slab_sum(J.slab + tps * 4096 + ec);     // slice-0 slabs
     const int dst = e < SLAB_EXTRA ? (mom ? md->extra_m[e] : md->extra_s[e]) : -1;
-    if (wave == 0 && dst >= 0) gp(J.grads)[dst] = v;
+    const bool wo = !mom && e >= DLAP_MAXL * 64 && e < DLAP_MAXL * 64 + 64;   // SDF output row
+    if (wave == 0 && dst >= 0) gp(J.grads)[dst] = wo ? v * dscale : v;
     return;
   }
   b -= nb_extra;
@@ -109,11 +121,13 @@ DLAP_DEV float pack_blob_elem(const ModelDesc* __restrict__ md, PP P, int e) {
   const int frag = e >> 9, lane = (e >> 3) & 63, j = e & 7;
   const int q = lane >> 4, n = lane & 15;
   float val = 0.f;
-  if (frag < D.s_fwd) {                         // SDF layer 0, natural k
+  if (frag < D.s_fwd) {                         // SDF layer 0, natural k = panel column
     const int u = frag / KS1, s = frag - u * KS1;
     const PackLayer& L = md->s[0];
     const int o = 16 * u + n, k = 32 * s + 8 * q + j;
-    if (o < L.out && k < L.in) val = P[L.w_off + o * L.ld + k];
+    // panel columns [0, F): characteristics; [ppc, ppc + Dm): the per-period inputs
+    const int c = k < md->F ? k : (k >= D.ppc && k < D.ppc + md->Dm ? md->F + (k - D.ppc) : -1);
+    if (o < L.out && c >= 0) val = P[L.w_off + o * L.ld + c];
   } else if (frag < D.s_bwd) {                  // SDF chain forward
     const int loc = frag - D.s_fwd, jl = loc / 8 + 1, r = loc % 8, u = r >> 1, s = r & 1;
     const PackLayer& L = md->s[jl];
@@ -141,13 +155,26 @@ DLAP_DEV float pack_blob_elem(const ModelDesc* __restrict__ md, PP P, int e) {
     const PackLayer& L = md->m[jl];
     const int i = 16 * u + n, o = 32 * s + perm_u(q, j);
     if (o < L.out && i < L.in) val = P[L.w_off + o * L.ld + i];
-  } else {                                      // SDF layer 0, per-period columns (W^T)
+  } else if (frag < D.s_wo) {                   // SDF layer 0, per-period columns (W^T)
     const int loc = frag - D.s_upp, u = loc >> 1, s = loc & 1;
     const PackLayer& L = md->s[0];
     const int d = 16 * u + n, o = 32 * s + perm_u(q, j);
     if (o < L.out && d < md->Dm) val = P[L.w_off + o * L.ld + md->F + d];
+  } else {                                      // SDF output row as row 0 of an A operand
+    const int s = frag - D.s_wo, i = 32 * s + perm_u(q, j);
+    if (n == 0 && i < md->s[md->nl_s - 1].out) val = P[md->so_w + i];
   }
   return val;
+}
+// whether blob fragment `frag` / aux float `e` belongs to a layer whose training copy carries
+// the dropout scale (hidden layers >= 1 of both towers, forward and transposed, and wo)
+DLAP_DEV bool blob_scaled(const ModelDesc* __restrict__ md, int frag) {
+  const MlpDims& D = md->md;
+  return (frag >= D.s_fwd && frag < D.m_fwd0) || (frag >= D.m_fwd && frag < D.s_upp) ||
+         (frag >= D.s_wo && frag < D.s_wo + 2);
+}
+DLAP_DEV bool aux_scaled(const ModelDesc* __restrict__ md, int e) {
+  return e >= md->md.a_wo && e < md->md.a_bo;
 }
 
 template <typename PP>
@@ -225,12 +252,26 @@ __global__ __launch_bounds__(256) void k_pack(const UpdJob* __restrict__ jobs,
   const int total = nproj + md->md.b0_frags * 512;
   const int e = blockIdx.x * 256 + threadIdx.x;
   const auto src = gp(static_cast<const float*>(J.params));
+  // two copies: evaluation weights, then the training weights with the dropout scale 1/(1-p)
+  // folded into every layer fed by dropped-out activations (the towers then apply the bare
+  // keep mask; k_finalize scales those gradients back)
+  const float dscale = md->dropout > 0.f ? 1.f / (1.f - md->dropout) : 1.f;
   if (e < nel) {
     const float v = pack_blob_elem(md, src, e);
-    if (md->md.fp32) ((DLAP_GLOBAL float*)(J.blob))[e] = v;         // reference-precision towers
-    else ((DLAP_GLOBAL __bf16*)(J.blob))[e] = (__bf16)v;
+    const float vt = blob_scaled(md, e >> 9) ? v * dscale : v;
+    if (md->md.fp32) {                                                // reference-precision towers
+      ((DLAP_GLOBAL float*)(J.blob))[e] = v;
+      ((DLAP_GLOBAL float*)(J.blob))[nel + e] = vt;
+    } else {
+      ((DLAP_GLOBAL __bf16*)(J.blob))[e] = (__bf16)v;
+      ((DLAP_GLOBAL __bf16*)(J.blob))[nel + e] = (__bf16)vt;
+    }
+  } else if (e < naux) {
+    const int a = e - nel;
+    const float v = pack_aux_elem(md, src, a);
+    gp(J.aux)[a] = v;
+    gp(J.aux)[md->md.aux_floats + a] = aux_scaled(md, a) ? v * dscale : v;
   }
-  else if (e < naux) gp(J.aux)[e - nel] = pack_aux_elem(md, src, e - nel);
   else if (e < nproj) gp(J.wproj)[e - naux] = pack_proj_elem(md, src, e - naux);
   else if (e < total) ((DLAP_GLOBAL __bf16*)(J.blob0))[e - nproj] = (__bf16)pack_blob0_elem(md, src, e - nproj);
   if (bump && blockIdx.x == 0 && threadIdx.x == 0) {

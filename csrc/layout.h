@@ -27,6 +27,10 @@ struct GradTile {
   int w_off, ld, col0;      // flat mapping of element (o, 64*chunk + i)
   int out, in, chunk;
   int slice;                // slab slice that owns the tile
+  int layer;                // tower layer (> 0: the packed training weights carry the dropout
+                            //   scale, so the gradient is scaled back by k_finalize)
+  int xmap;                 // 1: fused SDF layer 0 -- i is a panel column: [0, F) -> W0 column i,
+                            //   [ppc, ppc + Dm) -> W0 column F + i - ppc, else no weight
 };
 
 #define DLAP_MAX_TILES 16

@@ -50,7 +50,27 @@ struct LossJob {
   float* dw;             // [R] dL/dw_raw (compact rows)
   float* rstat;          // [T*4] residual statistics (nullptr: residual loss off)
   float* scal;           // [SC_NSCAL]
+  // Gram mode (k_gram.hip; moments frozen): the loss is the quadratic form s^T G s, so the
+  // asset passes are skipped and k_period_bwd evaluates G s per period. h is then only a flag
+  // (non-null: the conditional loss is wanted) and E / dE are not produced.
+  int gram;              // 1: Gram mode
+  const double* G;       // [2][T][T] Gc, Gu
+  double* gpart;         // [T][2] per-period s_t (G s)_t of Gc and Gu
 };
+
+// One (model, split) of the Gram build (k_gram.hip).
+struct GramJob {
+  const float* h;        // [T*N*K] frozen moments (nullptr: only Gu)
+  const float* Rm;       // [T*N] returns, zero at invalid entries
+  const float* invT;     // [N]
+  double* part;          // [nslice][2][T][T] split-K partials (scratch)
+  double* G;             // [2][T][T] out: Gc, Gu
+  int T, N, K;
+};
+int gram_slices(int T, int njobs);
+size_t gram_part_doubles(int T, int njobs);
+// all jobs of one launch share T (one split of every model)
+void launch_gram(const GramJob* jobs, int njobs, int T, int nslice, hipStream_t st);
 
 void launch_period_fwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st);
 // kmax: the moment count K of the jobs (sizes the output grid of the reduction pass)

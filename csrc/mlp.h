@@ -16,18 +16,19 @@ struct MlpJob {
   float* h_out;           // fwd: dense [T*N][K] moments (valid rows written)
   const float* dw;        // bwd sdf: compact [R] dL/dw_raw
   const float* dE;        // bwd mom: [N][K] dL/dE
+  const float* dh_ext;    // bwd mom, module API: dense [T*N][K] external dL/dh (replaces dE)
   const float* Rm;        // dense [T*N] returns (zero-filled)
   const float* sdfv;      // [T] SDF_t = 1 + P_t
   const float* invT;      // [N] 1 / max(T_i, 1)
   float* slab;            // bwd: per-wave gradient partials
   float* u_out;           // bwd sdf: [R][Dm] dL/d(per-period inputs) per row
   float* v_out;           // bwd mom: [R][64] dL/d(moment layer-0 pre-activation) per row
-  uint32_t* gbits;        // SDF dropout keep -> gate words, two halves by dropout-step parity:
-                          //   [parity][tile][layer][lane] = bits(b=0) | bits(b=1) << 16.
-                          //   k_dropmask writes keep bits, the train forward turns them into
-                          //   ReLU*keep gate bits in place, the backward reads the gates.
+  const uint32_t* gbits;  // SDF dropout keep words (split layout, common.h), two halves by
+                          //   dropout-step parity: [parity][tile][layer][lane]. k_dropmask
+                          //   writes them; the train forward and the backward (which recomputes
+                          //   the forward) read the half of their step. Moment-tower masks are
+                          //   hashed in the kernels (keep_word).
   int gb_half;            // words per parity half (ntiles * nl_sdf * 64)
-  uint32_t* mgbits;       // same for the moment tower's hidden layers (phase 2)
   const int* step;        // device step counter (dropout stream)
   const f32x4* z;         // wide path: [ntiles][zc][64] layer-0 pre-activations (k_proj0)
   bf16x8* dz_out;         // wide path, bwd: [ntiles][UB][64] layer-0 dz fragments (rows as k)
@@ -49,6 +50,10 @@ struct MlpDims {
   int s_fwd0, s_fwd, s_bwd;      // blob frag offsets: SDF layer 0, chain fwd base, chain bwd base
   int m_fwd0, m_fwd, m_bwd;      // moment tower
   int s_upp, ubpp;               // W0[:, F:F+Dm]^T fragments (ubpp blocks of 16 inputs, 2 k-steps)
+  int s_wo;                      // 2 fragments: the SDF output row (row 0 of an A operand)
+  int ppc;                       // fused path: panel column of per-period input 0 (a multiple of 8,
+                                 //   the last 8*ceil(Dm/8) columns of the KP-wide row)
+  int ppst;                      // row stride of the per-period inputs staged in LDS (Dm -> x4)
   int a_sb, a_wo, a_bo, a_pp, a_mb;   // aux offsets: SDF biases [nl][64], out row [64], out
                                       // bias, W0 per-period cols [Dm][64], moment biases [nl][64]
   int blob_frags, aux_floats;

@@ -18,6 +18,8 @@ struct RnnJob {
   float* xin;            // scratch [T][H]
   float* abias;          // [T][64] moment layer-0 per-period bias (nullptr: skip)
   const int* step;       // dropout stream counter
+  const float* h0;       // [nrnn][H] initial hidden state (zero unless a caller passed one)
+  const float* c0;       // [nrnn][H] initial cell state
   unsigned seed;
   int train;
 };

@@ -36,6 +36,10 @@ struct UpdJob {            // one model
   float* dg;               // scratch [T][4H]
   float* dx;               // scratch [T][H]
   const float* dab;        // [T][64]
+  const float* h0;         // [nrnn][H] initial LSTM state of the train split (zero by default)
+  const float* c0;
+  float* dh0;              // [nrnn][H] out: dL/d(initial state) (module API: a caller's hidden)
+  float* dc0;
   const float* scal;       // train-split job scalars of this step (SC_NSCAL) ...
   float* scal_prev;        // ... copied here by k_adam for the epoch bookkeeping
   int T;

@@ -1,0 +1,360 @@
+"""Production dropout path of the native engine, checked numerically.
+
+The engine draws its dropout masks from a counter hash (csrc/common.h ``dropout_key`` /
+``dropout_pair`` / ``dropout_keep``) instead of torch's ``bernoulli_`` stream,
+so the reference (`/root/reference/src/model.py:208-219`, nn.Dropout after every ReLU; nn.LSTM
+inter-layer dropout) cannot be matched draw for draw. Instead the masks are rebuilt here in
+numpy from the same hash, applied to the reference modules' fp32 math with explicit masks, and
+the engine's fp32 (reference-precision) results must match within 1e-5:
+
+* SDF hidden-layer dropout of phases 1 / 3 (keep words from ``k_dropmask``, ``relu_keep``);
+* SDF dropout in phase 2, where the frozen SDF still runs in train mode
+  (`/root/reference/src/train.py:66`; hashed inside the tower kernel, ``relu_dropout``);
+* moment hidden-layer dropout (phase 2, ``hidden_dim_moment``);
+* LSTM inter-layer dropout (2-layer macro LSTM).
+
+A 5-step trajectory checks that every step draws fresh masks (step counter), and the keep rate
+and the 1/(1-p) scale are checked on the matched masks. The wide layer-0 path (bf16 only) is
+checked against the same masked reference at the bf16 tolerance of the other wide-path tests.
+"""
+import copy
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from deeplearninginassetpricing_paperreplication_amd.config import default_cli_config
+from deeplearninginassetpricing_paperreplication_amd.data.synthetic import generate_panel_fast
+from deeplearninginassetpricing_paperreplication_amd.models.gan import AssetPricingGAN
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5
+M32 = 0xFFFFFFFF
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from deeplearninginassetpricing_paperreplication_amd.ops import native
+    native.load(required=True)
+
+
+# ---- the kernels' counter hash, in numpy (uint64 arithmetic masked to 32 bits) ---------------
+def fmix32(h):
+    h = np.asarray(h, dtype=np.uint64) & M32
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & M32
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & M32
+    h ^= h >> 16
+    return h
+
+
+def dropout_key(seed, step, layer):
+    inner = fmix32((step * 0x632BE59B + layer * 0x1B873593 + 0x5BD1E995) & M32)
+    return int(fmix32(((seed * 0x9E3779B1) & M32) ^ int(inner)))
+
+
+def tower_keep(seed, step, layer, rows, width, p):
+    """keep[row, unit] of relu_dropout / k_dropmask: one hash per unit pair, 16-bit halves."""
+    key = dropout_key(seed, step, layer)
+    r = np.asarray(rows, dtype=np.uint64)[:, None]
+    rowmix = ((r * 0xCC9E2D51) & M32) ^ (r >> 16)
+    n = np.arange(width, dtype=np.uint64)[None, :]
+    h = fmix32(np.uint64(key) ^ rowmix ^ (((n >> 1) * 0x27D4EB2F) & M32))
+    half = (h >> (16 * (n & 1))) & 0xFFFF
+    thr16 = int(p * 65536.0 + 0.5)
+    return half >= thr16
+
+
+def lstm_keep(seed, step, layer_in, T, H, p):
+    """keep[t, unit] of the LSTM inter-layer dropout on the output of layer ``layer_in``."""
+    key = dropout_key(seed, step, 32 + layer_in)
+    t = np.arange(T, dtype=np.uint64)[:, None]
+    k = np.arange(H, dtype=np.uint64)[None, :]
+    h = fmix32(np.uint64(key) ^ ((t * 0xCC9E2D51) & M32) ^ ((k * 0x27D4EB2F) & M32) ^ (t >> 16))
+    thr = int(p * 16777216.0 + 0.5)
+    return (h >> 8) >= thr
+
+
+# ---- reference modules with explicit masks ----------------------------------------------------
+class FixedDropout(nn.Module):
+    def __init__(self, keep, p):
+        super().__init__()
+        self.register_buffer("m", torch.from_numpy(keep.astype(np.float32)))
+        self.scale = 1.0 / (1.0 - p)
+
+    def forward(self, x):
+        return x * self.m * self.scale
+
+
+def _set_tower_masks(seq, seed, step, layer0, rows, p):
+    j = 0
+    for idx, mod in enumerate(list(seq)):
+        if isinstance(mod, nn.Dropout):
+            width = seq[idx - 2].out_features
+            seq[idx] = FixedDropout(tower_keep(seed, step, layer0 + j, rows, width, p), p)
+            j += 1
+
+
+def _manual_lstm(lstm: nn.LSTM, seed, step, p, train):
+    """nn.LSTM forward (batch 1, zero state) with the engine's inter-layer masks."""
+    def fwd(x, hidden=None):
+        T = x.shape[0]
+        H = lstm.hidden_size
+        inp = x
+        hs, cs = [], []
+        for l in range(lstm.num_layers):
+            w_ih, w_hh = getattr(lstm, f"weight_ih_l{l}"), getattr(lstm, f"weight_hh_l{l}")
+            b = getattr(lstm, f"bias_ih_l{l}") + getattr(lstm, f"bias_hh_l{l}")
+            if l > 0 and train and p > 0:
+                keep = torch.from_numpy(lstm_keep(seed, step, l - 1, T, H, p).astype(np.float32))
+                inp = inp * keep / (1.0 - p)
+            h = x.new_zeros(H)
+            c = x.new_zeros(H)
+            out = []
+            xw = inp @ w_ih.T + b
+            for t in range(T):
+                g = xw[t] + w_hh @ h
+                i, f, gg, o = g.chunk(4)
+                c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(gg)
+                h = torch.sigmoid(o) * torch.tanh(c)
+                out.append(h)
+            inp = torch.stack(out)
+            hs.append(h)
+            cs.append(c)
+        return inp, (torch.stack(hs)[:, None], torch.stack(cs)[:, None])
+    return fwd
+
+
+def _masked_reference(model, b, seed, step, phase):
+    """Copy of ``model`` whose dropout layers apply the engine's masks of (seed, step)."""
+    ref = copy.deepcopy(model)
+    T, N = b["mask"].shape
+    rows = np.arange(T * N)
+    p = model.spec.dropout
+    _set_tower_masks(ref.sdf_net.fc_layers, seed, step, 0, rows, p)
+    if isinstance(ref.moment_net.fc_layers, nn.Sequential):     # (phases 2 and 3 use the moments)
+        _set_tower_masks(ref.moment_net.fc_layers, seed, step, 16, rows, p)
+    if ref.sdf_net.macro_lstm is not None:
+        ref.sdf_net.macro_lstm.forward = _manual_lstm(ref.sdf_net.macro_lstm.lstm, seed, step, p, True)
+    return ref
+
+
+def _splits(T=(40, 12, 20), N=150, F=46, M=8, seed=5):
+    ret, feats, mask, mac = generate_panel_fast(sum(T), N, F, M, seed=seed)
+    mac = (mac - mac[:T[0]].mean(0)) / (mac[:T[0]].std(0, unbiased=False) + 1e-8)
+    cuts = [(0, T[0]), (T[0], T[0] + T[1]), (T[0] + T[1], sum(T))]
+    return [{"returns": ret[a:b].contiguous(), "individual_features": feats[a:b].contiguous(),
+             "mask": mask[a:b].contiguous(), "macro_features": mac[a:b].contiguous()} for a, b in cuts]
+
+
+PHASE_NAME = {1: "unconditional", 2: "moment", 3: "conditional"}
+
+
+def _ref_step(ref, b, phase):
+    """Loss and the trained scope's gradient of one reference step (train mode)."""
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import flatten_state
+    ref.train()
+    ref.zero_grad()
+    out = ref(b["macro_features"], b["individual_features"], b["returns"], b["mask"], phase=PHASE_NAME[phase])
+    out["loss"].backward()
+    g = flatten_state({k: (v.grad if v.grad is not None else torch.zeros_like(v))
+                       for k, v in ref.named_parameters()}, ref.spec)
+    return float(out["loss"].detach()), g
+
+
+def _engine(model, splits, seed, precision="fp32", wide=False):
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import GANEngine
+    old = os.environ.get("DLAP_WIDE")
+    if wide:
+        os.environ["DLAP_WIDE"] = "1"
+    try:
+        eng = GANEngine(model.spec, 1, max_epochs=32, precision=precision)
+    finally:
+        if wide:
+            if old is None:
+                os.environ.pop("DLAP_WIDE")
+            else:
+                os.environ["DLAP_WIDE"] = old
+    eng.set_data(*splits)
+    eng.set_model(0, model, seed)
+    return eng
+
+
+CASES = {
+    "sdf_p005": ({}, 0.05, (1, 3)),
+    "sdf_p030": ({}, 0.3, (1, 2, 3)),
+    "moment_hidden_p030": ({"hidden_dim_moment": [16]}, 0.3, (2, 3)),
+    "lstm2_p030": ({"num_units_rnn": [3, 4]}, 0.3, (1, 3)),
+}
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_dropout_step_matches_masked_reference(case):
+    """One training step per phase from a fresh engine (dropout step 0): the training loss and
+    the trained scope's gradient equal the reference modules run with the engine's masks."""
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import HIST
+    extra, p, phases = CASES[case]
+    splits = _splits()
+    b = splits[0]
+    cfg = default_cli_config(8, 46, dropout=p)
+    cfg.update(extra)
+    torch.manual_seed(11)
+    model = AssetPricingGAN(cfg)
+    seed = 1234
+    P_sdf = model.spec.param_counts()[0]
+    for phase in phases:
+        eng = _engine(copy.deepcopy(model), splits, seed)
+        eng.eng.begin_phase(phase)
+        eng.run(phase, 1, 1e-3, 0)
+        eng.eng.sync()
+        got_loss = eng.history_rows(0)[0, HIST["train_loss"]]
+        got_g = eng.eng.get_grads(0)
+        ref = _masked_reference(model, b, seed, 0, phase)
+        ref_loss, ref_g = _ref_step(ref, b, phase)
+        assert abs(got_loss - ref_loss) <= TOL * abs(ref_loss), (case, phase, got_loss, ref_loss)
+        sl = slice(0, P_sdf) if phase != 2 else slice(P_sdf, None)
+        err = np.linalg.norm(got_g[sl] - ref_g[sl]) / np.linalg.norm(ref_g[sl])
+        assert err < TOL, (case, phase, err)
+        # the masks are not a no-op: the same step with every dropout layer removed is far off
+        plain = copy.deepcopy(model)
+        for net in (plain.sdf_net, plain.moment_net):
+            if isinstance(net.fc_layers, nn.Sequential):
+                for idx, mod in enumerate(net.fc_layers):
+                    if isinstance(mod, nn.Dropout):
+                        net.fc_layers[idx] = nn.Identity()
+        if plain.sdf_net.macro_lstm is not None:
+            plain.sdf_net.macro_lstm.forward = _manual_lstm(plain.sdf_net.macro_lstm.lstm, seed, 0, p, False)
+        _, g0 = _ref_step(plain, b, phase)
+        assert np.linalg.norm(got_g[sl] - g0[sl]) > 100 * TOL * np.linalg.norm(g0[sl]), (case, phase)
+
+
+def test_dropout_trajectory_fresh_masks_each_step():
+    """5 consecutive phase-3 steps at p = 0.3: step s uses the masks of dropout step s (the
+    engine's counter advances with every update); losses and all parameters within 1e-5."""
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import HIST
+    splits = _splits()
+    b = splits[0]
+    cfg = default_cli_config(8, 46, dropout=0.3)
+    torch.manual_seed(12)
+    model = AssetPricingGAN(cfg)
+    seed = 77
+    lr = 1e-3
+    eng = _engine(copy.deepcopy(model), splits, seed)
+    eng.eng.begin_phase(3)
+    eng.run(3, 5, lr, 0)
+    eng.eng.sync()
+    got = eng.history_rows(0)[:, HIST["train_loss"]]
+    cur = copy.deepcopy(model)
+    opt = torch.optim.Adam(cur.sdf_net.parameters(), lr=lr)
+    ref_losses = []
+    for step in range(5):
+        ref = _masked_reference(cur, b, seed, step, 3)
+        ref.train()
+        ref.zero_grad()
+        out = ref(b["macro_features"], b["individual_features"], b["returns"], b["mask"], phase="conditional")
+        out["loss"].backward()
+        ref_losses.append(float(out["loss"]))
+        # carry the gradients back to `cur` (same parameter order) and step its optimiser
+        for pc, pr in zip(cur.parameters(), ref.parameters()):
+            pc.grad = None if pr.grad is None else pr.grad.clone()
+        torch.nn.utils.clip_grad_norm_(cur.sdf_net.parameters(), 1.0)
+        opt.step()
+    ref_losses = np.array(ref_losses)
+    assert np.abs(got - ref_losses).max() <= TOL * np.abs(ref_losses).max(), (got, ref_losses)
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import flatten_state
+    pg, pr = eng.params(0), flatten_state(cur, cur.spec)
+    P_sdf = cur.spec.param_counts()[0]
+    # the output bias is noise-only under the zero-mean normalisation (see test_engine_fp32_gpu)
+    keep = np.ones(P_sdf, bool)
+    keep[P_sdf - 1] = False
+    assert np.linalg.norm(pg[:P_sdf][keep] - pr[:P_sdf][keep]) <= TOL * np.linalg.norm(pr[:P_sdf][keep])
+    # consecutive steps draw different masks
+    rows = np.arange(40 * 150)
+    k0, k1 = tower_keep(seed, 0, 0, rows, 64, 0.3), tower_keep(seed, 1, 0, rows, 64, 0.3)
+    assert (k0 != k1).mean() > 0.3
+
+
+@pytest.mark.parametrize("p", [0.05, 0.3])
+def test_dropout_keep_rate_and_scale(p):
+    """The (engine-verified) masks keep each unit with probability 1 - p within binomial bounds,
+    per layer and per step, with no correlation between the two units of a hash pair, and the
+    kept activations are scaled by exactly 1 / (1 - p) (the masked-reference match above uses
+    that scale; here it is checked against a one-hot probe through the engine)."""
+    rows = np.arange(60000)
+    for layer in (0, 1, 16):
+        for step in (0, 1, 1000):
+            k = tower_keep(99, step, layer, rows, 64, p)
+            n = k.size
+            sd = np.sqrt(p * (1 - p) / n)
+            assert abs(k.mean() - (1 - p)) < 5 * sd, (layer, step, k.mean())
+            a, c = k[:, 0::2].ravel(), k[:, 1::2].ravel()
+            corr = np.corrcoef(a, c)[0, 1]
+            assert abs(corr) < 5 / np.sqrt(a.size), corr
+    kl = lstm_keep(99, 3, 0, 4096, 16, p)
+    assert abs(kl.mean() - (1 - p)) < 5 * np.sqrt(p * (1 - p) / kl.size)
+    # scale through the engine: a single-layer SDF whose every unit equals 1 before dropout
+    # (zero weights, bias 1) gives w = wo . (keep / (1 - p)); with wo = 1 that is
+    # (#kept) / (1 - p) per row -- read back as the raw weights of one train-mode forward
+    splits = _splits(T=(8, 4, 4), N=64)
+    cfg = default_cli_config(8, 46, hidden_dim=(64,), dropout=p, use_lstm=False)
+    cfg["normalize_w"] = False
+    model = AssetPricingGAN(cfg)
+    with torch.no_grad():
+        for prm in model.parameters():
+            prm.zero_()
+        model.sdf_net.fc_layers[0].bias.fill_(1.0)
+        model.sdf_net.output_proj.weight.fill_(1.0)
+    eng = _engine(model, splits, 5)
+    eng.eng.set_drop_step(0, 0)
+    eng.eng.forward_split(0, True, False)
+    w = eng.eng.read_ws(0, 0, "w")
+    ps = eng.splits[0]
+    ti = ps.rowti.reshape(-1, 2)
+    dense = ti[:, 0].astype(np.int64) * ps.N + ti[:, 1]
+    keep = tower_keep(5, 0, 0, dense, 64, p)
+    expect = keep.sum(1) / (1.0 - p)
+    assert np.abs(w - expect).max() <= 1e-4 * expect.max(), (w[:4], expect[:4])
+
+
+def test_dropout_wide_path_matches_masked_reference():
+    """The wide layer-0 path (DLAP_WIDE=1: k_mlp_fwd_zx / k_wgrad0, bf16 only) with dropout 0.3:
+    phase-3 training loss and SDF gradient equal the fused bf16 path's (same masks; the two only
+    differ in the layer-0 summation order) and track the masked fp32 reference at bf16 accuracy,
+    clearly closer than the unmasked reference."""
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import HIST
+    splits = _splits()
+    b = splits[0]
+    cfg = default_cli_config(8, 46, dropout=0.3)
+    torch.manual_seed(13)
+    model = AssetPricingGAN(cfg)
+    seed = 4321
+    P_sdf = model.spec.param_counts()[0]
+    got = {}
+    for wide in (True, False):
+        eng = _engine(copy.deepcopy(model), splits, seed, precision="bf16", wide=wide)
+        assert int(eng.desc["wide"]) == int(wide)
+        eng.eng.begin_phase(3)
+        eng.run(3, 1, 1e-3, 0)
+        eng.eng.sync()
+        got[wide] = (eng.history_rows(0)[0, HIST["train_loss"]], eng.eng.get_grads(0)[:P_sdf])
+    (lw, gw), (lf, gf) = got[True], got[False]
+    assert abs(lw - lf) <= 1e-2 * abs(lf), (lw, lf)
+    assert np.linalg.norm(gw - gf) <= 3e-2 * np.linalg.norm(gf)
+    ref_loss, ref_g = _ref_step(_masked_reference(model, b, seed, 0, 3), b, 3)
+    assert abs(lw - ref_loss) <= 6e-2 * abs(ref_loss)
+    err = np.linalg.norm(gw - ref_g[:P_sdf]) / np.linalg.norm(ref_g[:P_sdf])
+    assert err < 1e-1, err
+    # and the unmasked reference is clearly further away (the masks matter at p = 0.3)
+    plain = copy.deepcopy(model)
+    for idx, mod in enumerate(plain.sdf_net.fc_layers):
+        if isinstance(mod, nn.Dropout):
+            plain.sdf_net.fc_layers[idx] = nn.Identity()
+    _, g_plain = _ref_step(plain, b, 3)
+    err_plain = np.linalg.norm(gw - g_plain[:P_sdf]) / np.linalg.norm(g_plain[:P_sdf])
+    assert err_plain > 2 * err, (err_plain, err)
