@@ -87,12 +87,35 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+def visible_gpus() -> int:
+    """GPUs the ranks will see, counted without touching HIP (no torch.cuda call in the parent):
+    the KFD topology's GPU nodes (simd_count > 0), narrowed by the *_VISIBLE_DEVICES masks."""
+    import glob
+    nodes = glob.glob("/sys/class/kfd/kfd/topology/nodes/*/properties")
+    if not nodes:                        # no KFD sysfs (container without it): amdsmi's count,
+        return torch.cuda.device_count()  # which does not initialise HIP on this image
+    n = 0
+    for f in nodes:
+        try:
+            with open(f) as fh:
+                props = dict(line.split()[:2] for line in fh if len(line.split()) >= 2)
+        except OSError:
+            continue
+        if int(props.get("simd_count", "0")) > 0:
+            n += 1
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
 def spawn_ranks(n: int) -> int:
     """``python bench.py --gpus N`` without a launcher: start N child ranks (one per GPU) with
-    torchrun-style env and wait for them. The parent never touches the GPU (device_count does not
-    initialise HIP on this image), so the children own their devices. Returns the exit code."""
+    torchrun-style env and wait for them. The parent never touches the GPU (it counts devices from
+    sysfs, ``visible_gpus``), so the children own their devices. Returns the exit code."""
     share = os.environ.get("DLAP_SHARE_GPU", "0") == "1"
-    ndev = torch.cuda.device_count()
+    ndev = visible_gpus()
     if ndev < n and not share:
         print(f"bench.py: --gpus {n} requested but only {ndev} GPU(s) are visible", file=sys.stderr)
         return 2

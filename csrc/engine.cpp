@@ -135,6 +135,7 @@ struct ModelState {
   DevBuf<int> adam_step, drop_step, snap_flags, ep;
   DevBuf<uint16_t> blob, blob0;
   unsigned seed = 0;
+  unsigned tower_salt = 0;  // XOR-ed (mixed) into the towers' dropout seed only (N-sharding: per rank)
   float lr = 0.f;         // per-model learning rate override (0: use the run's lr)
 };
 
@@ -389,6 +390,14 @@ class Engine {
     h_valid_ = false;
   }
   void set_seed(int g, unsigned seed) { models_[check_g(g)].seed = seed; graphs_dirty_ = true; }
+  // salt of the SDF / moment tower dropout stream of model g (0 = none): the LSTM inter-layer
+  // masks keep the plain seed, so N-sharded ranks agree on the replicated LSTM while their
+  // local stocks draw independent tower masks
+  void set_tower_salt(int g, unsigned salt) { models_[check_g(g)].tower_salt = salt; graphs_dirty_ = true; }
+  unsigned tower_seed(int g) const {
+    const ModelState& S = models_[g];
+    return S.tower_salt ? S.seed ^ (S.tower_salt * 0x9E3779B9u + 0x7F4A7C15u) : S.seed;
+  }
   void set_lr(int g, float lr) { models_[check_g(g)].lr = lr; graphs_dirty_ = true; }
   py::dict get_opt_state(int g) {
     ModelState& S = models_[check_g(g)];
@@ -1122,7 +1131,7 @@ class Engine {
     J.z = reinterpret_cast<const f32x4*>(W.z.p);
     J.step = models_[g].drop_step.p;
     J.R = D.R; J.N = D.N; J.T = D.T;
-    J.seed = models_[g].seed;
+    J.seed = tower_seed(g);
     J.train = train; J.do_sdf = do_sdf; J.do_mom = do_mom;
     const int nsl = std::max(md_.nslice_s, md_.nslice_m);
     J.slab_base = g * nsl * gx_bwd_;
@@ -1682,6 +1691,7 @@ PYBIND11_MODULE(_dlap_hip, m) {
       .def("get_snapshot", &Engine::get_snapshot)
       .def("load_snapshot", &Engine::load_snapshot)
       .def("set_seed", &Engine::set_seed)
+      .def("set_tower_salt", &Engine::set_tower_salt)
       .def("get_opt_state", &Engine::get_opt_state)
       .def("set_opt_state", &Engine::set_opt_state)
       .def("get_tracker_state", &Engine::get_tracker_state)

@@ -7,7 +7,8 @@ Sharpe with ddof=0; individual test Sharpe; comparison with the paper's 0.75), s
 
 On a GPU the weights of all checkpoints that share an architecture are produced by ONE batched
 native-engine forward per split (models stacked along the engine's job axis) instead of one
-PyTorch forward per model.
+PyTorch forward per model; they stay on the device, where the K11 kernel (``k_ensemble``)
+averages, re-normalises and forms the portfolio series (one host transfer per split).
 """
 from __future__ import annotations
 
@@ -21,7 +22,8 @@ import torch
 
 from ..data.dataset import load_splits
 from ..models.gan import AssetPricingGAN
-from .portfolio import PAPER_TEST_SHARPE, average_weights, ensemble_sharpes, paper_metrics
+from .portfolio import (PAPER_TEST_SHARPE, average_weights, ensemble_sharpes, ensemble_sharpes_device,
+                        paper_metrics)
 from .portfolio import sharpe_ddof0 as compute_sharpe  # noqa: F401  (reference name)
 
 SPLITS = ("train", "valid", "test")
@@ -47,12 +49,20 @@ def get_weights_from_model(model, data: Dict, device: str = "cpu") -> np.ndarray
     return w.detach().cpu().numpy()
 
 
-def weights_batched_gpu(models: Sequence, batches: Dict[str, Dict]) -> List[Dict[str, np.ndarray]]:
-    """L1-normalised weights of every model on every split, one batched engine pass per split
-    for each group of models that share an architecture."""
+def weights_batched_gpu(models: Sequence, batches: Dict[str, Dict]) -> Dict[str, torch.Tensor]:
+    """L1-normalised weights of every model on every split as CUDA tensors [G, T, N] (model
+    order), one batched engine forward per split for each group of models that share an
+    architecture. Everything stays on the device: the engine's ``wn`` buffers are copied
+    device-to-device into the stack (ordered after torch's stream with events, no host sync) and
+    normalised there."""
     from ..engine.runner import GANEngine
     from ..models.losses import l1_normalize
-    out: List[Dict[str, np.ndarray]] = [dict() for _ in models]
+    dev = torch.device("cuda", torch.cuda.current_device())
+    ts = torch.cuda.current_stream(dev).cuda_stream
+    out = {}
+    for split in SPLITS:
+        T, N = batches[split]["mask"].shape
+        out[split] = torch.empty(len(models), T, N, dtype=torch.float32, device=dev)
     groups: Dict[object, List[int]] = {}
     for i, m in enumerate(models):
         groups.setdefault(m.spec, []).append(i)
@@ -61,13 +71,17 @@ def weights_batched_gpu(models: Sequence, batches: Dict[str, Dict]) -> List[Dict
         eng.set_data(batches["train"], batches["valid"], batches["test"])
         for g, i in enumerate(idx):
             eng.set_model(g, models[i], 0)
+        e = eng.eng
+        e.join_from(ts)
         for s, split in enumerate(SPLITS):
-            b = batches[split]
-            T, N = b["mask"].shape
-            eng.eng.forward_split(s, False, False)
+            e.forward_split(s, False, False)
             for g, i in enumerate(idx):
-                w = torch.from_numpy(eng.eng.read_ws(g, s, "wn").reshape(T, N))
-                out[i][split] = l1_normalize(w, b["mask"]).numpy()
+                e.copy_ws(g, s, "wn", out[split][i].data_ptr())
+        e.join_to(ts)
+        e.sync()         # the engine (and its buffers) may be freed after this group
+    for split in SPLITS:
+        m = batches[split]["mask"].to(dev)
+        out[split] = l1_normalize(out[split], m[None].expand_as(out[split]))
     return out
 
 
@@ -89,13 +103,19 @@ def evaluate_ensemble(checkpoint_dirs: Sequence[str], data_dir: str, device: str
     for i, d in enumerate(checkpoint_dirs):
         say(f"  Model {i + 1}/{len(checkpoint_dirs)}: {os.path.basename(os.path.normpath(d))}")
         models.append(load_model(d, "cpu")[0])
-    if str(device).startswith("cuda"):
-        weights = weights_batched_gpu(models, batches)
-    else:
-        weights = [{s: get_weights_from_model(m, batches[s], "cpu") for s in SPLITS} for m in models]
     np_batches = {s: {"returns": batches[s]["returns"].numpy(), "mask": batches[s]["mask"].numpy()}
                   for s in SPLITS}
-    res = ensemble_sharpes(weights, np_batches)
+    if str(device).startswith("cuda"):
+        # batched engine forward + K11 (k_ensemble) averaging on the device: the [T] ensemble
+        # and [G, T] individual portfolio series are the only host transfers
+        wdev = weights_batched_gpu(models, batches)
+        res = ensemble_sharpes_device(wdev, np_batches)
+        weights = None
+        if paper:
+            weights = [{s: wdev[s][i].cpu().numpy() for s in SPLITS} for i in range(len(models))]
+    else:
+        weights = [{s: get_weights_from_model(m, batches[s], "cpu") for s in SPLITS} for m in models]
+        res = ensemble_sharpes(weights, np_batches)
     ind = res["individual_sharpes"]
     say(); say(bar); say("INDIVIDUAL MODEL RESULTS (for comparison)"); say(bar); say()
     for i, s in enumerate(ind):

@@ -55,7 +55,8 @@ class _Panel:
                    for s, b in self.batches.items()}
         models = [load_model(d, "cpu")[0] for d in checkpoint_dirs]
         if str(device).startswith("cuda"):
-            self.weights = weights_batched_gpu(models, self.batches)
+            wdev = weights_batched_gpu(models, self.batches)
+            self.weights = [{s: wdev[s][i].cpu().numpy() for s in SPLITS} for i in range(len(models))]
         else:
             self.weights = [{s: get_weights_from_model(m, self.batches[s]) for s in SPLITS} for m in models]
 

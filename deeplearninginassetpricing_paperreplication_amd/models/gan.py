@@ -165,7 +165,7 @@ class AssetPricingGAN(nn.Module):
                 phase: str = "conditional") -> Dict[str, torch.Tensor]:
         if individual_features.is_cuda:
             from ..ops.fused import gan_forward
-            return gan_forward(self, macro_features, individual_features, returns, mask, phase)
+            return gan_forward(self, macro_features, individual_features, returns, mask, phase, hidden)
         weights, new_hidden = self.sdf_net(macro_features, individual_features, mask, hidden)
         moments = self.moment_net(self._moment_input(macro_features, individual_features))
         zero = torch.zeros((), device=weights.device)
@@ -195,7 +195,7 @@ class AssetPricingGAN(nn.Module):
                     normalized: bool = False):
         if individual_features.is_cuda:
             from ..ops.fused import gan_weights
-            return gan_weights(self, macro_features, individual_features, mask, normalized), None
+            return gan_weights(self, macro_features, individual_features, mask, normalized, hidden)
         w, new_hidden = self.sdf_net(macro_features, individual_features, mask, hidden)
         if normalized:
             w = L.l1_normalize(w, mask)
@@ -222,9 +222,9 @@ class SimpleSDF(nn.Module):
         self.net = nn.Sequential(*mods)
 
     def forward(self, macro_features, individual_features, returns, mask):
-        if individual_features.is_cuda:          # native engine (ops.fused.simple_forward)
-            if not any(isinstance(m, nn.ReLU) for m in self.net):
-                raise NotImplementedError("SimpleSDF on the GPU engine needs at least one hidden layer")
+        # native engine (ops.fused.simple_forward); without hidden layers the model is one
+        # Linear -- a library GEMV, no tower to fuse -- and the torch ops below run it
+        if individual_features.is_cuda and any(isinstance(m, nn.ReLU) for m in self.net):
             from ..ops.fused import simple_forward
             return simple_forward(self, macro_features, individual_features, returns, mask)
         T, N, _ = individual_features.shape

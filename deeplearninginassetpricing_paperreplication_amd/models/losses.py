@@ -61,18 +61,15 @@ def residual_loss(weights: torch.Tensor, returns: torch.Tensor, mask: torch.Tens
     m = mask.float()
     n = m.sum(dim=1)
     use = n >= 2
-    if not bool(use.any()):
-        return torch.zeros((), device=weights.device, dtype=weights.dtype)
     ww = (weights * weights * m).sum(dim=1)
     rw = (returns * weights * m).sum(dim=1)
     has = use & (ww > 1e-8)
     beta = torch.where(has, rw / torch.where(has, ww, torch.ones_like(ww)), torch.zeros_like(ww))
     resid = ((returns - beta.unsqueeze(1) * weights) ** 2 * m).sum(dim=1) / n.clamp(min=1)
     rsq = (returns ** 2 * m).sum(dim=1) / n.clamp(min=1)
-    if not bool(has.any()):
-        return torch.zeros((), device=weights.device, dtype=weights.dtype)
-    resid_mean = (resid * has.float()).sum() / has.float().sum()
-    rsq_mean = (rsq * use.float()).sum() / use.float().sum()
+    # no host sync: with no usable period the masked numerators are 0 and the loss is exactly 0
+    resid_mean = (resid * has.float()).sum() / has.float().sum().clamp(min=1)
+    rsq_mean = (rsq * use.float()).sum() / use.float().sum().clamp(min=1)
     return resid_mean / rsq_mean.clamp(min=1e-8)
 
 

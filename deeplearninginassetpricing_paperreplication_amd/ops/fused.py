@@ -13,21 +13,35 @@ changed since the last call), results come back as device-to-device copies into 
 and the dropout stream advances with a one-int kernel -- a forward / backward pair issues no
 host synchronisation (a training step's only sync is the caller's ``.item()``). The engine keeps
 its own copy of the panel (compacted valid rows) and re-uploads it only when the input tensors
-changed. ``loss`` is differentiable w.r.t. the module's parameters through ``_EngineLoss`` (the
-engine's analytic backward); the other outputs are detached, as in every training / evaluation
-path of the reference. ``hidden`` is the engine LSTM's final (h_n, c_n) of every layer.
+changed.
 
-Gradient scopes per phase (what ``loss.backward()`` produces, as in autograd):
+Autograd (as the reference's modules, `/root/reference/src/model.py:553-563`):
+  * ``loss`` -> the engine's analytic backward of the fused loss (``_EngineLoss``);
+  * ``weights`` / ``portfolio_returns`` -> the raw SDF weights enter torch through ``_TowerW``
+    (zero-mean normalisation and the portfolio sum are torch ops) whose backward is the engine's
+    SDF tower backward from the incoming dL/dw (``Engine.xs_backward``, phase 1);
+  * ``moments`` -> ``_TowerH``: the engine's moment tower backward from dL/dh (phase 2);
+  * ``hidden`` (an initial (h0, c0) passed in) -> dL/d(h0, c0) from the LSTM backward.
+So a caller's loss built from any output backpropagates to the parameters; combined losses
+accumulate through the separate paths. The residual term (``residual_loss_factor``) is a torch
+function of the differentiable weights, the engine computes the moment losses only (this also
+gives the 'moment' phase's SDF gradient with a residual term).
+
+Gradient scopes of ``loss`` per phase (what ``loss.backward()`` produces, as in autograd):
   * 'unconditional': SDF params <- engine phase-1 backward; moment params get no gradient.
   * 'conditional'  : SDF params <- phase-3 backward; moment params <- -(phase-2 backward)
                      (phase 2 differentiates -L_cond).
-  * 'moment'       : moment params <- phase-2 backward; SDF params <- -(phase-3 backward)
-                     (only exact with residual_loss_factor == 0; with a residual term the SDF
-                     side is unsupported and raises, the reference freezes it in that phase).
+  * 'moment'       : moment params <- phase-2 backward; SDF params <- -(phase-3 backward).
+
+The tower precision is ``set_precision('bf16' | 'fp32')`` (default bf16, or the
+``DLAP_MODULE_PRECISION`` environment variable); fp32 is the reference's precision.
+A repeated forward redraws the dropout masks: backpropagate a forward's outputs before the
+next forward of the same model (the engine recomputes the masks of the last forward).
 """
 from __future__ import annotations
 
 import dataclasses
+import os
 from collections import OrderedDict
 from typing import Dict, List, Optional
 
@@ -42,23 +56,37 @@ _CACHE_MAX = 4
 SC = dict(loss_cond=0, loss_unc=1, loss_res=2, train_sharpe=3)
 
 
+_PRECISION = {"value": os.environ.get("DLAP_MODULE_PRECISION", "bf16")}
+
+
+def set_precision(precision: str) -> None:
+    """Tower precision of the module-level GPU path: 'bf16' (default) or 'fp32' (reference)."""
+    if precision not in ("bf16", "fp32"):
+        raise ValueError(f"precision must be 'bf16' or 'fp32', not {precision!r}")
+    _PRECISION["value"] = precision
+
+
 class _Slot:
-    def __init__(self, spec):
+    def __init__(self, spec, precision):
         from ..engine.runner import GANEngine
-        self.eng = GANEngine(spec, 1, max_epochs=8)
+        self.eng = GANEngine(spec, 1, max_epochs=8, precision=precision)
         self.spec = spec
         self.data_key = None
         self.param_key = None
         self.T = self.N = 0
+        self.idx = None                 # flat indices of the valid (t, i): the engine's row order
+        self.hidden_set = False
         self.step = 0
-        self.eng.eng.set_seed(0, 0x5EED)
+        # the dropout stream: seeded from torch's generator (torch.manual_seed reproduces it)
+        self.eng.eng.set_seed(0, int(torch.randint(0, 2 ** 31 - 1, (1,)).item()))
 
 
 def _slot(spec) -> _Slot:
-    key = repr(spec)
+    prec = _PRECISION["value"]
+    key = (repr(spec), prec)
     s = _CACHE.get(key)
     if s is None:
-        s = _Slot(spec)
+        s = _Slot(spec, prec)
         _CACHE[key] = s
         while len(_CACHE) > _CACHE_MAX:
             _CACHE.popitem(last=False)
@@ -97,10 +125,12 @@ def _release(s: _Slot, ts: int):
 
 
 def _prepare(model, spec: ModelSpec, params: List[torch.Tensor], flat_fn, macro, individual, returns, mask,
-             training: bool) -> _Slot:
+             training: bool, hidden=None) -> _Slot:
     # eval mode: an engine built without dropout, so the analytic backward of an eval forward
-    # (rare, but legal in autograd) sees exactly the forward's activations
+    # (rare, but legal in autograd) sees exactly the forward's activations; the residual term is
+    # a torch function of the differentiable weights (the engine computes the moment losses)
     sp = spec if training else dataclasses.replace(spec, dropout=0.0)
+    sp = dataclasses.replace(sp, residual_loss_factor=0.0)
     s = _slot(sp)
     dev = individual.device
     torch.cuda.set_device(dev)
@@ -113,6 +143,7 @@ def _prepare(model, spec: ModelSpec, params: List[torch.Tensor], flat_fn, macro,
         s.eng.set_data(batch)
         s.data_key = key
         s.T, s.N = int(mask.shape[0]), int(mask.shape[1])
+        s.idx = mask.detach().reshape(-1).bool().nonzero().reshape(-1)   # (one sync per new panel)
     pkey = tuple((p.data_ptr(), p._version) for p in params)
     if pkey != s.param_key:
         s._flat = flat_fn(dev).contiguous()            # kept alive until the next call
@@ -120,6 +151,14 @@ def _prepare(model, spec: ModelSpec, params: List[torch.Tensor], flat_fn, macro,
     if pkey != s.param_key:
         s.eng.eng.set_params_dev(0, s._flat.data_ptr())
         s.param_key = pkey
+    if hidden is not None:
+        h0, c0 = (x.detach().reshape(-1).to(dev, torch.float32).contiguous() for x in hidden)
+        s._hidden = (h0, c0)                                       # kept alive until copied
+        s.eng.eng.set_hidden(0, 0, h0.data_ptr(), c0.data_ptr())
+        s.hidden_set = True
+    elif s.hidden_set:
+        s.eng.eng.set_hidden(0, 0, 0, 0)
+        s.hidden_set = False
     if training:
         # fresh dropout masks per call (the reference draws new Bernoulli masks every forward)
         s.step += 1
@@ -135,10 +174,24 @@ def _copy(s: _Slot, name: str, n: int, dev) -> torch.Tensor:
     return out
 
 
+def _hidden_grad(s: _Slot, spec: ModelSpec, dev, ts):
+    """dL/d(h0, c0) of the last LSTM backward, shaped like nn.LSTM's state [layers, 1, H]."""
+    Lr, H = spec.rnn_layers, spec.rnn_hidden
+    dh = torch.empty(Lr, 1, H, dtype=torch.float32, device=dev)
+    dc = torch.empty(Lr, 1, H, dtype=torch.float32, device=dev)
+    s.eng.eng.join_from(ts)
+    s.eng.eng.copy_hidden_grad(0, dh.data_ptr(), dc.data_ptr())
+    _release(s, ts)
+    return dh, dc
+
+
 class _EngineLoss(torch.autograd.Function):
+    """The engine's fused moment loss (no residual term) as a function of the parameters and of
+    an initial LSTM state (h0, c0) when one was passed (``nh`` = 2, else 0)."""
+
     @staticmethod
-    def forward(ctx, loss_value, slot, spec, phase_id, res_factor, to_params, *params):
-        ctx.slot, ctx.spec, ctx.phase_id, ctx.res, ctx.to_params = slot, spec, phase_id, res_factor, to_params
+    def forward(ctx, loss_value, slot, spec, phase_id, to_params, nh, *inputs):
+        ctx.slot, ctx.spec, ctx.phase_id, ctx.to_params, ctx.nh = slot, spec, phase_id, to_params, nh
         return loss_value.clone()
 
     @staticmethod
@@ -149,6 +202,7 @@ class _EngineLoss(torch.autograd.Function):
         ts = _bind(s, dev)
         P = sum(int(n) for n in ctx.spec.param_counts())
         P_sdf = ctx.spec.param_counts()[0]
+        hg = [None, None]
 
         def grads(phase):
             out = torch.empty(P, dtype=torch.float32, device=dev)
@@ -156,6 +210,10 @@ class _EngineLoss(torch.autograd.Function):
             eng.backward_only(phase, False)
             eng.copy_grads(0, out.data_ptr())
             _release(s, ts)
+            if phase != 2 and ctx.nh:  # the SDF-side LSTM backward also gave dL/d(h0, c0)
+                dh, dc = _hidden_grad(s, ctx.spec, dev, ts)
+                sign = -1.0 if ctx.phase_id == 2 else 1.0
+                hg[0], hg[1] = sign * dh * g, sign * dc * g
             return out
 
         flat = torch.zeros(P, dtype=torch.float32, device=dev)
@@ -166,10 +224,68 @@ class _EngineLoss(torch.autograd.Function):
             flat[P_sdf:] = -grads(2)[P_sdf:]
         else:
             flat[P_sdf:] = grads(2)[P_sdf:]
-            if ctx.res > 0:
-                raise NotImplementedError("SDF gradient of the 'moment' loss with a residual term")
             flat[:P_sdf] = -grads(3)[:P_sdf]
-        return (None, None, None, None, None, None, *ctx.to_params(flat * g))
+        return (None, None, None, None, None, None, *ctx.to_params(flat * g), *hg[:ctx.nh])
+
+
+class _TowerW(torch.autograd.Function):
+    """Raw SDF weights [T, N] (zero where masked) of the engine's forward as a function of the
+    SDF parameters (and of (h0, c0) when passed): backward = the engine's SDF tower + LSTM
+    backward from the incoming dL/dw (``Engine.xs_backward`` phase 1)."""
+
+    @staticmethod
+    def forward(ctx, w_raw, slot, spec, to_params, nh, *inputs):
+        ctx.slot, ctx.spec, ctx.to_params, ctx.nh = slot, spec, to_params, nh
+        return w_raw.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        s = ctx.slot
+        dev = g.device
+        ts = _bind(s, dev)
+        P = sum(int(n) for n in ctx.spec.param_counts())
+        P_sdf = ctx.spec.param_counts()[0]
+        dwc = g.reshape(-1).index_select(0, s.idx).float().contiguous()     # engine row order
+        if dwc.numel() == 0:
+            dwc = torch.zeros(1, device=dev)
+        out = torch.empty(P, dtype=torch.float32, device=dev)
+        s.eng.eng.join_from(ts)
+        s.eng.eng.xs_backward(1, dwc.data_ptr(), 0, 0)
+        s.eng.eng.copy_grads(0, out.data_ptr())
+        _release(s, ts)
+        s._keep = dwc
+        flat = torch.zeros(P, dtype=torch.float32, device=dev)
+        flat[:P_sdf] = out[:P_sdf]
+        hg = list(_hidden_grad(s, ctx.spec, dev, ts)) if ctx.nh else []
+        return (None, None, None, None, None, *ctx.to_params(flat), *hg)
+
+
+class _TowerH(torch.autograd.Function):
+    """Moments [K, T, N] of the engine's forward as a function of the moment parameters:
+    backward = the engine's moment tower backward from dL/dh (``Engine.xs_backward`` phase 2)."""
+
+    @staticmethod
+    def forward(ctx, h, slot, spec, to_params, *params):
+        ctx.slot, ctx.spec, ctx.to_params = slot, spec, to_params
+        return h.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        s = ctx.slot
+        dev = g.device
+        ts = _bind(s, dev)
+        P = sum(int(n) for n in ctx.spec.param_counts())
+        P_sdf = ctx.spec.param_counts()[0]
+        dh = g.permute(1, 2, 0).float().contiguous()                       # engine layout [T][N][K]
+        out = torch.empty(P, dtype=torch.float32, device=dev)
+        s.eng.eng.join_from(ts)
+        s.eng.eng.xs_backward(2, 0, 0, 0, dh.data_ptr())
+        s.eng.eng.copy_grads(0, out.data_ptr())
+        _release(s, ts)
+        s._keep_h = dh
+        flat = torch.zeros(P, dtype=torch.float32, device=dev)
+        flat[P_sdf:] = out[P_sdf:]
+        return (None, None, None, None, *ctx.to_params(flat))
 
 
 def _split_flat(spec: ModelSpec, params: List[torch.Tensor]):
@@ -180,30 +296,45 @@ def _split_flat(spec: ModelSpec, params: List[torch.Tensor]):
     return to_params
 
 
-def gan_forward(model, macro, individual, returns, mask, phase: str = "conditional") -> Dict:
+def _dense_raw(s: _Slot, dev) -> torch.Tensor:
+    """The engine's raw SDF weights of the train split as a dense [T, N] tensor (0 where masked)."""
+    R = int(s.idx.numel())
+    wc = _copy(s, "w", max(R, 1), dev)
+    return torch.zeros(s.T * s.N, dtype=torch.float32, device=dev).index_copy(0, s.idx, wc[:R]).reshape(s.T, s.N)
+
+
+def gan_forward(model, macro, individual, returns, mask, phase: str = "conditional", hidden=None) -> Dict:
     if phase not in _PHASE:
         raise ValueError(f"unknown phase {phase!r}")
     dev = individual.device
+    spec = model.spec
     params = _ordered_params(model)
-    s = _prepare(model, model.spec, params, lambda d: _flat_params(params, d), macro, individual, returns,
-                 mask, bool(model.training))
+    if hidden is not None and (spec.rnn_layers == 0 or macro is None):
+        hidden = None                                # (no LSTM: the reference ignores it too)
+    s = _prepare(model, spec, params, lambda d: _flat_params(params, d), macro, individual, returns,
+                 mask, bool(model.training), hidden)
     eng = s.eng.eng
     eng.forward_split(0, bool(model.training), True, False)
-    T, N, K = s.T, s.N, model.spec.num_moments
+    T, N, K = s.T, s.N, spec.num_moments
+    res_f = float(spec.residual_loss_factor)
+    grad = torch.is_grad_enabled() and (any(q.requires_grad for q in params) or
+                                        (hidden is not None and any(x.requires_grad for x in hidden)))
     sc = _copy(s, "scal", 8, dev)
-    wn = _copy(s, "wn", T * N, dev).reshape(T, N)
     h = _copy(s, "h", T * N * K, dev).reshape(T, N, K).permute(2, 0, 1)
-    p = _copy(s, "P", T, dev)
-    hidden = None
-    if model.spec.rnn_layers > 0 and macro is not None:
-        Lr, H = model.spec.rnn_layers, model.spec.rnn_hidden
-        h_n = torch.empty(Lr, 1, H, device=dev)
-        c_n = torch.empty(Lr, 1, H, device=dev)
-        eng.copy_hidden(0, h_n.data_ptr(), c_n.data_ptr())
-        hidden = (h_n, c_n)
-    _release(s, s.ts)                  # torch's stream waits for the engine's results
-    l_cond, l_unc, l_res = sc[SC["loss_cond"]], sc[SC["loss_unc"]], sc[SC["loss_res"]]
-    res_f = float(model.spec.residual_loss_factor)
+    w_raw = _dense_raw(s, dev) if (grad or res_f > 0) else None
+    wn = _copy(s, "wn", T * N, dev).reshape(T, N) if w_raw is None else None
+    p = _copy(s, "P", T, dev) if w_raw is None else None
+    new_hidden = _new_hidden(s, spec, macro, dev)
+    _release(s, s.ts)                 # torch's stream waits for the engine's results
+    hin = list(hidden) if hidden is not None else []
+    if w_raw is not None:
+        to_p = _split_flat(spec, params)
+        if grad:
+            w_raw = _TowerW.apply(w_raw, s, spec, to_p, len(hin), *params, *hin)
+            h = _TowerH.apply(h, s, spec, to_p, *params)
+        wn = L.zero_mean_normalize(w_raw, mask) if spec.normalize_w else w_raw * mask.float()
+        p = L.portfolio_returns(wn, returns, mask, spec.weighted_loss)
+    l_cond, l_unc = sc[SC["loss_cond"]], sc[SC["loss_unc"]]
     zero = torch.zeros((), device=dev)
     if phase == "unconditional":
         total, l_cond_out, l_unc_out = l_unc, zero, l_unc
@@ -211,16 +342,17 @@ def gan_forward(model, macro, individual, returns, mask, phase: str = "condition
         total, l_cond_out, l_unc_out = -l_cond, l_cond, zero
     else:
         total, l_cond_out, l_unc_out = l_cond, l_cond, l_unc
-    if res_f > 0:
-        total = total + res_f * l_res
     loss = total.clone()
-    if torch.is_grad_enabled() and any(q.requires_grad for q in params):
-        loss = _EngineLoss.apply(loss, s, model.spec, _PHASE[phase], res_f, _split_flat(model.spec, params),
-                                 *params)
+    if grad:
+        loss = _EngineLoss.apply(loss, s, spec, _PHASE[phase], _split_flat(spec, params), len(hin), *params, *hin)
+    l_res = zero
+    if res_f > 0:
+        l_res = L.residual_loss(wn, returns, mask)
+        loss = loss + res_f * l_res
     return {
         "weights": wn, "loss": loss, "loss_unconditional": l_unc_out, "loss_conditional": l_cond_out,
-        "loss_residual": l_res if res_f > 0 else zero,
-        "sharpe": L.sharpe_monitor(p), "portfolio_returns": p, "hidden": hidden, "moments": h,
+        "loss_residual": l_res, "sharpe": L.sharpe_monitor(p), "portfolio_returns": p,
+        "hidden": new_hidden, "moments": h,
     }
 
 
@@ -236,17 +368,44 @@ def _zeros_like_mask(mask):
     return zeros
 
 
-def gan_weights(model, macro, individual, mask, normalized: bool = False) -> torch.Tensor:
+def _new_hidden(s: _Slot, spec: ModelSpec, macro, dev):
+    """Final LSTM state (h_n, c_n) of the last forward, shaped like nn.LSTM's; None without an LSTM."""
+    if spec.rnn_layers == 0 or macro is None:
+        return None
+    Lr, H = spec.rnn_layers, spec.rnn_hidden
+    h_n = torch.empty(Lr, 1, H, device=dev)
+    c_n = torch.empty(Lr, 1, H, device=dev)
+    s.eng.eng.copy_hidden(0, h_n.data_ptr(), c_n.data_ptr())
+    return h_n, c_n
+
+
+def gan_weights(model, macro, individual, mask, normalized: bool = False, hidden=None):
+    """``get_weights`` on the engine: (weights, new LSTM state). The weights are differentiable
+    in the SDF parameters (and in ``hidden``) when grad mode is on."""
     # get_weights has no returns argument: a cached zero panel keeps the upload cache valid
+    spec = model.spec
     params = _ordered_params(model)
-    s = _prepare(model, model.spec, params, lambda d: _flat_params(params, d), macro, individual,
-                 _zeros_like_mask(mask), mask, bool(model.training))
+    if hidden is not None and (spec.rnn_layers == 0 or macro is None):
+        hidden = None
+    s = _prepare(model, spec, params, lambda d: _flat_params(params, d), macro, individual,
+                 _zeros_like_mask(mask), mask, bool(model.training), hidden)
     s.eng.eng.forward_split(0, bool(model.training), False, False)
-    w = _copy(s, "wn", s.T * s.N, individual.device).reshape(s.T, s.N)
+    dev = individual.device
+    grad = torch.is_grad_enabled() and (any(q.requires_grad for q in params) or
+                                        (hidden is not None and any(x.requires_grad for x in hidden)))
+    if grad:
+        w_raw = _dense_raw(s, dev)
+    else:
+        w = _copy(s, "wn", s.T * s.N, dev).reshape(s.T, s.N)
+    new_hidden = _new_hidden(s, spec, macro, dev)
     _release(s, s.ts)
+    if grad:
+        hin = list(hidden) if hidden is not None else []
+        w_raw = _TowerW.apply(w_raw, s, spec, _split_flat(spec, params), len(hin), *params, *hin)
+        w = L.zero_mean_normalize(w_raw, mask) if spec.normalize_w else w_raw * mask.float()
     if normalized:
         w = L.l1_normalize(w, mask)
-    return w
+    return w, new_hidden
 
 
 # ---- SimpleSDF (`/root/reference/src/model.py:620-694`) on the engine ---------------------
@@ -315,5 +474,5 @@ def simple_forward(model, macro, individual, returns, mask) -> Dict:
     _release(s, s.ts)
     loss = sc[SC["loss_unc"]].clone()
     if torch.is_grad_enabled() and any(q.requires_grad for q in params):
-        loss = _EngineLoss.apply(loss, s, s.spec, 1, 0.0, _simple_to_params(model, spec), *params)
+        loss = _EngineLoss.apply(loss, s, s.spec, 1, _simple_to_params(model, spec), 0, *params)
     return {"weights": w, "loss": loss, "sharpe": L.sharpe_monitor(p), "portfolio_returns": p}

@@ -173,12 +173,25 @@ def run_bucket(entries, idx: List[int], batches: Dict[str, Dict], device: torch.
     return out
 
 
-def plan(entries, world: int, balance: str = "lpt") -> Tuple[List[List[int]], List[List[int]], List[float]]:
+def plan(entries, world: int, balance: str = "lpt", dist: Optional[comm.Dist] = None
+         ) -> Tuple[List[List[int]], List[List[int]], List[float]]:
     """(buckets, per-rank bucket lists, per-bucket cost). ``balance``: "lpt" (cost-aware,
-    default) or "round_robin"."""
+    default) or "round_robin".
+
+    With an active process group the ranks plan from RANK 0's cost vector (one all-gather of
+    the [n_buckets] costs): every rank reads ``sweep_costs.json`` from its own filesystem, and
+    LPT is only consistent when all ranks see the same costs -- a stale or missing table on one
+    node would otherwise give ranks different ``owners`` and misplace rows in the result
+    all-gather without an error."""
     bks = buckets(entries)
     table = _load_costs()
     costs = [bucket_cost(ModelSpec.from_config(entries[b[0]][0]), len(b), table) for b in bks]
+    if dist is not None and dist.active:
+        allc = comm.all_gather_rows(dist, np.asarray([costs], np.float64), dist.world, [dist.rank])
+        if not np.array_equal(allc[0], allc[dist.rank]):
+            print(f"[sweep rank {dist.rank}] bucket costs differ from rank 0's "
+                  f"(sweep_costs.json out of sync?); planning with rank 0's", flush=True)
+        costs = [float(c) for c in allc[0]]
     if balance == "lpt":
         owners = comm.assign_lpt(costs, world)
     else:
@@ -191,7 +204,7 @@ def run_sweep(batches: Dict[str, Dict], entries, dist: Optional[comm.Dist] = Non
               rank_sign: float = -1.0, fail_buckets: Sequence[int] = (), verbose: bool = False,
               concurrency: Optional[int] = None, balance: str = "lpt") -> Dict:
     d = dist or comm.Dist()
-    bks, owners, costs = plan(entries, d.world, balance)
+    bks, owners, costs = plan(entries, d.world, balance, d)
     mine = owners[d.rank]
     local = {}
     errors = {}

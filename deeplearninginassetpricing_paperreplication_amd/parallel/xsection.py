@@ -100,7 +100,7 @@ class EngineTowers:
     `MacroLSTM` (`/root/reference/src/model.py:21-279`)."""
 
     def __init__(self, model: AssetPricingGAN, shards: Sequence[Optional[Dict]], device,
-                 seed: int = 0, precision: str = "bf16"):
+                 seed: int = 0, precision: str = "bf16", tower_salt: int = 0):
         from ..engine.runner import GANEngine
         self.device = torch.device(device)
         self.spec = model.spec
@@ -108,8 +108,11 @@ class EngineTowers:
         dev = [None if b is None else {k: (v.to(self.device) if isinstance(v, torch.Tensor) else v)
                                        for k, v in b.items() if k != "n_total"} for b in shards]
         self.eng.set_data(*dev)
-        # the same seed on every rank: the replicated LSTM draws identical inter-layer masks
+        # the same seed on every rank: the replicated LSTM draws identical inter-layer masks; the
+        # towers' dropout is salted per rank so local stock i of two shards gets independent masks
+        # (the reference draws an independent Bernoulli mask for every (t, stock))
         self.eng.eng.set_seed(0, int(seed) & 0xFFFFFFFF)
+        self.eng.eng.set_tower_salt(0, int(tower_salt) & 0xFFFFFFFF)
         self.masks = {}
         for s, b in enumerate(dev):
             if b is not None:
@@ -265,7 +268,8 @@ class XSectionGAN(AssetPricingGAN):
     def attach_engine(self, shards: Sequence[Optional[Dict]], device, precision: str = "bf16") -> "XSectionGAN":
         """Run the local towers on the native engine (``shards``: this rank's train / valid /
         test dicts, as passed to train_epoch / evaluate)."""
-        self.et = EngineTowers(self, shards, device, seed=self.lstm_seed, precision=precision)
+        self.et = EngineTowers(self, shards, device, seed=self.lstm_seed, precision=precision,
+                               tower_salt=self.dist.rank + 1 if self.dist.active else 0)
         return self
 
     def _engine_pass(self, mask, want_mom: bool):
@@ -279,6 +283,18 @@ class XSectionGAN(AssetPricingGAN):
         if torch.is_grad_enabled() and s == 0:
             w = _TowerSDF.apply(et, s, w, *params[:n_sdf])
         return s, w, h, params[n_sdf:]
+
+    def _global_n(self, returns) -> int:
+        """Total stocks over all ranks for a local width N_r: one all-reduce (and host read) per
+        distinct local width, cached -- a training loop's forwards issue no host sync for it."""
+        n_loc = int(returns.shape[1])
+        if not self.dist.active:
+            return n_loc
+        cache = self.__dict__.setdefault("_n_total", {})
+        if n_loc not in cache:
+            cache[n_loc] = int(all_reduce_sum(torch.tensor([float(n_loc)], device=returns.device),
+                                              self.dist).item())
+        return cache[n_loc]
 
     def _normalize(self, w_raw, mask):
         m = mask.float()
@@ -339,14 +355,13 @@ class XSectionGAN(AssetPricingGAN):
         n, ww, rw, rr = s
         use = n >= 2
         has = use & (ww > 1e-8)
-        if not bool(use.any()) or not bool(has.any()):
-            return torch.zeros((), device=w.device)
         beta = torch.where(has, rw / torch.where(has, ww, torch.ones_like(ww)), torch.zeros_like(ww))
         nc = n.clamp(min=1)
         resid = (rr - 2 * beta * rw + beta * beta * ww) / nc
         rsq = rr / nc
-        resid_mean = (resid * has.float()).sum() / has.float().sum()
-        rsq_mean = (rsq * use.float()).sum() / use.float().sum()
+        # (no host sync: without a usable period both masked numerators are 0 -> loss 0)
+        resid_mean = (resid * has.float()).sum() / has.float().sum().clamp(min=1)
+        rsq_mean = (rsq * use.float()).sum() / use.float().sum().clamp(min=1)
         return resid_mean / rsq_mean.clamp(min=1e-8)
 
     def forward(self, macro_features, individual_features, returns, mask, hidden=None,
@@ -354,8 +369,7 @@ class XSectionGAN(AssetPricingGAN):
         """Same dict as ``AssetPricingGAN.forward`` (`model.py:485-563`): loss, losses, sharpe
         and portfolio returns are global; weights [T, N_r] and moments [K, T, N_r] local."""
         if n_total is None:
-            n_total = int(all_reduce_sum(torch.tensor([float(returns.shape[1])], device=returns.device),
-                                         self.dist).item()) if self.dist.active else returns.shape[1]
+            n_total = self._global_n(returns)
         m = mask.float()
         eng = None
         if self.et is not None:

@@ -87,6 +87,14 @@ def _worker(rank, world, port, outdir, job):
         own[0, mine] = 1.0
         owned = comm.all_gather_rows(d, own, d.world, [d.rank])
         out = {"loads": loads.tolist(), "owned": owned.tolist(), "owners": owners, "n": len(bks)}
+    elif job == "sweep_plan_skew":
+        # rank 1 sees a different (stale) cost table: planning still agrees (rank 0's costs)
+        from deeplearninginassetpricing_paperreplication_amd.parallel import sweep
+        entries = sweep.paper_grid(178, 46)
+        if d.rank == 1:
+            sweep._load_costs = lambda: {sweep.arch_key(sweep.ModelSpec.from_config(entries[0][0])): 1e3}
+        bks, owners, costs = sweep.plan(entries, d.world, "lpt", d)
+        out = {"owners": owners, "costs": costs}
     with open(os.path.join(outdir, f"r{rank}.json"), "w") as fh:
         json.dump(out, fh)
     comm.shutdown(d)
@@ -177,3 +185,10 @@ def test_lpt_assignment_properties():
     loads = [sum(costs[i] for i in o) for o in owners]
     assert max(loads) - min(loads) <= max(costs)
     assert comm.assign_lpt(costs, 3) == owners                  # deterministic
+
+
+def test_sweep_plan_uses_rank0_costs(tmp_path):
+    """each rank reads sweep_costs.json itself; if one rank's table differs, LPT must
+    not diverge across ranks (the result all-gather places rows by ``owners``)."""
+    r = _run("sweep_plan_skew", tmp_path)
+    assert r[0]["owners"] == r[1]["owners"] and r[0]["costs"] == r[1]["costs"]

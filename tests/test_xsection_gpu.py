@@ -160,3 +160,29 @@ def test_engine_xsection_two_ranks_equal_unsharded(tmp_path):
         ge = torch.tensor(res[phase]["grad"])
         assert abs(res[phase]["loss"] - o["loss"].item()) <= 2e-4 * abs(o["loss"].item()), phase
         assert float((ge - gt).norm() / gt.norm()) < 1e-3, phase
+
+
+def test_tower_dropout_independent_across_ranks():
+    """every rank's EngineTowers used the same dropout seed, so local stock i of two
+    shards drew the same tower masks. The towers are now salted per rank (the LSTM keeps the
+    shared seed): equal salts reproduce the masks, different salts give independent ones."""
+    from deeplearninginassetpricing_paperreplication_amd.models.gan import AssetPricingGAN
+    from deeplearninginassetpricing_paperreplication_amd.ops.fused import _ordered_params
+    dev = torch.device("cuda:0")
+    sh = _shards(dev)
+    cfg = default_cli_config(8, 46, dropout=0.3)
+    torch.manual_seed(0)
+    model = AssetPricingGAN(cfg).to(dev)
+    params = _ordered_params(model)
+    outs = {}
+    for salt in (1, 1, 2):
+        et = X.EngineTowers(model, sh, dev, seed=11, precision="fp32", tower_salt=salt)
+        et.sync_params(params, True)
+        w, _ = et.forward(0, True, False)
+        outs.setdefault(salt, []).append(w.clone())
+        torch.cuda.synchronize()
+    m = sh[0]["mask"]
+    a, b, c = outs[1][0][m], outs[1][1][m], outs[2][0][m]
+    assert torch.equal(a, b)
+    frac = float((a != c).float().mean())
+    assert frac > 0.5, frac                # different masks change (almost) every row's output
