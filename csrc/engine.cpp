@@ -188,6 +188,7 @@ class Engine {
     own_st_ = st_;
     HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_gram_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_mid_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_a_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_m3_, hipEventDisableTiming));
@@ -213,6 +214,9 @@ class Engine {
     gram_on_ = env_int("DLAP_GRAM", 1) != 0;
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
                residual, fp32);
+    // fp32 wide path: layer 0 through k_proj0 + the ZIN towers (the fused-layer-0 k_mlp_fwd_zx
+    // is bf16 only)
+    if (fp32) zx_eval_ = zx_train_ = false;
     d_desc_.alloc(sizeof(ModelDesc));
     HIP_LEGACY(hipMemcpy(d_desc_.p, &md_, sizeof(ModelDesc), hipMemcpyHostToDevice));
     models_.resize(G);
@@ -225,7 +229,7 @@ class Engine {
       S.hist.alloc((size_t)max_epochs_ * HIST_W);
       S.adam_step.alloc(2); S.drop_step.alloc(1); S.snap_flags.alloc(2); S.ep.alloc(2);
       S.blob.alloc((size_t)2 * md_.md.blob_frags * 512 * xw());   // bf16 (or fp32: 2 u16 each)
-      S.blob0.alloc((size_t)std::max(1, md_.md.b0_frags) * 512);
+      S.blob0.alloc((size_t)std::max(1, md_.md.b0_frags) * 512 * xw());
       S.wproj.alloc((size_t)(md_.proj_mp + 1) * md_.proj_np);
     }
     ws_.resize((size_t)G * 3);
@@ -253,6 +257,7 @@ class Engine {
     for (auto& kv : graphs_) retire_graph_exec(kv.second);
     if (ev_fork_) (void)hipEventDestroy(ev_fork_);
     if (ev_join_) (void)hipEventDestroy(ev_join_);
+    if (ev_gram_) (void)hipEventDestroy(ev_gram_);
     if (ev_mid_) (void)hipEventDestroy(ev_mid_);
     if (ev_a_) (void)hipEventDestroy(ev_a_);
     for (hipEvent_t e : {ev_m3_, ev_b3_, ev_f3_, ev_in_, ev_out_}) if (e) (void)hipEventDestroy(e);
@@ -359,8 +364,8 @@ class Engine {
     alloc_ws(s);
     if (md_.md.wide && s == 0) {    // rows-as-k copy of the train panel for the weight gradient
       const size_t ntl = (size_t)(R + 31) / 32;
-      D.XT.alloc(std::max<size_t>(ntl * (md_.md.KX / 16) * 512, 1), false);
-      if (R > 0) launch_xt_build(D.X.p, D.XT.p, R, md_.md.KX, st_);
+      D.XT.alloc(std::max<size_t>(ntl * (md_.md.KX / 16) * 512 * xw(), 1), false);
+      if (R > 0) launch_xt_build(D.X.p, D.XT.p, R, md_.md.KX, md_.md.fp32 != 0, st_);
       sync();
     }
     graphs_dirty_ = true;
@@ -505,14 +510,17 @@ class Engine {
     if (ext_stream_) throw std::runtime_error("run_epochs needs the engine's own streams (set_stream(0, False))");
     if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
     if (n <= 0) return;
-    if (phase == 2) h_valid_ = false;     // the moment net trains: the cached moments go stale
-    else ensure_moments(true);
+    const bool pipe = phase != 2 && n_eval_jobs_ > 0 && pipeline_;
+    // the moment net trains in phase 2: the cached moments go stale. Else refresh them (and the
+    // Gram matrices); with the pipelined graphs the evaluation splits' Gram builds overlap the
+    // head epoch (which trains only) on the evaluation stream
+    if (phase == 2) h_valid_ = false;
+    else ensure_moments(true, pipe && use_graph);
     struct GramScope {                    // epoch graphs run the loss in Gram mode
       bool& f;
       explicit GramScope(bool& x) : f(x) { f = true; }
       ~GramScope() { f = false; }
     } gram_scope(gram_run_);
-    const bool pipe = phase != 2 && n_eval_jobs_ > 0 && pipeline_;
     if (!use_graph) {
       for (int e = 0; e < n; ++e) enqueue_epoch(phase, lr, ignore_epoch, sel);
       return;
@@ -537,6 +545,7 @@ class Engine {
       });
     HTRACE("launch head");
     HIP_OK(hipGraphLaunch(head, st_));
+    join_eval_gram();                     // the next graphs evaluate
     int e = 1;
     if (bodyU)
       for (; e + U <= n; e += U) HIP_OK(hipGraphLaunch(bodyU, st_));
@@ -760,6 +769,7 @@ class Engine {
   }
   void sync() {
     g_blocking.fetch_add(1, std::memory_order_relaxed);
+    join_eval_gram();
     HIP_OK(hipStreamSynchronize(st_));
   }
   uintptr_t stream() const { return (uintptr_t)st_; }
@@ -782,6 +792,8 @@ class Engine {
   hipStream_t st3_ = nullptr;
   hipEvent_t ev_m3_ = nullptr, ev_b3_ = nullptr, ev_f3_ = nullptr;
   hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;   // join_from / join_to
+  hipEvent_t ev_gram_ = nullptr;                     // deferred evaluation-split Gram builds done
+  bool eval_gram_pending_ = false;
   bool split_tail_ = false;                  // DLAP_SPLIT_TAIL
   int eval_gx_ = 0;                          // cap on the evaluation tower grid (DLAP_EVAL_GX)
   int b_wait_ = 0;                           // evaluation towers after train towers (DLAP_B_WAIT)
@@ -964,11 +976,9 @@ class Engine {
     D.zc = 8 + 2 * d.WMB;
     D.b0_frags = wide ? (4 + d.WMB) * D.KSX : 0;
     D.fp32 = fp32 ? 1 : 0;
-    if (fp32 && wide)
-      throw std::invalid_argument("precision fp32: the wide layer-0 path (F + per-period inputs > 128) is bf16 only");
     if (fp32 && (size_t)D.blob_frags * 2048 + (size_t)D.aux_floats * 4 > 150 * 1024)
       throw std::invalid_argument("precision fp32: this architecture's fp32 weight fragments exceed the LDS budget");
-    if ((size_t)D.b0_frags * 1024 > 160 * 1024)
+    if (!fp32 && (size_t)D.b0_frags * 1024 > 160 * 1024)     // (k_mlp_fwd_zx stages them; fp32: L2)
       throw std::invalid_argument("feature dim too large for the wide layer-0 kernel (LDS budget)");
     // gradient tiles: layer-0 chunks first (none on the wide path: k_wgrad0), then one tile per
     // later layer (slice = tile, TPS 1)
@@ -1067,8 +1077,8 @@ class Engine {
         ModelSplitWS& W = ws(g, s);
         W.z.alloc(std::max<size_t>(ntl * md_.md.zc * 256, 1), false);
         if (s == 0) {
-          W.dzs.alloc(std::max<size_t>(ntl * 4 * 512, 1), false);
-          W.dzm.alloc(std::max<size_t>(ntl * md_.WMB * 512, 1), false);
+          W.dzs.alloc(std::max<size_t>(ntl * 4 * 512 * xw(), 1), false);      // (fp32: 2 u16 each)
+          W.dzm.alloc(std::max<size_t>(ntl * md_.WMB * 512 * xw(), 1), false);
         }
       }
       if (s == 0) {
@@ -1193,32 +1203,56 @@ class Engine {
   // Gram build job tables of every split (rebuild_jobs): the train split's conditional matrix
   // only if its moments are cacheable. One scratch area, reused split after split.
   void build_gram_jobs() {
-    size_t need = 0;
-    for (int s = 0; s < 3; ++s)
-      if (splits_[s].set) need = std::max(need, gram_part_doubles(splits_[s].T, G_));
-    gram_scratch_.alloc(std::max<size_t>(need, 1), false);
+    // split-K scratch: the train split's region, then one region the valid / test builds share
+    // (those two run one after the other, possibly on the evaluation stream beside the train
+    // split's build and the first epoch: build_gram(defer))
+    const size_t n0 = splits_[0].set ? gram_part_doubles(splits_[0].T, G_) : 0;
+    size_t n12 = 0;
+    for (int s = 1; s < 3; ++s)
+      if (splits_[s].set) n12 = std::max(n12, gram_part_doubles(splits_[s].T, G_));
+    gram_scratch_.alloc(std::max<size_t>(n0 + n12, 1), false);
     for (int s = 0; s < 3; ++s) {
       const SplitDev& D = splits_[s];
       if (!D.set || D.T == 0) continue;
       const bool cond = gram_cond_ok() && (s != 0 || cache_train_h());
       const size_t per = (size_t)gram_slices(D.T, G_) * 2 * D.T * D.T;
+      double* base = gram_scratch_.p + (s == 0 ? 0 : n0);
       std::vector<GramJob> jobs;
       for (int g = 0; g < G_; ++g) {
         jobs.push_back(gram_job(g, s, cond));
-        jobs.back().part = gram_scratch_.p + per * g;
+        jobs.back().part = base + per * g;
       }
       upload(j_gram_[s], jobs);
     }
   }
   // Build the Gram matrices of every (model, split) from the current cached moments.
-  // Stream-ordered on st_ (no host synchronisation).
-  void build_gram() {
+  // Stream-ordered on st_ (no host synchronisation). defer: the evaluation splits' builds go
+  // to the evaluation stream st2_ (after the moment refresh queued so far) and
+  // eval_gram_pending_ is set: the caller joins ev_gram_ into st_ before the first graph that
+  // evaluates (the pipelined head trains only, so they overlap it).
+  void build_gram(bool defer = false) {
     for (int s = 0; s < 3; ++s) {
       const SplitDev& D = splits_[s];
       if (!D.set || D.T == 0) continue;
+      hipStream_t st = st_;
+      if (s > 0 && defer) {
+        if (!eval_gram_pending_) {
+          HIP_OK(hipEventRecord(ev_fork_, st_));
+          HIP_OK(hipStreamWaitEvent(st2_, ev_fork_, 0));
+        }
+        eval_gram_pending_ = true;
+        st = st2_;
+      }
       HTRACE("launch_gram split=%d", s);
-      launch_gram(as<GramJob>(j_gram_[s]), G_, D.T, gram_slices(D.T, G_), st_);
+      launch_gram(as<GramJob>(j_gram_[s]), G_, D.T, gram_slices(D.T, G_), st);
     }
+    if (eval_gram_pending_) HIP_OK(hipEventRecord(ev_gram_, st2_));
+  }
+  // st_ waits for deferred evaluation-split Gram builds (no-op when none is pending)
+  void join_eval_gram() {
+    if (!eval_gram_pending_) return;
+    HIP_OK(hipStreamWaitEvent(st_, ev_gram_, 0));
+    eval_gram_pending_ = false;
   }
 
   void rebuild_jobs() {
@@ -1345,15 +1379,15 @@ class Engine {
   // read them) if the moment parameters may have changed since they were computed.
   // with_gram: also (re)build the Gram matrices (epoch graphs: run_epochs); the module-API
   // steps use the dense loss passes and skip it.
-  void ensure_moments(bool with_gram = false) {
+  void ensure_moments(bool with_gram = false, bool defer_eval_gram = false) {
     if (!h_cache_ || n_mom_jobs_ == 0) return;
     if (h_valid_) {
-      if (with_gram && gram_on_ && !gram_valid_) { build_gram(); gram_valid_ = true; }
+      if (with_gram && gram_on_ && !gram_valid_) { build_gram(defer_eval_gram); gram_valid_ = true; }
       return;
     }
     HTRACE("ensure_moments jobs=%d tmax=%d gx=%d", n_mom_jobs_, tmax_all_, gx_mom_);
     HTRACE("launch_prologue");
-    launch_prologue(as<RnnJob>(j_rnn_mom_), n_mom_jobs_, tmax_all_, dd(), md_, st_);
+    launch_prologue(as<RnnJob>(j_rnn_mom_), n_mom_jobs_, tmax_all_, dd(), md_, st_, true, false);
     if (md_.md.wide && zx_eval_) {
       HTRACE("launch_mlp_fwd_zx");
       launch_mlp_fwd_zx(as<MlpJob>(j_mlp_mom_), n_mom_jobs_, std::max(1, zx_gx_ / n_mom_jobs_), md_.md, md_.WMB, st_);
@@ -1365,7 +1399,7 @@ class Engine {
     }
     h_valid_ = true;
     gram_valid_ = false;
-    if (with_gram && gram_on_) { build_gram(); gram_valid_ = true; }
+    if (with_gram && gram_on_) { build_gram(defer_eval_gram); gram_valid_ = true; }
   }
   bool dropmask_on(int phase) const { return md_.dropout > 0.f && phase != 2; }
   // keep masks of the step *drop_step + offset* (phases 1/3: the SDF tower's dropout)
@@ -1602,6 +1636,7 @@ class Engine {
   void fwd_only(int s, bool train_mode, bool do_mom, bool wait) {
     const SplitDev& D = splits_[s];
     if (!D.set) throw std::runtime_error("split not set");
+    join_eval_gram();
     // job tables of (split, mode) for every model, built once per rebuild (module API calls
     // issue no host allocation / synchronous copy). The train split keeps its LSTM state
     // (final (h, c) of every layer for the module API).

@@ -975,7 +975,7 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
       }
       if constexpr (ZIN) {
         if (j == 0 && s0) {                         // layer-0 dz for k_wgrad0
-          const auto dzo = gp(J.dz_out) + (size_t)tile * 4 * 64 + lane;
+          const auto dzo = gp(reinterpret_cast<Frag*>(J.dz_out)) + (size_t)tile * 4 * 64 + lane;
 #pragma unroll
           for (int u = 0; u < 4; ++u) dzo[u * 64] = dzN[u];
         }
@@ -1223,7 +1223,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
       }
       if constexpr (ZIN) {
         if (j == 0 && slice == 0) {                 // layer-0 dz for k_wgrad0
-          const auto dzo = gp(J.dz_out) + (size_t)tile * WMB * 64 + lane;
+          const auto dzo = gp(reinterpret_cast<Frag*>(J.dz_out)) + (size_t)tile * WMB * 64 + lane;
 #pragma unroll
           for (int u = 0; u < WMB; ++u) dzo[u * 64] = dzN[u];
         }
@@ -1358,10 +1358,10 @@ void launch_mlp_fwd(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int
                     hipStream_t st) {
   dim3 grid(gx, njobs), block(256);
   size_t sh = mlp_lds_bytes(D);
-  if (D.wide) {
-    if (D.fp32) dlap_throw_hip(hipErrorInvalidValue, "mlp_fwd: fp32 towers need the fused path", __FILE__, __LINE__);
-#define FZ_CASE(W) if (WMB == W) { hipLaunchKernelGGL((k_mlp_fwd<PrecBF16, 2, W, true>), grid, block, sh, st, jobs, D); HIP_OK(hipGetLastError()); return; }
-    FZ_CASE(1) FZ_CASE(2) FZ_CASE(4)
+  if (D.wide) {      // layer 0 from k_proj0's z (bf16, or fp32 reference precision)
+#define FZ_CASE(PR, W) if (WMB == W) { hipLaunchKernelGGL((k_mlp_fwd<PR, 2, W, true>), grid, block, sh, st, jobs, D); HIP_OK(hipGetLastError()); return; }
+    if (D.fp32) { FZ_CASE(PrecF32, 1) FZ_CASE(PrecF32, 2) FZ_CASE(PrecF32, 4) }
+    else { FZ_CASE(PrecBF16, 1) FZ_CASE(PrecBF16, 2) FZ_CASE(PrecBF16, 4) }
 #undef FZ_CASE
   }
   const bool ok = D.fp32 ? launch_mlp_fwd_p<PrecF32>(jobs, grid, block, sh, D, KS1, WMB, st)
@@ -1395,9 +1395,9 @@ void launch_mlp_bwd_sdf(const MlpJob* jobs, int njobs, int gx, int nslice, int t
   dim3 grid(gx, njobs, nslice), block(256);
   size_t sh = bwd_lds_bytes(D, slab_stride);
   if (D.wide) {
-    if (D.fp32) dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_sdf: fp32 towers need the fused path", __FILE__, __LINE__);
-#define SZ_CASE(N, T) if (D.nl_sdf == N && tps == T) { hipLaunchKernelGGL((k_mlp_bwd_sdf<PrecBF16, 2, N, T, true>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
-    SZ_CASE(1, 1) SZ_CASE(2, 1) SZ_CASE(3, 1) SZ_CASE(4, 1) SZ_CASE(2, 2)
+#define SZ_CASE(PR, N, T) if (D.nl_sdf == N && tps == T) { hipLaunchKernelGGL((k_mlp_bwd_sdf<PR, 2, N, T, true>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
+    if (D.fp32) { SZ_CASE(PrecF32, 1, 1) SZ_CASE(PrecF32, 2, 1) SZ_CASE(PrecF32, 3, 1) SZ_CASE(PrecF32, 4, 1) SZ_CASE(PrecF32, 2, 2) }
+    else { SZ_CASE(PrecBF16, 1, 1) SZ_CASE(PrecBF16, 2, 1) SZ_CASE(PrecBF16, 3, 1) SZ_CASE(PrecBF16, 4, 1) SZ_CASE(PrecBF16, 2, 2) }
 #undef SZ_CASE
     dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_sdf: unsupported depth (wide)", __FILE__, __LINE__);
   }
@@ -1424,11 +1424,16 @@ void launch_mlp_bwd_mom(const MlpJob* jobs, int njobs, int gx, int nslice, int t
   dim3 grid(gx, njobs, nslice), block(256);
   size_t sh = bwd_lds_bytes(D, slab_stride);
   if (D.wide) {
-    if (D.fp32) dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_mom: fp32 towers need the fused path", __FILE__, __LINE__);
-#define MZ_CASE(W, N) if (WMB == W && D.nl_mom == N && tps == 1) { hipLaunchKernelGGL((k_mlp_bwd_mom<PrecBF16, 2, W, N, 1, true>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
-    MZ_CASE(1, 1) MZ_CASE(2, 1) MZ_CASE(4, 1)
-    MZ_CASE(1, 2) MZ_CASE(2, 2) MZ_CASE(4, 2)
-    MZ_CASE(1, 3) MZ_CASE(2, 3) MZ_CASE(4, 3)
+#define MZ_CASE(PR, W, N) if (WMB == W && D.nl_mom == N && tps == 1) { hipLaunchKernelGGL((k_mlp_bwd_mom<PR, 2, W, N, 1, true>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
+    if (D.fp32) {
+      MZ_CASE(PrecF32, 1, 1) MZ_CASE(PrecF32, 2, 1) MZ_CASE(PrecF32, 4, 1)
+      MZ_CASE(PrecF32, 1, 2) MZ_CASE(PrecF32, 2, 2) MZ_CASE(PrecF32, 4, 2)
+      MZ_CASE(PrecF32, 1, 3) MZ_CASE(PrecF32, 2, 3) MZ_CASE(PrecF32, 4, 3)
+    } else {
+      MZ_CASE(PrecBF16, 1, 1) MZ_CASE(PrecBF16, 2, 1) MZ_CASE(PrecBF16, 4, 1)
+      MZ_CASE(PrecBF16, 1, 2) MZ_CASE(PrecBF16, 2, 2) MZ_CASE(PrecBF16, 4, 2)
+      MZ_CASE(PrecBF16, 1, 3) MZ_CASE(PrecBF16, 2, 3) MZ_CASE(PrecBF16, 4, 3)
+    }
 #undef MZ_CASE
     dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_mom: unsupported depth/width (wide)", __FILE__, __LINE__);
   }

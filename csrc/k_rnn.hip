@@ -550,7 +550,7 @@ static const bool g_rtrace = [] { const char* v = std::getenv("DLAP_TRACE_HOST")
 #define RTRACE(...) do { if (g_rtrace) { fprintf(stderr, "[dlap-trace] " __VA_ARGS__); fputc('\n', stderr); fflush(stderr); } } while (0)
 
 void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* md, const ModelDesc& mh,
-                     hipStream_t st, bool abias) {
+                     hipStream_t st, bool abias, bool lstm) {
   // DLAP_LSTM_FUSE_PROJ=1: the LSTM workgroup projects its own inputs (k_lstm_gls<.., FUSE>) and
   // k_proj only builds the moment network's per-period bias table. Off by default: one
   // workgroup streams the whole macro panel through one CU (15 us at T = 240, M = 178, against
@@ -565,8 +565,8 @@ void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* m
   const int G4 = mh.nrnn > 0 ? 4 * mh.H : 0;
   // column tiles for k_proj: all (abias, unfused), the moment ones only (abias, fused; a tile
   // shared by the last gates and the first moment columns stays), the gates only, or none
-  const int y0 = abias && fuse ? G4 / 16 : 0;
-  const int ny = abias ? mh.proj_np / 16 - y0 : (fuse ? 0 : (G4 + 15) / 16);
+  const int y0 = abias && (fuse || !lstm) ? G4 / 16 : 0;
+  const int ny = abias ? mh.proj_np / 16 - y0 : (fuse || !lstm ? 0 : (G4 + 15) / 16);
   RTRACE("prologue jobs=%p njobs=%d tmax=%d H=%d nrnn=%d proj_np=%d y0=%d ny=%d fuse=%d st=%p", (const void*)jobs,
          njobs, tmax, mh.H, mh.nrnn, mh.proj_np, y0, ny, (int)fuse, (void*)st);
   if (ny > 0) {
@@ -574,7 +574,7 @@ void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* m
     HIP_OK(hipGetLastError());
   }
   RTRACE("prologue proj launched");
-  if (mh.nrnn > 0) {
+  if (mh.nrnn > 0 && lstm) {
     const bool stage = tmax * 4 * mh.H <= 12288;     // 48 KiB of LDS
     const size_t sh = stage ? (size_t)tmax * 4 * mh.H * sizeof(float) : 0;
 #define L_CASE(HM) \

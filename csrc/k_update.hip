@@ -273,7 +273,11 @@ __global__ __launch_bounds__(256) void k_pack(const UpdJob* __restrict__ jobs,
     gp(J.aux)[md->md.aux_floats + a] = aux_scaled(md, a) ? v * dscale : v;
   }
   else if (e < nproj) gp(J.wproj)[e - naux] = pack_proj_elem(md, src, e - naux);
-  else if (e < total) ((DLAP_GLOBAL __bf16*)(J.blob0))[e - nproj] = (__bf16)pack_blob0_elem(md, src, e - nproj);
+  else if (e < total) {
+    const float v = pack_blob0_elem(md, src, e - nproj);
+    if (md->md.fp32) ((DLAP_GLOBAL float*)(J.blob0))[e - nproj] = v;
+    else ((DLAP_GLOBAL __bf16*)(J.blob0))[e - nproj] = (__bf16)v;
+  }
   if (bump && blockIdx.x == 0 && threadIdx.x == 0) {
     gp(J.adam_step)[bump - 1] = gp(J.adam_step)[bump - 1] + 1;
     gp(J.drop_step)[0] = gp(J.drop_step)[0] + 1;

@@ -25,8 +25,9 @@ struct RnnJob {
 };
 
 // abias: also build the moment network's per-period layer-0 bias table (a tower launched after
-// this prologue runs the moment network).
+// this prologue runs the moment network). lstm = false: the bias table only (moment refresh:
+// the moment network does not read the LSTM state).
 void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* md, const ModelDesc& mh,
-                     hipStream_t st, bool abias = true);
+                     hipStream_t st, bool abias = true, bool lstm = true);
 
 std::vector<long long> rnn_timestamps();

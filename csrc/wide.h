@@ -6,7 +6,8 @@
 struct ModelDesc;
 
 // XT (rows-as-k fragments of the train panel) from the row-major panel X [R][KX].
-void launch_xt_build(const u16* X, u16* XT, int R, int KX, hipStream_t st);
+// f32: the reference-precision panel (fp32 elements, stored as 2 x u16).
+void launch_xt_build(const u16* X, u16* XT, int R, int KX, bool f32, hipStream_t st);
 // z = X . W0x^T of the SDF (do_sdf) and moment (do_mom) towers for every job.
 void launch_proj0(const WideJob* jobs, int njobs, int gx, const MlpDims& D, int WMB, hipStream_t st);
 // Column blocks (16 wide) of the layer-0 weight gradient: the KX panel columns (the SDF's

@@ -56,7 +56,6 @@ def weights_batched_gpu(models: Sequence, batches: Dict[str, Dict]) -> Dict[str,
     device-to-device into the stack (ordered after torch's stream with events, no host sync) and
     normalised there."""
     from ..engine.runner import GANEngine
-    from ..models.losses import l1_normalize
     dev = torch.device("cuda", torch.cuda.current_device())
     ts = torch.cuda.current_stream(dev).cuda_stream
     out = {}
@@ -79,9 +78,10 @@ def weights_batched_gpu(models: Sequence, batches: Dict[str, Dict]) -> Dict[str,
                 e.copy_ws(g, s, "wn", out[split][i].data_ptr())
         e.join_to(ts)
         e.sync()         # the engine (and its buffers) may be freed after this group
-    for split in SPLITS:
-        m = batches[split]["mask"].to(dev)
-        out[split] = l1_normalize(out[split], m[None].expand_as(out[split]))
+    for split in SPLITS:                 # per (model, period) L1 normalisation over the stocks
+        m = batches[split]["mask"].to(dev).float()
+        W = out[split]
+        out[split] = W / (W.abs() * m[None]).sum(dim=2, keepdim=True).clamp(min=1e-8)
     return out
 
 

@@ -82,7 +82,7 @@ class GANEngine:
 
     ``precision``: "bf16" (production: bf16 tower GEMM operands, fp32 accumulation / master
     weights / losses) or "fp32" (the reference's precision end to end: fp32 panel rows and
-    weight fragments through fp32 MFMA tiles; fused layer-0 path only)."""
+    weight fragments through fp32 MFMA tiles, the wide layer-0 path included)."""
 
     def __init__(self, spec: ModelSpec, n_models: int = 1, max_epochs: int = 4096, precision: str = "bf16"):
         if precision not in ("bf16", "fp32"):

@@ -143,7 +143,9 @@ def _prepare(model, spec: ModelSpec, params: List[torch.Tensor], flat_fn, macro,
         s.eng.set_data(batch)
         s.data_key = key
         s.T, s.N = int(mask.shape[0]), int(mask.shape[1])
-        s.idx = mask.detach().reshape(-1).bool().nonzero().reshape(-1)   # (one sync per new panel)
+        mflat = mask.detach().reshape(-1).bool()
+        s.idx = mflat.nonzero().reshape(-1)              # (one sync per new panel)
+        s.midx = (~mflat).nonzero().reshape(-1)          # masked entries (moments only)
     pkey = tuple((p.data_ptr(), p._version) for p in params)
     if pkey != s.param_key:
         s._flat = flat_fn(dev).contiguous()            # kept alive until the next call
@@ -303,6 +305,23 @@ def _dense_raw(s: _Slot, dev) -> torch.Tensor:
     return torch.zeros(s.T * s.N, dtype=torch.float32, device=dev).index_copy(0, s.idx, wc[:R]).reshape(s.T, s.N)
 
 
+def _masked_moments(model, s: _Slot, h: torch.Tensor, macro, individual) -> torch.Tensor:
+    """The engine computes the moments of the valid (t, i) only (the losses never read the
+    others); the module returns all of them, as the reference does. The masked entries' moments
+    come from the moment network's own modules on just those rows' inputs [macro_t ; x_ti]
+    (differentiable; a small GEMM chain over the masked rows)."""
+    if s.midx.numel() == 0:
+        return h
+    T, N, K = s.T, s.N, h.shape[0]
+    x = individual.reshape(T * N, -1).index_select(0, s.midx)
+    if macro is not None and model.spec.macro_dim > 0:
+        x = torch.cat([macro.index_select(0, torch.div(s.midx, N, rounding_mode="floor")), x], 1)
+    net = model.moment_net
+    hm = torch.tanh(net.output_proj(net.fc_layers(x)))                  # [n_masked, K]
+    flat = h.permute(1, 2, 0).reshape(T * N, K).index_copy(0, s.midx, hm.to(h.dtype))
+    return flat.reshape(T, N, K).permute(2, 0, 1)
+
+
 def gan_forward(model, macro, individual, returns, mask, phase: str = "conditional", hidden=None) -> Dict:
     if phase not in _PHASE:
         raise ValueError(f"unknown phase {phase!r}")
@@ -334,6 +353,7 @@ def gan_forward(model, macro, individual, returns, mask, phase: str = "condition
             h = _TowerH.apply(h, s, spec, to_p, *params)
         wn = L.zero_mean_normalize(w_raw, mask) if spec.normalize_w else w_raw * mask.float()
         p = L.portfolio_returns(wn, returns, mask, spec.weighted_loss)
+    h = _masked_moments(model, s, h, macro, individual)
     l_cond, l_unc = sc[SC["loss_cond"]], sc[SC["loss_unc"]]
     zero = torch.zeros((), device=dev)
     if phase == "unconditional":

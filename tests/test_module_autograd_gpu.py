@@ -159,8 +159,9 @@ def test_get_weights_differentiable():
     wc, _ = cpu.get_weights(b["macro_features"], b["individual_features"], b["mask"], normalized=True)
     wg, _ = gpu.get_weights(bc["macro_features"], bc["individual_features"], bc["mask"], normalized=True)
     assert torch.allclose(wg.detach().cpu(), wc.detach(), rtol=1e-5, atol=1e-7)
-    (wc * torch.arange(wc.numel()).reshape(wc.shape)).sum().backward()
-    (wg * torch.arange(wg.numel(), device="cuda").reshape(wg.shape)).sum().backward()
+    r = torch.randn(wc.shape, generator=torch.Generator().manual_seed(1))
+    ((wc * r).sum() + (wc ** 2).sum()).backward()
+    ((wg * r.cuda()).sum() + (wg ** 2).sum()).backward()
     _close(_grads(gpu), _grads(cpu))
 
 
@@ -176,6 +177,6 @@ def test_simple_sdf_without_hidden_layers():
     assert abs(float(out_g["loss"]) - float(out_c["loss"])) <= TOL * abs(float(out_c["loss"]))
     out_c["loss"].backward()
     out_g["loss"].backward()
-    for pc, pg in zip(cpu.parameters(), gpu.parameters()):
-        err = float((pg.grad.cpu() - pc.grad).norm() / pc.grad.norm())
-        assert err < TOL, err
+    # (the Linear's bias cancels out of the zero-mean weights: its gradient is rounding noise)
+    gc, gg = cpu.net[-1].weight.grad, gpu.net[-1].weight.grad.cpu()
+    assert float((gg - gc).norm() / gc.norm()) < TOL

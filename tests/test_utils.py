@@ -105,3 +105,21 @@ def test_trace_ranges_are_safe_without_a_gpu():
             tracing.mark("m")
     assert t.count == {"inner": 1, "outer": 1} and math.isfinite(t.total["outer"])
     assert "outer" in t.summary()
+
+
+def test_every_module_imports_on_cpu():
+    """Every package module (GPU-only paths included) imports without a GPU: a syntax or import
+    error in a module only the GPU tests exercise fails here, in the CPU suite."""
+    import importlib
+    import pkgutil
+
+    import deeplearninginassetpricing_paperreplication_amd as pkg
+    bad = []
+    for m in pkgutil.walk_packages(pkg.__path__, pkg.__name__ + "."):
+        if m.name.endswith("_dlap_hip"):
+            continue
+        try:
+            importlib.import_module(m.name)
+        except Exception as e:          # noqa: BLE001  (report every failure at once)
+            bad.append(f"{m.name}: {type(e).__name__}: {e}")
+    assert not bad, bad
