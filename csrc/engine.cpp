@@ -69,18 +69,40 @@ static std::atomic<int> g_live_engines{0};
 // synchronised; destroying the executor right away and having the allocator hand its memory
 // to the next executor crashed the next hipGraphLaunch inside the runtime (measured: the
 // pipelined body graph of a fresh engine, created right after the previous engine died, got the
-// address of the freshly destroyed one and segfaulted at its first launch). Executors are
-// therefore destroyed only after many later retirements (their handlers long finished); a few
-// hundred stay alive at most (a few KiB each).
+// address of the freshly destroyed one and segfaulted at its first launch). An executor is
+// therefore destroyed only when (a) an event recorded on its launch stream at retirement (after
+// its last launch) has completed, and (b) at least RETIRE_LAG later executors have been retired
+// since (its completion handler long finished). A few hundred stay alive at most (a few KiB each).
+struct RetiredExec {
+  hipGraphExec_t exec;
+  hipEvent_t done;      // recorded after the executor's last launch (nullptr: none recorded)
+  long long seq;        // retirement number
+};
 static std::mutex g_retired_mu;
-static std::vector<hipGraphExec_t> g_retired;
-static void retire_graph_exec(hipGraphExec_t e) {
-  std::lock_guard<std::mutex> g(g_retired_mu);
-  g_retired.push_back(e);
-  if (g_retired.size() >= 512) {
-    for (size_t i = 0; i < 256; ++i) (void)hipGraphExecDestroy(g_retired[i]);
-    g_retired.erase(g_retired.begin(), g_retired.begin() + 256);
+static std::vector<RetiredExec> g_retired;
+static long long g_retire_seq = 0;
+static constexpr long long RETIRE_LAG = 256;
+static void retire_graph_exec(hipGraphExec_t e, hipStream_t st) {
+  hipEvent_t ev = nullptr;
+  if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess) {
+    if (hipEventRecord(ev, st) != hipSuccess) { (void)hipEventDestroy(ev); ev = nullptr; }
   }
+  std::lock_guard<std::mutex> g(g_retired_mu);
+  g_retired.push_back({e, ev, g_retire_seq++});
+  if (g_retired.size() < 2 * RETIRE_LAG) return;
+  std::vector<RetiredExec> keep;
+  keep.reserve(g_retired.size());
+  for (const RetiredExec& r : g_retired) {
+    const bool old = g_retire_seq - r.seq >= RETIRE_LAG;
+    const bool finished = r.done == nullptr || hipEventQuery(r.done) == hipSuccess;
+    if (old && finished) {
+      (void)hipGraphExecDestroy(r.exec);
+      if (r.done) (void)hipEventDestroy(r.done);
+    } else {
+      keep.push_back(r);
+    }
+  }
+  g_retired.swap(keep);
 }
 
 namespace {
@@ -209,7 +231,7 @@ class Engine {
     zx_eval_ = env_int("DLAP_ZX_EVAL", 1) != 0;
     zx_train_ = env_int("DLAP_ZX_TRAIN", 1) != 0;
     zx_gx_ = std::max(1, env_int("DLAP_ZX_GX", 256));
-    train_first_ = env_int("DLAP_TRAIN_FIRST", 1) != 0;
+    train_first_ = env_int("DLAP_TRAIN_FIRST", 1);
     h_cache_ = env_int("DLAP_H_CACHE", 1) != 0;
     gram_on_ = env_int("DLAP_GRAM", 1) != 0;
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
@@ -254,7 +276,7 @@ class Engine {
     if (st3_) (void)hipStreamSynchronize(st3_);
     if (st_) (void)hipStreamSynchronize(st_);
     if (own_st_ && own_st_ != st_) (void)hipStreamSynchronize(own_st_);
-    for (auto& kv : graphs_) retire_graph_exec(kv.second);
+    for (auto& kv : graphs_) retire_graph_exec(kv.second, st_);
     if (ev_fork_) (void)hipEventDestroy(ev_fork_);
     if (ev_join_) (void)hipEventDestroy(ev_join_);
     if (ev_gram_) (void)hipEventDestroy(ev_gram_);
@@ -802,7 +824,8 @@ class Engine {
   int zx_gx_ = 256;                          // their workgroups over all evaluation jobs (DLAP_ZX_GX)
   bool side_metrics_ = false;                // train metrics on the side stream st3_ (DLAP_SIDE_METRICS)
   bool defer_metrics_ = true;                // pipelined epochs: train metrics on the evaluation branch
-  bool train_first_ = true;                  // capture the training chain before the evaluation branch
+  int train_first_ = 1;                      // capture the training chain before the evaluation branch
+                                             // (2: with the evaluation LSTM prologue right behind the training one)
   // Moment cache: the moment net only changes in phase 2, so outside it the moments h of every
   // split are constant (eval mode has no dropout; the train split's only if the moment tower has
   // no dropout-carrying hidden layer). They are computed once (refresh_moments) when the moment
@@ -1257,7 +1280,7 @@ class Engine {
 
   void rebuild_jobs() {
     HTRACE("rebuild_jobs");
-    for (auto& kv : graphs_) retire_graph_exec(kv.second);
+    for (auto& kv : graphs_) retire_graph_exec(kv.second, st_);
     graphs_.clear();
     fwd_tables_.clear();
     j_mlp_bwd_dh_.free();
@@ -1425,6 +1448,10 @@ class Engine {
     // the latency-bound LSTM first, before the streaming projection loads the memory system
     HTRACE("launch_prologue");
     launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_, train_mom(phase));
+    // pipelined epoch, train_first_ == 2: the evaluation branch's LSTM prologue is enqueued right
+    // behind the training one, so its (serial, few-CU) recurrence starts at the epoch start
+    // instead of behind every training-chain node of the graph
+    if (eval_prologue_hook_) { enqueue_eval_prologue(eval_prologue_hook_); eval_prologue_hook_ = nullptr; }
     const bool zx_train = md_.md.wide && zx_train_;
     if (md_.md.wide && !zx_train)
       launch_proj0(as<WideJob>(j_wide_train_[phase]), G_, gx_proj_[0], md_.md, md_.WMB, st_);
@@ -1504,6 +1531,7 @@ class Engine {
   }
   // join whatever was forked onto st3_ back into st_ (required before a graph capture ends)
   bool side_open_ = false;
+  hipStream_t eval_prologue_hook_ = nullptr;   // see enqueue_train_grads
   void join_side() {
     if (!side_open_) return;
     HIP_OK(hipEventRecord(ev_f3_, st3_));
@@ -1574,8 +1602,12 @@ class Engine {
     if (b_wait_ == 0 && train_first_) {
       // same graph topology, training-chain nodes first (they land on the graph's first queue)
       const bool defer = !side_metrics_ && defer_metrics_;
+      const bool inter = train_first_ == 2 && n_eval_jobs_ > 0;
+      if (inter) eval_prologue_hook_ = st2_;
       enqueue_train_grads(phase, side_metrics_ ? st3_ : nullptr, true, 0, false, defer);   // this epoch's fwd/bwd
-      enqueue_eval(st2_);                                 // previous epoch's evaluation
+      eval_prologue_hook_ = nullptr;
+      if (inter) enqueue_eval_towers(st2_);               // previous epoch's evaluation
+      else enqueue_eval(st2_);
       if (side_metrics_) HIP_OK(hipStreamWaitEvent(st2_, ev_m3_, 0));   // train metrics
       if (defer && phase != 2) {                          // this epoch's train metrics, after its
         HIP_OK(hipStreamWaitEvent(st2_, ev_mid_, 0));     // asset pass (read by the next bookkeeping)

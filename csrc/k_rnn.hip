@@ -424,6 +424,9 @@ __global__ __launch_bounds__(FUSE ? LSTM_FUSE_THREADS : 64) void k_lstm_gls(cons
     if (w > 0) return;
   }
   const int L = threadIdx.x;
+  // the recurrence is one latency-bound wave: top issue priority on its SIMD, so the tower waves
+  // of a concurrent branch (pipelined evaluation / training) do not stretch its serial chain
+  __builtin_amdgcn_s_setprio(3);
   const bool gl = L < G4, ul = L < H;
   const int row = gl ? L : 0;
   const bool is_g = gl && L >= 2 * H && L < 3 * H;
@@ -660,6 +663,7 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
     }
     __syncthreads();
     if (l == 0) RNN_TS(9, tsm);
+    if (wave == 0) __builtin_amdgcn_s_setprio(3);     // serial chain: see k_lstm_gls
     if (wave == 0 && HM == 4 && H == 4) {
       // Gate-per-lane BPTT (H = 4): lane L (mod 16) owns gate row L = 4q + k and keeps the
       // recurrent state of unit k replicated, so d_L = (q == 3 ? dh : dc) * coef is lane-local

@@ -1,4 +1,4 @@
-"""Oracle Sharpe ceiling of the synthetic factor-model panel (an addition; the reference has no
+"""Oracle Sharpe yardsticks of the synthetic factor-model panel (an addition; the reference has no
 such yardstick, and its 0.55-0.75 test Sharpe target refers to the real data,
 `/root/reference/notebooks/demo_full.ipynb:867`).
 
@@ -14,9 +14,16 @@ factors: at t it holds ``a_tk = rho f_{t-1,k} / sigma_k^2`` units of factor k, e
     SR_k^2 = E[x_k]^2 / Var(x_k) = rho^2 / (1 - rho^2) / (1 + 2 rho^2 / (1 - rho^2)),
     SR*    = sqrt(K) SR_k  (independent factors)  = 0.2225 at rho = 0.1, K = 5,
 
-independent of the factor volatilities. No SDF built from these data can beat it in population;
-finite test windows scatter around it (the standard error of a monthly Sharpe over T periods is
-about 1 / sqrt(T): 0.058 on the 300-month test split).
+independent of the factor volatilities. This is the *conditional mean-variance oracle*, not an
+upper bound on the unconditional Sharpe: weights mu_t / sigma^2 maximise each month's conditional
+Sharpe, while the unconditionally efficient managed portfolio holds mu_t / (sigma^2 + mu_t^2) and
+reaches (Hansen-Richard / Ferson-Siegel bound, ``unconditional_bound``)
+
+    SR_u^2 = E[S_t^2 / (1 + S_t^2)] / (1 - E[S_t^2 / (1 + S_t^2)]),   S_t^2 = q chi^2_K,
+
+slightly above SR* (0.2226 vs 0.2225 at rho = 0.1, K = 5), so ``fraction_of_population`` may
+exceed 1 without a bug. Finite test windows scatter around both (the standard error of a monthly
+Sharpe over T periods is about 1 / sqrt(T): 0.058 on the 300-month test split).
 
 ``oracle_report`` also evaluates on the generated panel (paper sign: the SDF factor return):
   * ``true_signal``       a_tk from the true f_{t-1} and the true factor returns f_t;
@@ -48,6 +55,16 @@ def population_sharpe(rho: float = 0.1, K: int = 5) -> float:
     """Population monthly Sharpe of the conditional mean-variance factor-timing SDF."""
     q = rho * rho / (1.0 - rho * rho)            # = E[x_k] / Var-scale, see module docstring
     return math.sqrt(K) * math.sqrt(q / (1.0 + 2.0 * q))
+
+
+def unconditional_bound(rho: float = 0.1, K: int = 5) -> float:
+    """Population Sharpe of the unconditionally efficient managed portfolio (the maximum over all
+    strategies using f_{t-1}): sqrt(E[s/(1+s)] / (1 - E[s/(1+s)])) with s = q chi^2_K the squared
+    conditional Sharpe, integrated against the chi^2_K density."""
+    from scipy import integrate, stats
+    q = rho * rho / (1.0 - rho * rho)
+    e = integrate.quad(lambda x: q * x / (1.0 + q * x) * stats.chi2.pdf(x, K), 0.0, np.inf)[0]
+    return math.sqrt(e / (1.0 - e))
 
 
 def _sharpe(x: np.ndarray) -> float:
@@ -102,7 +119,8 @@ def oracle_report(ret, mask, macro, latent: Dict, cuts: Sequence[int]) -> Dict:
         am[:, k] = coef * m / vols[k] ** 2
     x_mac = (am * fh).sum(1)
     bounds = np.cumsum([0] + list(cuts))
-    out = {"population": population_sharpe(rho, K), "rho": rho, "K": K,
+    out = {"population": population_sharpe(rho, K), "unconditional_bound": unconditional_bound(rho, K),
+           "rho": rho, "K": K,
            "test_se": 1.0 / math.sqrt(max(int(cuts[2]), 1))}
     for name, x in (("true_signal", x_true), ("tradable", x_trad), ("macro_signal", x_mac)):
         out[name] = {sp: _sharpe(x[bounds[i]:bounds[i + 1]][1 if i == 0 else 0:])
@@ -113,7 +131,8 @@ def oracle_report(ret, mask, macro, latent: Dict, cuts: Sequence[int]) -> Dict:
 def oracle_for_panel(T_split=(240, 60, 300), N=3000, F=46, M=178, seed: int = 0,
                      device: str = "cpu", ensemble_test_sharpe: Optional[float] = None) -> Dict:
     """Oracle report of the panel ``bench.make_panel`` / ``generate_panel_fast`` draws for
-    ``seed``; with ``ensemble_test_sharpe``, also the fraction of the ceiling it reaches."""
+    ``seed``; with ``ensemble_test_sharpe``, also the fraction of the conditional-MV oracle it reaches (may exceed 1: the
+    oracle is not an upper bound, see ``unconditional_bound``)."""
     from ..data.synthetic import generate_panel_fast
     ret, _, mask, mac, lat = generate_panel_fast(sum(T_split), N, F, M, seed=seed, device=device,
                                                  return_latent=True)
@@ -123,5 +142,6 @@ def oracle_for_panel(T_split=(240, 60, 300), N=3000, F=46, M=178, seed: int = 0,
     if ensemble_test_sharpe is not None:
         rep["ensemble_test_sharpe"] = float(ensemble_test_sharpe)
         rep["fraction_of_population"] = float(ensemble_test_sharpe) / rep["population"]
+        rep["fraction_of_unconditional_bound"] = float(ensemble_test_sharpe) / rep["unconditional_bound"]
         rep["fraction_of_true_signal_test"] = float(ensemble_test_sharpe) / rep["true_signal"]["test"]
     return rep

@@ -65,6 +65,16 @@ def _close(ga, gb, tol=TOL, skip=("sdf_net.output_proj.bias",)):
         assert err < tol or float((a - b).abs().max()) < 1e-9, (k, err, nb)
 
 
+def _close_out(g, c, tol=TOL):
+    """An output tensor within tol in relative norm and 1e-6 elementwise (fp32 sums in another
+    order: an entry near zero carries ~1e-7 absolute rounding noise, which a per-entry rtol
+    cannot absorb)."""
+    a, b = g.detach().double().cpu(), c.detach().double()
+    err = float((a - b).norm()) / max(float(b.norm()), 1e-30)
+    mx = float((a - b).abs().max())
+    assert err < tol and mx < 1e-6, (err, mx)
+
+
 def _pair(cfg_extra=None, seed=0):
     cfg = default_cli_config(8, 46, dropout=0.0)
     cfg.update(cfg_extra or {})
@@ -95,7 +105,7 @@ def test_custom_loss_of_outputs_backpropagates(output):
     custom(out_c, w).backward()
     out_g = gpu(*_args(bc), phase="conditional")
     custom(out_g, w.cuda()).backward()
-    assert torch.allclose(out_g[output].detach().cpu(), out_c[output].detach(), rtol=1e-5, atol=1e-7)
+    _close_out(out_g[output], out_c[output])
     _close(_grads(gpu), _grads(cpu))
 
 
