@@ -234,11 +234,15 @@ class Engine {
     train_first_ = env_int("DLAP_TRAIN_FIRST", 1);
     h_cache_ = env_int("DLAP_H_CACHE", 1) != 0;
     gram_on_ = env_int("DLAP_GRAM", 1) != 0;
+    rnn_overlap_ = env_int("DLAP_RNN_OVERLAP", 1) != 0;
+    rnn_overlap_eval_ = env_int("DLAP_RNN_OVERLAP_EVAL", 0) != 0;
+    prog_mode_ = env_int("DLAP_PROG_MODE", 1);
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
                residual, fp32);
     // fp32 wide path: layer 0 through k_proj0 + the ZIN towers (the fused-layer-0 k_mlp_fwd_zx
     // is bf16 only)
     if (fp32) zx_eval_ = zx_train_ = false;
+    prog_.alloc((size_t)G * 3 * 16);      // per (model, split): [0] published periods, [1] spin timeouts
     d_desc_.alloc(sizeof(ModelDesc));
     HIP_LEGACY(hipMemcpy(d_desc_.p, &md_, sizeof(ModelDesc), hipMemcpyHostToDevice));
     models_.resize(G);
@@ -631,12 +635,17 @@ class Engine {
     if (phase != 2) ensure_moments();
     const SplitDev& D = splits_[0];
     enqueue_dropmask(phase, 0, st_);
-    launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_, train_mom(phase));
+    const bool fused = fused_fwd(phase);
+    if (fused) launch_proj(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_, train_mom(phase));
+    else launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_, train_mom(phase));
     const bool zx_train = md_.md.wide && zx_train_;
     if (md_.md.wide && !zx_train)
       launch_proj0(as<WideJob>(j_wide_train_[phase]), G_, gx_proj_[0], md_.md, md_.WMB, st_);
     if (zx_train)
       launch_mlp_fwd_zx(as<MlpJob>(j_mlp_train_[phase]), G_, std::max(1, zx_gx_ / G_), md_.md, md_.WMB, st_, true);
+    else if (fused)
+      launch_mlp_fwd_rnn(as<MlpJob>(j_mlp_train_[phase]), as<RnnJob>(j_rnn_train_), dd(), G_,
+                         phase == 2 ? gx_fwd_[0] : gx_fwd13_, md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, D.T, st_);
     else
       launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, phase == 2 ? gx_fwd_[0] : gx_fwd13_, md_.md, md_.KS1,
                      md_.WMB, st_);
@@ -853,6 +862,32 @@ class Engine {
   }
   // whether the training towers of a phase run the moment network (and so need its
   // per-period bias table from the prologue)
+  // fused LSTM + training tower forward (k_mlp_fwd_rnn): the towers trail the recurrence
+  // period by period instead of starting after it (DLAP_RNN_OVERLAP=0: two launches)
+  bool rnn_overlap_ = true;
+  bool rnn_overlap_eval_ = false;            // ... also on the evaluation branch (DLAP_RNN_OVERLAP_EVAL)
+  int prog_mode_ = 1;                        // DLAP_PROG_MODE (see MlpJob::prog_mode)
+  DevBuf<int> prog_;
+  bool fused_eval() const {
+    return rnn_overlap_ && rnn_overlap_eval_ && md_.nrnn > 0 && !md_.md.wide && n_eval_jobs_ > 0 &&
+           mlp_fwd_rnn_supported(md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, tmax_eval_);
+  }
+ public:
+  bool fused_fwd(int phase) const {
+    (void)phase;
+    return rnn_overlap_ && md_.nrnn > 0 && !md_.md.wide &&
+           mlp_fwd_rnn_supported(md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, splits_[0].T);
+  }
+  // spin waits of the fused forward that gave up (0 unless the dispatch-order argument failed)
+  int prog_timeouts() {
+    sync();
+    std::vector<int> h((size_t)G_ * 3 * 16);
+    HIP_LEGACY(hipMemcpy(h.data(), prog_.p, h.size() * sizeof(int), hipMemcpyDeviceToHost));
+    int n = 0;
+    for (int k = 0; k < 3 * G_; ++k) n += h[16 * k + 1];
+    return n;
+  }
+ private:
   bool train_mom(int phase) const { return phase == 2 || (phase == 3 && !cache_train_h()); }
   ModelDesc md_{};
   DevBuf<char> d_desc_;
@@ -1138,8 +1173,13 @@ class Engine {
     J.h0 = W.h0.p; J.c0 = W.c0.p;
     J.seed = models_[g].seed;
     J.train = train;
+    if (s == 0 && train) J.prog = prog_ptr(g, 0);
     return J;
   }
+  // progress counter of the fused LSTM + tower forward of (model, split); set only on the job
+  // tables that launch it (training split: train tables; evaluation splits: the eval tables)
+  int* prog_ptr(int g, int s) { return prog_.p + 16 * (3 * g + s); }
+  void set_prog(MlpJob& J, int g, int s) { J.prog = prog_ptr(g, s); J.prog_err = prog_ptr(g, s) + 1; J.prog_mode = prog_mode_; }
   const float* pp_ptr(int g, int s) {
     if (md_.nrnn > 0) return ws(g, s).pp.p;
     if (md_.Dm > 0) return splits_[s].macro.p;   // raw macro feeds the SDF directly
@@ -1166,6 +1206,7 @@ class Engine {
     J.R = D.R; J.N = D.N; J.T = D.T;
     J.seed = tower_seed(g);
     J.train = train; J.do_sdf = do_sdf; J.do_mom = do_mom;
+    if (s == 0 && train) set_prog(J, g, 0);
     const int nsl = std::max(md_.nslice_s, md_.nslice_m);
     J.slab_base = g * nsl * gx_bwd_;
     return J;
@@ -1297,6 +1338,8 @@ class Engine {
         if (!splits_[s].set) continue;
         re.push_back(rnn_job(g, s, false));
         me.push_back(mlp_job(g, s, false, true, !h_cache_));
+        re.back().prog = prog_ptr(g, s);
+        set_prog(me.back(), g, s);
         we.push_back(wide_job(g, s, true, !h_cache_));
         le.push_back(loss_job(g, s, 0, gram_eval()));
         tmax_eval_ = std::max(tmax_eval_, splits_[s].T);
@@ -1446,8 +1489,11 @@ class Engine {
     const LossJob* lj = loss_tab(phase, gram);
     if (!premasked) enqueue_dropmask(phase, 0, st_);
     // the latency-bound LSTM first, before the streaming projection loads the memory system
-    HTRACE("launch_prologue");
-    launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_, train_mom(phase));
+    // (fused: only its input projection here, the recurrence runs inside the tower launch)
+    const bool fused = fused_fwd(phase);
+    HTRACE("launch_prologue fused=%d", (int)fused);
+    if (fused) launch_proj(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_, train_mom(phase));
+    else launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_, train_mom(phase));
     // pipelined epoch, train_first_ == 2: the evaluation branch's LSTM prologue is enqueued right
     // behind the training one, so its (serial, few-CU) recurrence starts at the epoch start
     // instead of behind every training-chain node of the graph
@@ -1458,6 +1504,9 @@ class Engine {
     if (mark == 3) HIP_OK(hipEventRecord(ev_a_, st_));
     if (zx_train)      // layer 0 streamed inside the training towers, z stored for the backward
       launch_mlp_fwd_zx(as<MlpJob>(j_mlp_train_[phase]), G_, std::max(1, zx_gx_ / G_), md_.md, md_.WMB, st_, true);
+    else if (fused)
+      launch_mlp_fwd_rnn(as<MlpJob>(j_mlp_train_[phase]), as<RnnJob>(j_rnn_train_), dd(), G_,
+                         phase == 2 ? gx_fwd_[0] : gx_fwd13_, md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, D.T, st_);
     else
       launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, phase == 2 ? gx_fwd_[0] : gx_fwd13_, md_.md, md_.KS1,
                      md_.WMB, st_);
@@ -1550,7 +1599,9 @@ class Engine {
   void enqueue_eval_prologue(hipStream_t st) {
     if (n_eval_jobs_ == 0) return;
     HTRACE("launch_prologue");
-    launch_prologue(as<RnnJob>(j_rnn_eval_), n_eval_jobs_, tmax_eval_, dd(), md_, st, !h_cache_);
+    // fused: the input projections only, the recurrences run inside the tower launch
+    if (fused_eval()) launch_proj(as<RnnJob>(j_rnn_eval_), n_eval_jobs_, tmax_eval_, dd(), md_, st, !h_cache_);
+    else launch_prologue(as<RnnJob>(j_rnn_eval_), n_eval_jobs_, tmax_eval_, dd(), md_, st, !h_cache_);
   }
   void enqueue_eval_towers(hipStream_t st) {
     if (n_eval_jobs_ == 0) return;
@@ -1563,7 +1614,11 @@ class Engine {
       if (md_.md.wide)
         launch_proj0(as<WideJob>(j_wide_eval_), n_eval_jobs_, std::max(gx_proj_[1], gx_proj_[2]), md_.md, md_.WMB, st);
       HTRACE("launch_mlp_fwd");
-      launch_mlp_fwd(as<MlpJob>(j_mlp_eval_), n_eval_jobs_, gx, md_.md, md_.KS1, md_.WMB, st);
+      if (fused_eval())
+        launch_mlp_fwd_rnn(as<MlpJob>(j_mlp_eval_), as<RnnJob>(j_rnn_eval_), dd(), n_eval_jobs_, gx, md_.md, md_.KS1,
+                           md_.WMB, md_.H, md_.nrnn, tmax_eval_, st);
+      else
+        launch_mlp_fwd(as<MlpJob>(j_mlp_eval_), n_eval_jobs_, gx, md_.md, md_.KS1, md_.WMB, st);
     }
     HTRACE("launch_period_fwd");
     launch_period_fwd(as<LossJob>(j_loss_eval_), n_eval_jobs_, tmax_eval_, st);
@@ -1773,6 +1828,8 @@ PYBIND11_MODULE(_dlap_hip, m) {
       .def_static("blocking_calls", []() { return (long long)g_blocking.load(); })
       .def_static("live_engines", []() { return g_live_engines.load(); })
       .def_static("rnn_timestamps", []() { return rnn_timestamps(); })
+      .def("fused_forward", [](Engine& e, int phase) { return e.fused_fwd(phase); })
+      .def("prog_timeouts", &Engine::prog_timeouts)
       .def_static("loss_timestamps", []() { return loss_timestamps(); })
       .def_static("mlp_timestamps", []() { return mlp_timestamps(); })
       .def("forward_split", &Engine::forward_split, py::arg("s"), py::arg("train_mode"), py::arg("do_mom"),

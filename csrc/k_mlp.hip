@@ -29,9 +29,11 @@
 // (k(q, j) = row 4q + (j&3) of block j>>2), so dW tiles accumulate in registers across the
 // whole persistent loop. Bias sums use the same rows-as-k operands against a one-hot
 // column selector: every layer's bias gradient shares 4 accumulator tiles.
+#include <algorithm>
 #include "common.h"
 #include "layout.h"
 #include "mlp.h"
+#include "lstm_gls.h"
 
 DLAP_DEV int lane_id() { return threadIdx.x & 63; }
 // A wave-uniform zero the compiler cannot see through (an empty asm statement defines it):
@@ -54,10 +56,12 @@ DLAP_DEV int opaque_zero() {
 
 // In-kernel timestamps (wall clock, 100 MHz) of k_mlp_fwd's first / last workgroup, wave 0:
 // [0] start, [1] weights staged, [2] first tile done, [3] loop done; [4..7] same, last block.
-__device__ long long g_mlp_ts[8];
+// [8..12]: fused LSTM + tower forward, workgroup 0: start, recurrence start / end, LSTM body
+// done, publisher done (k_mlp_fwd_rnn).
+__device__ long long g_mlp_ts[16];
 #define MLP_TS(slot) do { \
-    if ((threadIdx.x & 255) == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x - 1) && J.gbits) \
-      g_mlp_ts[(blockIdx.x == 0 ? 0 : 4) + (slot)] = wall_clock64(); } while (0)
+    if ((threadIdx.x & 255) == 0 && (bx == 0 || bx == gxw - 1) && J.gbits) \
+      g_mlp_ts[(bx == 0 ? 0 : 4) + (slot)] = wall_clock64(); } while (0)
 template <typename F>
 DLAP_DEV F ldsf(const F* lds, int frag) { return lds[frag * 64 + lane_id()]; }
 DLAP_DEV int perm_unit(int q, int j) { return j < 4 ? 4 * q + j : 16 + 4 * q + (j - 4); }
@@ -249,7 +253,9 @@ DLAP_DEV void issue_tile(const MlpJob& J, int tile, TileIn<P, KS1>& in) {
 // of each row's period written into the panel row's last columns [ppc, ppc + Dm) (zero in
 // HBM): the lane groups whose 8 columns fall there take pp[t][col - ppc .. +7] -- from the LDS
 // copy (row stride ppst, zero-padded) with two 16-byte reads, else from global memory.
-template <class P, int KS1, bool INS = true>
+// FRESH: the per-period inputs are being published by a concurrent LSTM (k_mlp_fwd_rnn, prog
+// mode 1): read them with agent-scope atomic loads, which bypass the non-coherent caches.
+template <class P, int KS1, bool INS = true, bool FRESH = false>
 DLAP_DEV RowInfo finish_tile(const MlpJob& J, const MlpDims& D, int tile, TileIn<P, KS1>& in,
                              typename P::Frag (&xf)[2][KS1], const float* spp = nullptr) {
   RowInfo ri;
@@ -279,7 +285,13 @@ DLAP_DEV RowInfo finish_tile(const MlpJob& J, const MlpDims& D, int tile, TileIn
           const auto row = gp(J.pp) + ri.t[b] * D.Dm;
           f = P::zero();
 #pragma unroll
-          for (int j = 0; j < 8; ++j) P::set(f, j, c0 + j < D.Dm ? row[min(max(c0 + j, 0), D.Dm - 1)] : 0.f);
+          for (int j = 0; j < 8; ++j) {
+            const auto src = row + min(max(c0 + j, 0), D.Dm - 1);
+            float v;
+            if constexpr (FRESH) v = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else v = *src;
+            P::set(f, j, c0 + j < D.Dm ? v : 0.f);
+          }
         }
         xf[b][s] = (c0 >= 0 && ok) ? f : xf[b][s];
       }
@@ -524,11 +536,36 @@ DLAP_DEV void sdf_keep_words(bool pre, const uint32_t (&kw_pre)[4], const DropCt
   }
 }
 
-template <class P, int KS1, int WMB, bool ZIN>
-__global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __restrict__ jobs, MlpDims D) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
+// Bounded spin on the fused forward's progress counter (k_mlp_fwd_rnn): wave-uniform, s_sleep
+// between polls; gives up after ~0.1 s (the dispatch-order argument below says it never has to)
+// and counts that in *err, so no wave can hang the GPU.
+#define PROG_SPIN_LIMIT (1u << 22)
+DLAP_DEV int prog_wait(const int* prog, int* err, int need, int seen, bool fence) {
+  if (need <= seen) return seen;
+  int v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  unsigned spins = 0;
+  while (v < need) {
+    __builtin_amdgcn_s_sleep(2);
+    v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (++spins > PROG_SPIN_LIMIT) {
+      if ((threadIdx.x & 63) == 0) atomicAdd(err, 1);
+      v = 1 << 30;
+      break;
+    }
+  }
+  // the outputs published before the counter are visible to this wave's loads from here on
+  // (prog mode 0; mode 1 reads them with cache-bypassing loads instead of invalidating)
+  if (fence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return v;
+}
+
+// Tower forward over the tiles of workgroup `bx` of `gxw` (k_mlp_fwd: the whole grid.x; the
+// fused k_mlp_fwd_rnn: grid.x - 1, its workgroup 0 runs the LSTM). WAIT: the per-period inputs
+// are produced concurrently by that LSTM -- before a tile is finished, the wave waits until the
+// periods of its rows are published (J.prog) and reads them from global memory.
+template <class P, int KS1, int WMB, bool ZIN, bool WAIT>
+DLAP_DEV void mlp_fwd_body(const MlpJob& J, const MlpDims& D, char* smem, const int bx, const int gxw) {
   using Frag = typename P::Frag;
-  const MlpJob& J = jobs[blockIdx.y];
   Frag* lds = reinterpret_cast<Frag*>(smem);
   float* aux = aux_lds_ptr(smem, D);
   float* spp = pp_lds_ptr(smem, D);
@@ -536,8 +573,9 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __r
   const int wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   const int ntiles = (J.R + 31) >> 5;
   const int q = lane_id() >> 4, lane = lane_id();
-  const int stride = gridDim.x * nwaves;
-  int tile = blockIdx.x * nwaves + wave;
+  const int stride = gxw * nwaves;
+  int tile = bx * nwaves + wave;
+  int seen = 0;                          // WAIT: periods known to be published
   TileIn<P, KS1> cur, nxt;
   ZTile<WMB> zcur, znxt;                 // ZIN: layer-0 pre-activations instead of X rows
   AbPre<WMB> ab_cur, ab_nxt;
@@ -597,7 +635,13 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __r
     }
     Frag xf[2][KS1];
     RowInfo ri;
+    if constexpr (WAIT) {
+      // the tile's last row (clamped to R - 1) has its largest period
+      const int tl = __builtin_amdgcn_readlane(cur.ti[1].x, 15);
+      seen = prog_wait(J.prog, J.prog_err, tl + 1, seen, J.prog_mode == 0);
+    }
     if constexpr (ZIN) ri = finish_ztile<WMB>(J, tile, zcur);
+    else if (WAIT && J.prog_mode != 0) ri = finish_tile<P, KS1, true, true>(J, D, tile, cur, xf, spp);
     else ri = finish_tile<P, KS1>(J, D, tile, cur, xf, spp);
     if (J.do_sdf) {
       float w[2];
@@ -642,6 +686,72 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __r
     if (first) { MLP_TS(2); first = false; }
   }
   MLP_TS(3);
+}
+
+template <class P, int KS1, int WMB, bool ZIN>
+__global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __restrict__ jobs, MlpDims D) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  mlp_fwd_body<P, KS1, WMB, ZIN, false>(jobs[blockIdx.y], D, smem, blockIdx.x, gridDim.x);
+}
+
+// ============================== fused LSTM + training tower forward =======================
+// The towers need the LSTM output of a row's period only, so the recurrence and the tower
+// forward run as ONE launch: workgroup (0, job) runs the LSTM of that job's model on wave 0
+// (lstm_gls_body, layer-0 input projections from k_proj), wave 1 publishes its progress --
+// it polls the LDS step counter the recurrence bumps every 8 periods, copies the new outputs
+// to J.out and release-stores the count to the job's global counter -- and every other
+// workgroup runs the tower forward, waiting per tile for the periods of its rows. Tiles are
+// visited in period order (tile index = bx * waves + wave, strided by the grid), so the
+// towers trail the recurrence period by period instead of starting after it.
+// Forward progress: workgroups are dispatched in linear-ID order on every XCD and each tower
+// workgroup depends only on workgroup (0, its job), whose ID is lower, so the lowest unfinished
+// workgroup can always run; the spin is bounded anyway (prog_wait).
+DLAP_DEV void lstm_publish(const RnnJob& J, const ModelDesc* __restrict__ md, const float* sm, const int* sprog) {
+  const int T = J.T, H = md->H, lane = threadIdx.x & 63;
+  const float* shb = sm + gls_out_offset(T, H, md->nrnn);
+  const auto out = gp(J.out);
+  int done = 0;
+  unsigned spins = 0;
+  while (done < T) {
+    const int p = __builtin_amdgcn_readfirstlane(__hip_atomic_load(sprog, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
+    if (p <= done) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > PROG_SPIN_LIMIT) {          // (never: the recurrence always finishes)
+        if (lane == 0) atomicAdd(J.prog + 1, 1);
+        if (lane == 0) __hip_atomic_store(J.prog, T, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+      }
+      continue;
+    }
+    for (int i = done * H + lane; i < p * H; i += 64) out[i] = shb[i];
+    // release: the outputs above are visible before the count (L2 written back, agent scope)
+    if (lane == 0) __hip_atomic_store(J.prog, p, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    done = p;
+  }
+}
+
+template <class P, int KS1, int WMB, int HM, bool DPPG>
+__global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd_rnn(const MlpJob* __restrict__ jobs, MlpDims D,
+                                                                  const RnnJob* __restrict__ rjobs,
+                                                                  const ModelDesc* __restrict__ md) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (blockIdx.x == 0) {
+    __shared__ int s_prog;
+    const RnnJob& R = rjobs[blockIdx.y];
+    const bool tsm = blockIdx.y == 0 && jobs[0].gbits;
+    if (threadIdx.x == 0) s_prog = 0;
+    if (tsm && threadIdx.x == 0) g_mlp_ts[8] = wall_clock64();
+    __syncthreads();
+    const int w = threadIdx.x >> 6;
+    if (w == 0) {
+      lstm_gls_body<HM, DPPG, true, true>(R, md, reinterpret_cast<float*>(smem), &s_prog, tsm ? g_mlp_ts : nullptr, 8);
+    } else if (w == 1) {
+      lstm_publish(R, md, reinterpret_cast<const float*>(smem), &s_prog);
+      if (tsm && threadIdx.x == 64) g_mlp_ts[12] = wall_clock64();
+    }
+    return;
+  }
+  mlp_fwd_body<P, KS1, WMB, false, true>(jobs[blockIdx.y], D, smem, blockIdx.x - 1, gridDim.x - 1);
 }
 
 // ============================== wide evaluation forward ==================================
@@ -1369,6 +1479,42 @@ void launch_mlp_fwd(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int
   if (!ok) dlap_throw_hip(hipErrorInvalidValue, "mlp_fwd: unsupported (KS1, WMB)", __FILE__, __LINE__);
 }
 
+// Fused LSTM + training tower forward (k_mlp_fwd_rnn): grid (1 + gx, jobs). Instantiated for
+// the paper / sweep LSTM widths (H = 4: DPP gate gathers, H = 8) on the fused layer-0 path;
+// returns false for anything else (the caller then launches the LSTM and the towers separately).
+static size_t fwd_rnn_lds(const MlpDims& D0, int H, int tmax) {
+  MlpDims D = D0;
+  D.pp_lds_floats = 0;
+  return std::max(lds_bytes_of(D), gls_lds_floats(tmax, H) * sizeof(float));
+}
+bool mlp_fwd_rnn_supported(const MlpDims& D, int KS1, int WMB, int H, int nrnn, int tmax) {
+  if (D.wide || nrnn <= 0 || D.Dm != H || tmax <= 0) return false;
+  if (!(H == 4 || (H == 8 && !D.fp32))) return false;
+  if (!(KS1 == 2 || KS1 == 4) || !(WMB == 1 || WMB == 2 || WMB == 4)) return false;
+  return fwd_rnn_lds(D, H, tmax) <= 64 * 1024;
+}
+bool launch_mlp_fwd_rnn(const MlpJob* jobs, const RnnJob* rjobs, const ModelDesc* md, int njobs, int gx,
+                        const MlpDims& D0, int KS1, int WMB, int H, int nrnn, int tmax, hipStream_t st) {
+  if (!mlp_fwd_rnn_supported(D0, KS1, WMB, H, nrnn, tmax))
+    dlap_throw_hip(hipErrorInvalidValue, "mlp_fwd_rnn: unsupported shape", __FILE__, __LINE__);
+  MlpDims D = D0;
+  D.pp_lds_floats = 0;                 // the per-period inputs are read as they are published
+  const size_t sh = fwd_rnn_lds(D0, H, tmax);
+  dim3 grid(gx + 1, njobs), block(256);
+#define R_CASE(PR, K, W, HM, DP) \
+  if (KS1 == K && WMB == W && H == HM) { \
+    hipLaunchKernelGGL((k_mlp_fwd_rnn<PR, K, W, HM, DP>), grid, block, sh, st, jobs, D, rjobs, md); \
+    HIP_OK(hipGetLastError()); return true; }
+#define R_KW(PR, HM, DP) R_CASE(PR, 2, 1, HM, DP) R_CASE(PR, 2, 2, HM, DP) R_CASE(PR, 2, 4, HM, DP) \
+  R_CASE(PR, 4, 1, HM, DP) R_CASE(PR, 4, 2, HM, DP) R_CASE(PR, 4, 4, HM, DP)
+  if (D.fp32) { R_KW(PrecF32, 4, true) }
+  else { R_KW(PrecBF16, 4, true) R_KW(PrecBF16, 8, false) }
+#undef R_KW
+#undef R_CASE
+  dlap_throw_hip(hipErrorInvalidValue, "mlp_fwd_rnn: no instantiation", __FILE__, __LINE__);
+  return false;
+}
+
 void launch_mlp_fwd_zx(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int WMB, hipStream_t st,
                        bool train) {
   dim3 grid(gx, njobs), block(512);
@@ -1443,7 +1589,7 @@ void launch_mlp_bwd_mom(const MlpJob* jobs, int njobs, int gx, int nslice, int t
 }
 
 std::vector<long long> mlp_timestamps() {
-  std::vector<long long> v(8);
-  HIP_OK(hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(g_mlp_ts), sizeof(long long) * 8));
+  std::vector<long long> v(16);
+  HIP_OK(hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(g_mlp_ts), sizeof(long long) * 16));
   return v;
 }

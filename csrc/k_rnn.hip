@@ -25,6 +25,7 @@
 #include "layout.h"
 #include "rnn.h"
 #include "update.h"
+#include "lstm_gls.h"
 
 #define DLAP_MAX_M 1024
 
@@ -92,6 +93,8 @@ __global__ __launch_bounds__(64) void k_proj(const RnnJob* __restrict__ jobs,
   if (o0 >= G4 && !J.abias) return;
   const bool tsm = blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0;
   RNN_TS(12, tsm);
+  // the fused forward's progress counter starts from zero (read only by kernels after this one)
+  if (J.prog && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) gp(J.prog)[0] = 0;
   const f32x4 acc = proj_tile(J, md, t0, o0);
   const int l = threadIdx.x, n = l & 15, kq = l >> 4;
   const int o = o0 + n;
@@ -122,40 +125,6 @@ __global__ __launch_bounds__(64) void k_proj(const RnnJob* __restrict__ jobs,
 // so they stay at h = c = 0 and contribute nothing): the time loop has no branches, no
 // memory loads outside LDS, and only fire-and-forget global stores, so nothing on the serial
 // chain waits on HBM.
-template <int HM>
-DLAP_DEV float bcast_dot(const float (&w)[HM], float v) {
-  // sum_j w[j] * v(lane j) as a balanced tree (dependency depth log2 HM + 1)
-  float p[HM];
-#pragma unroll
-  for (int j = 0; j < HM; ++j) p[j] = w[j] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
-#pragma unroll
-  for (int w2 = 1; w2 < HM; w2 *= 2)
-#pragma unroll
-    for (int j = 0; j + w2 < HM; j += 2 * w2) p[j] += p[j + w2];
-  return p[0];
-}
-
-// Same dot product with h_j taken from lane j of the lane's own 16-lane row by a DPP
-// row_newbcast operand (gfx90a+): no VALU -> SGPR -> VALU round trip through v_readlane on the
-// recurrence's critical path. Valid when every lane that uses the result sits in row 0 and the
-// source units are lanes 0..HM-1 (the gate-per-lane form with 4H <= 16).
-template <int J>
-DLAP_DEV float row_bcast(float v) {
-  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + J, 0xF, 0xF, true));
-}
-template <int HM>
-DLAP_DEV float bcast_dot_row(const float (&w)[HM], float v) {
-  static_assert(HM >= 1 && HM <= 4, "row-broadcast dot: 1..4 units");
-  float p0 = w[0] * row_bcast<0>(v);
-  if constexpr (HM == 1) return p0;
-  float p1 = w[1] * row_bcast<1>(v);
-  if constexpr (HM == 2) return p0 + p1;
-  p0 = fmaf(w[2], row_bcast<2>(v), p0);
-  if constexpr (HM == 3) return p0 + p1;
-  p1 = fmaf(w[3], row_bcast<3>(v), p1);
-  return p0 + p1;
-}
-
 template <int HM, bool STAGE>
 __global__ __launch_bounds__(64) void k_lstm(const RnnJob* __restrict__ jobs,
                                              const ModelDesc* __restrict__ md) {
@@ -268,18 +237,6 @@ DLAP_DEV float dppf(float x) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, 0xF, 0xF, false));
 }
 
-template <int HM, bool DPPG>
-DLAP_DEV float gl_gather(float y, int off_units, int q) {
-  if constexpr (DPPG) {
-    // lane l receives lane (l - n) mod 16 for row_ror:n  ->  n = 16 - q*H reads lane l + q*H
-    if (q == 1) return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(y), 0x120 + (16 - HM), 0xF, 0xF, false));
-    if (q == 2) return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(y), 0x120 + (16 - 2 * HM), 0xF, 0xF, false));
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(y), 0x120 + (16 - 3 * HM), 0xF, 0xF, false));
-  } else {
-    return __shfl(y, (int)(threadIdx.x & 63) + off_units, 64);
-  }
-}
-
 template <int HM, bool DPPG, bool STAGE>
 __global__ __launch_bounds__(64) void k_lstm_gl(const RnnJob* __restrict__ jobs,
                                                 const ModelDesc* __restrict__ md) {
@@ -384,16 +341,7 @@ __global__ __launch_bounds__(64) void k_lstm_gl(const RnnJob* __restrict__ jobs,
 }
 
 // ---------------------------------------------------------------------- k_lstm_gls -----
-// k_lstm_gl with every per-step output kept in LDS: the serial loop is branch-free (all 64
-// lanes run the same instructions, results on non-owner lanes are discarded with selects and
-// go to a junk slot) and issues three ds_write per step instead of up to four exec-masked
-// global stores. The saved gates / cells / outputs are flushed to global memory once per
-// layer with coalesced stores; a deeper layer reads its input from the LDS ring directly.
-// Tanh of the g gate and of the cell use 2 sigm(2x) - 1 without the small-|x| Taylor switch:
-// its absolute error (~1e-7) is at fp32 rounding level for the cell update.
-// LDS (floats): xg [T][4H] | gates [T][4H] | cells [T][H] | outputs 2 x [T][H] | junk [64].
-static inline size_t gls_lds_floats(int T, int H) { return (size_t)T * (8 * H + 3 * H) + 64; }
-
+// k_lstm_gl with every per-step output kept in LDS (lstm_gls.h): one wave per job.
 // FUSE: the workgroup (LSTM_FUSE_THREADS) first computes the layer-0 input projections of its
 // job straight into the LDS staging area with all its waves (k_proj + the staging copy in one
 // launch), then waves 1.. exit and wave 0 runs the recurrence (see launch_prologue).
@@ -403,11 +351,12 @@ __global__ __launch_bounds__(FUSE ? LSTM_FUSE_THREADS : 64) void k_lstm_gls(cons
                                                                             const ModelDesc* __restrict__ md) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const RnnJob& J = jobs[blockIdx.x];
-  const int nrnn = md->nrnn;
-  if (nrnn == 0) return;
-  const int T = J.T, H = DPPG ? HM : md->H, G4 = 4 * H;
+  if (md->nrnn == 0) return;
+  const int tsb = J.sc != nullptr ? 0 : 4;
+  const bool tsm = J.sc != nullptr || blockIdx.x == gridDim.x - 1;
+  RNN_TS(tsb + 0, tsm);
   if constexpr (FUSE) {
-    RNN_TS((J.sc != nullptr ? 0 : 4) + 0, J.sc != nullptr || blockIdx.x == gridDim.x - 1);
+    const int T = J.T, G4 = 4 * (DPPG ? HM : md->H);
     const int w = threadIdx.x >> 6, nw = blockDim.x >> 6, l = threadIdx.x & 63;
     const int nto = (G4 + 15) >> 4, ntiles = ((T + 15) >> 4) * nto;
     for (int tile = w; tile < ntiles; tile += nw) {
@@ -423,134 +372,21 @@ __global__ __launch_bounds__(FUSE ? LSTM_FUSE_THREADS : 64) void k_lstm_gls(cons
     __syncthreads();
     if (w > 0) return;
   }
-  const int L = threadIdx.x;
-  // the recurrence is one latency-bound wave: top issue priority on its SIMD, so the tower waves
-  // of a concurrent branch (pipelined evaluation / training) do not stretch its serial chain
-  __builtin_amdgcn_s_setprio(3);
-  const bool gl = L < G4, ul = L < H;
-  const int row = gl ? L : 0;
-  const bool is_g = gl && L >= 2 * H && L < 3 * H;
-  // Pre-scaled exponent domain: a gate row's pre-activation is carried as kx * pre with
-  // kx = -ka log2(e), so act = kb / (1 + exp2(.)) + kc needs no multiply on the chain. The
-  // cell is carried as c' = KC c (KC = -2 log2 e), so tanh(c) = 2 / (1 + exp2(c')) - 1; the
-  // g lanes produce KC g directly (kb, kc scaled by KC) so c' = f c' + i (KC g).
-  constexpr float LOG2E = 1.4426950408889634f;
-  constexpr float KC = -2.f * LOG2E;
-  const float kx = is_g ? -2.f * LOG2E : -LOG2E;
-  const float kb = is_g ? 2.f * KC : 1.f, kc = is_g ? -KC : 0.f;
-  const float ysave = is_g ? 1.f / KC : 1.f;      // saved gates are the unscaled activations
-  const bool drop = J.train && md->dropout > 0.f;
-  const uint32_t thr = (uint32_t)(md->dropout * 16777216.f + 0.5f);
-  const float scale = drop ? 1.f / (1.f - md->dropout) : 1.f;
-  const uint32_t step = J.step ? (uint32_t)*gp(J.step) : 0u;
-  const auto params = gp(J.params);
-  const bool save = J.sc != nullptr;
-  const int tsb = save ? 0 : 4;
-  const bool tsm = save || blockIdx.x == gridDim.x - 1;
-  if (!FUSE) RNN_TS(tsb + 0, tsm);
-  float* sx = sm;
-  float* sgb = sx + (size_t)T * G4;
-  float* scb = sgb + (size_t)T * G4;
-  float* shb0 = scb + (size_t)T * H;
-  float* junk = shb0 + (size_t)2 * T * H;
-  if constexpr (!FUSE) {
-    const auto xg = gp(J.xg);
-    for (int i = L; i < T * G4; i += 64) sx[i] = xg[i];
-    __syncthreads();
-  }
-  for (int l = 0; l < nrnn; ++l) {
-    float whh[HM], wih[HM];
-#pragma unroll
-    for (int j = 0; j < HM; ++j) {
-      const bool ok = gl && j < H;
-      const int jj = j < H ? j : 0;
-      const float a = params[md->lstm_w_hh[l] + row * H + jj];
-      const float b = l > 0 ? params[md->lstm_w_ih[l] + row * H + jj] : 0.f;
-      whh[j] = ok ? a * kx : 0.f;
-      wih[j] = ok ? b * kx : 0.f;
-    }
-    const float bb = l > 0 ? params[md->lstm_b_ih[l] + row] + params[md->lstm_b_hh[l] + row] : 0.f;
-    const float bias = gl ? bb * kx : 0.f;
-    if (l == 0) RNN_TS(tsb + 1, tsm);
-    float* shb = shb0 + (size_t)(l & 1) * T * H;            // this layer's outputs
-    const float* sin = shb0 + (size_t)((l + 1) & 1) * T * H; // previous layer's outputs
-    // per-lane LDS destinations (non-owner lanes write their junk slot)
-    float* gdst = gl ? sgb + L : junk + L;
-    float* udst_c = ul ? scb + L : junk + L;
-    float* udst_h = ul ? shb + L : junk + L;
-    const int gstride = gl ? G4 : 0, ustride = ul ? H : 0;
-    // h / c on lanes >= H are bounded garbage: the broadcast reads lanes j < HM only, and
-    // lanes H <= j < HM carry zero weights
-    float h = ul && J.h0 ? gp(J.h0)[l * H + L] : 0.f, c = ul && J.c0 ? gp(J.c0)[l * H + L] * KC : 0.f;
-    auto cell = [&](int t, float pre) {
-      if constexpr (DPPG) pre += bcast_dot_row<HM>(whh, h);
-      else pre += bcast_dot<HM>(whh, h);
-      const float y = kb * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(pre)) + kc;
-      const float gf = gl_gather<HM, DPPG>(y, H, 1);
-      const float gg = gl_gather<HM, DPPG>(y, 2 * H, 2);
-      const float go = gl_gather<HM, DPPG>(y, 3 * H, 3);
-      c = gf * c + y * gg;                                  // y = i on the unit lanes
-      h = go * (2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(c)) - 1.f);
-      gdst[t * gstride] = y * ysave;
-      udst_c[t * ustride] = c * (1.f / KC);
-      udst_h[t * ustride] = h;
-    };
-    if (l == 0) {
-      // inputs in chunks of CH steps, the next chunk's LDS reads issued a whole chunk ahead:
-      // inside a chunk the recurrence has no LDS load (and no wait on the per-step LDS stores,
-      // which a one-step-ahead read kept on the chain through the shared LDS counter)
-      constexpr int CH = 8;
-      float xa[CH], xb[CH];
-      auto ldch = [&](int t0, float (&x)[CH]) {
-#pragma unroll
-        for (int k = 0; k < CH; ++k) x[k] = sx[min(t0 + k, T - 1) * G4 + row];
-      };
-      const int tfull = T / CH * CH;
-      ldch(0, xa);
-      for (int t0 = 0; t0 < tfull; t0 += CH) {
-        ldch(t0 + CH, xb);
-#pragma unroll
-        for (int k = 0; k < CH; ++k) cell(t0 + k, xa[k] * kx);
-#pragma unroll
-        for (int k = 0; k < CH; ++k) xa[k] = xb[k];
-      }
-      for (int t = tfull; t < T; ++t) cell(t, sx[t * G4 + row] * kx);
-    } else {
-      const uint32_t key_in = dropout_key(J.seed, step, 32 + (l - 1));
-      float nx = ul ? sin[L] : 0.f;
-      for (int t = 0; t < T; ++t) {
-        float xv = ul ? nx : 0.f;
-        nx = sin[(t + 1 < T ? t + 1 : t) * H + (ul ? L : 0)];
-        if (drop) xv = dropout_keep(key_in, (uint32_t)t, (uint32_t)(ul ? L : 0), thr) ? xv * scale : 0.f;
-        float pre = bias;
-#pragma unroll
-        for (int j = 0; j < HM; ++j)
-          pre += wih[j] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), j));
-        cell(t, pre);
-      }
-    }
-    if (l == 0) RNN_TS(tsb + 2, tsm);
-    __syncthreads();
-    // flush: saved gates / cells / outputs (train), tower input (last layer)
-    const bool last = l + 1 == nrnn;
-    if (save) {
-      const auto sg = gp(J.sg) + (size_t)l * T * G4;
-      const auto sc = gp(J.sc) + (size_t)l * T * H;
-      const auto sh = gp(J.sh) + (size_t)l * T * H;
-      for (int i = L; i < T * G4; i += 64) sg[i] = sgb[i];
-      for (int i = L; i < T * H; i += 64) { sc[i] = scb[i]; sh[i] = shb[i]; }
-    }
-    if (last) {
-      const auto out = gp(J.out);
-      for (int i = L; i < T * H; i += 64) out[i] = shb[i];
-    }
-    __syncthreads();
-  }
-  RNN_TS(tsb + 3, tsm);
+  lstm_gls_body<HM, DPPG, !FUSE, false>(J, md, sm, nullptr, tsm ? g_rnn_ts : nullptr, tsb);
 }
 
 static const bool g_rtrace = [] { const char* v = std::getenv("DLAP_TRACE_HOST"); return v && *v == '1'; }();
 #define RTRACE(...) do { if (g_rtrace) { fprintf(stderr, "[dlap-trace] " __VA_ARGS__); fputc('\n', stderr); fflush(stderr); } } while (0)
+
+void launch_proj(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* md, const ModelDesc& mh,
+                 hipStream_t st, bool abias) {
+  const int G4 = mh.nrnn > 0 ? 4 * mh.H : 0;
+  const int ny = abias ? mh.proj_np / 16 : (G4 + 15) / 16;
+  RTRACE("proj jobs=%p njobs=%d tmax=%d ny=%d st=%p", (const void*)jobs, njobs, tmax, ny, (void*)st);
+  if (ny <= 0) return;
+  hipLaunchKernelGGL(k_proj, dim3((tmax + 15) / 16, ny, njobs), dim3(64), 0, st, jobs, md, 0);
+  HIP_OK(hipGetLastError());
+}
 
 void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* md, const ModelDesc& mh,
                      hipStream_t st, bool abias, bool lstm) {

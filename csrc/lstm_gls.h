@@ -1,0 +1,221 @@
+// The gate-per-lane LSTM recurrence with every per-step output kept in LDS (k_lstm_gls), shared
+// by the stand-alone prologue kernel (k_rnn.hip) and the fused LSTM + training-tower forward
+// (k_mlp_fwd_rnn in k_mlp.hip), where it runs on wave 0 of workgroup 0 and publishes its
+// progress period by period to the tower workgroups.
+//
+// Reference: `MacroLSTM.forward` (`/root/reference/src/model.py:21-84`), one nn.LSTM over the
+// T-sequence with batch 1, PyTorch gate order i, f, g, o, both biases.
+#pragma once
+#include "common.h"
+#include "layout.h"
+#include "rnn.h"
+
+// sum_j w[j] * v(lane j) as a balanced tree (dependency depth log2 HM + 1)
+template <int HM>
+DLAP_DEV float bcast_dot(const float (&w)[HM], float v) {
+  float p[HM];
+#pragma unroll
+  for (int j = 0; j < HM; ++j) p[j] = w[j] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+#pragma unroll
+  for (int w2 = 1; w2 < HM; w2 *= 2)
+#pragma unroll
+    for (int j = 0; j + w2 < HM; j += 2 * w2) p[j] += p[j + w2];
+  return p[0];
+}
+
+// Same dot product with h_j taken from lane j of the lane's own 16-lane row by a DPP
+// row_newbcast operand (gfx90a+): no VALU -> SGPR -> VALU round trip through v_readlane on the
+// recurrence's critical path. Valid when every lane that uses the result sits in row 0 and the
+// source units are lanes 0..HM-1 (the gate-per-lane form with 4H <= 16).
+template <int J>
+DLAP_DEV float row_bcast(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + J, 0xF, 0xF, true));
+}
+template <int HM>
+DLAP_DEV float bcast_dot_row(const float (&w)[HM], float v) {
+  static_assert(HM >= 1 && HM <= 4, "row-broadcast dot: 1..4 units");
+  float p0 = w[0] * row_bcast<0>(v);
+  if constexpr (HM == 1) return p0;
+  float p1 = w[1] * row_bcast<1>(v);
+  if constexpr (HM == 2) return p0 + p1;
+  p0 = fmaf(w[2], row_bcast<2>(v), p0);
+  if constexpr (HM == 3) return p0 + p1;
+  p1 = fmaf(w[3], row_bcast<3>(v), p1);
+  return p0 + p1;
+}
+
+// Gate-per-lane gather: lane L owns gate row L (q = L / H, unit L % H); the f/g/o values are
+// moved onto the unit lanes (DPP row rotates when 4H <= 16, ds_bpermute otherwise).
+template <int HM, bool DPPG>
+DLAP_DEV float gl_gather(float y, int off_units, int q) {
+  if constexpr (DPPG) {
+    // lane l receives lane (l - n) mod 16 for row_ror:n  ->  n = 16 - q*H reads lane l + q*H
+    if (q == 1) return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(y), 0x120 + (16 - HM), 0xF, 0xF, false));
+    if (q == 2) return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(y), 0x120 + (16 - 2 * HM), 0xF, 0xF, false));
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(y), 0x120 + (16 - 3 * HM), 0xF, 0xF, false));
+  } else {
+    return __shfl(y, (int)(threadIdx.x & 63) + off_units, 64);
+  }
+}
+
+// LDS ordering among the lanes of ONE wave (the recurrence runs on a single wave; the fused
+// kernel's publisher wave never takes part in a workgroup barrier, so none is used here).
+DLAP_DEV void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// LDS (floats): xg [T][4H] | gates [T][4H] | cells [T][H] | outputs 2 x [T][H] | junk [64].
+__host__ __device__ inline size_t gls_lds_floats(int T, int H) { return (size_t)T * (8 * H + 3 * H) + 64; }
+// the last layer's output ring inside that image
+__host__ __device__ inline size_t gls_out_offset(int T, int H, int nrnn) {
+  return (size_t)T * (8 * H + H) + (size_t)((nrnn - 1) & 1) * T * H;
+}
+
+// The recurrence on one wave (lanes = threadIdx.x & 63). The serial loop is branch-free (all 64
+// lanes run the same instructions, results on non-owner lanes are discarded with selects and go
+// to a junk slot) and issues three ds_write per step. The saved gates / cells / outputs are
+// flushed to global memory once per layer with coalesced stores; a deeper layer reads its input
+// from the LDS ring directly. Tanh of the g gate and of the cell use 2 sigm(2x) - 1 (absolute
+// error ~1e-7, fp32 rounding level for the cell update).
+//   STAGEX: copy the layer-0 input projections xg (global) into LDS first (else the caller
+//           has put them there);
+//   PUB:    every 8 steps of the last layer store the number of finished periods to *sprog
+//           (LDS, workgroup-scope release); the output flush to J.out is left to the
+//           publisher wave (lstm_publish in k_mlp.hip).
+//   ts:     optional in-kernel timestamps (slots tsb + 1, tsb + 2, tsb + 3).
+template <int HM, bool DPPG, bool STAGEX, bool PUB>
+DLAP_DEV void lstm_gls_body(const RnnJob& J, const ModelDesc* __restrict__ md, float* sm, int* sprog,
+                            long long* ts, int tsb) {
+  const int nrnn = md->nrnn;
+  const int T = J.T, H = DPPG ? HM : md->H, G4 = 4 * H;
+  const int L = threadIdx.x & 63;
+  auto stamp = [&](int slot) { if (ts && L == 0) ts[tsb + slot] = wall_clock64(); };
+  auto publish = [&](int v) {
+    if constexpr (PUB) __hip_atomic_store(sprog, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  };
+  // the recurrence is one latency-bound wave: top issue priority on its SIMD, so the tower waves
+  // of a concurrent branch (pipelined evaluation / training) do not stretch its serial chain
+  __builtin_amdgcn_s_setprio(3);
+  const bool gl = L < G4, ul = L < H;
+  const int row = gl ? L : 0;
+  const bool is_g = gl && L >= 2 * H && L < 3 * H;
+  // Pre-scaled exponent domain: a gate row's pre-activation is carried as kx * pre with
+  // kx = -ka log2(e), so act = kb / (1 + exp2(.)) + kc needs no multiply on the chain. The
+  // cell is carried as c' = KC c (KC = -2 log2 e), so tanh(c) = 2 / (1 + exp2(c')) - 1; the
+  // g lanes produce KC g directly (kb, kc scaled by KC) so c' = f c' + i (KC g).
+  constexpr float LOG2E = 1.4426950408889634f;
+  constexpr float KC = -2.f * LOG2E;
+  const float kx = is_g ? -2.f * LOG2E : -LOG2E;
+  const float kb = is_g ? 2.f * KC : 1.f, kc = is_g ? -KC : 0.f;
+  const float ysave = is_g ? 1.f / KC : 1.f;      // saved gates are the unscaled activations
+  const bool drop = J.train && md->dropout > 0.f;
+  const uint32_t thr = (uint32_t)(md->dropout * 16777216.f + 0.5f);
+  const float scale = drop ? 1.f / (1.f - md->dropout) : 1.f;
+  const uint32_t step = J.step ? (uint32_t)*gp(J.step) : 0u;
+  const auto params = gp(J.params);
+  const bool save = J.sc != nullptr;
+  float* sx = sm;
+  float* sgb = sx + (size_t)T * G4;
+  float* scb = sgb + (size_t)T * G4;
+  float* shb0 = scb + (size_t)T * H;
+  float* junk = shb0 + (size_t)2 * T * H;
+  if constexpr (STAGEX) {
+    const auto xg = gp(J.xg);
+    for (int i = L; i < T * G4; i += 64) sx[i] = xg[i];
+    wave_lds_sync();
+  }
+  for (int l = 0; l < nrnn; ++l) {
+    const bool last = l + 1 == nrnn;
+    float whh[HM], wih[HM];
+#pragma unroll
+    for (int j = 0; j < HM; ++j) {
+      const bool ok = gl && j < H;
+      const int jj = j < H ? j : 0;
+      const float a = params[md->lstm_w_hh[l] + row * H + jj];
+      const float b = l > 0 ? params[md->lstm_w_ih[l] + row * H + jj] : 0.f;
+      whh[j] = ok ? a * kx : 0.f;
+      wih[j] = ok ? b * kx : 0.f;
+    }
+    const float bb = l > 0 ? params[md->lstm_b_ih[l] + row] + params[md->lstm_b_hh[l] + row] : 0.f;
+    const float bias = gl ? bb * kx : 0.f;
+    if (l == 0) stamp(1);
+    float* shb = shb0 + (size_t)(l & 1) * T * H;            // this layer's outputs
+    const float* sin = shb0 + (size_t)((l + 1) & 1) * T * H; // previous layer's outputs
+    // per-lane LDS destinations (non-owner lanes write their junk slot)
+    float* gdst = gl ? sgb + L : junk + L;
+    float* udst_c = ul ? scb + L : junk + L;
+    float* udst_h = ul ? shb + L : junk + L;
+    const int gstride = gl ? G4 : 0, ustride = ul ? H : 0;
+    // h / c on lanes >= H are bounded garbage: the broadcast reads lanes j < HM only, and
+    // lanes H <= j < HM carry zero weights
+    float h = ul && J.h0 ? gp(J.h0)[l * H + L] : 0.f, c = ul && J.c0 ? gp(J.c0)[l * H + L] * KC : 0.f;
+    auto cell = [&](int t, float pre) {
+      if constexpr (DPPG) pre += bcast_dot_row<HM>(whh, h);
+      else pre += bcast_dot<HM>(whh, h);
+      const float y = kb * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(pre)) + kc;
+      const float gf = gl_gather<HM, DPPG>(y, H, 1);
+      const float gg = gl_gather<HM, DPPG>(y, 2 * H, 2);
+      const float go = gl_gather<HM, DPPG>(y, 3 * H, 3);
+      c = gf * c + y * gg;                                  // y = i on the unit lanes
+      h = go * (2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(c)) - 1.f);
+      gdst[t * gstride] = y * ysave;
+      udst_c[t * ustride] = c * (1.f / KC);
+      udst_h[t * ustride] = h;
+    };
+    if (l == 0) {
+      // inputs in chunks of CH steps, the next chunk's LDS reads issued a whole chunk ahead:
+      // inside a chunk the recurrence has no LDS load (and no wait on the per-step LDS stores,
+      // which a one-step-ahead read kept on the chain through the shared LDS counter)
+      constexpr int CH = 8;
+      float xa[CH], xb[CH];
+      auto ldch = [&](int t0, float (&x)[CH]) {
+#pragma unroll
+        for (int k = 0; k < CH; ++k) x[k] = sx[min(t0 + k, T - 1) * G4 + row];
+      };
+      const int tfull = T / CH * CH;
+      ldch(0, xa);
+      for (int t0 = 0; t0 < tfull; t0 += CH) {
+        ldch(t0 + CH, xb);
+#pragma unroll
+        for (int k = 0; k < CH; ++k) cell(t0 + k, xa[k] * kx);
+#pragma unroll
+        for (int k = 0; k < CH; ++k) xa[k] = xb[k];
+        if (PUB && last) publish(t0 + CH);
+      }
+      for (int t = tfull; t < T; ++t) cell(t, sx[t * G4 + row] * kx);
+    } else {
+      const uint32_t key_in = dropout_key(J.seed, step, 32 + (l - 1));
+      float nx = ul ? sin[L] : 0.f;
+      for (int t = 0; t < T; ++t) {
+        float xv = ul ? nx : 0.f;
+        nx = sin[(t + 1 < T ? t + 1 : t) * H + (ul ? L : 0)];
+        if (drop) xv = dropout_keep(key_in, (uint32_t)t, (uint32_t)(ul ? L : 0), thr) ? xv * scale : 0.f;
+        float pre = bias;
+#pragma unroll
+        for (int j = 0; j < HM; ++j)
+          pre += wih[j] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), j));
+        cell(t, pre);
+        if (PUB && last && (t & 7) == 7) publish(t + 1);
+      }
+    }
+    if (PUB && last) publish(T);
+    if (l == 0) stamp(2);
+    wave_lds_sync();
+    // flush: saved gates / cells / outputs (train), tower input (last layer)
+    if (save) {
+      const auto sg = gp(J.sg) + (size_t)l * T * G4;
+      const auto sc = gp(J.sc) + (size_t)l * T * H;
+      const auto sh = gp(J.sh) + (size_t)l * T * H;
+      for (int i = L; i < T * G4; i += 64) sg[i] = sgb[i];
+      for (int i = L; i < T * H; i += 64) { sc[i] = scb[i]; sh[i] = shb[i]; }
+    }
+    if (last && !PUB) {
+      const auto out = gp(J.out);
+      for (int i = L; i < T * H; i += 64) out[i] = shb[i];
+    }
+    wave_lds_sync();
+  }
+  stamp(3);
+}

@@ -33,6 +33,9 @@ struct MlpJob {
   const f32x4* z;         // wide path: [ntiles][zc][64] layer-0 pre-activations (k_proj0)
   bf16x8* dz_out;         // wide path, bwd: [ntiles][UB][64] layer-0 dz fragments (rows as k)
   f32x4* z_out;           // wide path, fused training forward: where it stores the layer-0 z
+  const int* prog;        // fused LSTM + tower forward (k_mlp_fwd_rnn): periods of pp published
+  int* prog_err;          //   ... and the spin-timeout counter (0 unless a wait gave up)
+  int prog_mode;          //   0: acquire fence after the wait; 1: cache-bypassing pp loads
   int store_mz;           // ... including the moment blocks (phase 2: the moment backward reads them)
   int R, N, T;
   unsigned seed;
@@ -92,6 +95,12 @@ void launch_mlp_fwd_zx(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, 
                        bool train = false);
 void launch_mlp_bwd_sdf(const MlpJob* jobs, int njobs, int gx, int nslice, int tps, const MlpDims& D,
                         int KS1, int slab_stride, hipStream_t st);
+struct RnnJob;
+struct ModelDesc;
+// fused LSTM + training tower forward; false = not instantiated for this shape (see k_mlp.hip)
+bool mlp_fwd_rnn_supported(const MlpDims& D, int KS1, int WMB, int H, int nrnn, int tmax);
+bool launch_mlp_fwd_rnn(const MlpJob* jobs, const RnnJob* rjobs, const ModelDesc* md, int njobs, int gx,
+                        const MlpDims& D, int KS1, int WMB, int H, int nrnn, int tmax, hipStream_t st);
 void launch_dropmask(const MlpJob* jobs, int njobs, int ntiles, const MlpDims& D, int step_offset,
                      hipStream_t st);
 void launch_mlp_bwd_mom(const MlpJob* jobs, int njobs, int gx, int nslice, int tps, const MlpDims& D,

@@ -20,6 +20,8 @@ struct RnnJob {
   const int* step;       // dropout stream counter
   const float* h0;       // [nrnn][H] initial hidden state (zero unless a caller passed one)
   const float* c0;       // [nrnn][H] initial cell state
+  int* prog;             // fused LSTM + tower forward: [0] periods published, [1] spin timeouts;
+                         //   k_proj zeroes [0] ahead of every launch (stream order)
   unsigned seed;
   int train;
 };
@@ -29,5 +31,10 @@ struct RnnJob {
 // the moment network does not read the LSTM state).
 void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* md, const ModelDesc& mh,
                      hipStream_t st, bool abias = true, bool lstm = true);
+
+// k_proj only (layer-0 gate projections, and the moment bias table when abias): the fused
+// LSTM + tower forward runs the recurrence itself
+void launch_proj(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* md, const ModelDesc& mh,
+                 hipStream_t st, bool abias);
 
 std::vector<long long> rnn_timestamps();

@@ -628,3 +628,27 @@ def test_epochs_past_history_capacity_are_dropped_not_written_out_of_bounds():
     assert np.isfinite(h[:, 1]).all()
     after = eng.params(0)
     assert np.isfinite(after).all() and np.abs(after - before).max() > 0
+
+
+@pytest.mark.parametrize("rnn,G,dropout", [([4], 1, 0.05), ([8], 2, 0.05), ([4, 4], 1, 0.3)])
+def test_fused_lstm_tower_forward_equals_two_launches(monkeypatch, rnn, G, dropout):
+    """k_mlp_fwd_rnn (the LSTM on workgroup 0 publishing its periods, the towers trailing it)
+    against the separate LSTM + tower launches: bitwise-equal parameters and history through
+    all three phases (graph replays, pipelined), and no spin wait ever gave up."""
+    cfg = default_cli_config(8, 46, rnn_dim=rnn, dropout=dropout)
+    data = _batch()
+    res = []
+    for overlap in ("0", "1"):
+        monkeypatch.setenv("DLAP_RNN_OVERLAP", overlap)
+        eng, _ = _engine(cfg, n_models=G, seeds=(5, 6), data=data)
+        assert eng.eng.fused_forward(1) == (overlap == "1")
+        for ph, n in ((1, 4), (2, 2), (3, 5)):
+            eng.eng.begin_phase(ph)
+            eng.run(ph, n, 1e-3, 1, 1.0, True)
+        eng.eng.backward_only(3)
+        eng.eng.sync()
+        assert eng.eng.prog_timeouts() == 0
+        res.append([(eng.history_rows(g), eng.params(g), eng.eng.get_grads(g)) for g in range(G)])
+    for a, b in zip(res[0], res[1]):
+        for x, y in zip(a, b):
+            np.testing.assert_array_equal(np.nan_to_num(x), np.nan_to_num(y))

@@ -41,6 +41,10 @@ def main():
         print(f"  k_mlp_fwd blk0 : stage {um(0, 1):7.1f}  tile1 {um(1, 2):7.1f}  rest {um(2, 3):7.1f}")
         print(f"  k_mlp_fwd last : stage {um(4, 5):7.1f}  tile1 {um(5, 6):7.1f}  rest {um(6, 7):7.1f}  "
               f"start-lag {(m[4] - m[0]) / 100.0:7.1f}  end-lag {(m[7] - m[3]) / 100.0:7.1f}")
+        if eng.eng.fused_forward(3):
+            print(f"  fused fwd blk0 : start->recur {um(8, 9):7.1f}  recur {um(9, 10):7.1f}  flush {um(10, 11):7.1f}  "
+                  f"publisher-end {um(8, 12):7.1f}  first tower start {(m[0] - m[8]) / 100.0:7.1f}  "
+                  f"last tower end {(max(m[3], m[7]) - m[8]) / 100.0:7.1f}")
         lt = np.array(mod.Engine.loss_timestamps(), dtype=np.int64)
         ul = lambda a, b: (lt[b] - lt[a]) / 100.0  # noqa: E731
         print(f"  k_job_metrics  : losses {ul(0, 1):7.1f}  pass0 {ul(1, 2):7.1f}  pass1 {ul(2, 3):7.1f}")
