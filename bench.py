@@ -173,6 +173,7 @@ def measure_ensemble(d, cfg, pc, seed_panel: int = 0):
         "panel_setup_s_rank0": round(t_panel, 3),
         "train_wall_s_per_rank": [round(x, 3) for x in res["train_wall_s_per_rank"]],
         "models_per_rank": [len(comm.shard(len(ENSEMBLE_SEEDS), r, d.world)) for r in range(d.world)],
+        "breakdown_s_per_rank": res.get("breakdown_s_per_rank"),
         "schedule": [256, 64, 1024], "seeds": list(ENSEMBLE_SEEDS), "failed": res["failed"],
         "test_sharpe": res.get("test_sharpe"), "valid_sharpe": res.get("valid_sharpe"),
         "reference_cpu_estimate_s": round(9 * 1344 / REF_EPOCHS_PER_S, 1),

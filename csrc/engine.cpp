@@ -35,6 +35,7 @@
 
 #include "layout.h"
 #include "loss.h"
+#include <chrono>
 #include "mlp.h"
 #include "rnn.h"
 #include "update.h"
@@ -864,15 +865,21 @@ class Engine {
   // per-period bias table from the prologue)
   // fused LSTM + training tower forward (k_mlp_fwd_rnn): the towers trail the recurrence
   // period by period instead of starting after it (DLAP_RNN_OVERLAP=0: two launches)
+  double capture_s_ = 0.0;                   // host time spent capturing / instantiating graphs
   bool rnn_overlap_ = true;
   bool rnn_overlap_eval_ = false;            // ... also on the evaluation branch (DLAP_RNN_OVERLAP_EVAL)
+  // the evaluation being enqueued runs alone on the GPU (the pipeline's tail, the sequential
+  // epoch): fused there in any case -- beside the training chain the spinning tower workgroups
+  // of both fused launches compete for the same CUs (profiles/r3_knobs_fused_eval.log)
+  bool eval_solo_ = false;
   int prog_mode_ = 1;                        // DLAP_PROG_MODE (see MlpJob::prog_mode)
   DevBuf<int> prog_;
   bool fused_eval() const {
-    return rnn_overlap_ && rnn_overlap_eval_ && md_.nrnn > 0 && !md_.md.wide && n_eval_jobs_ > 0 &&
+    return rnn_overlap_ && (rnn_overlap_eval_ || eval_solo_) && md_.nrnn > 0 && !md_.md.wide && n_eval_jobs_ > 0 &&
            mlp_fwd_rnn_supported(md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, tmax_eval_);
   }
  public:
+  double capture_seconds() const { return capture_s_; }
   bool fused_fwd(int phase) const {
     (void)phase;
     return rnn_overlap_ && md_.nrnn > 0 && !md_.md.wide &&
@@ -1642,7 +1649,7 @@ class Engine {
     enqueue_train_grads(phase);
     HTRACE("launch_update");
     launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);
-    if (phase != 2) enqueue_eval(st_);
+    if (phase != 2) { SoloScope solo(eval_solo_); enqueue_eval(st_); }
     enqueue_epoch_end(phase, ignore_epoch, sel, st_);
   }
   void enqueue_head(int phase, float lr) {
@@ -1693,14 +1700,20 @@ class Engine {
     HTRACE("launch_update");
     launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);
   }
+  struct SoloScope {
+    bool& f;
+    explicit SoloScope(bool& x) : f(x) { f = true; }
+    ~SoloScope() { f = false; }
+  };
   void enqueue_tail(int phase, int ignore_epoch, float sel) {
-    enqueue_eval(st_);
+    { SoloScope solo(eval_solo_); enqueue_eval(st_); }
     enqueue_epoch_end(phase, ignore_epoch, sel, st_);
   }
   template <typename F>
   hipGraphExec_t graph_for(const std::string& key, F&& enqueue) {
     auto it = graphs_.find(key);
     if (it != graphs_.end()) return it->second;
+    const auto t_cap = std::chrono::steady_clock::now();
     hipGraph_t graph;
     {
       std::lock_guard<std::mutex> g(g_legacy_mu);
@@ -1718,6 +1731,7 @@ class Engine {
     // latency-critical region)
     HIP_OK(hipGraphUpload(exec, st_));
     graphs_.emplace(key, exec);
+    capture_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t_cap).count();
     return exec;
   }
   void fwd_only(int s, bool train_mode, bool do_mom, bool wait) {
@@ -1830,6 +1844,7 @@ PYBIND11_MODULE(_dlap_hip, m) {
       .def_static("rnn_timestamps", []() { return rnn_timestamps(); })
       .def("fused_forward", [](Engine& e, int phase) { return e.fused_fwd(phase); })
       .def("prog_timeouts", &Engine::prog_timeouts)
+      .def("capture_seconds", [](Engine& e) { return e.capture_seconds(); })
       .def_static("loss_timestamps", []() { return loss_timestamps(); })
       .def_static("mlp_timestamps", []() { return mlp_timestamps(); })
       .def("forward_split", &Engine::forward_split, py::arg("s"), py::arg("train_mode"), py::arg("do_mom"),

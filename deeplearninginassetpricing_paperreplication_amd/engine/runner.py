@@ -229,19 +229,23 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
     say(f"  SDF network: {n_sdf:,}")
     say(f"  Moment network: {n_mom:,}")
     total = num_epochs_unc + num_epochs_moment + num_epochs
-    eng = GANEngine(spec, n_models, max_epochs=max(total, 1), precision=precision)
-    eng.set_data(train_data, valid_data, test_data)
-    for g, m in enumerate(models):
-        eng.set_model(g, m, seeds[g])
-        if lrs is not None:
-            eng.eng.set_lr(g, float(lrs[g]))
+    timers = Timers()
+    with trace_range("engine-build", timers):
+        eng = GANEngine(spec, n_models, max_epochs=max(total, 1), precision=precision)
+    with trace_range("panel-compaction", timers):
+        eng.set_data(train_data, valid_data, test_data)
+    with trace_range("set-params", timers):
+        for g, m in enumerate(models):
+            eng.set_model(g, m, seeds[g])
+            if lrs is not None:
+                eng.eng.set_lr(g, float(lrs[g]))
+        eng.eng.sync()
     template = AssetPricingGAN(config)
     t_start = time.time()
     best_state = [False] * n_models
     schedule = (num_epochs_unc, num_epochs_moment, num_epochs)
     if resume_path is None and n_models == 1 and save_dirs[0]:
         resume_path = os.path.join(save_dirs[0], ckpt.RESUME_FILE)
-    timers = Timers()
     monitor = NonFiniteMonitor(n_models, HIST, nan_policy)
     start = (1, 0)                  # (phase, epochs done in it) to continue from
     run_fp = ckpt.run_fingerprint(lr, ignore_epoch, selection_sign,
@@ -347,7 +351,8 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
     say("\n" + "=" * 70 + "\nTraining Complete!")
     say(f"Total time: {elapsed / 60:.1f} minutes")
     say(f"Total epochs: {total} ({num_epochs_unc} + {num_epochs_moment} + {num_epochs})\n" + "=" * 70)
-    finals = {s: eng.evaluate(s) for s in eng.splits}
+    with trace_range("final-eval", timers):
+        finals = {s: eng.evaluate(s) for s in eng.splits}
     if verbose:
         print("\nBest Model Performance (normalized weights):")
         for s, name in ((0, "Train"), (1, "Valid"), (2, "Test ")):
@@ -368,6 +373,8 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
     train_3phase_gpu.last_engine = eng
     train_3phase_gpu.last_elapsed = elapsed
     train_3phase_gpu.last_timers = timers
+    # host time of the graph captures (inside the first run of every phase's epoch ranges)
+    train_3phase_gpu.last_capture_s = float(eng.eng.capture_seconds())
     train_3phase_gpu.last_nonfinite = monitor.nonfinite_models
     if n_models == 1:
         return out_models[0], hists[0]

@@ -52,7 +52,8 @@ def train_members(config: Dict, batches: Dict[str, Dict], seeds: Sequence[int], 
                   selection_sign: float = 1.0, fail_seeds: Sequence[int] = ()) -> List[Dict]:
     """Train ``seeds`` on this process. Returns one record per seed:
     ``{seed, ok, error, weights: {split: [T, N] float32}, history}``."""
-    recs = [{"seed": int(s), "ok": False, "error": None, "weights": None, "history": None} for s in seeds]
+    recs = [{"seed": int(s), "ok": False, "error": None, "weights": None, "history": None, "timing": None}
+            for s in seeds]
     dirs = [None] * len(seeds)
     if save_root:
         for i, s in enumerate(seeds):
@@ -80,6 +81,10 @@ def train_members(config: Dict, batches: Dict[str, Dict], seeds: Sequence[int], 
                 seeds=[seeds[i] for i in todo], save_dirs=[dirs[i] for i in todo])
             if len(todo) == 1:
                 res_m, res_h = [res_m], [res_h]
+            tm = dict(train_3phase_gpu.last_timers.total)
+            tm["graph-capture"] = train_3phase_gpu.last_capture_s
+            for i in todo:
+                recs[i]["timing"] = tm
             for k, i in enumerate(todo):
                 fe = res_m[k].engine_final_eval
                 recs[i].update(ok=True, history=res_h[k],
@@ -120,6 +125,13 @@ def run_ensemble(config: Dict, batches: Dict[str, Dict], seeds: Sequence[int] = 
     recs = train_members(config, batches, [seeds[i] for i in mine], d.device, epochs, lr, ignore_epoch,
                          print_freq, save_root, verbose, selection_sign, fail_seeds)
     t_train = time.time() - t0
+    # per-rank breakdown of the non-epoch costs (BREAKDOWN order), seconds
+    tm = next((r["timing"] for r in recs if r.get("timing")), None) or {}
+    epochs_s = sum(v for k, v in tm.items() if k.endswith("-epochs"))
+    parts = {"engine_build": tm.get("engine-build", 0.0), "panel_compaction": tm.get("panel-compaction", 0.0),
+             "set_params": tm.get("set-params", 0.0), "graph_capture": tm.get("graph-capture", 0.0),
+             "epochs": max(0.0, epochs_s - tm.get("graph-capture", 0.0)), "final_eval": tm.get("final-eval", 0.0)}
+    t1 = time.time()
     ok_local = np.array([r["ok"] for r in recs], dtype=np.float32).reshape(-1, 1)
     ok = comm.all_gather_rows(d, ok_local, len(seeds), mine)[:, 0] > 0.5
     weights: List[Dict[str, np.ndarray]] = [dict() for _ in seeds]
@@ -127,19 +139,26 @@ def run_ensemble(config: Dict, batches: Dict[str, Dict], seeds: Sequence[int] = 
     wdev = {}
     for sp in SPLITS:
         T, N = batches[sp]["mask"].shape
+        if on_gpu:
+            # RCCL all-gather into the rank's GPU, the ensemble math stays there (K11 kernel): the
+            # members' weights go to the device once, nothing comes back to the host
+            loc_t = torch.full((len(recs), T, N), float("nan"), dtype=torch.float32, device=d.device)
+            for k, r in enumerate(recs):
+                if r["ok"]:
+                    loc_t[k].copy_(torch.from_numpy(r["weights"][sp]), non_blocking=True)
+            allt = comm.all_gather_rows_tensor(d, loc_t, len(seeds), mine)
+            wdev[sp] = allt.to(d.device)    # (a gloo rehearsal gathers on the host)
+            continue
         loc = np.full((len(recs), T, N), np.nan, np.float32)
         for k, r in enumerate(recs):
             if r["ok"]:
                 loc[k] = r["weights"][sp]
-        if on_gpu:
-            # RCCL all-gather into the rank's GPU, the ensemble math stays there (K11 kernel)
-            allt = comm.all_gather_rows_tensor(d, torch.from_numpy(loc).to(d.device), len(seeds), mine)
-            wdev[sp] = allt.to(d.device)    # (a gloo rehearsal gathers on the host)
-            allw = allt.cpu().numpy()
-        else:
-            allw = comm.all_gather_rows(d, loc, len(seeds), mine)   # one collective per split
+        allw = comm.all_gather_rows(d, loc, len(seeds), mine)   # one collective per split
         for i in range(len(seeds)):
             weights[i][sp] = allw[i]
+    if on_gpu:
+        torch.cuda.synchronize(d.device)
+    parts["all_gather"] = time.time() - t1
     walls = comm.all_gather_rows(d, np.array([[t_train]], np.float64), d.world, [d.rank])[:, 0]
     good = [i for i in range(len(seeds)) if ok[i]]
     np_b = {sp: {"returns": _host(batches[sp]["returns"]), "mask": _host(batches[sp]["mask"])} for sp in SPLITS}
@@ -156,6 +175,11 @@ def run_ensemble(config: Dict, batches: Dict[str, Dict], seeds: Sequence[int] = 
         ind = np.full(len(seeds), np.nan)
         ind[good] = res["individual_sharpes"]
         out["individual_sharpes"] = ind.tolist()
+    parts["ensemble_metrics"] = time.time() - t1 - parts["all_gather"]
+    parts["train_total"] = t_train
+    keys = list(parts)
+    rows = comm.all_gather_rows(d, np.array([[parts[k] for k in keys]], np.float64), d.world, [d.rank])
+    out["breakdown_s_per_rank"] = [{k: round(float(v), 4) for k, v in zip(keys, row)} for row in rows]
     out["errors"] = {int(r["seed"]): r["error"] for r in recs if r["error"]}
     return out
 
