@@ -232,7 +232,8 @@ class Engine {
     zx_eval_ = env_int("DLAP_ZX_EVAL", 1) != 0;
     zx_train_ = env_int("DLAP_ZX_TRAIN", 1) != 0;
     zx_gx_ = std::max(1, env_int("DLAP_ZX_GX", 256));
-    train_first_ = env_int("DLAP_TRAIN_FIRST", 1);
+    train_first_ = env_int("DLAP_TRAIN_FIRST", 2);
+    eval_after_bwd_ = env_int("DLAP_EVAL_AFTER_BWD", 0) != 0;
     h_cache_ = env_int("DLAP_H_CACHE", 1) != 0;
     gram_on_ = env_int("DLAP_GRAM", 1) != 0;
     rnn_overlap_ = env_int("DLAP_RNN_OVERLAP", 1) != 0;
@@ -872,6 +873,7 @@ class Engine {
   // epoch): fused there in any case -- beside the training chain the spinning tower workgroups
   // of both fused launches compete for the same CUs (profiles/r3_knobs_fused_eval.log)
   bool eval_solo_ = false;
+  bool eval_after_bwd_ = false;              // DLAP_EVAL_AFTER_BWD (see enqueue_pipe)
   int prog_mode_ = 1;                        // DLAP_PROG_MODE (see MlpJob::prog_mode)
   DevBuf<int> prog_;
   bool fused_eval() const {
@@ -1666,8 +1668,13 @@ class Engine {
       const bool defer = !side_metrics_ && defer_metrics_;
       const bool inter = train_first_ == 2 && n_eval_jobs_ > 0;
       if (inter) eval_prologue_hook_ = st2_;
-      enqueue_train_grads(phase, side_metrics_ ? st3_ : nullptr, true, 0, false, defer);   // this epoch's fwd/bwd
+      // eval_after_bwd_: the evaluation towers wait for the training tower backward, so the
+      // two largest launches of the epoch do not share the CUs; the evaluation then fills the
+      // GPU beside the few-CU serial tail (finalize, BPTT, weight gradient)
+      const int mark = inter && eval_after_bwd_ ? 1 : 0;
+      enqueue_train_grads(phase, side_metrics_ ? st3_ : nullptr, true, mark, false, defer);   // this epoch's fwd/bwd
       eval_prologue_hook_ = nullptr;
+      if (mark) HIP_OK(hipStreamWaitEvent(st2_, ev_a_, 0));
       if (inter) enqueue_eval_towers(st2_);               // previous epoch's evaluation
       else enqueue_eval(st2_);
       if (side_metrics_) HIP_OK(hipStreamWaitEvent(st2_, ev_m3_, 0));   // train metrics
