@@ -254,7 +254,13 @@ DLAP_DEV void issue_tile(const MlpJob& J, int tile, TileIn<P, KS1>& in) {
 // HBM): the lane groups whose 8 columns fall there take pp[t][col - ppc .. +7] -- from the LDS
 // copy (row stride ppst, zero-padded) with two 16-byte reads, else from global memory.
 // FRESH: the per-period inputs are being published by a concurrent LSTM (k_mlp_fwd_rnn, prog
-// mode 1): read them with agent-scope atomic loads, which bypass the non-coherent caches.
+// mode 1): read them with agent-scope atomic loads, which bypass the non-coherent caches (the
+// per-XCD L2 may hold the previous epoch's lines). Ordering: the publisher writes the outputs,
+// then release-stores the count (L2 written back first); the reader's load of a period is
+// issued only after its poll has returned a count covering it (the value decides the loop exit,
+// so the compiler waits for it), so the load reaches the coherence point after the outputs
+// did. Mode 0 instead fences with an agent-scope acquire after the wait, which invalidates the
+// caches per tile and measured 17 us slower (profiles/r3_fused_fwd_inkernel_timing.txt).
 template <class P, int KS1, bool INS = true, bool FRESH = false>
 DLAP_DEV RowInfo finish_tile(const MlpJob& J, const MlpDims& D, int tile, TileIn<P, KS1>& in,
                              typename P::Frag (&xf)[2][KS1], const float* spp = nullptr) {
