@@ -156,6 +156,9 @@ def run_bucket(entries, idx: List[int], batches: Dict[str, Dict], device: torch.
                                   seeds=[seed + 17 * k for k in range(len(idx))], lrs=lrs)
         if len(idx) == 1:
             ms = [ms]
+        tm = dict(train_3phase_gpu.last_timers.total)
+        tm["graph-capture"] = train_3phase_gpu.last_capture_s
+        run_bucket.last_timing = tm
         finals = [m.engine_final_eval for m in ms]
         for k, fe in enumerate(finals):
             out[k, 1:6] = [fe[1]["sharpe"], fe[2]["sharpe"], fe[0]["sharpe"], fe[1]["loss"], fe[2]["loss"]]
@@ -218,6 +221,7 @@ def run_sweep(batches: Dict[str, Dict], entries, dist: Optional[comm.Dist] = Non
     inits = {b: (_init_models(entries[bks[b][0]][0], [seed] * len(bks[b])) if d.device.type == "cuda" else None)
              for b in mine}
     done = [0]
+    timing: Dict[str, float] = {}
 
     def one(b):
         try:
@@ -228,6 +232,9 @@ def run_sweep(batches: Dict[str, Dict], entries, dist: Optional[comm.Dist] = Non
                 raise RuntimeError("injected failure")
             res = run_bucket(entries, bks[b], batches, d.device, epochs, ignore_epoch, seed, selection_sign,
                              models=inits[b])
+            tm = getattr(run_bucket, "last_timing", None) or {}
+            for k, v in tm.items():            # this rank's time per stage, summed over its buckets
+                timing[k] = timing.get(k, 0.0) + v
             done[0] += 1
             if verbose:
                 print(f"[sweep rank {d.rank}] bucket {done[0]}/{len(mine)} ({len(bks[b])} configs) "
@@ -273,7 +280,8 @@ def run_sweep(batches: Dict[str, Dict], entries, dist: Optional[comm.Dist] = Non
             "best_point": entries[best][2] if best >= 0 else None,
             "best_valid_sharpe": float(table[best, 1]) if best >= 0 else None,
             "best_test_sharpe": float(table[best, 2]) if best >= 0 else None,
-            "table": table, "metrics": METRICS, "errors_local": errors}
+            "table": table, "metrics": METRICS, "errors_local": errors,
+            "stage_s_local": {k: round(v, 3) for k, v in timing.items()}}
 
 
 def main(argv=None):
