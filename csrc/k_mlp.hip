@@ -747,10 +747,16 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd_rnn(const MlpJob*
     const bool tsm = blockIdx.y == 0 && jobs[0].gbits;
     if (threadIdx.x == 0) s_prog = 0;
     if (tsm && threadIdx.x == 0) g_mlp_ts[8] = wall_clock64();
+    {   // layer-0 input projections (k_proj) into the LDS staging area with all four waves
+      float* sx = reinterpret_cast<float*>(smem);
+      const auto xg = gp(R.xg);
+      const int n = md->nrnn > 0 ? R.T * 4 * md->H : 0;
+      for (int i = threadIdx.x; i < n; i += blockDim.x) sx[i] = xg[i];
+    }
     __syncthreads();
     const int w = threadIdx.x >> 6;
     if (w == 0) {
-      lstm_gls_body<HM, DPPG, true, true>(R, md, reinterpret_cast<float*>(smem), &s_prog, tsm ? g_mlp_ts : nullptr, 8);
+      lstm_gls_body<HM, DPPG, false, true>(R, md, reinterpret_cast<float*>(smem), &s_prog, tsm ? g_mlp_ts : nullptr, 8);
     } else if (w == 1) {
       lstm_publish(R, md, reinterpret_cast<const float*>(smem), &s_prog);
       if (tsm && threadIdx.x == 64) g_mlp_ts[12] = wall_clock64();
