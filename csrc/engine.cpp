@@ -1674,6 +1674,24 @@ class Engine {
       const int mark = inter && eval_after_bwd_ ? 1 : 0;
       enqueue_train_grads(phase, side_metrics_ ? st3_ : nullptr, true, mark, false, defer);   // this epoch's fwd/bwd
       eval_prologue_hook_ = nullptr;
+      if (mark && !side_metrics_) {
+        // the work of the evaluation branch that does not need the towers runs beside the
+        // training backward: this epoch's train metrics (after its loss pass) and the next
+        // epoch's dropout masks; then the towers, their losses and the bookkeeping
+        if (defer && phase != 2) {
+          HIP_OK(hipStreamWaitEvent(st2_, ev_mid_, 0));
+          launch_job_metrics(loss_tab(phase, use_gram(phase)), G_, st2_);
+        }
+        enqueue_dropmask(phase, 1, st2_);
+        HIP_OK(hipStreamWaitEvent(st2_, ev_a_, 0));
+        enqueue_eval_towers(st2_);
+        enqueue_epoch_end(phase, ignore_epoch, sel, st2_);
+        HIP_OK(hipEventRecord(ev_join_, st2_));
+        HIP_OK(hipStreamWaitEvent(st_, ev_join_, 0));
+        HTRACE("launch_update");
+        launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);
+        return;
+      }
       if (mark) HIP_OK(hipStreamWaitEvent(st2_, ev_a_, 0));
       if (inter) enqueue_eval_towers(st2_);               // previous epoch's evaluation
       else enqueue_eval(st2_);
