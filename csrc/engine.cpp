@@ -164,6 +164,14 @@ struct ModelState {
 
 }  // namespace
 
+// Per-model workgroups of a tower launch over G batched models (grid.y = model): the single-
+// model grid tuned at 600x3000 (`one`) divided by G, at least `lo`. The whole launch then keeps
+// roughly the single-model workgroup count instead of G times it: fewer weight stagings per
+// row and, in the backward, G-fold fewer gradient slabs for k_finalize to reduce. Measured
+// (profiles/r3_knobs_grids_batched.log): 9 models 1.045 -> 0.823 ms per epoch, 2 models
+// 0.337 -> 0.271 ms.
+static int grid_per_model(int one, int lo, int G) { return std::max(lo, one / std::max(1, G)); }
+
 static int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
   return v && *v ? std::atoi(v) : dflt;
@@ -220,8 +228,10 @@ class Engine {
     HIP_OK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
     // evaluation tower grid cap: the evaluation branch is within a few us of the training chain,
-    // so it gets as many workgroups as the training forward (profiles/r2_knobs_grids.log)
-    eval_gx_ = env_int("DLAP_EVAL_GX", 512);
+    // so it gets as many workgroups as the training forward (profiles/r2_knobs_grids.log). Per
+    // job: with G batched models the launch has 2G evaluation jobs, so the per-job grid shrinks
+    // with G (see grid_per_model)
+    eval_gx_ = env_int("DLAP_EVAL_GX", grid_per_model(512, 96, G));
     b_wait_ = env_int("DLAP_B_WAIT", 0);
     // both off: a third graph branch changes how the runtime maps the graph onto its hardware
     // queues -- the evaluation branch then shared a queue with the training backward and ran
@@ -1127,16 +1137,17 @@ class Engine {
     }
     if (s == 0) {
       const int ntiles = (R + 31) / 32;
-      gx_bwd_ = std::max(1, std::min((ntiles + 3) / 4, env_int("DLAP_GX_BWD", 256)));
+      gx_bwd_ = std::max(1, std::min((ntiles + 3) / 4, env_int("DLAP_GX_BWD", grid_per_model(256, 64, G_))));
       const int nsl = std::max(md_.nslice_s, md_.nslice_m);
       slab_.alloc((size_t)G_ * nsl * gx_bwd_ * slab_stride());
     }
     // tower-forward grids (measured, 600x3000x46 epoch graph): the phase-1/3 training forward
     // runs SDF-only (moments cached) beside the evaluation branch and is fastest with one
     // workgroup per CU (256); phase 2 (moment tower, no evaluation branch) with 1024
-    gx_fwd_[s] = std::max(1, std::min(((R + 31) / 32 + 3) / 4, env_int("DLAP_GX_FWD", 1024)));
+    gx_fwd_[s] = std::max(1, std::min(((R + 31) / 32 + 3) / 4,
+                                      env_int("DLAP_GX_FWD", G_ <= 2 ? 1024 : grid_per_model(1024, 128, G_))));
     if (s == 0) {
-      gx_fwd13_ = std::max(1, std::min(((R + 31) / 32 + 3) / 4, env_int("DLAP_GX_FWD13", 384)));
+      gx_fwd13_ = std::max(1, std::min(((R + 31) / 32 + 3) / 4, env_int("DLAP_GX_FWD13", grid_per_model(384, 96, G_))));
     }
     if (md_.md.wide) {
       const size_t ntl = (size_t)(R + 31) / 32;
