@@ -23,6 +23,7 @@
 //   Unconditional-only jobs (h == nullptr) run the inner axis over stocks directly.
 //   Block partials go to part[job][block-slice][2][T][T] (upper-triangle tiles only).
 // k_gram_reduce: fixed-order sum over the slices, mirrored to the full symmetric matrices.
+#include <cstdlib>
 #include "common.h"
 #include "loss.h"
 
@@ -192,10 +193,13 @@ __global__ __launch_bounds__(256) void k_gram_reduce(const GramJob* __restrict__
   gp(J.G)[T2 + e] = su;
 }
 
-// workgroups per tile (each GB_WAVES slices of the inner axis): ~1024 workgroups per launch
+// workgroups per tile (each GB_WAVES slices of the inner axis): ~256 workgroups per launch
+// (DLAP_GRAM_WG; fewer slices leave CUs to the head epoch that the evaluation-split builds
+// overlap and shrink the reduce pass: profiles/r3_knobs_gram_grid.log)
 int gram_slices(int T, int njobs) {
+  static const int target = [] { const char* v = std::getenv("DLAP_GRAM_WG"); return v ? std::atoi(v) : 256; }();
   const int nt = (T + 31) / 32, npair = nt * (nt + 1) / 2;
-  const int want = 1024 / std::max(1, npair * njobs);
+  const int want = target / std::max(1, npair * njobs);
   return std::max(1, std::min(64, want));
 }
 
