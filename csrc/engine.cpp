@@ -228,10 +228,11 @@ class Engine {
     HIP_OK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
     // evaluation tower grid cap: the evaluation branch is within a few us of the training chain,
-    // so it gets as many workgroups as the training forward (profiles/r2_knobs_grids.log). Per
+    // (profiles/r2_knobs_grids.log); 384 measured best on the round-3 tree (profiles/
+    // r3_knobs_grids_single_model.log: 0.2314-0.2319 vs 0.238 ms per driver-argument epoch). Per
     // job: with G batched models the launch has 2G evaluation jobs, so the per-job grid shrinks
     // with G (see grid_per_model)
-    eval_gx_ = env_int("DLAP_EVAL_GX", grid_per_model(512, 96, G));
+    eval_gx_ = env_int("DLAP_EVAL_GX", grid_per_model(384, 96, G));
     b_wait_ = env_int("DLAP_B_WAIT", 0);
     // both off: a third graph branch changes how the runtime maps the graph onto its hardware
     // queues -- the evaluation branch then shared a queue with the training backward and ran
