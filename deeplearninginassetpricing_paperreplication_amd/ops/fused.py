@@ -42,6 +42,7 @@ from __future__ import annotations
 
 import dataclasses
 import os
+import weakref
 from collections import OrderedDict
 from typing import Dict, List, Optional
 
@@ -79,6 +80,36 @@ class _Slot:
         self.step = 0
         # the dropout stream: seeded from torch's generator (torch.manual_seed reproduces it)
         self.eng.eng.set_seed(0, int(torch.randint(0, 2 ** 31 - 1, (1,)).item()))
+
+
+class _ParamKey:
+    """Identity of the uploaded parameter set: the parameter objects themselves (weak
+    references) plus their storage addresses and autograd versions. Addresses alone are not
+    enough: once a model is freed the caching allocator hands its storage to the next one, whose
+    fresh parameters then carry the same addresses and version 0."""
+
+    def __init__(self, params: List[torch.Tensor]):
+        self.refs = [weakref.ref(p) for p in params]
+        self.sig = tuple((p.data_ptr(), p._version) for p in params)
+
+    def matches(self, params: List[torch.Tensor]) -> bool:
+        return (len(params) == len(self.refs) and all(r() is p for r, p in zip(self.refs, params))
+                and self.sig == tuple((p.data_ptr(), p._version) for p in params))
+
+
+def invalidate_param_cache() -> None:
+    """Make the next module-level GPU call re-upload the parameters and the panel.
+
+    The engine keeps the last uploaded parameter vector and skips the upload while the very same
+    parameter objects have the same storage and autograd versions; in-place edits through
+    ``p.data`` (``p.data.copy_(...)``, ``p.data.mul_(...)``) do not bump the version counter, so
+    call this after them (``load_state_dict`` and optimiser steps bump it and need nothing). The
+    panel is cached on (storage address, shape, version, dtype) of its tensors, so a training loop
+    that moves the same host panel to the device every epoch reuses the upload; call this too
+    after writing new values into a panel tensor in place."""
+    for s in _CACHE.values():
+        s.param_key = None
+        s.data_key = None
 
 
 def _slot(spec) -> _Slot:
@@ -146,13 +177,13 @@ def _prepare(model, spec: ModelSpec, params: List[torch.Tensor], flat_fn, macro,
         mflat = mask.detach().reshape(-1).bool()
         s.idx = mflat.nonzero().reshape(-1)              # (one sync per new panel)
         s.midx = (~mflat).nonzero().reshape(-1)          # masked entries (moments only)
-    pkey = tuple((p.data_ptr(), p._version) for p in params)
-    if pkey != s.param_key:
+    fresh = s.param_key is None or not s.param_key.matches(params)
+    if fresh:
         s._flat = flat_fn(dev).contiguous()            # kept alive until the next call
     s.ts = _bind(s, dev)               # the engine waits for torch's queued work (panel, params)
-    if pkey != s.param_key:
+    if fresh:
         s.eng.eng.set_params_dev(0, s._flat.data_ptr())
-        s.param_key = pkey
+        s.param_key = _ParamKey(params)
     if hidden is not None:
         h0, c0 = (x.detach().reshape(-1).to(dev, torch.float32).contiguous() for x in hidden)
         s._hidden = (h0, c0)                                       # kept alive until copied

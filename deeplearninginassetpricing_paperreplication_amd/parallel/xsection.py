@@ -142,15 +142,16 @@ class EngineTowers:
         return torch.cuda.current_stream(self.device).cuda_stream
 
     def sync_params(self, params: Sequence[torch.Tensor], training: bool):
-        from ..ops.fused import _flat_params
-        key = tuple((p.data_ptr(), p._version) for p in params)
-        if key != self.param_key:
-            self._flat = _flat_params(list(params), self.device).contiguous()
+        from ..ops.fused import _ParamKey, _flat_params
+        params = list(params)
+        fresh = self.param_key is None or not self.param_key.matches(params)
+        if fresh:
+            self._flat = _flat_params(params, self.device).contiguous()
         ts = self._ts()
         self.eng.eng.join_from(ts)
-        if key != self.param_key:
+        if fresh:
             self.eng.eng.set_params_dev(0, self._flat.data_ptr())
-            self.param_key = key
+            self.param_key = _ParamKey(params)
         if training:
             self.step += 1
             self.eng.eng.set_drop_step(0, self.step)

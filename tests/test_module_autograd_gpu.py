@@ -190,3 +190,24 @@ def test_simple_sdf_without_hidden_layers():
     # (the Linear's bias cancels out of the zero-mean weights: its gradient is rounding noise)
     gc, gg = cpu.net[-1].weight.grad, gpu.net[-1].weight.grad.cpu()
     assert float((gg - gc).norm() / gc.norm()) < TOL
+
+
+def test_param_cache_sees_data_edits_after_invalidation():
+    """ADVICE r2: the engine skips re-uploading unchanged parameters (storage + autograd version);
+    an in-place edit through ``p.data`` keeps the version, so ``invalidate_param_cache`` is the
+    documented way to make the next call see it. Either way the outputs match the CPU modules
+    after the same edit."""
+    from deeplearninginassetpricing_paperreplication_amd.ops import fused
+    b = _batch()
+    cpu, gpu = _pair()
+    bc = _cuda(b)
+    with torch.no_grad():
+        gpu(*_args(bc), phase="conditional")            # parameters uploaded and cached
+    for m in (cpu, gpu):
+        for p in m.sdf_net.parameters():
+            p.data.mul_(0.5)
+    fused.invalidate_param_cache()
+    with torch.no_grad():
+        out_g = gpu(*_args(bc), phase="conditional")
+        out_c = cpu(*_args(b), phase="conditional")
+    _close_out(out_g["weights"], out_c["weights"])
