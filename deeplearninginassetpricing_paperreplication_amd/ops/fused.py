@@ -333,6 +333,9 @@ def _dense_raw(s: _Slot, dev) -> torch.Tensor:
     """The engine's raw SDF weights of the train split as a dense [T, N] tensor (0 where masked)."""
     R = int(s.idx.numel())
     wc = _copy(s, "w", max(R, 1), dev)
+    # torch's stream reads wc below: it must wait for the engine's copy first (without this the
+    # scatter raced the copy and could read the allocator's previous contents of wc)
+    _release(s, s.ts)
     return torch.zeros(s.T * s.N, dtype=torch.float32, device=dev).index_copy(0, s.idx, wc[:R]).reshape(s.T, s.N)
 
 
