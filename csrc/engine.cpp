@@ -227,7 +227,7 @@ class Engine {
     HIP_OK(hipEventCreateWithFlags(&ev_f3_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
-    // evaluation tower grid cap: the evaluation branch is within a few us of the training chain,
+    // evaluation tower grid cap: the evaluation branch is within a few us of the training chain
     // (profiles/r2_knobs_grids.log); 384 measured best on the round-3 tree (profiles/
     // r3_knobs_grids_single_model.log: 0.2314-0.2319 vs 0.238 ms per driver-argument epoch). Per
     // job: with G batched models the launch has 2G evaluation jobs, so the per-job grid shrinks
