@@ -257,6 +257,9 @@ def main():
     phase_t = [evs[i].elapsed_time(evs[i + 1]) / 1e3 / k for i, k in enumerate((n1, n2, n3))]
     hist = eng.history_rows(0)
     finite = bool(np.isfinite(hist[:, 1]).all())
+    # spin waits of the fused LSTM + tower forward that gave up (0 = every published period was
+    # waited for; anything else means results of that launch are invalid)
+    fused_timeouts = int(eng.eng.prog_timeouts())
     K = n1 + n2 + n3
     if dist:
         dt = float(max(comm.all_gather_rows(d, np.array([[dt]]), world, [rank])[:, 0]))
@@ -285,7 +288,8 @@ def main():
                        "backend": d.backend, "schedule_mix": [n1, n2, n3]},
             "ms_per_epoch_phase": [round(x * 1e3, 4) for x in phase_t],
             "full_schedule_s_per_model_batch": round(full_s, 3),
-            "hipgraph": use_graph, "finite": finite, "panel_setup_s": round(t_gen, 2),
+            "hipgraph": use_graph, "finite": finite, "fused_wait_timeouts": fused_timeouts,
+            "panel_setup_s": round(t_gen, 2),
             "ensemble9": ens,
         }
         print(json.dumps(out), flush=True)

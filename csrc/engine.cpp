@@ -893,8 +893,12 @@ class Engine {
   }
  public:
   double capture_seconds() const { return capture_s_; }
+  // phases 1 / 3 only: phase 2's training forward runs on the 1024-workgroup grid, more than the
+  // GPU holds at once; that is still deadlock-free (the LSTM workgroup is dispatched first), but
+  // with two processes sharing one GPU (the gloo rehearsal) phase-2 epochs stalled until a spin
+  // wait gave up (profiles/r3_rehearsal_bench_n2_fused_phase2.log)
   bool fused_fwd(int phase) const {
-    (void)phase;
+    if (phase == 2) return false;
     return rnn_overlap_ && md_.nrnn > 0 && !md_.md.wide &&
            mlp_fwd_rnn_supported(md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, splits_[0].T);
   }

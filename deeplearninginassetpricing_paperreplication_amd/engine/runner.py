@@ -299,6 +299,9 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
             done = mk + 1
             for g in range(n_models):
                 monitor.check(g, eng.history_rows(g), raise_ok=n_models == 1)
+            if eng.eng.prog_timeouts():
+                raise RuntimeError("fused LSTM + tower forward: a spin wait gave up (the GPU is shared "
+                                   "with other processes?); rerun with DLAP_RNN_OVERLAP=0")
             write_resume(phase, done)
             if stop_after is not None and tuple(stop_after) == (phase, done):
                 raise _Stop()

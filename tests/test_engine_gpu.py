@@ -642,6 +642,7 @@ def test_fused_lstm_tower_forward_equals_two_launches(monkeypatch, rnn, G, dropo
         monkeypatch.setenv("DLAP_RNN_OVERLAP", overlap)
         eng, _ = _engine(cfg, n_models=G, seeds=(5, 6), data=data)
         assert eng.eng.fused_forward(1) == (overlap == "1")
+        assert not eng.eng.fused_forward(2)   # phase 2 keeps the two launches (engine.cpp fused_fwd)
         for ph, n in ((1, 4), (2, 2), (3, 5)):
             eng.eng.begin_phase(ph)
             eng.run(ph, n, 1e-3, 1, 1.0, True)
