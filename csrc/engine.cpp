@@ -37,6 +37,7 @@
 #include "loss.h"
 #include <chrono>
 #include "mlp.h"
+#include "panel.h"
 #include "rnn.h"
 #include "update.h"
 #include "wide.h"
@@ -160,6 +161,7 @@ struct ModelState {
   unsigned seed = 0;
   unsigned tower_salt = 0;  // XOR-ed (mixed) into the towers' dropout seed only (N-sharding: per rank)
   float lr = 0.f;         // per-model learning rate override (0: use the run's lr)
+  float dropout = 0.f;    // per-model dropout rate (sweep members batched in one engine may differ)
 };
 
 }  // namespace
@@ -250,6 +252,8 @@ class Engine {
     rnn_overlap_ = env_int("DLAP_RNN_OVERLAP", 1) != 0;
     rnn_overlap_eval_ = env_int("DLAP_RNN_OVERLAP_EVAL", 0) != 0;
     prog_mode_ = env_int("DLAP_PROG_MODE", 1);
+    prog_limit_ = (unsigned)env_int("DLAP_PROG_SPIN_LIMIT", 1 << 22);
+    fused_p2_ = env_int("DLAP_FUSED_PHASE2", 0) != 0;
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
                residual, fp32);
     // fp32 wide path: layer 0 through k_proj0 + the ZIN towers (the fused-layer-0 k_mlp_fwd_zx
@@ -261,6 +265,7 @@ class Engine {
     models_.resize(G);
     for (int g = 0; g < G; ++g) {
       ModelState& S = models_[g];
+      S.dropout = dropout;
       S.params.alloc(md_.P); S.grads.alloc(md_.P); S.m.alloc(md_.P); S.v.alloc(md_.P);
       S.snap_loss.alloc(md_.P); S.snap_sharpe.alloc(md_.P);
       // packed weights: evaluation copy, then the training copy (dropout scale folded in)
@@ -272,18 +277,21 @@ class Engine {
       S.wproj.alloc((size_t)(md_.proj_mp + 1) * md_.proj_np);
     }
     ws_.resize((size_t)G * 3);
-    {   // per-model re-pack jobs (buffers allocated above, never reallocated)
-      std::vector<UpdJob> pj(G);
-      for (int g = 0; g < G; ++g) {
-        ModelState& S = models_[g];
-        pj[g].params = S.params.p;
-        pj[g].blob = reinterpret_cast<bf16x8*>(S.blob.p);
-        pj[g].blob0 = reinterpret_cast<bf16x8*>(S.blob0.p);
-        pj[g].aux = S.aux.p;
-        pj[g].wproj = S.wproj.p;
-      }
-      upload(j_pack_, pj);
+    upload_pack_jobs();
+  }
+  // per-model re-pack jobs (buffers allocated in the constructor, never reallocated)
+  void upload_pack_jobs() {
+    std::vector<UpdJob> pj(G_);
+    for (int g = 0; g < G_; ++g) {
+      ModelState& S = models_[g];
+      pj[g].params = S.params.p;
+      pj[g].blob = reinterpret_cast<bf16x8*>(S.blob.p);
+      pj[g].blob0 = reinterpret_cast<bf16x8*>(S.blob0.p);
+      pj[g].aux = S.aux.p;
+      pj[g].wproj = S.wproj.p;
+      pj[g].dropout = S.dropout;
     }
+    upload(j_pack_, pj);
   }
   ~Engine() {
     g_live_engines.fetch_sub(1);
@@ -362,42 +370,118 @@ class Engine {
       for (int r = 0; r < R; ++r) rc[r] = Rm.data()[(size_t)ti[2 * r] * N + ti[2 * r + 1]];
       up(D.Rc, rc.data(), R);
     }
-    up(D.row_ptr, row_ptr.data(), T + 1);
     up(D.Rm, Rm.data(), (size_t)T * N);
     up(D.mask, mask.data(), (size_t)T * N);
     if (md_.M > 0) up(D.macro, macro.data(), (size_t)T * md_.M);
-    // per-period / per-asset constants (host, double accumulation)
-    std::vector<float> nt(T), inv_nt(T), meanr(T), rr(T), invt(N);
-    std::vector<double> ti(N, 0.0);
-    const float* r = Rm.data();
-    const float* mk = mask.data();
-    double nbar = 0;
-    for (int t = 0; t < T; ++t) {
-      double n = 0, sr = 0, s2 = 0;
-      for (int i = 0; i < N; ++i) {
-        const float m = mk[(size_t)t * N + i];
-        n += m; sr += (double)r[(size_t)t * N + i] * m; s2 += (double)r[(size_t)t * N + i] * r[(size_t)t * N + i] * m;
-        ti[i] += m;
-      }
-      nt[t] = (float)n;
-      const double nc = n < 1 ? 1 : n;
-      inv_nt[t] = (float)(1.0 / nc);
-      meanr[t] = (float)(sr / nc);
-      rr[t] = (float)s2;
-      nbar += nc;
+    // per-period / per-asset constants: the same device kernels as the device-compaction path
+    // (set_split_dense), from the uploaded dense Rm / mask, so both paths agree bitwise
+    alloc_stats(D, T, N);
+    PanelIn in{};
+    in.ret = D.Rm.p; in.maskf = D.mask.p; in.T = T; in.N = N;
+    PanelOut out = panel_out(D);
+    out.dense_out = 0;
+    launch_panel_stats(in, out, st_);
+    int R_dev = 0;
+    finish_stats(D, &R_dev);
+    if (R_dev != R) throw std::invalid_argument("mask and compact rows disagree");
+    std::vector<int> rp(T + 1);
+    HIP_LEGACY(hipMemcpy(rp.data(), D.row_ptr.p, (T + 1) * sizeof(int), hipMemcpyDeviceToHost));
+    if (std::memcmp(rp.data(), row_ptr.data(), (T + 1) * sizeof(int)) != 0)
+      throw std::invalid_argument("row_ptr does not match the mask");
+    finish_split(s);
+  }
+
+  // ---- device split preparation (k_panel.hip) ------------------------------------------------
+  void alloc_stats(SplitDev& D, int T, int N) {
+    D.Nt.alloc(T, false); D.invNt.alloc(T, false); D.meanR.alloc(T, false); D.RR.alloc(T, false);
+    D.invT.alloc(std::max(N, 1), false); D.row_ptr.alloc(T + 1, false);
+    cnt_scratch_.alloc(std::max(T, 1), false);
+    nbar_scratch_.alloc(1, false);
+  }
+  PanelOut panel_out(SplitDev& D) {
+    PanelOut o{};
+    o.Rm = D.Rm.p; o.mask = D.mask.p; o.Nt = D.Nt.p; o.invNt = D.invNt.p; o.meanR = D.meanR.p; o.RR = D.RR.p;
+    o.invT = D.invT.p; o.cnt = cnt_scratch_.p; o.row_ptr = D.row_ptr.p; o.nbar = nbar_scratch_.p;
+    o.KP = md_.KP; o.fp32 = md_.md.fp32; o.dense_out = 1;
+    return o;
+  }
+  // N-bar and the row count to the host (the one synchronisation of a split upload)
+  void finish_stats(SplitDev& D, int* R) {
+    struct { int r; float nb; } h{};
+    HIP_OK(hipMemcpyAsync(&h.r, D.row_ptr.p + D.T, sizeof(int), hipMemcpyDeviceToHost, st_));
+    HIP_OK(hipMemcpyAsync(&h.nb, nbar_scratch_.p, sizeof(float), hipMemcpyDeviceToHost, st_));
+    sync();
+    *R = h.r;
+    D.Nbar = h.nb;
+  }
+  // Dense split already in device memory (torch CUDA tensors: feats [T][N][F] fp32, ret [T][N]
+  // fp32, mask [T][N] bool (mask_bool) or fp32 0/1, macro [T][M] fp32 or 0): the compacted
+  // layout is built on the GPU -- no host copy of the panel, one synchronisation (the row
+  // count). `ext` is the caller's stream the inputs were produced on (joined first); the call
+  // returns after the inputs are no longer read.
+  void set_split_dense(int s, uintptr_t feats, uintptr_t ret, uintptr_t mask, bool mask_bool, uintptr_t macro,
+                       int T, int N, int F, uintptr_t ext) {
+    if (s < 0 || s > 2) throw std::invalid_argument("split must be 0, 1 or 2");
+    if (T > DLAP_MAX_T) throw std::invalid_argument("T exceeds DLAP_MAX_T");
+    if (F != md_.F) throw std::invalid_argument("feature dim does not match the engine");
+    if ((long)T * N > (long)INT32_MAX) throw std::invalid_argument("panel too large");
+    if (md_.M > 0 && !macro) throw std::invalid_argument("macro series required");
+    install_crash_handler();
+    join_from(ext);
+    SplitDev& D = splits_[s];
+    D.T = T; D.N = N;
+    D.Rm.alloc((size_t)T * N, false);
+    D.mask.alloc((size_t)T * N, false);
+    alloc_stats(D, T, N);
+    PanelIn in{};
+    in.feats = reinterpret_cast<const float*>(feats);
+    in.ret = reinterpret_cast<const float*>(ret);
+    if (mask_bool) in.maskb = reinterpret_cast<const uint8_t*>(mask);
+    else in.maskf = reinterpret_cast<const float*>(mask);
+    in.T = T; in.N = N; in.F = F;
+    PanelOut out = panel_out(D);
+    launch_panel_stats(in, out, st_);
+    int R = 0;
+    finish_stats(D, &R);
+    D.R = R;
+    D.rowti.alloc((size_t)2 * std::max(R, 1), false);
+    D.Rc.alloc(std::max(R, 1), false);
+    D.X.alloc(std::max<size_t>((size_t)R * md_.KP * xw(), 1), false);
+    out.rowti = reinterpret_cast<int2*>(D.rowti.p); out.Rc = D.Rc.p; out.X = D.X.p;
+    launch_panel_compact(in, out, R, st_);
+    if (md_.M > 0) {
+      D.macro.alloc((size_t)T * md_.M, false);
+      HIP_OK(hipMemcpyAsync(D.macro.p, reinterpret_cast<const void*>(macro), (size_t)T * md_.M * sizeof(float),
+                            hipMemcpyDeviceToDevice, st_));
     }
-    for (int i = 0; i < N; ++i) invt[i] = (float)(1.0 / (ti[i] < 1 ? 1 : ti[i]));
-    // N̄ = mean_t max(N_t, 1) in fp32 like torch's .mean()
-    float nb = 0.f;
-    {
-      double acc = 0;
-      for (int t = 0; t < T; ++t) acc += (nt[t] < 1.f ? 1.f : nt[t]);
-      nb = (float)(acc / T);
-    }
-    (void)nbar;
-    D.Nbar = nb;
-    up(D.Nt, nt.data(), T); up(D.invNt, inv_nt.data(), T); up(D.meanR, meanr.data(), T);
-    up(D.RR, rr.data(), T); up(D.invT, invt.data(), N);
+    sync();                                   // the caller may free the inputs on return
+    finish_split(s);
+  }
+  // host copies of a split's compacted layout (tests: the device compaction vs prepare_split)
+  py::dict read_split(int s) {
+    SplitDev& D = splits_[s];
+    sync();
+    py::dict d;
+    d["T"] = D.T; d["N"] = D.N; d["R"] = D.R; d["Nbar"] = D.Nbar;
+    auto dl = [&](auto& buf, size_t n) {
+      using E = typename std::remove_reference<decltype(*buf.p)>::type;
+      py::array_t<E> a(n);
+      if (n) HIP_LEGACY(hipMemcpy(a.mutable_data(), buf.p, n * sizeof(E), hipMemcpyDeviceToHost));
+      return a;
+    };
+    d["X"] = dl(D.X, (size_t)D.R * md_.KP * xw());
+    d["rowti"] = dl(D.rowti, (size_t)2 * D.R);
+    d["row_ptr"] = dl(D.row_ptr, (size_t)D.T + 1);
+    d["Rm"] = dl(D.Rm, (size_t)D.T * D.N); d["mask"] = dl(D.mask, (size_t)D.T * D.N);
+    d["Rc"] = dl(D.Rc, (size_t)D.R);
+    d["Nt"] = dl(D.Nt, (size_t)D.T); d["invNt"] = dl(D.invNt, (size_t)D.T);
+    d["meanR"] = dl(D.meanR, (size_t)D.T); d["RR"] = dl(D.RR, (size_t)D.T); d["invT"] = dl(D.invT, (size_t)D.N);
+    d["macro"] = dl(D.macro, (size_t)D.T * md_.M);
+    return d;
+  }
+  void finish_split(int s) {
+    SplitDev& D = splits_[s];
+    const int R = D.R;
     D.set = true;
     h_valid_ = false;
     alloc_ws(s);
@@ -443,6 +527,23 @@ class Engine {
     return S.tower_salt ? S.seed ^ (S.tower_salt * 0x9E3779B9u + 0x7F4A7C15u) : S.seed;
   }
   void set_lr(int g, float lr) { models_[check_g(g)].lr = lr; graphs_dirty_ = true; }
+  // Per-model dropout rate (BASELINE config 4's dropout axis batched inside one engine): the
+  // model's keep threshold, its train-blob scale 1/(1-p) and its gradient scale-back all follow
+  // it; a batched member with rate p trains bit-identically to a solo engine built with p.
+  void set_dropout(int g, float p) {
+    check_g(g);
+    if (!(p >= 0.f && p < 1.f)) throw std::invalid_argument("dropout must be in [0, 1)");
+    models_[g].dropout = p;
+    float mx = 0.f;
+    for (const ModelState& S : models_) mx = std::max(mx, S.dropout);
+    md_.dropout = md_.md.dropout = mx;          // structural switches: any model with dropout
+    HIP_LEGACY(hipMemcpy(d_desc_.p, &md_, sizeof(ModelDesc), hipMemcpyHostToDevice));
+    upload_pack_jobs();
+    pack(g);                                     // its train blob carries the new scale
+    h_valid_ = false;
+    graphs_dirty_ = true;
+  }
+  float get_dropout(int g) const { return models_[check_g(g)].dropout; }
   py::dict get_opt_state(int g) {
     ModelState& S = models_[check_g(g)];
     py::dict d;
@@ -553,6 +654,7 @@ class Engine {
     // the moment net trains in phase 2: the cached moments go stale. Else refresh them (and the
     // Gram matrices); with the pipelined graphs the evaluation splits' Gram builds overlap the
     // head epoch (which trains only) on the evaluation stream
+    cur_phase_ = phase;
     if (phase == 2) h_valid_ = false;
     else ensure_moments(true, pipe && use_graph);
     struct GramScope {                    // epoch graphs run the loss in Gram mode
@@ -594,6 +696,8 @@ class Engine {
     HTRACE("run_epochs done");
   }
   void set_pipeline(bool on) { pipeline_ = on; }
+  // job tables (and the fused launches' co-residency capacities) current
+  void ensure_jobs() { if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; } }
 
   // Pieces used by the module-level API / tests (no bookkeeping).
   void forward_split(int s, bool train_mode, bool do_mom, bool wait = true) {
@@ -658,7 +762,7 @@ class Engine {
       launch_mlp_fwd_zx(as<MlpJob>(j_mlp_train_[phase]), G_, std::max(1, zx_gx_ / G_), md_.md, md_.WMB, st_, true);
     else if (fused)
       launch_mlp_fwd_rnn(as<MlpJob>(j_mlp_train_[phase]), as<RnnJob>(j_rnn_train_), dd(), G_,
-                         phase == 2 ? gx_fwd_[0] : gx_fwd13_, md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, D.T, st_);
+                         fused_train_gx(phase), md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, D.T, st_);
     else
       launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, phase == 2 ? gx_fwd_[0] : gx_fwd13_, md_.md, md_.KS1,
                      md_.WMB, st_);
@@ -680,10 +784,10 @@ class Engine {
     }
     if (phase == 2)
       launch_mlp_bwd_mom(as<MlpJob>(dh ? j_mlp_bwd_dh_ : j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_m, 1, md_.md,
-                         md_.KS1, md_.WMB, slab_stride(), st_);
+                         md_.KS1, md_.WMB, slab_stride(), fpw_, st_);
     else
       launch_mlp_bwd_sdf(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_s, md_.tps_s, md_.md, md_.KS1,
-                         slab_stride(), st_);
+                         slab_stride(), fpw_, st_);
     if (md_.md.wide)
       launch_wgrad0(as<WideJob>(j_wide_bwd_[phase]), G_, dd(), md_.md, phase == 2, md_.WMB, nsplit_, st_);
     enqueue_train_tail(phase);
@@ -801,9 +905,47 @@ class Engine {
   // (re)build the Gram matrices from the current moments now (tests; run_epochs does it itself)
   void refresh_gram() {
     if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; }
+    cur_phase_ = 0;                          // every split's matrices
     ensure_moments(true);
   }
   bool gram_enabled(int phase) const { return phase == 0 ? gram_eval() : gram_train(phase); }
+  // Cost model of the loss mode of one phase: the Gram form saves the dense
+  // asset passes every epoch but costs a T x T build per split after each moment refresh; over
+  // `epochs` epochs of `phase` use it where epochs x saving > build. A function of the schedule
+  // and the shapes only (never of runtime state), so a run split into print segments or resumed
+  // mid-phase makes the same choice. Coefficients (us, one model, measured at 600x3000x46 on
+  // MI355X, profiles/r3_final_kernel_stats_short.txt, r2_final_kernel_stats.txt): dense asset pass
+  // per T N (K+1) element 1.8e-6 (train, one pass) / 6.6e-6 (evaluation, split pass), Gram build
+  // per T^2 x inner element 7.7e-8, Gram per-epoch extra per T^2 5e-5. DLAP_GRAM_PLAN=0: Gram
+  // wherever it applies (the round-3 behaviour).
+  void plan_phase(int phase, int epochs) {
+    if (phase < 1 || phase > 3) return;
+    plan_tr_[phase] = plan_ev_[phase] = true;
+    if (phase == 2 || epochs <= 0 || env_int("DLAP_GRAM_PLAN", 1) == 0) return;
+    const double cb = 7.7e-8, cq = 5e-5, cdt = 1.8e-6, cde = 6.6e-6;
+    const double K = md_.K;
+    const SplitDev& D0 = splits_[0];
+    if (D0.set && D0.T > 0) {
+      const bool cond = phase == 3;
+      const double T = D0.T, N = D0.N;
+      const double build = cb * T * T * N * (cond ? K : 1.0);
+      const double save = cdt * T * N * (cond ? K + 1.0 : 1.0) - cq * T * T;
+      plan_tr_[phase] = epochs * save > build;
+    }
+    double build = 0.0, save = 0.0;
+    for (int sp = 1; sp < 3; ++sp) {
+      const SplitDev& D = splits_[sp];
+      if (!D.set || D.T == 0) continue;
+      const double T = D.T, N = D.N;
+      build += cb * T * T * N * K;
+      save += cde * T * N * (K + 1.0) - cq * T * T;
+    }
+    plan_ev_[phase] = epochs * save > build;
+  }
+  py::tuple gram_plan(int phase) const {
+    const int p = (phase >= 1 && phase <= 3) ? phase : 1;
+    return py::make_tuple(plan_tr_[p], plan_ev_[p]);
+  }
   py::array_t<uint16_t> read_blob(int g) {
     sync();  // (already synchronous)
     ModelState& S = models_[check_g(g)];
@@ -867,9 +1009,13 @@ class Engine {
   DevBuf<double> gram_scratch_;              // split-K partials of the Gram build
   DevBuf<char> j_gram_[3];                   // Gram build jobs per split (every model)
   DevBuf<char> j_loss_gram_[4];              // phase training loss jobs in Gram mode (epoch graphs)
-  bool gram_valid_ = false;                  // G matches the cached moments (build_gram ran)
+  bool gram_valid_[3] = {false, false, false};   // G of split s matches the cached moments
   bool gram_run_ = false;                    // inside run_epochs (epoch graphs use Gram mode)
-  bool use_gram(int phase) const { return gram_run_ && gram_train(phase); }
+  // Dense or Gram losses per phase (plan_phase): a Gram build pays off only over enough epochs
+  int cur_phase_ = 0;                        // phase of the run being enqueued
+  bool plan_tr_[4] = {true, true, true, true}, plan_ev_[4] = {true, true, true, true};
+  bool use_gram(int phase) const { return gram_run_ && gram_train(phase) && plan_tr_[phase]; }
+  bool eval_gram_now() const { return gram_run_ && gram_eval() && plan_ev_[cur_phase_]; }
   const LossJob* loss_tab(int phase, bool gram) const {
     return gram ? as<LossJob>(j_loss_gram_[phase]) : as<LossJob>(j_loss_train_[phase]);
   }
@@ -886,10 +1032,30 @@ class Engine {
   bool eval_solo_ = false;
   bool eval_after_bwd_ = false;              // DLAP_EVAL_AFTER_BWD (see enqueue_pipe)
   int prog_mode_ = 1;                        // DLAP_PROG_MODE (see MlpJob::prog_mode)
+  unsigned prog_limit_ = 1u << 22;           // DLAP_PROG_SPIN_LIMIT (see MlpJob::prog_limit)
+  bool fused_p2_ = false;                    // DLAP_FUSED_PHASE2: fused training forward in phase 2 too
   DevBuf<int> prog_;
+  // Co-residency guarantee of the fused LSTM + tower launches: resident workgroups of the fused
+  // kernel on the device (occupancy query, rebuild_jobs) for the train split / the evaluation
+  // splits; DLAP_FUSED_CAP overrides (tests of the fallback).
+  int cap_train_ = 0, cap_eval_ = 0;
+  // grid of a fused launch of njobs jobs wanting `want` tower workgroups each: capped so that
+  // (1 + gx) * njobs workgroups are all resident at once; 0 = does not fit (two launches then)
+  static int fused_grid(int want, int njobs, int cap) {
+    if (cap <= 0 || njobs <= 0) return 0;
+    const int gx = std::min(want, cap / njobs - 1);
+    return gx >= 16 ? gx : 0;
+  }
+  int eval_grid() const {
+    int gx = std::max(gx_fwd_[1], gx_fwd_[2]);
+    if (eval_gx_ > 0) gx = std::min(gx, eval_gx_);
+    return gx;
+  }
+  int train_fwd_grid(int phase) const { return phase == 2 ? gx_fwd_[0] : gx_fwd13_; }
   bool fused_eval() const {
     return rnn_overlap_ && (rnn_overlap_eval_ || eval_solo_) && md_.nrnn > 0 && !md_.md.wide && n_eval_jobs_ > 0 &&
-           mlp_fwd_rnn_supported(md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, tmax_eval_);
+           mlp_fwd_rnn_supported(md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, tmax_eval_) &&
+           fused_grid(eval_grid(), n_eval_jobs_, cap_eval_) > 0;
   }
  public:
   double capture_seconds() const { return capture_s_; }
@@ -898,9 +1064,28 @@ class Engine {
   // with two processes sharing one GPU (the gloo rehearsal) phase-2 epochs stalled until a spin
   // wait gave up (profiles/r3_rehearsal_bench_n2_fused_phase2.log)
   bool fused_fwd(int phase) const {
-    if (phase == 2) return false;
+    if (phase == 2 && !fused_p2_) return false;
     return rnn_overlap_ && md_.nrnn > 0 && !md_.md.wide &&
-           mlp_fwd_rnn_supported(md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, splits_[0].T);
+           mlp_fwd_rnn_supported(md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, splits_[0].T) &&
+           fused_grid(train_fwd_grid(phase), G_, cap_train_) > 0;
+  }
+  // the capped grids of the fused launches (valid when fused_fwd / fused_eval)
+  int fused_train_gx(int phase) const { return fused_grid(train_fwd_grid(phase), G_, cap_train_); }
+  int fused_eval_gx() const { return fused_grid(eval_grid(), n_eval_jobs_, cap_eval_); }
+  // zero the spin-timeout counters (tests: the device poison is permanent otherwise)
+  void reset_prog_errors() {
+    sync();
+    std::vector<int> h((size_t)G_ * 3 * 16);
+    HIP_LEGACY(hipMemcpy(h.data(), prog_.p, h.size() * sizeof(int), hipMemcpyDeviceToHost));
+    for (int k = 0; k < 3 * G_; ++k) h[16 * k + 1] = 0;
+    HIP_LEGACY(hipMemcpy(prog_.p, h.data(), h.size() * sizeof(int), hipMemcpyHostToDevice));
+  }
+  py::dict fused_info() const {
+    py::dict d;
+    d["cap_train"] = cap_train_; d["cap_eval"] = cap_eval_;
+    for (int ph = 1; ph <= 3; ++ph) d[("train_gx_p" + std::to_string(ph)).c_str()] = fused_fwd(ph) ? fused_train_gx(ph) : 0;
+    d["eval_gx_solo"] = fused_grid(eval_grid(), n_eval_jobs_, cap_eval_);
+    return d;
   }
   // spin waits of the fused forward that gave up (0 unless the dispatch-order argument failed)
   int prog_timeouts() {
@@ -919,6 +1104,11 @@ class Engine {
   std::vector<ModelState> models_;
   std::vector<ModelSplitWS> ws_;
   DevBuf<float> slab_;
+  DevBuf<int> cnt_scratch_;                  // split preparation: per-period counts
+  DevBuf<float> nbar_scratch_;               // ... and N-bar
+  int nfine_ = 4;                            // fine backward slabs per model and slice (from R)
+  int fpw_ = 1;                              // fine slabs per backward workgroup (1 or 4)
+  int slabs_stored() const { return nfine_ / fpw_; }
   int gx_bwd_ = 1, gx_fwd_[3] = {1, 1, 1};
   int gx_fwd13_ = 1;                         // training forward grid of phases 1 / 3
   int nsplit_ = 1, gx_proj_[3] = {1, 1, 1};  // wide path: wgrad row splits, proj grid per split
@@ -930,13 +1120,15 @@ class Engine {
   DevBuf<char> j_wide_train_[4], j_wide_eval_, j_wide_bwd_[4];   // wide path (k_wide.hip)
   DevBuf<char> j_rnn_mom_, j_mlp_mom_, j_wide_mom_;             // moment refresh (every split)
   DevBuf<char> j_mlp_bwd_dh_;                                   // moment backward from an external dL/dh
+  DevBuf<char> j_loss_eval_dense_;                              // evaluation loss jobs, dense passes
   int n_mom_jobs_ = 0, tmax_all_ = 0, gx_mom_ = 1;
   int n_eval_jobs_ = 0;
   int tmax_eval_ = 0, nmax_eval_ = 0;
 
-  static std::string graph_key(int phase, float lr, int ig, float sel, int kind) {
+  std::string graph_key(int phase, float lr, int ig, float sel, int kind) const {
     char b[160];
-    snprintf(b, sizeof b, "%d/%.9g/%d/%.3g/%d", phase, lr, ig, sel, kind);
+    const int p = (phase >= 1 && phase <= 3) ? phase : 0;
+    snprintf(b, sizeof b, "%d/%.9g/%d/%.3g/%d/%d%d", phase, lr, ig, sel, kind, (int)plan_tr_[p], (int)plan_ev_[p]);
     return b;
   }
   bool pipeline_ = true;
@@ -1141,10 +1333,15 @@ class Engine {
       }
     }
     if (s == 0) {
+      // backward row partition: nfine_ fine slabs per model (one per workgroup of the tuned
+      // single-model grid, 256 at 600x3000), a function of R only -- the gradient summation
+      // order is the same whether a model trains alone or batched with others (VERDICT r3
+      // item 1). The launch shape (fine slabs per workgroup) is chosen in rebuild_jobs.
       const int ntiles = (R + 31) / 32;
-      gx_bwd_ = std::max(1, std::min((ntiles + 3) / 4, env_int("DLAP_GX_BWD", grid_per_model(256, 64, G_))));
+      const int ncoarse = std::max(1, std::min(env_int("DLAP_NSLAB_COARSE", 64), ((ntiles + 3) / 4 + 3) / 4));
+      nfine_ = 4 * ncoarse;
       const int nsl = std::max(md_.nslice_s, md_.nslice_m);
-      slab_.alloc((size_t)G_ * nsl * gx_bwd_ * slab_stride());
+      slab_.alloc((size_t)G_ * nsl * nfine_ * slab_stride());
     }
     // tower-forward grids (measured, 600x3000x46 epoch graph): the phase-1/3 training forward
     // runs SDF-only (moments cached) beside the evaluation branch and is fastest with one
@@ -1198,13 +1395,16 @@ class Engine {
     J.h0 = W.h0.p; J.c0 = W.c0.p;
     J.seed = models_[g].seed;
     J.train = train;
+    J.dropout = models_[g].dropout;
     if (s == 0 && train) J.prog = prog_ptr(g, 0);
     return J;
   }
   // progress counter of the fused LSTM + tower forward of (model, split); set only on the job
   // tables that launch it (training split: train tables; evaluation splits: the eval tables)
   int* prog_ptr(int g, int s) { return prog_.p + 16 * (3 * g + s); }
-  void set_prog(MlpJob& J, int g, int s) { J.prog = prog_ptr(g, s); J.prog_err = prog_ptr(g, s) + 1; J.prog_mode = prog_mode_; }
+  void set_prog(MlpJob& J, int g, int s) {
+    J.prog = prog_ptr(g, s); J.prog_err = prog_ptr(g, s) + 1; J.prog_mode = prog_mode_; J.prog_limit = prog_limit_;
+  }
   const float* pp_ptr(int g, int s) {
     if (md_.nrnn > 0) return ws(g, s).pp.p;
     if (md_.Dm > 0) return splits_[s].macro.p;   // raw macro feeds the SDF directly
@@ -1230,10 +1430,13 @@ class Engine {
     J.step = models_[g].drop_step.p;
     J.R = D.R; J.N = D.N; J.T = D.T;
     J.seed = tower_seed(g);
+    J.dropout = models_[g].dropout;
     J.train = train; J.do_sdf = do_sdf; J.do_mom = do_mom;
     if (s == 0 && train) set_prog(J, g, 0);
     const int nsl = std::max(md_.nslice_s, md_.nslice_m);
-    J.slab_base = g * nsl * gx_bwd_;
+    J.slab_base = g * nsl * slabs_stored();
+    J.nslab = nfine_;
+    J.fpw = fpw_;
     return J;
   }
   // wide path: projection (do_sdf / do_mom = towers to project) or weight-gradient job
@@ -1304,7 +1507,7 @@ class Engine {
       const SplitDev& D = splits_[s];
       if (!D.set || D.T == 0) continue;
       const bool cond = gram_cond_ok() && (s != 0 || cache_train_h());
-      const size_t per = (size_t)gram_slices(D.T, G_) * 2 * D.T * D.T;
+      const size_t per = (size_t)gram_slices(D.T) * 2 * D.T * D.T;
       double* base = gram_scratch_.p + (s == 0 ? 0 : n0);
       std::vector<GramJob> jobs;
       for (int g = 0; g < G_; ++g) {
@@ -1322,7 +1525,10 @@ class Engine {
   void build_gram(bool defer = false) {
     for (int s = 0; s < 3; ++s) {
       const SplitDev& D = splits_[s];
-      if (!D.set || D.T == 0) continue;
+      if (!D.set || D.T == 0 || gram_valid_[s]) continue;
+      // only what the current run's plan reads (run_epochs sets cur_phase_; 0: everything)
+      if (cur_phase_ >= 1 && cur_phase_ <= 3 && !(s == 0 ? plan_tr_[cur_phase_] : plan_ev_[cur_phase_])) continue;
+      gram_valid_[s] = true;
       hipStream_t st = st_;
       if (s > 0 && defer) {
         if (!eval_gram_pending_) {
@@ -1333,7 +1539,7 @@ class Engine {
         st = st2_;
       }
       HTRACE("launch_gram split=%d", s);
-      launch_gram(as<GramJob>(j_gram_[s]), G_, D.T, gram_slices(D.T, G_), st);
+      launch_gram(as<GramJob>(j_gram_[s]), G_, D.T, gram_slices(D.T), st);
     }
     if (eval_gram_pending_) HIP_OK(hipEventRecord(ev_gram_, st2_));
   }
@@ -1350,8 +1556,16 @@ class Engine {
     graphs_.clear();
     fwd_tables_.clear();
     j_mlp_bwd_dh_.free();
+    {   // backward launch shape over the fixed fine-slab partition: one workgroup per fine slab
+        // for one or two models (the tuned single-model grid), four fine slabs per workgroup
+        // from three models on (about the round-3 per-model grids: fewer weight stagings and
+        // a quarter of the slabs for k_finalize), if the coarse accumulator fits in LDS
+      const int want = env_int("DLAP_BWD_FPW", G_ >= 3 ? 4 : 1);
+      fpw_ = (want == 4 && mlp_bwd_lds_bytes(md_.md, slab_stride(), 4) <= 160 * 1024) ? 4 : 1;
+      gx_bwd_ = nfine_ / fpw_;
+    }
     std::vector<RnnJob> rt, re;
-    std::vector<LossJob> le;
+    std::vector<LossJob> le, led;
     std::vector<MlpJob> me;
     std::vector<FinJob> fj;
     std::vector<UpdJob> uj;
@@ -1367,15 +1581,18 @@ class Engine {
         set_prog(me.back(), g, s);
         we.push_back(wide_job(g, s, true, !h_cache_));
         le.push_back(loss_job(g, s, 0, gram_eval()));
+        led.push_back(loss_job(g, s, 0, false));
         tmax_eval_ = std::max(tmax_eval_, splits_[s].T);
         nmax_eval_ = std::max(nmax_eval_, splits_[s].N);
       }
       ModelSplitWS& W = ws(g, 0);
       FinJob F{};
       const int nsl = std::max(md_.nslice_s, md_.nslice_m);
-      F.slab = slab_.p + (size_t)g * nsl * gx_bwd_ * slab_stride();
+      F.slab = slab_.p + (size_t)g * nsl * slabs_stored() * slab_stride();
       F.grads = models_[g].grads.p; F.row_ptr = splits_[0].row_ptr.p;
-      F.u = W.u.p; F.dpp = W.dpp.p; F.v = W.v.p; F.dab = W.dab.p; F.T = splits_[0].T; F.nslab = gx_bwd_;
+      F.u = W.u.p; F.dpp = W.dpp.p; F.v = W.v.p; F.dab = W.dab.p; F.T = splits_[0].T;
+      F.nslab = slabs_stored(); F.group = fpw_ == 1 ? 4 : 1;
+      F.dropout = models_[g].dropout;
       fj.push_back(F);
       ModelState& S = models_[g];
       UpdJob U{};
@@ -1386,13 +1603,21 @@ class Engine {
       U.dpp = W.dpp.p; U.macro = splits_[0].macro.p; U.sg = W.sg.p; U.sc = W.sc.p; U.sh = W.sh.p;
       U.dg = W.dg.p; U.dx = W.dx.p; U.dab = W.dab.p; U.scal = W.scal.p; U.scal_prev = W.scal_prev.p;
       U.h0 = W.h0.p; U.c0 = W.c0.p; U.dh0 = W.dh0.p; U.dc0 = W.dc0.p;
-      U.T = splits_[0].T; U.seed = S.seed; U.lr = S.lr;
+      U.T = splits_[0].T; U.seed = S.seed; U.lr = S.lr; U.prog = prog_ptr(g, 0); U.dropout = S.dropout;
       uj.push_back(U);
     }
     n_eval_jobs_ = (int)le.size();
+    {   // co-residency capacity of the fused launches (no GPU query when they cannot run)
+      const int force = env_int("DLAP_FUSED_CAP", -1);
+      const bool can = rnn_overlap_ && md_.nrnn > 0 && !md_.md.wide;
+      cap_train_ = !can || !splits_[0].set ? 0
+                   : force >= 0 ? force : mlp_fwd_rnn_capacity(md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, splits_[0].T);
+      cap_eval_ = !can || n_eval_jobs_ == 0 ? 0
+                  : force >= 0 ? force : mlp_fwd_rnn_capacity(md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, tmax_eval_);
+    }
     if (gram_on_) build_gram_jobs();
-    gram_valid_ = false;
-    upload(j_rnn_train_, rt); upload(j_rnn_eval_, re); upload(j_mlp_eval_, me); upload(j_loss_eval_, le);
+    for (bool& v : gram_valid_) v = false;
+    upload(j_rnn_train_, rt); upload(j_rnn_eval_, re); upload(j_mlp_eval_, me); upload(j_loss_eval_, le); upload(j_loss_eval_dense_, led);
     upload(j_fin_, fj); upload(j_upd_, uj); upload(j_wide_eval_, we);
     {   // moment refresh: eval-mode moment tower (and its per-period bias) of every split
       std::vector<RnnJob> rm;
@@ -1440,6 +1665,7 @@ class Engine {
         E.snap_flags = S.snap_flags.p; E.params = S.params.p;
         E.snap_loss = S.snap_loss.p; E.snap_sharpe = S.snap_sharpe.p;
         E.max_ep = max_epochs_;
+        E.prog = prog_ptr(g, 0);
         ej.push_back(E);
       }
       upload(j_mlp_train_[phase], mt); upload(j_mlp_bwd_[phase], mb); upload(j_loss_train_[phase], lt);
@@ -1473,7 +1699,7 @@ class Engine {
   void ensure_moments(bool with_gram = false, bool defer_eval_gram = false) {
     if (!h_cache_ || n_mom_jobs_ == 0) return;
     if (h_valid_) {
-      if (with_gram && gram_on_ && !gram_valid_) { build_gram(defer_eval_gram); gram_valid_ = true; }
+      if (with_gram && gram_on_) build_gram(defer_eval_gram);
       return;
     }
     HTRACE("ensure_moments jobs=%d tmax=%d gx=%d", n_mom_jobs_, tmax_all_, gx_mom_);
@@ -1489,8 +1715,8 @@ class Engine {
       launch_mlp_fwd(as<MlpJob>(j_mlp_mom_), n_mom_jobs_, gx_mom_, md_.md, md_.KS1, md_.WMB, st_);
     }
     h_valid_ = true;
-    gram_valid_ = false;
-    if (with_gram && gram_on_) { build_gram(defer_eval_gram); gram_valid_ = true; }
+    for (bool& v : gram_valid_) v = false;
+    if (with_gram && gram_on_) build_gram(defer_eval_gram);
   }
   bool dropmask_on(int phase) const { return md_.dropout > 0.f && phase != 2; }
   // keep masks of the step *drop_step + offset* (phases 1/3: the SDF tower's dropout)
@@ -1531,7 +1757,7 @@ class Engine {
       launch_mlp_fwd_zx(as<MlpJob>(j_mlp_train_[phase]), G_, std::max(1, zx_gx_ / G_), md_.md, md_.WMB, st_, true);
     else if (fused)
       launch_mlp_fwd_rnn(as<MlpJob>(j_mlp_train_[phase]), as<RnnJob>(j_rnn_train_), dd(), G_,
-                         phase == 2 ? gx_fwd_[0] : gx_fwd13_, md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, D.T, st_);
+                         fused_train_gx(phase), md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, D.T, st_);
     else
       launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, phase == 2 ? gx_fwd_[0] : gx_fwd13_, md_.md, md_.KS1,
                      md_.WMB, st_);
@@ -1565,7 +1791,7 @@ class Engine {
     if (phase == 2) {
       HTRACE("launch_mlp_bwd_mom");
       launch_mlp_bwd_mom(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_m, 1, md_.md, md_.KS1,
-                         md_.WMB, slab_stride(), st_);
+                         md_.WMB, slab_stride(), fpw_, st_);
     } else {
       if (!gram) {
         HTRACE("launch_period_bwd");
@@ -1573,7 +1799,7 @@ class Engine {
       }
       HTRACE("launch_mlp_bwd_sdf");
       launch_mlp_bwd_sdf(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_s, md_.tps_s, md_.md, md_.KS1,
-                         slab_stride(), st_);
+                         slab_stride(), fpw_, st_);
     }
     if (md_.md.wide)   // layer-0 weight gradient from the tower's dz fragments
       launch_wgrad0(as<WideJob>(j_wide_bwd_[phase]), G_, dd(), md_.md, phase == 2, md_.WMB, nsplit_, st_);
@@ -1630,8 +1856,7 @@ class Engine {
   }
   void enqueue_eval_towers(hipStream_t st) {
     if (n_eval_jobs_ == 0) return;
-    int gx = std::max(gx_fwd_[1], gx_fwd_[2]);
-    if (eval_gx_ > 0) gx = std::min(gx, eval_gx_);
+    const int gx = eval_grid();
     if (md_.md.wide && zx_eval_) {     // layer 0 streamed inside the evaluation towers
       HTRACE("launch_mlp_fwd_zx");
       launch_mlp_fwd_zx(as<MlpJob>(j_mlp_eval_), n_eval_jobs_, std::max(1, zx_gx_ / n_eval_jobs_), md_.md, md_.WMB, st);
@@ -1640,22 +1865,24 @@ class Engine {
         launch_proj0(as<WideJob>(j_wide_eval_), n_eval_jobs_, std::max(gx_proj_[1], gx_proj_[2]), md_.md, md_.WMB, st);
       HTRACE("launch_mlp_fwd");
       if (fused_eval())
-        launch_mlp_fwd_rnn(as<MlpJob>(j_mlp_eval_), as<RnnJob>(j_rnn_eval_), dd(), n_eval_jobs_, gx, md_.md, md_.KS1,
-                           md_.WMB, md_.H, md_.nrnn, tmax_eval_, st);
+        launch_mlp_fwd_rnn(as<MlpJob>(j_mlp_eval_), as<RnnJob>(j_rnn_eval_), dd(), n_eval_jobs_, fused_eval_gx(),
+                           md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, tmax_eval_, st);
       else
         launch_mlp_fwd(as<MlpJob>(j_mlp_eval_), n_eval_jobs_, gx, md_.md, md_.KS1, md_.WMB, st);
     }
+    const bool eg = eval_gram_now();
+    const LossJob* le = as<LossJob>(eg ? j_loss_eval_ : j_loss_eval_dense_);
     HTRACE("launch_period_fwd");
-    launch_period_fwd(as<LossJob>(j_loss_eval_), n_eval_jobs_, tmax_eval_, st);
-    if (gram_run_ && gram_eval()) {  // quadratic-form terms per period (no asset passes)
+    launch_period_fwd(le, n_eval_jobs_, tmax_eval_, st);
+    if (eg) {                        // quadratic-form terms per period (no asset passes)
       HTRACE("launch_period_bwd(eval)");
-      launch_period_bwd(as<LossJob>(j_loss_eval_), n_eval_jobs_, tmax_eval_, st);
+      launch_period_bwd(le, n_eval_jobs_, tmax_eval_, st);
     } else {
       HTRACE("launch_asset");
-      launch_asset(as<LossJob>(j_loss_eval_), n_eval_jobs_, nmax_eval_, md_.K, st);
+      launch_asset(le, n_eval_jobs_, nmax_eval_, md_.K, st);
     }
     HTRACE("launch_job_metrics");
-    launch_job_metrics(as<LossJob>(j_loss_eval_), n_eval_jobs_, st);
+    launch_job_metrics(le, n_eval_jobs_, st);
   }
   void enqueue_epoch_end(int phase, int ignore_epoch, float sel, hipStream_t st) {
     HTRACE("launch_epoch_end");
@@ -1862,6 +2089,10 @@ PYBIND11_MODULE(_dlap_hip, m) {
       .def("describe", &Engine::describe)
       .def("set_split", &Engine::set_split)
       .def("set_split_dev", &Engine::set_split_dev)
+      .def("set_split_dense", &Engine::set_split_dense, py::arg("s"), py::arg("feats"), py::arg("ret"),
+           py::arg("mask"), py::arg("mask_bool"), py::arg("macro"), py::arg("T"), py::arg("N"), py::arg("F"),
+           py::arg("stream") = 0)
+      .def("read_split", &Engine::read_split)
       .def("set_params", &Engine::set_params)
       .def("get_params", &Engine::get_params)
       .def("get_grads", &Engine::get_grads)
@@ -1879,12 +2110,18 @@ PYBIND11_MODULE(_dlap_hip, m) {
       .def("history", &Engine::history)
       .def("run_epochs", &Engine::run_epochs, py::call_guard<py::gil_scoped_release>())
       .def("set_pipeline", &Engine::set_pipeline)
+      .def("plan_phase", &Engine::plan_phase)
+      .def("gram_plan", &Engine::gram_plan)
       .def("set_lr", &Engine::set_lr)
+      .def("set_dropout", &Engine::set_dropout)
+      .def("get_dropout", &Engine::get_dropout)
       .def_static("blocking_calls", []() { return (long long)g_blocking.load(); })
       .def_static("live_engines", []() { return g_live_engines.load(); })
       .def_static("rnn_timestamps", []() { return rnn_timestamps(); })
-      .def("fused_forward", [](Engine& e, int phase) { return e.fused_fwd(phase); })
+      .def("fused_forward", [](Engine& e, int phase) { e.ensure_jobs(); return e.fused_fwd(phase); })
       .def("prog_timeouts", &Engine::prog_timeouts)
+      .def("reset_prog_errors", &Engine::reset_prog_errors)
+      .def("fused_info", [](Engine& e) { e.ensure_jobs(); return e.fused_info(); })
       .def("capture_seconds", [](Engine& e) { return e.capture_seconds(); })
       .def_static("loss_timestamps", []() { return loss_timestamps(); })
       .def_static("mlp_timestamps", []() { return mlp_timestamps(); })

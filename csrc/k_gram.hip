@@ -193,18 +193,20 @@ __global__ __launch_bounds__(256) void k_gram_reduce(const GramJob* __restrict__
   gp(J.G)[T2 + e] = su;
 }
 
-// workgroups per tile (each GB_WAVES slices of the inner axis): ~256 workgroups per launch
+// workgroups per tile (each GB_WAVES slices of the inner axis): ~256 workgroups per model
 // (DLAP_GRAM_WG; fewer slices leave CUs to the head epoch that the evaluation-split builds
-// overlap and shrink the reduce pass: profiles/r3_knobs_gram_grid.log)
-int gram_slices(int T, int njobs) {
+// overlap and shrink the reduce pass: profiles/r3_knobs_gram_grid.log). A function of T only:
+// the split-K partition -- and so the bits of G -- must not depend on how many models share
+// the launch.
+int gram_slices(int T) {
   static const int target = [] { const char* v = std::getenv("DLAP_GRAM_WG"); return v ? std::atoi(v) : 256; }();
   const int nt = (T + 31) / 32, npair = nt * (nt + 1) / 2;
-  const int want = target / std::max(1, npair * njobs);
+  const int want = target / std::max(1, npair);
   return std::max(1, std::min(64, want));
 }
 
 size_t gram_part_doubles(int T, int njobs) {
-  return (size_t)njobs * gram_slices(T, njobs) * 2 * (size_t)T * T;
+  return (size_t)njobs * gram_slices(T) * 2 * (size_t)T * T;
 }
 
 void launch_gram(const GramJob* jobs, int njobs, int T, int nslice, hipStream_t st) {

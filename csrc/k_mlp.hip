@@ -111,8 +111,8 @@ struct DropCtx {
 DLAP_DEV uint32_t load_step(const MlpJob& J) { return J.step ? (uint32_t)*gp(J.step) : 0u; }
 DLAP_DEV DropCtx drop_ctx(const MlpJob& J, const MlpDims& D, uint32_t step) {
   DropCtx dc;
-  dc.on = J.train && D.dropout > 0.f;
-  dc.thr16 = (uint32_t)(D.dropout * 65536.f + 0.5f);
+  dc.on = J.train && J.dropout > 0.f;
+  dc.thr16 = (uint32_t)(J.dropout * 65536.f + 0.5f);
   dc.seed = J.seed;
   dc.step = step;
   return dc;
@@ -543,22 +543,29 @@ DLAP_DEV void sdf_keep_words(bool pre, const uint32_t (&kw_pre)[4], const DropCt
 }
 
 // Bounded spin on the fused forward's progress counter (k_mlp_fwd_rnn): wave-uniform, s_sleep
-// between polls; gives up after ~0.1 s (the dispatch-order argument below says it never has to)
-// and counts that in *err, so no wave can hang the GPU.
-#define PROG_SPIN_LIMIT (1u << 22)
-DLAP_DEV int prog_wait(const int* prog, int* err, int need, int seen, bool fence) {
+// between polls. The engine launches the fused forward only when its whole grid is co-resident
+// (occupancy query, engine.cpp fused_fits), so the wait always ends; it is bounded anyway
+// (~0.1 s, MlpJob::prog_limit): a wave that gives up counts it in *err and returns -1, and the
+// caller then stops WITHOUT writing anything -- the launch is invalid, k_adam skips the update
+// and k_epoch_end records a NaN epoch for that model (the device-side poison), and the host
+// raises at its next synchronisation (runner.py). Nothing is ever computed on unpublished data.
+DLAP_DEV int prog_wait(const int* prog, int* err, int need, int seen, bool fence, unsigned limit) {
   if (need <= seen) return seen;
   int v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   unsigned spins = 0;
   while (v < need) {
+    if (spins++ >= limit) {
+      if ((threadIdx.x & 63) == 0) atomicAdd(err, 1);
+      return -1;
+    }
     __builtin_amdgcn_s_sleep(2);
     v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(prog, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    if (++spins > PROG_SPIN_LIMIT) {
-      if ((threadIdx.x & 63) == 0) atomicAdd(err, 1);
-      v = 1 << 30;
-      break;
-    }
   }
+  // Compiler-only barrier: the relaxed loads of the published outputs (finish_tile FRESH) must
+  // not be hoisted above the poll that decided the exit (different addresses, so the language
+  // model alone would allow it). The hardware order follows from the exit branch waiting for
+  // the poll's value. Costs no instruction.
+  asm volatile("" ::: "memory");
   // the outputs published before the counter are visible to this wave's loads from here on
   // (prog mode 0; mode 1 reads them with cache-bypassing loads instead of invalidating)
   if (fence) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -590,7 +597,7 @@ DLAP_DEV void mlp_fwd_body(const MlpJob& J, const MlpDims& D, char* smem, const 
   // prologue: the step counter, the first tile's panel rows and keep words (both parity
   // halves: the step is not known yet) are all in flight with the weight staging
   const uint32_t stp = load_step(J);
-  const bool pre = J.gbits && J.train && D.dropout > 0.f;   // keep words pre-generated (k_dropmask)
+  const bool pre = J.gbits && J.train && J.dropout > 0.f;   // keep words pre-generated (k_dropmask)
   constexpr int KWM = 4;                           // max SDF hidden layers (engine limit)
   uint32_t kw_cur[KWM], kw_nxt[KWM], kw_alt[KWM];
   auto issue_kw = [&](const DLAP_GLOBAL uint32_t* base, int t, uint32_t (&kw)[KWM], int nls) {
@@ -644,7 +651,8 @@ DLAP_DEV void mlp_fwd_body(const MlpJob& J, const MlpDims& D, char* smem, const 
     if constexpr (WAIT) {
       // the tile's last row (clamped to R - 1) has its largest period
       const int tl = __builtin_amdgcn_readlane(cur.ti[1].x, 15);
-      seen = prog_wait(J.prog, J.prog_err, tl + 1, seen, J.prog_mode == 0);
+      seen = prog_wait(J.prog, J.prog_err, tl + 1, seen, J.prog_mode == 0, J.prog_limit);
+      if (seen < 0) break;               // gave up: no writes from this wave (launch invalid)
     }
     if constexpr (ZIN) ri = finish_ztile<WMB>(J, tile, zcur);
     else if (WAIT && J.prog_mode != 0) ri = finish_tile<P, KS1, true, true>(J, D, tile, cur, xf, spp);
@@ -722,9 +730,10 @@ DLAP_DEV void lstm_publish(const RnnJob& J, const ModelDesc* __restrict__ md, co
     const int p = __builtin_amdgcn_readfirstlane(__hip_atomic_load(sprog, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP));
     if (p <= done) {
       __builtin_amdgcn_s_sleep(1);
-      if (++spins > PROG_SPIN_LIMIT) {          // (never: the recurrence always finishes)
+      // (never: the recurrence runs in the same workgroup and always finishes.) Giving up
+      // publishes nothing more: the waiting tower waves then give up too, without writes.
+      if (++spins > (1u << 22)) {
         if (lane == 0) atomicAdd(J.prog + 1, 1);
-        if (lane == 0) __hip_atomic_store(J.prog, T, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
         return;
       }
       continue;
@@ -944,9 +953,48 @@ DLAP_DEV float* wg_slab_begin(char* smem, int slab_stride) {
   __syncthreads();
   return red;
 }
-DLAP_DEV void wg_slab_store(const MlpJob& J, const float* red, int slab_stride) {
-  const auto slab = gp(J.slab) + (size_t)(J.slab_base + blockIdx.z * gridDim.x + blockIdx.x) * slab_stride;
-  for (int i = threadIdx.x; i < slab_stride; i += blockDim.x) slab[i] = red[i];
+// LDS image of a slab (bank-conflict-free wave adds): the global slab layout is natural --
+// gradient tile t element (o, i) at t*4096 + 64 o + i, then the extra rows (per-layer bias rows
+// of 64, the output row, the output bias) -- but in LDS
+//   * tile elements store i with bit 4 flipped for odd o>>2: a wave adds (o = 16u + 4q + r,
+//     i = 16v + n) with lane n + 16q, so the lanes of q and q+1 (one 32-lane group of
+//     ds_read_b32 / ds_write_b32, bank = dword mod 32) hit opposite bank halves instead of the
+//     same 16 banks (2-way);
+//   * bias row j stores column c at (c + 5 j) mod 64, so the up-to-6 layer lanes (n = j) of a
+//     group are 5 banks apart instead of all on one bank (16-way was ~2/3 of the 832 conflicts
+//     per wave measured on k_mlp_bwd_sdf, profiles/r3_final_pmc_summary.txt).
+template <int TPS>
+DLAP_DEV int slab_lds(int e) {
+  if (e < TPS * 4096) return e ^ ((((e >> 6) >> 2) & 1) << 4);
+  const int x = e - TPS * 4096;
+  if (x < DLAP_MAXL * 64) {
+    const int j = x >> 6;
+    return TPS * 4096 + (j << 6) + (((x & 63) + 5 * j) & 63);
+  }
+  return e;
+}
+
+// Fine slab k (of J.fpw) of this workgroup is complete in `red` (after the wave loop's final
+// barrier). fpw == 1: store it as fine slab blockIdx.x of the slice. Else add it, in order, to
+// the coarse accumulator red_c (natural layout, LDS beyond the staging area; each thread
+// touches the same elements every time, so no barrier is needed between the passes) and store
+// the coarse slab after the last one: ((s0 + s1) + s2) + s3 -- exactly the grouping k_finalize
+// applies to stored fine slabs, so either launch shape gives the same gradient bits.
+template <int TPS>
+DLAP_DEV void wg_slab_finish(const MlpJob& J, const float* red, float* red_c, int slab_stride, int k) {
+  if (J.fpw == 1) {
+    const auto slab = gp(J.slab) + (size_t)(J.slab_base + blockIdx.z * J.nslab + blockIdx.x) * slab_stride;
+    for (int i = threadIdx.x; i < slab_stride; i += blockDim.x) slab[i] = red[slab_lds<TPS>(i)];
+    return;
+  }
+  for (int i = threadIdx.x; i < slab_stride; i += blockDim.x) {
+    const float v = red[slab_lds<TPS>(i)];
+    red_c[i] = k ? red_c[i] + v : v;
+  }
+  if (k + 1 < J.fpw) return;
+  const int ncoarse = J.nslab / J.fpw;
+  const auto slab = gp(J.slab) + (size_t)(J.slab_base + blockIdx.z * ncoarse + blockIdx.x) * slab_stride;
+  for (int i = threadIdx.x; i < slab_stride; i += blockDim.x) slab[i] = red_c[i];
 }
 
 // SDF backward. NL = number of hidden (MFMA) layers, all 64 wide.
@@ -962,11 +1010,13 @@ DLAP_DEV void wg_slab_store(const MlpJob& J, const float* red, int slab_stride) 
 // its backward chain at that layer and leaves the bias / output-layer / per-period input
 // gradients to slice 0, so its live state (and register budget) is that of its own role.
 template <class P, int KS1, int NL, int TPS, bool ZIN, int TLC>
-DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, char* smem, int slice, int C0) {
+DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, char* smem, int slice, int C0,
+                           int red_off) {
   using Frag = typename P::Frag;
   Frag* lds = reinterpret_cast<Frag*>(smem);
   float* aux = aux_lds_ptr(smem, D);
   float* spp = pp_lds_ptr(smem, D);
+  float* red_c = reinterpret_cast<float*>(smem + red_off);
   const int lane = lane_id(), q = lane >> 4, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   const int ntiles = (J.R + 31) >> 5;
   const bool s0 = TLC <= 0 && slice == 0;      // the slice that owns the extra gradients (-2: slice 0)
@@ -974,7 +1024,20 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
   const Frag selP0 = make_sel<P>(true, 0), selP1 = make_sel<P>(true, 1);
   const Frag selN0 = make_sel<P>(false, 0), selN1 = make_sel<P>(false, 1);
   const int pst = D.pp_lds_floats > 0 ? D.ppst : D.Dm;
-
+  int tl[TPS], tc[TPS];
+#pragma unroll
+  for (int t = 0; t < TPS; ++t) {
+    const int tid = slice * TPS + t;
+    tl[t] = TLC == -2 ? t : TLC >= 0 ? TLC : (tid < C0 ? 0 : tid - C0 + 1);
+    tc[t] = (TLC == -2 || TLC > 0) ? 0 : (tid < C0 ? tid : 0);
+  }
+  // fine slab vs = blockIdx.x * fpw + k owns tiles vs * waves + wave, strided by nslab * waves:
+  // the partition (and so every fp32 partial) depends on R only, never on the launch grid
+  const int stride = J.nslab * nwaves;
+  const uint32_t stp = load_step(J);
+  const bool pre = J.gbits && J.train && J.dropout > 0.f;   // keep words of this step (k_dropmask)
+  for (int kf = 0; kf < J.fpw; ++kf) {
+  if (kf) __syncthreads();                      // the previous slab's LDS reads are done
   f32x4 dW[TPS][4][4];
 #pragma unroll
   for (int t = 0; t < TPS; ++t)
@@ -986,22 +1049,11 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
 #pragma unroll
   for (int u = 0; u < 4; ++u) { gbias[u] = zero4(); gwo[u] = zero4(); }
   float gbo = 0.f;
-  int tl[TPS], tc[TPS];
-#pragma unroll
-  for (int t = 0; t < TPS; ++t) {
-    const int tid = slice * TPS + t;
-    tl[t] = TLC == -2 ? t : TLC >= 0 ? TLC : (tid < C0 ? 0 : tid - C0 + 1);
-    tc[t] = (TLC == -2 || TLC > 0) ? 0 : (tid < C0 ? tid : 0);
-  }
-
-  const int stride = gridDim.x * nwaves;
-  int tile = blockIdx.x * nwaves + wave;
+  int tile = (blockIdx.x * J.fpw + kf) * nwaves + wave;
   TileIn<P, KS1> cur, nxt;
   ZTile<1> zcur, znxt;
   // prologue as k_mlp_fwd: step, first tile and its keep words of both parities in flight with
-  // the staging
-  const uint32_t stp = load_step(J);
-  const bool pre = J.gbits && J.train && D.dropout > 0.f;   // keep words of this step (k_dropmask)
+  // the staging (re-staged per fine slab: the slab reduction reuses the staging area)
   uint32_t kw_cur[NL], kw_nxt[NL], kw_alt[NL];
   if (tile < ntiles) {
     if constexpr (ZIN) issue_ztile<1, true>(J, D, tile, zcur, true, false);
@@ -1179,14 +1231,15 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
           for (int v = 0; v < 4; ++v)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              red[t * 4096 + (16 * u + 4 * q + r) * 64 + 16 * v + (lane & 15)] += dW[t][u][v][r];
+              red[t * 4096 + (16 * u + 4 * q + r) * 64 + ((16 * v + (lane & 15)) ^ ((q & 1) << 4))] += dW[t][u][v][r];
       if (s0) {
         float* ex = red + TPS * 4096;
+        const int jl = lane & 15;
 #pragma unroll
         for (int u = 0; u < 4; ++u)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
-            if ((lane & 15) < DLAP_MAXL) ex[(lane & 15) * 64 + 16 * u + 4 * q + r] += gbias[u][r];
+            if (jl < DLAP_MAXL) ex[jl * 64 + ((16 * u + 4 * q + r + 5 * jl) & 63)] += gbias[u][r];
             float v = gwo[u][r];
             v += __shfl_xor(v, 1, 64); v += __shfl_xor(v, 2, 64);
             v += __shfl_xor(v, 4, 64); v += __shfl_xor(v, 8, 64);
@@ -1198,12 +1251,13 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
     }
     __syncthreads();
   }
-  wg_slab_store(J, red, slab_stride);
+  wg_slab_finish<TPS>(J, red, red_c, slab_stride, kf);
+  }
 }
 
 template <class P, int KS1, int NL, int TPS, bool ZIN>
 __global__ __launch_bounds__(256, TPS == 1 ? DLAP_BWD1_WPS : 1) void k_mlp_bwd_sdf(const MlpJob* __restrict__ jobs, MlpDims D,
-                                                        int slab_stride) {
+                                                        int slab_stride, int red_off) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const MlpJob& J = jobs[blockIdx.y];
   const int slice = blockIdx.z;
@@ -1212,14 +1266,14 @@ __global__ __launch_bounds__(256, TPS == 1 ? DLAP_BWD1_WPS : 1) void k_mlp_bwd_s
   const int C0 = ZIN ? (D.Dm + 63) / 64 : KS1 / 2;
   if constexpr (TPS == 1) {
     const int tl = slice < C0 ? 0 : slice - C0 + 1;     // block-uniform: one role per slice
-    if (tl == 0) bwd_sdf_body<P, KS1, NL, 1, ZIN, 0>(J, D, slab_stride, smem, slice, C0);
-    if constexpr (NL > 1) if (tl == 1) bwd_sdf_body<P, KS1, NL, 1, ZIN, 1>(J, D, slab_stride, smem, slice, C0);
-    if constexpr (NL > 2) if (tl == 2) bwd_sdf_body<P, KS1, NL, 1, ZIN, 2>(J, D, slab_stride, smem, slice, C0);
-    if constexpr (NL > 3) if (tl == 3) bwd_sdf_body<P, KS1, NL, 1, ZIN, 3>(J, D, slab_stride, smem, slice, C0);
+    if (tl == 0) bwd_sdf_body<P, KS1, NL, 1, ZIN, 0>(J, D, slab_stride, smem, slice, C0, red_off);
+    if constexpr (NL > 1) if (tl == 1) bwd_sdf_body<P, KS1, NL, 1, ZIN, 1>(J, D, slab_stride, smem, slice, C0, red_off);
+    if constexpr (NL > 2) if (tl == 2) bwd_sdf_body<P, KS1, NL, 1, ZIN, 2>(J, D, slab_stride, smem, slice, C0, red_off);
+    if constexpr (NL > 3) if (tl == 3) bwd_sdf_body<P, KS1, NL, 1, ZIN, 3>(J, D, slab_stride, smem, slice, C0, red_off);
   } else if (TPS == 2 && C0 == 1) {     // the engine's TPS = 2 case: tiles (layer 0, layer 1)
-    bwd_sdf_body<P, KS1, NL, TPS, ZIN, -2>(J, D, slab_stride, smem, slice, C0);
+    bwd_sdf_body<P, KS1, NL, TPS, ZIN, -2>(J, D, slab_stride, smem, slice, C0, red_off);
   } else {
-    bwd_sdf_body<P, KS1, NL, TPS, ZIN, -1>(J, D, slab_stride, smem, slice, C0);
+    bwd_sdf_body<P, KS1, NL, TPS, ZIN, -1>(J, D, slab_stride, smem, slice, C0, red_off);
   }
 }
 
@@ -1229,20 +1283,31 @@ __global__ __launch_bounds__(256, TPS == 1 ? DLAP_BWD1_WPS : 1) void k_mlp_bwd_s
 // ZIN: as k_mlp_bwd_sdf (layer 0 from z, layer-0 dz stored as J.dz_out [tile][WMB][64]).
 template <class P, int KS1, int WMB, int NLM, int TPS, bool ZIN>
 __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict__ jobs, MlpDims D,
-                                                        int slab_stride) {
+                                                        int slab_stride, int red_off) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int KSM = (WMB + 1) / 2;
   using Frag = typename P::Frag;
   const MlpJob& J = jobs[blockIdx.y];
   Frag* lds = reinterpret_cast<Frag*>(smem);
   float* aux = aux_lds_ptr(smem, D);
+  float* red_c = reinterpret_cast<float*>(smem + red_off);
   const int lane = lane_id(), q = lane >> 4, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   const int ntiles = (J.R + 31) >> 5;
   const int slice = blockIdx.z;
   constexpr int C0 = ZIN ? 0 : KS1 / 2;
   const Frag selP0 = make_sel<P>(true, 0), selP1 = make_sel<P>(true, 1);
   const Frag selN0 = make_sel<P>(false, 0), selN1 = make_sel<P>(false, 1);
-
+  int tl[TPS], tc[TPS];
+#pragma unroll
+  for (int t = 0; t < TPS; ++t) {
+    const int tid = slice * TPS + t;
+    tl[t] = tid < C0 ? 0 : tid - C0 + 1;
+    tc[t] = tid < C0 ? tid : 0;
+  }
+  // fine slabs as k_mlp_bwd_sdf (partition of the rows by R only)
+  const int stride = J.nslab * nwaves;
+  for (int kf = 0; kf < J.fpw; ++kf) {
+  if (kf) __syncthreads();
   f32x4 dW[TPS][WMB][4];
 #pragma unroll
   for (int t = 0; t < TPS; ++t)
@@ -1253,16 +1318,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
   f32x4 gbias[WMB];
 #pragma unroll
   for (int u = 0; u < WMB; ++u) gbias[u] = zero4();
-  int tl[TPS], tc[TPS];
-#pragma unroll
-  for (int t = 0; t < TPS; ++t) {
-    const int tid = slice * TPS + t;
-    tl[t] = tid < C0 ? 0 : tid - C0 + 1;
-    tc[t] = tid < C0 ? tid : 0;
-  }
-
-  const int stride = gridDim.x * nwaves;
-  int tile = blockIdx.x * nwaves + wave;
+  int tile = (blockIdx.x * J.fpw + kf) * nwaves + wave;
   TileIn<P, KS1> cur, nxt;
   ZTile<WMB> zcur, znxt;
   AbPre<WMB> ab_cur, ab_nxt;
@@ -1413,19 +1469,21 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
           for (int v = 0; v < 4; ++v)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              red[t * 4096 + (16 * u + 4 * q + r) * 64 + 16 * v + (lane & 15)] += dW[t][u][v][r];
+              red[t * 4096 + (16 * u + 4 * q + r) * 64 + ((16 * v + (lane & 15)) ^ ((q & 1) << 4))] += dW[t][u][v][r];
       if (slice == 0) {
         float* ex = red + TPS * 4096;
+        const int jl = lane & 15;
 #pragma unroll
         for (int u = 0; u < WMB; ++u)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            if ((lane & 15) < DLAP_MAXL) ex[(lane & 15) * 64 + 16 * u + 4 * q + r] += gbias[u][r];
+            if (jl < DLAP_MAXL) ex[jl * 64 + ((16 * u + 4 * q + r + 5 * jl) & 63)] += gbias[u][r];
       }
     }
     __syncthreads();
   }
-  wg_slab_store(J, red, slab_stride);
+  wg_slab_finish<TPS>(J, red, red_c, slab_stride, kf);
+  }
 }
 
 // ============================== dropout keep-mask generator ===========================
@@ -1440,7 +1498,8 @@ __global__ __launch_bounds__(256) void k_dropmask(const MlpJob* __restrict__ job
   const int tile = gid >> 6, lane = gid & 63, q = lane >> 4;
   if (tile >= ntiles) return;
   const uint32_t step = (J.step ? (uint32_t)*gp(J.step) : 0u) + (uint32_t)step_offset;
-  const uint32_t thr16 = (uint32_t)(D.dropout * 65536.f + 0.5f);
+  if (!(J.dropout > 0.f)) return;        // (no keep words: this model's towers do not read them)
+  const uint32_t thr16 = (uint32_t)(J.dropout * 65536.f + 0.5f);
   uint32_t rowmix[2];
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
@@ -1462,9 +1521,14 @@ void launch_dropmask(const MlpJob* jobs, int njobs, int ntiles, const MlpDims& D
 
 // ---- host launchers -------------------------------------------------------------------
 size_t mlp_lds_bytes(const MlpDims& D) { return lds_bytes_of(D); }
-static size_t bwd_lds_bytes(const MlpDims& D, int slab_stride) {
-  size_t a = mlp_lds_bytes(D), b = (size_t)slab_stride * 4;
-  return a > b ? a : b;
+// backward LDS: the staging area (reused by the fine slab reduction), then with fpw > 1 the
+// coarse accumulator at red_off
+static size_t bwd_red_off(const MlpDims& D, int slab_stride) {
+  const size_t a = mlp_lds_bytes(D), b = (size_t)slab_stride * 4;
+  return ((a > b ? a : b) + 15) & ~(size_t)15;
+}
+size_t mlp_bwd_lds_bytes(const MlpDims& D, int slab_stride, int fpw) {
+  return bwd_red_off(D, slab_stride) + (fpw > 1 ? (size_t)slab_stride * 4 : 0);
 }
 
 template <class P>
@@ -1505,6 +1569,30 @@ bool mlp_fwd_rnn_supported(const MlpDims& D, int KS1, int WMB, int H, int nrnn, 
   if (!(KS1 == 2 || KS1 == 4) || !(WMB == 1 || WMB == 2 || WMB == 4)) return false;
   return fwd_rnn_lds(D, H, tmax) <= 64 * 1024;
 }
+// Workgroups of the fused kernel the whole device holds at once (occupancy query x CUs): the
+// engine launches it only with (1 + gx) * njobs at most this, so every tower workgroup is
+// co-resident with the LSTM workgroup it waits for -- forward progress does not rest on the
+// dispatch order. 0 = not instantiated for this shape.
+int mlp_fwd_rnn_capacity(const MlpDims& D0, int KS1, int WMB, int H, int nrnn, int tmax) {
+  if (!mlp_fwd_rnn_supported(D0, KS1, WMB, H, nrnn, tmax)) return 0;
+  const size_t sh = fwd_rnn_lds(D0, H, tmax);
+  int per_cu = 0;
+#define O_CASE(PR, K, W, HM, DP) \
+  if (KS1 == K && WMB == W && H == HM) \
+    HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_mlp_fwd_rnn<PR, K, W, HM, DP>, 256, sh));
+#define O_KW(PR, HM, DP) O_CASE(PR, 2, 1, HM, DP) O_CASE(PR, 2, 2, HM, DP) O_CASE(PR, 2, 4, HM, DP) \
+  O_CASE(PR, 4, 1, HM, DP) O_CASE(PR, 4, 2, HM, DP) O_CASE(PR, 4, 4, HM, DP)
+  if (D0.fp32) { O_KW(PrecF32, 4, true) }
+  else { O_KW(PrecBF16, 4, true) O_KW(PrecBF16, 8, false) }
+#undef O_KW
+#undef O_CASE
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  int ncu = 0;
+  HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  return per_cu * ncu;
+}
+
 bool launch_mlp_fwd_rnn(const MlpJob* jobs, const RnnJob* rjobs, const ModelDesc* md, int njobs, int gx,
                         const MlpDims& D0, int KS1, int WMB, int H, int nrnn, int tmax, hipStream_t st) {
   if (!mlp_fwd_rnn_supported(D0, KS1, WMB, H, nrnn, tmax))
@@ -1539,8 +1627,8 @@ void launch_mlp_fwd_zx(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, 
 
 template <class P>
 static bool launch_bwd_sdf_p(const MlpJob* jobs, dim3 grid, dim3 block, size_t sh, int tps, const MlpDims& D,
-                             int KS1, int slab_stride, hipStream_t st) {
-#define S_CASE(K, N, T) if (KS1 == K && D.nl_sdf == N && tps == T) { hipLaunchKernelGGL((k_mlp_bwd_sdf<P, K, N, T, false>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return true; }
+                             int KS1, int slab_stride, int roff, hipStream_t st) {
+#define S_CASE(K, N, T) if (KS1 == K && D.nl_sdf == N && tps == T) { hipLaunchKernelGGL((k_mlp_bwd_sdf<P, K, N, T, false>), grid, block, sh, st, jobs, D, slab_stride, roff); HIP_OK(hipGetLastError()); return true; }
   S_CASE(2, 1, 1) S_CASE(2, 2, 1) S_CASE(2, 3, 1) S_CASE(2, 4, 1)
   S_CASE(2, 2, 2)
   S_CASE(4, 1, 1) S_CASE(4, 2, 1) S_CASE(4, 3, 1) S_CASE(4, 4, 1)
@@ -1549,25 +1637,26 @@ static bool launch_bwd_sdf_p(const MlpJob* jobs, dim3 grid, dim3 block, size_t s
 }
 
 void launch_mlp_bwd_sdf(const MlpJob* jobs, int njobs, int gx, int nslice, int tps, const MlpDims& D,
-                        int KS1, int slab_stride, hipStream_t st) {
+                        int KS1, int slab_stride, int fpw, hipStream_t st) {
   dim3 grid(gx, njobs, nslice), block(256);
-  size_t sh = bwd_lds_bytes(D, slab_stride);
+  const size_t sh = mlp_bwd_lds_bytes(D, slab_stride, fpw);
+  const int roff = fpw > 1 ? (int)bwd_red_off(D, slab_stride) : 0;
   if (D.wide) {
-#define SZ_CASE(PR, N, T) if (D.nl_sdf == N && tps == T) { hipLaunchKernelGGL((k_mlp_bwd_sdf<PR, 2, N, T, true>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
+#define SZ_CASE(PR, N, T) if (D.nl_sdf == N && tps == T) { hipLaunchKernelGGL((k_mlp_bwd_sdf<PR, 2, N, T, true>), grid, block, sh, st, jobs, D, slab_stride, roff); HIP_OK(hipGetLastError()); return; }
     if (D.fp32) { SZ_CASE(PrecF32, 1, 1) SZ_CASE(PrecF32, 2, 1) SZ_CASE(PrecF32, 3, 1) SZ_CASE(PrecF32, 4, 1) SZ_CASE(PrecF32, 2, 2) }
     else { SZ_CASE(PrecBF16, 1, 1) SZ_CASE(PrecBF16, 2, 1) SZ_CASE(PrecBF16, 3, 1) SZ_CASE(PrecBF16, 4, 1) SZ_CASE(PrecBF16, 2, 2) }
 #undef SZ_CASE
     dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_sdf: unsupported depth (wide)", __FILE__, __LINE__);
   }
-  const bool ok = D.fp32 ? launch_bwd_sdf_p<PrecF32>(jobs, grid, block, sh, tps, D, KS1, slab_stride, st)
-                         : launch_bwd_sdf_p<PrecBF16>(jobs, grid, block, sh, tps, D, KS1, slab_stride, st);
+  const bool ok = D.fp32 ? launch_bwd_sdf_p<PrecF32>(jobs, grid, block, sh, tps, D, KS1, slab_stride, roff, st)
+                         : launch_bwd_sdf_p<PrecBF16>(jobs, grid, block, sh, tps, D, KS1, slab_stride, roff, st);
   if (!ok) dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_sdf: unsupported depth/tiling", __FILE__, __LINE__);
 }
 
 template <class P>
 static bool launch_bwd_mom_p(const MlpJob* jobs, dim3 grid, dim3 block, size_t sh, int tps, const MlpDims& D,
-                             int KS1, int WMB, int slab_stride, hipStream_t st) {
-#define M_CASE(K, W, N) if (KS1 == K && WMB == W && D.nl_mom == N && tps == 1) { hipLaunchKernelGGL((k_mlp_bwd_mom<P, K, W, N, 1, false>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return true; }
+                             int KS1, int WMB, int slab_stride, int roff, hipStream_t st) {
+#define M_CASE(K, W, N) if (KS1 == K && WMB == W && D.nl_mom == N && tps == 1) { hipLaunchKernelGGL((k_mlp_bwd_mom<P, K, W, N, 1, false>), grid, block, sh, st, jobs, D, slab_stride, roff); HIP_OK(hipGetLastError()); return true; }
   M_CASE(2, 1, 1) M_CASE(2, 2, 1) M_CASE(2, 4, 1)
   M_CASE(2, 1, 2) M_CASE(2, 2, 2) M_CASE(2, 4, 2)
   M_CASE(2, 1, 3) M_CASE(2, 2, 3) M_CASE(2, 4, 3)
@@ -1578,11 +1667,12 @@ static bool launch_bwd_mom_p(const MlpJob* jobs, dim3 grid, dim3 block, size_t s
 }
 
 void launch_mlp_bwd_mom(const MlpJob* jobs, int njobs, int gx, int nslice, int tps, const MlpDims& D,
-                        int KS1, int WMB, int slab_stride, hipStream_t st) {
+                        int KS1, int WMB, int slab_stride, int fpw, hipStream_t st) {
   dim3 grid(gx, njobs, nslice), block(256);
-  size_t sh = bwd_lds_bytes(D, slab_stride);
+  const size_t sh = mlp_bwd_lds_bytes(D, slab_stride, fpw);
+  const int roff = fpw > 1 ? (int)bwd_red_off(D, slab_stride) : 0;
   if (D.wide) {
-#define MZ_CASE(PR, W, N) if (WMB == W && D.nl_mom == N && tps == 1) { hipLaunchKernelGGL((k_mlp_bwd_mom<PR, 2, W, N, 1, true>), grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
+#define MZ_CASE(PR, W, N) if (WMB == W && D.nl_mom == N && tps == 1) { hipLaunchKernelGGL((k_mlp_bwd_mom<PR, 2, W, N, 1, true>), grid, block, sh, st, jobs, D, slab_stride, roff); HIP_OK(hipGetLastError()); return; }
     if (D.fp32) {
       MZ_CASE(PrecF32, 1, 1) MZ_CASE(PrecF32, 2, 1) MZ_CASE(PrecF32, 4, 1)
       MZ_CASE(PrecF32, 1, 2) MZ_CASE(PrecF32, 2, 2) MZ_CASE(PrecF32, 4, 2)
@@ -1595,8 +1685,8 @@ void launch_mlp_bwd_mom(const MlpJob* jobs, int njobs, int gx, int nslice, int t
 #undef MZ_CASE
     dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_mom: unsupported depth/width (wide)", __FILE__, __LINE__);
   }
-  const bool ok = D.fp32 ? launch_bwd_mom_p<PrecF32>(jobs, grid, block, sh, tps, D, KS1, WMB, slab_stride, st)
-                         : launch_bwd_mom_p<PrecBF16>(jobs, grid, block, sh, tps, D, KS1, WMB, slab_stride, st);
+  const bool ok = D.fp32 ? launch_bwd_mom_p<PrecF32>(jobs, grid, block, sh, tps, D, KS1, WMB, slab_stride, roff, st)
+                         : launch_bwd_mom_p<PrecBF16>(jobs, grid, block, sh, tps, D, KS1, WMB, slab_stride, roff, st);
   if (!ok) dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_mom: unsupported depth/width", __FILE__, __LINE__);
 }
 

@@ -136,9 +136,9 @@ __global__ __launch_bounds__(64) void k_lstm(const RnnJob* __restrict__ jobs,
   const int lane = threadIdx.x;
   const bool act = lane < H;
   const int k = act ? lane : 0;
-  const bool drop = J.train && md->dropout > 0.f;
-  const uint32_t thr = (uint32_t)(md->dropout * 16777216.f + 0.5f);
-  const float scale = drop ? 1.f / (1.f - md->dropout) : 1.f;
+  const bool drop = J.train && J.dropout > 0.f;
+  const uint32_t thr = (uint32_t)(J.dropout * 16777216.f + 0.5f);
+  const float scale = drop ? 1.f / (1.f - J.dropout) : 1.f;
   const uint32_t step = J.step ? (uint32_t)*gp(J.step) : 0u;
   const auto params = gp(J.params);
   const auto xg = gp(J.xg);
@@ -252,9 +252,9 @@ __global__ __launch_bounds__(64) void k_lstm_gl(const RnnJob* __restrict__ jobs,
   const bool is_g = gl && L >= 2 * H && L < 3 * H;
   const float ka = is_g ? 2.f : 1.f;      // act(x) = kb * sigm(ka x) + kc
   const float kb = is_g ? 2.f : 1.f, kc = is_g ? -1.f : 0.f;
-  const bool drop = J.train && md->dropout > 0.f;
-  const uint32_t thr = (uint32_t)(md->dropout * 16777216.f + 0.5f);
-  const float scale = drop ? 1.f / (1.f - md->dropout) : 1.f;
+  const bool drop = J.train && J.dropout > 0.f;
+  const uint32_t thr = (uint32_t)(J.dropout * 16777216.f + 0.5f);
+  const float scale = drop ? 1.f / (1.f - J.dropout) : 1.f;
   const uint32_t step = J.step ? (uint32_t)*gp(J.step) : 0u;
   const auto params = gp(J.params);
   const auto xg = gp(J.xg);
@@ -462,9 +462,9 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
   if (md->nrnn == 0) return;
   const int T = J.T, M = md->M, H = md->H, G4 = 4 * H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const bool drop = md->dropout > 0.f;
-  const uint32_t thr = (uint32_t)(md->dropout * 16777216.f + 0.5f);
-  const float scale = drop ? 1.f / (1.f - md->dropout) : 1.f;
+  const bool drop = J.dropout > 0.f;
+  const uint32_t thr = (uint32_t)(J.dropout * 16777216.f + 0.5f);
+  const float scale = drop ? 1.f / (1.f - J.dropout) : 1.f;
   const uint32_t step = (uint32_t)*gp(J.drop_step);
   const auto params = gp(J.params);
   const auto grads = gp(J.grads);

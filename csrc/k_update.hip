@@ -30,18 +30,32 @@ __global__ __launch_bounds__(256) void k_finalize(const FinJob* __restrict__ job
   int b = blockIdx.x + b0;       // b0: first block of a partial launch (see launch_finalize)
   // slab sums: lane = element, the 4 waves split the slabs (each sums its quarter in order,
   // 16 independent loads in flight), then a fixed-order LDS combine
+  // (group 4: the stored slabs are fine slabs, summed in groups ((s0 + s1) + s2) + s3 first --
+  // the coarse slabs a launch with 4 fine slabs per workgroup stores; see wg_slab_finish)
   auto slab_sum = [&](const float* src) {
     const auto s0 = gp(src);
     float acc = 0.f;
+    if (J.group == 4) {
+      const int nc = J.nslab >> 2;
+#pragma unroll 4
+      for (int k = wave; k < nc; k += 4) {
+        const size_t b = (size_t)4 * k * slab_stride;
+        float c = s0[b] + s0[b + slab_stride];
+        c += s0[b + 2 * (size_t)slab_stride];
+        c += s0[b + 3 * (size_t)slab_stride];
+        acc += c;
+      }
+    } else {
 #pragma unroll 16
-    for (int k = wave; k < J.nslab; k += 4) acc += s0[(size_t)k * slab_stride];
+      for (int k = wave; k < J.nslab; k += 4) acc += s0[(size_t)k * slab_stride];
+    }
     red[wave][lane] = acc;
     __syncthreads();
     return red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
   };
   // the packed training weights of layers >= 1 and the SDF output row carry the dropout scale
   // 1/(1-p) (k_pack), so their slab sums are gradients w.r.t. the scaled weights: scale back
-  const float dscale = md->dropout > 0.f ? 1.f / (1.f - md->dropout) : 1.f;
+  const float dscale = J.dropout > 0.f ? 1.f / (1.f - J.dropout) : 1.f;
   if (b < nb_tiles) {
     const int ti = b >> 6, e = ((b & 63) << 6) + lane;
     const GradTile& G = mom ? md->tile_m[ti] : md->tile_s[ti];
@@ -255,7 +269,7 @@ __global__ __launch_bounds__(256) void k_pack(const UpdJob* __restrict__ jobs,
   // two copies: evaluation weights, then the training weights with the dropout scale 1/(1-p)
   // folded into every layer fed by dropped-out activations (the towers then apply the bare
   // keep mask; k_finalize scales those gradients back)
-  const float dscale = md->dropout > 0.f ? 1.f / (1.f - md->dropout) : 1.f;
+  const float dscale = J.dropout > 0.f ? 1.f / (1.f - J.dropout) : 1.f;
   if (e < nel) {
     const float v = pack_blob_elem(md, src, e);
     const float vt = blob_scaled(md, e >> 9) ? v * dscale : v;
@@ -308,6 +322,12 @@ void launch_pack(float* const*, const UpdJob* jobs, int njobs, const ModelDesc* 
 }
 
 // ============================================================ update ====================
+DLAP_DEV bool prog_poisoned(const int* prog) {
+  if (!prog) return false;
+  const auto p = gp(prog);
+  return (p[1] | p[16 + 1] | p[32 + 1]) != 0;
+}
+
 // Clip-by-global-norm + Adam over the phase's scope. grid (blocks, models): every block
 // reduces the full scope norm itself (fixed order -> identical in all blocks, no grid
 // barrier) and updates its own ADAM_PB-parameter range.
@@ -316,6 +336,9 @@ __global__ __launch_bounds__(256) void k_adam(const UpdJob* __restrict__ jobs,
                                               const ModelDesc* __restrict__ md, int phase, float lr) {
   const UpdJob& J = jobs[blockIdx.y];
   __shared__ float red[4];
+  // a fused forward of this model gave up a wait (its outputs are incomplete): no update, now or
+  // later (block-uniform; every launch that can bump the counters precedes this one on the stream)
+  if (prog_poisoned(J.prog)) return;
   // the train split's scalars of this step, kept for the (possibly deferred) bookkeeping
   if (blockIdx.x == 0 && J.scal && threadIdx.x < SC_NSCAL) gp(J.scal_prev)[threadIdx.x] = gp(J.scal)[threadIdx.x];
   const bool mom = phase == 2;
@@ -402,6 +425,7 @@ __global__ __launch_bounds__(EPOCH_END_THREADS) void k_epoch_end(const EpochJob*
       te[c] = ht ? gp(J.sc_test)[c] : 0.f;
     }
     const int ep = gp(J.ep)[0], ep_ph = gp(J.ep)[1];
+    const bool poisoned = prog_poisoned(J.prog);     // see k_adam: a NaN epoch, no bookkeeping
     const float gn = gp(J.gnorm)[0];
     const float best0 = gp(J.best)[0], best1 = gp(J.best)[1], best2 = gp(J.best)[2];
     // past the history capacity the row goes to a per-block scratch instead of out of bounds
@@ -423,7 +447,10 @@ __global__ __launch_bounds__(EPOCH_END_THREADS) void k_epoch_end(const EpochJob*
     r[H_TRAIN_LRES] = tr[SC_LRES];
     r[H_GNORM] = gn;
     int up_loss = 0, up_sr = 0;
-    if (hv) {
+    if (poisoned) {
+#pragma unroll
+      for (int c = 1; c < HIST_W; ++c) r[c] = __builtin_nanf("");
+    } else if (hv) {
       const float vloss = phase == 1 ? va[SC_LUNC] : va[SC_LCOND];
       r[H_VALID_LOSS] = vloss;
       r[H_VALID_SHARPE] = va[SC_SHARPE];

@@ -67,7 +67,7 @@ struct GramJob {
   double* G;             // [2][T][T] out: Gc, Gu
   int T, N, K;
 };
-int gram_slices(int T, int njobs);
+int gram_slices(int T);
 size_t gram_part_doubles(int T, int njobs);
 // all jobs of one launch share T (one split of every model)
 void launch_gram(const GramJob* jobs, int njobs, int T, int nslice, hipStream_t st);

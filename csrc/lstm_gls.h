@@ -110,9 +110,9 @@ DLAP_DEV void lstm_gls_body(const RnnJob& J, const ModelDesc* __restrict__ md, f
   const float kx = is_g ? -2.f * LOG2E : -LOG2E;
   const float kb = is_g ? 2.f * KC : 1.f, kc = is_g ? -KC : 0.f;
   const float ysave = is_g ? 1.f / KC : 1.f;      // saved gates are the unscaled activations
-  const bool drop = J.train && md->dropout > 0.f;
-  const uint32_t thr = (uint32_t)(md->dropout * 16777216.f + 0.5f);
-  const float scale = drop ? 1.f / (1.f - md->dropout) : 1.f;
+  const bool drop = J.train && J.dropout > 0.f;
+  const uint32_t thr = (uint32_t)(J.dropout * 16777216.f + 0.5f);
+  const float scale = drop ? 1.f / (1.f - J.dropout) : 1.f;
   const uint32_t step = J.step ? (uint32_t)*gp(J.step) : 0u;
   const auto params = gp(J.params);
   const bool save = J.sc != nullptr;

@@ -36,12 +36,21 @@ struct MlpJob {
   const int* prog;        // fused LSTM + tower forward (k_mlp_fwd_rnn): periods of pp published
   int* prog_err;          //   ... and the spin-timeout counter (0 unless a wait gave up)
   int prog_mode;          //   0: acquire fence after the wait; 1: cache-bypassing pp loads
+  unsigned prog_limit;    //   polls before a wait gives up (DLAP_PROG_SPIN_LIMIT; tests force 0)
   int store_mz;           // ... including the moment blocks (phase 2: the moment backward reads them)
   int R, N, T;
   unsigned seed;
+  float dropout;          // this job's model's dropout rate (batched sweep members may differ)
   int train;              // dropout active
   int do_sdf, do_mom;     // fwd: towers to evaluate
   int slab_base;          // bwd: first slab index of this job
+  int nslab;              // bwd: fine slabs per slice of this job's model -- a function of R only
+                          //   (fine slab v owns tiles v*waves + wave + k*nslab*waves), so the
+                          //   gradient summation order never depends on how many models share
+                          //   the launch
+  int fpw;                // bwd: fine slabs walked per workgroup (1: each stored; 4: a group of 4
+                          //   summed in order ((s0+s1)+s2)+s3 in LDS and stored as one coarse
+                          //   slab -- k_finalize forms the same groups from stored fine slabs)
 };
 
 // Scalars every tower kernel needs (small, passed by value).
@@ -49,7 +58,7 @@ struct MlpDims {
   int F, Dm, K, cm1;      // features, per-period cols, moments, moment layer-0 width
   int nrnn;               // >0: an LSTM feeds the per-period columns (per-row dpp needed)
   int nl_sdf, nl_mom;     // MFMA layers per tower
-  float dropout;
+  float dropout;                 // largest dropout rate of the engine's models (kernels use MlpJob::dropout)
   int s_fwd0, s_fwd, s_bwd;      // blob frag offsets: SDF layer 0, chain fwd base, chain bwd base
   int m_fwd0, m_fwd, m_bwd;      // moment tower
   int s_upp, ubpp;               // W0[:, F:F+Dm]^T fragments (ubpp blocks of 16 inputs, 2 k-steps)
@@ -93,17 +102,22 @@ void launch_mlp_fwd(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int
 // wide path, evaluation forward: layer 0 streamed from X inside the tower kernel (no z)
 void launch_mlp_fwd_zx(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int WMB, hipStream_t st,
                        bool train = false);
+// backward launches: grid (nslab / fpw, jobs, nslice) -- every job's nslab / fpw must match
 void launch_mlp_bwd_sdf(const MlpJob* jobs, int njobs, int gx, int nslice, int tps, const MlpDims& D,
-                        int KS1, int slab_stride, hipStream_t st);
+                        int KS1, int slab_stride, int fpw, hipStream_t st);
+// LDS bytes of a backward launch walking fpw fine slabs per workgroup (> 160 KiB: use fpw = 1)
+size_t mlp_bwd_lds_bytes(const MlpDims& D, int slab_stride, int fpw);
 struct RnnJob;
 struct ModelDesc;
 // fused LSTM + training tower forward; false = not instantiated for this shape (see k_mlp.hip)
 bool mlp_fwd_rnn_supported(const MlpDims& D, int KS1, int WMB, int H, int nrnn, int tmax);
+// resident workgroups of the fused kernel on the device (0: not instantiated for this shape)
+int mlp_fwd_rnn_capacity(const MlpDims& D, int KS1, int WMB, int H, int nrnn, int tmax);
 bool launch_mlp_fwd_rnn(const MlpJob* jobs, const RnnJob* rjobs, const ModelDesc* md, int njobs, int gx,
                         const MlpDims& D, int KS1, int WMB, int H, int nrnn, int tmax, hipStream_t st);
 void launch_dropmask(const MlpJob* jobs, int njobs, int ntiles, const MlpDims& D, int step_offset,
                      hipStream_t st);
 void launch_mlp_bwd_mom(const MlpJob* jobs, int njobs, int gx, int nslice, int tps, const MlpDims& D,
-                        int KS1, int WMB, int slab_stride, hipStream_t st);
+                        int KS1, int WMB, int slab_stride, int fpw, hipStream_t st);
 
 std::vector<long long> mlp_timestamps();

@@ -24,6 +24,7 @@ struct RnnJob {
                          //   k_proj zeroes [0] ahead of every launch (stream order)
   unsigned seed;
   int train;
+  float dropout;         // this model's dropout rate (LSTM inter-layer dropout, train mode)
 };
 
 // abias: also build the moment network's per-period layer-0 bias table (a tower launched after

@@ -13,7 +13,9 @@ struct FinJob {            // one model
   const float* v;          // [R][64] per-row d(moment layer-0 pre-activation)
   float* dab;              // [T][64]
   int T;
-  int nslab;               // slabs per slice
+  float dropout;           // the model's dropout rate (gradients of scaled weights are scaled back)
+  int nslab;               // slabs stored per slice
+  int group;               // 4: they are fine slabs, summed in groups of 4 first; 1: coarse slabs
 };
 
 struct UpdJob {            // one model
@@ -44,8 +46,12 @@ struct UpdJob {            // one model
   float* scal_prev;        // ... copied here by k_adam for the epoch bookkeeping
   int T;
   unsigned seed;
+  float dropout;           // the model's dropout rate (k_pack folds 1/(1-p) into the train blob)
   float lr;                // > 0: this model's learning rate (sweeps batch configs that
                            // differ only in lr); 0: the launch-wide lr
+  const int* prog;         // the model's fused-forward progress records (3 splits, 16 ints each;
+                           // [16 s + 1] = spin waits that gave up): non-zero poisons the model --
+                           // k_adam skips every later update, k_epoch_end records NaN epochs
 };
 
 // History row written per epoch by k_epoch_end (HIST_W floats).
@@ -69,6 +75,7 @@ struct EpochJob {          // one model
   float* snap_loss;        // [P]
   float* snap_sharpe;      // [P]
   int max_ep;              // rows of hist: epochs past the capacity are not recorded
+  const int* prog;         // as UpdJob::prog (a poisoned model records NaN epochs, no snapshots)
 };
 
 void launch_finalize(const FinJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,

@@ -8,35 +8,78 @@ Contract (`/root/reference/src/data_loader.py:11-237`):
     valid / test receive the train statistics;
   * ``get_full_batch`` hands out zero-copy CPU tensors.
 
-Unlike the reference, loading is memory-mapped friendly (``np.load(mmap_mode)``) so the
-scaled 600×30000×512 panels do not need two full host copies.
+Host memory: the reference keeps the raw array plus full copies of returns, features and
+their zero-filled versions (~4 panel copies). Here an uncompressed (``np.savez``) member is
+memory-mapped straight out of the archive (``_npz_member``: no read into RAM at all), and the
+mask / zero-fill run over period chunks into the one output array, so the resident cost is one
+float32 panel (plus the decompressed raw array for ``savez_compressed`` files, which cannot be
+mapped).
 """
 from __future__ import annotations
 
 from typing import Optional, Sequence
 
+import zipfile
+
 import numpy as np
 import torch
 
 MISSING_VALUE = -99.99
+_CHUNK_BYTES = 256 << 20          # period chunk of the masking pass
+
+
+def _npz_member(path: str, name: str):
+    """Array ``name`` of the ``.npz`` at ``path``: a read-only ``np.memmap`` into the archive when
+    the member is stored uncompressed (``np.savez``), else the decompressed array."""
+    with zipfile.ZipFile(path) as zf:
+        info = zf.getinfo(name + ".npy")
+        if info.compress_type == zipfile.ZIP_STORED:
+            with zf.open(info) as f:
+                version = np.lib.format.read_magic(f)
+                if version == (1, 0):
+                    shape, fortran, dtype = np.lib.format.read_array_header_1_0(f)
+                else:
+                    shape, fortran, dtype = np.lib.format.read_array_header_2_0(f)
+                header = f.tell()
+            if not dtype.hasobject:
+                with open(path, "rb") as fh:          # data offset = local header + npy header
+                    fh.seek(info.header_offset + 26)
+                    ln = int.from_bytes(fh.read(2), "little") + int.from_bytes(fh.read(2), "little")
+                start = info.header_offset + 30 + ln + header
+                return np.memmap(path, dtype=dtype, mode="r", offset=start, shape=shape,
+                                 order="F" if fortran else "C")
+    with np.load(path) as z:
+        return z[name]
 
 
 class AssetPricingDataset(torch.utils.data.Dataset):
     def __init__(self, path_individual_feature: str, path_macro_feature: Optional[str] = None,
                  macro_idx: Optional[Sequence[int]] = None, mean_macro: Optional[np.ndarray] = None,
                  std_macro: Optional[np.ndarray] = None, normalize_macro: bool = True):
-        z = np.load(path_individual_feature)
-        raw = z["data"]
-        self.dates = z["date"] if "date" in z.files else np.arange(raw.shape[0])
-        self.variable_names = z["variable"] if "variable" in z.files else None
-        ret = np.asarray(raw[:, :, 0], dtype=np.float32)
-        feat = np.asarray(raw[:, :, 1:], dtype=np.float32)
-        thr = MISSING_VALUE + 1
-        mask = (ret > thr) & ~np.isnan(ret)
-        mask &= np.all(feat > thr, axis=2)
-        self.mask = mask
-        self.returns = np.where(mask, ret, np.float32(0.0)).astype(np.float32)
-        self.individual_features = np.where(mask[:, :, None], feat, np.float32(0.0)).astype(np.float32)
+        with np.load(path_individual_feature) as z:
+            files = set(z.files)
+            self.dates = z["date"] if "date" in files else None
+            self.variable_names = z["variable"] if "variable" in files else None
+        raw = _npz_member(path_individual_feature, "data")
+        T, N, C = raw.shape
+        if self.dates is None:
+            self.dates = np.arange(T)
+        thr = np.float32(MISSING_VALUE + 1)
+        self.mask = np.empty((T, N), dtype=bool)
+        self.returns = np.empty((T, N), dtype=np.float32)
+        self.individual_features = np.empty((T, N, C - 1), dtype=np.float32)
+        step = max(1, _CHUNK_BYTES // max(1, N * C * 4))
+        for t0 in range(0, T, step):       # one period chunk in flight: mask, zero-fill, copy out
+            blk = np.asarray(raw[t0:t0 + step], dtype=np.float32)
+            ret, feat = blk[:, :, 0], blk[:, :, 1:]
+            m = (ret > thr) & ~np.isnan(ret)
+            m &= np.all(feat > thr, axis=2)
+            self.mask[t0:t0 + step] = m
+            self.returns[t0:t0 + step] = np.where(m, ret, np.float32(0.0))
+            out = self.individual_features[t0:t0 + step]
+            out[...] = feat
+            out[~m] = 0.0
+        del raw
 
         self.mean_macro = self.std_macro = None
         self.macro_features = None

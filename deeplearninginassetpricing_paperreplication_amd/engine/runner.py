@@ -9,9 +9,7 @@ final on-disk state equals the reference's "last writer wins" sequence.
 from __future__ import annotations
 
 import os
-import threading
 import time
-from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence
 
 import numpy as np
@@ -19,7 +17,6 @@ import torch
 
 from ..config import ModelSpec
 from ..ops.native import load as load_native
-from .panel import prepare_split, prepare_split_device
 
 HIST = dict(phase=0, train_loss=1, train_sharpe=2, valid_loss=3, valid_sharpe=4, test_loss=5,
             test_sharpe=6, train_loss_unc=7, train_loss_cond=8, grad_norm=9, valid_loss_unc=10,
@@ -49,32 +46,25 @@ def unflatten_state(flat: np.ndarray, spec: ModelSpec) -> Dict[str, torch.Tensor
     return out
 
 
-_PREP_CACHE: "OrderedDict[tuple, object]" = OrderedDict()
+def _on_device(x, dtype: torch.dtype, dev: torch.device) -> torch.Tensor:
+    t = x if isinstance(x, torch.Tensor) else torch.as_tensor(np.asarray(x))
+    return t.detach().to(device=dev, dtype=dtype).contiguous()
 
 
-_PREP_LOCK = threading.Lock()
+class SplitInfo:
+    """Shape of a split the engine holds (T, N, R valid rows); ``rowti`` [R, 2] is read back from
+    the device on first use (tests)."""
 
+    def __init__(self, eng, s: int, T: int, N: int, R: int):
+        self._eng, self._s = eng, s
+        self.T, self.N, self.R = T, N, R
+        self._rowti = None
 
-def _prepared(batch: Dict, KP: int, fp32: bool = False):
-    """Host compaction of a split, memoised on the identity/version of its input tensors: the
-    ensemble and sweep drivers build one engine per architecture bucket over the same panel."""
-    def tk(t):
-        return (id(t), t.data_ptr(), t._version) if isinstance(t, torch.Tensor) else (id(t),)
-    key = (KP, fp32) + tuple(tk(batch.get(k)) for k in ("individual_features", "returns", "mask", "macro_features"))
-    with _PREP_LOCK:       # drivers may build engines from several threads
-        return _prepared_locked(batch, KP, key, fp32)
-
-
-def _prepared_locked(batch: Dict, KP: int, key, fp32: bool = False):
-    hit = _PREP_CACHE.get(key)
-    if hit is None:
-        # the entry keeps the inputs alive, so their ids cannot be reused while it exists
-        hit = (prepare_split(batch, KP, fp32), [batch.get(k) for k in ("individual_features", "returns", "mask",
-                                                                   "macro_features")])
-        _PREP_CACHE[key] = hit
-        while len(_PREP_CACHE) > 6:
-            _PREP_CACHE.popitem(last=False)
-    return hit[0]
+    @property
+    def rowti(self) -> np.ndarray:
+        if self._rowti is None:
+            self._rowti = np.asarray(self._eng.read_split(self._s)["rowti"]).reshape(-1, 2)
+        return self._rowti
 
 
 class GANEngine:
@@ -103,22 +93,26 @@ class GANEngine:
 
     # ---- data -----------------------------------------------------------------------
     def set_data(self, train: Dict, valid: Optional[Dict] = None, test: Optional[Dict] = None):
+        """Upload the splits. The engine builds its compacted layout on the GPU from the dense
+        split (``Engine.set_split_dense``, k_panel.hip): CUDA tensors are read in place, host
+        arrays are copied to the device once; nothing comes back to the host but the row count."""
+        dev = torch.device("cuda", torch.cuda.current_device())
         for s, b in enumerate((train, valid, test)):
             if b is None:
                 continue
-            x = b["individual_features"]
-            if isinstance(x, torch.Tensor) and x.is_cuda:
-                # compact on the GPU, hand the engine a device pointer (no host copy of X)
-                ps = prepare_split_device(b, self.KP, fp32=self.fp32)
-                self.eng.set_split_dev(s, ps.X.data_ptr(), ps.X.numel() * (2 if self.fp32 else 1),
-                                       ps.rowti.reshape(-1), ps.row_ptr,
-                                       ps.Rm, ps.mask, ps.macro.reshape(-1), ps.T, ps.N)
-                ps.X = None                                  # the engine keeps its own copy
-            else:
-                ps = _prepared(b, self.KP, self.fp32)
-                self.eng.set_split(s, ps.X.reshape(-1), ps.rowti.reshape(-1), ps.row_ptr, ps.Rm, ps.mask,
-                                   ps.macro.reshape(-1), ps.T, ps.N)
-            self.splits[s] = ps
+            feats = _on_device(b["individual_features"], torch.float32, dev)
+            ret = _on_device(b["returns"], torch.float32, dev)
+            mask = _on_device(b["mask"], torch.bool, dev)
+            T, N, F = feats.shape
+            macro, mptr = None, 0
+            if self.spec.macro_dim > 0:
+                macro = _on_device(b["macro_features"], torch.float32, dev)
+                if tuple(macro.shape) != (T, self.spec.macro_dim):
+                    raise ValueError(f"macro_features must be [{T}, {self.spec.macro_dim}], not {tuple(macro.shape)}")
+                mptr = macro.data_ptr()
+            self.eng.set_split_dense(s, feats.data_ptr(), ret.data_ptr(), mask.data_ptr(), True, mptr,
+                                     int(T), int(N), int(F), torch.cuda.current_stream(dev).cuda_stream)
+            self.splits[s] = SplitInfo(self.eng, s, int(T), int(N), int(self.eng.split_rows(s)))
 
     # ---- parameters -----------------------------------------------------------------
     def set_model(self, g: int, model, seed: int):
@@ -141,25 +135,37 @@ class GANEngine:
     def history_rows(self, g: int) -> np.ndarray:
         return self.eng.history(g)
 
-    def evaluate(self, s: int) -> List[Dict]:
-        """Eval-mode forward of split ``s`` for every model: metrics of `src/train.py:106-153`."""
+    def evaluate(self, s: int, device_weights: bool = False) -> List[Dict]:
+        """Eval-mode forward of split ``s`` for every model: metrics of `src/train.py:106-153`.
+        ``device_weights``: the L1-normalised weights stay on the GPU (a CUDA tensor, for the
+        ensemble all-gather) instead of a host copy of every [T, N] array."""
         self.eng.forward_split(s, False, True)
         out = []
+        ps = self.splits[s]
+        dev = torch.device("cuda", torch.cuda.current_device())
         for g in range(self.G):
             sc = self.eng.read_ws(g, s, "scal")
             port = self.eng.read_ws(g, s, "port")
-            w = self.eng.read_ws(g, s, "wn")
-            ps = self.splits[s]
             lres = sc[SC["loss_res"]] * self.spec.residual_loss_factor
             sd_u = float(np.std(port, ddof=1)) if len(port) > 1 else float("nan")
             sh = 0.0 if sd_u < 1e-8 else float(np.mean(port) / sd_u)
-            l1 = np.abs(w.reshape(ps.T, ps.N)).sum(axis=1, keepdims=True)
-            wn = w.reshape(ps.T, ps.N) / np.maximum(l1, 1e-8)
+            if device_weights:
+                w = torch.empty(ps.T * ps.N, dtype=torch.float32, device=dev)
+                ts = torch.cuda.current_stream(dev).cuda_stream
+                self.eng.join_from(ts)                 # (w may reuse memory torch still reads)
+                self.eng.copy_ws(g, s, "wn", w.data_ptr())
+                self.eng.join_to(ts)
+                w = w.view(ps.T, ps.N)
+                wn = w / w.abs().sum(dim=1, keepdim=True).clamp_min(1e-8)
+            else:
+                w = self.eng.read_ws(g, s, "wn").reshape(ps.T, ps.N)
+                l1 = np.abs(w).sum(axis=1, keepdims=True)
+                wn = torch.from_numpy((w / np.maximum(l1, 1e-8)).astype(np.float32))
             out.append({
                 "loss": float(sc[SC["loss_cond"]] + lres), "loss_unc": float(sc[SC["loss_unc"]]),
                 "loss_cond": float(sc[SC["loss_cond"]]), "sharpe": sh,
                 "max_drawdown": float(sc[SC["mdd"]]), "mean_return": float(np.mean(port)),
-                "std_return": float(np.std(port)), "weights": torch.from_numpy(wn.astype(np.float32)),
+                "std_return": float(np.std(port)), "weights": wn,
                 "portfolio_returns": port,
             })
         return out
@@ -188,13 +194,14 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
                      num_epochs_unc=256, num_epochs_moment=64, num_epochs=1024, lr=1e-3,
                      print_freq=128, save_dir=None, ignore_epoch=64, seed=None,
                      precision="bf16", selection_sign=1.0, verbose=True, n_models=1,
-                     models=None, seeds=None, save_dirs=None, lrs=None, resume=False,
-                     resume_path=None, nan_policy="warn", stop_after=None):
+                     models=None, seeds=None, save_dirs=None, lrs=None, dropouts=None, resume=False,
+                     resume_path=None, nan_policy="warn", stop_after=None, final_weights_device=False):
     """GPU executor of the 3-phase schedule; with ``n_models > 1`` trains an ensemble batch.
 
     Returns ``(model, history)`` for a single model, or ``(models, histories)`` when
     ``n_models > 1`` (``models``/``seeds``/``save_dirs`` give per-member inputs; ``lrs`` gives
-    per-member learning rates, e.g. the lr axis of a hyperparameter sweep).
+    per-member learning rates, e.g. the lr axis of a hyperparameter sweep; ``dropouts`` per-member
+    dropout rates, the sweep's dropout axis -- a member trains exactly as a solo run with its rate).
 
     Fault tolerance (additions, see ``utils``):
       resume_path -- where the resume record is written at every print boundary and phase end
@@ -205,6 +212,8 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
                      checked at the print boundaries (``history['nonfinite_epoch']``);
       stop_after  -- (phase, epochs) : stop once that many epochs of that phase are done
                      (used to test interruption; the resume record is written first).
+    ``final_weights_device``: the final evaluation's L1-normalised weights stay on the GPU
+    (``engine_final_eval[s]["weights"]`` is then a CUDA tensor; the ensemble all-gathers them).
     """
     from ..models.gan import AssetPricingGAN
     from ..utils import checkpoint as ckpt
@@ -239,6 +248,8 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
             eng.set_model(g, m, seeds[g])
             if lrs is not None:
                 eng.eng.set_lr(g, float(lrs[g]))
+            if dropouts is not None:
+                eng.eng.set_dropout(g, float(dropouts[g]))
         eng.eng.sync()
     template = AssetPricingGAN(config)
     t_start = time.time()
@@ -275,12 +286,18 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
     class _Stop(Exception):
         pass
 
+    def check_fused(e):
+        if e.eng.prog_timeouts():
+            raise RuntimeError("fused LSTM + tower forward: a spin wait gave up, so the run stopped updating "
+                               "(the GPU is shared with other processes?); rerun with DLAP_RNN_OVERLAP=0")
+
     def run_phase(phase, n, title, tag):
         if phase < start[0]:
             return
         if verbose:
             print("\n" + "=" * 70 + f"\n{title}\nEpochs: {n}\n" + "=" * 70 + "\n")
         done = start[1] if phase == start[0] else 0
+        eng.eng.plan_phase(phase, n)          # dense or Gram losses for this phase (cost model)
         if done == 0:
             eng.eng.begin_phase(phase)
         ep0 = eng.eng.epoch_count(0) - done
@@ -297,11 +314,11 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
                 eng.eng.sync()
             dt = (time.time() - t0) / k
             done = mk + 1
+            # first: a fused forward that gave up a wait poisons its model on the device (no
+            # update, NaN epochs) -- report that cause, not the NaN it leaves in the history
+            check_fused(eng)
             for g in range(n_models):
                 monitor.check(g, eng.history_rows(g), raise_ok=n_models == 1)
-            if eng.eng.prog_timeouts():
-                raise RuntimeError("fused LSTM + tower forward: a spin wait gave up (the GPU is shared "
-                                   "with other processes?); rerun with DLAP_RNN_OVERLAP=0")
             write_resume(phase, done)
             if stop_after is not None and tuple(stop_after) == (phase, done):
                 raise _Stop()
@@ -332,6 +349,9 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
         run_phase(1, num_epochs_unc, "PHASE 1: Training Unconditional Loss (E[w*R]^2)", "unc")
         if start[0] <= 1:
             say("\nPhase 1 Complete!")
+            if verbose:      # the device tracker holds sel * Sharpe (`src/train.py:287`)
+                b1 = float(eng.eng.get_tracker_state(0)["best_sharpe"])
+                say(f"Best validation Sharpe (phase 1): {selection_sign * b1:.4f}")
             for g in range(n_models):
                 if best_state[g]:
                     eng.eng.load_snapshot(g, 1)
@@ -355,7 +375,8 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
     say(f"Total time: {elapsed / 60:.1f} minutes")
     say(f"Total epochs: {total} ({num_epochs_unc} + {num_epochs_moment} + {num_epochs})\n" + "=" * 70)
     with trace_range("final-eval", timers):
-        finals = {s: eng.evaluate(s) for s in eng.splits}
+        finals = {s: eng.evaluate(s, device_weights=final_weights_device) for s in eng.splits}
+    check_fused(eng)
     if verbose:
         print("\nBest Model Performance (normalized weights):")
         for s, name in ((0, "Train"), (1, "Valid"), (2, "Test ")):

@@ -104,9 +104,9 @@ def invalidate_param_cache() -> None:
     parameter objects have the same storage and autograd versions; in-place edits through
     ``p.data`` (``p.data.copy_(...)``, ``p.data.mul_(...)``) do not bump the version counter, so
     call this after them (``load_state_dict`` and optimiser steps bump it and need nothing). The
-    panel is cached on (storage address, shape, version, dtype) of its tensors, so a training loop
-    that moves the same host panel to the device every epoch reuses the upload; call this too
-    after writing new values into a panel tensor in place."""
+    panel is cached the same way (the tensor objects plus storage address, shape, version and
+    dtype: a different tensor at a recycled address is a new panel); call this too after writing
+    new values into a panel tensor in place through ``.data``."""
     for s in _CACHE.values():
         s.param_key = None
         s.data_key = None
@@ -130,6 +130,25 @@ def _tkey(t: Optional[torch.Tensor]):
     if t is None:
         return None
     return (t.data_ptr(), tuple(t.shape), t._version, str(t.dtype))
+
+
+class _PanelKey:
+    """Identity of the uploaded panel: weak references to its tensor objects plus their
+    (address, shape, version, dtype). As for the parameters (``_ParamKey``), the address alone is
+    not enough: a loop that calls ``x.cuda()`` on a new host batch every step gets the freed
+    block back at the same address with version 0."""
+
+    def __init__(self, tensors):
+        self.refs = [None if t is None else weakref.ref(t) for t in tensors]
+        self.sig = tuple(_tkey(t) for t in tensors)
+
+    def matches(self, tensors) -> bool:
+        if len(tensors) != len(self.refs):
+            return False
+        for r, t in zip(self.refs, tensors):
+            if (r is None) != (t is None) or (r is not None and r() is not t):
+                return False
+        return self.sig == tuple(_tkey(t) for t in tensors)
 
 
 def _ordered_params(model) -> List[torch.Tensor]:
@@ -165,14 +184,14 @@ def _prepare(model, spec: ModelSpec, params: List[torch.Tensor], flat_fn, macro,
     s = _slot(sp)
     dev = individual.device
     torch.cuda.set_device(dev)
-    key = (_tkey(macro), _tkey(individual), _tkey(returns), _tkey(mask))
-    if key != s.data_key:
+    panel = (macro, individual, returns, mask)
+    if s.data_key is None or not s.data_key.matches(panel):
         batch = {"individual_features": individual.detach(), "returns": returns.detach(),
                  "mask": mask.detach()}
         if macro is not None and spec.macro_dim > 0:
             batch["macro_features"] = macro.detach()
         s.eng.set_data(batch)
-        s.data_key = key
+        s.data_key = _PanelKey(panel)
         s.T, s.N = int(mask.shape[0]), int(mask.shape[1])
         mflat = mask.detach().reshape(-1).bool()
         s.idx = mflat.nonzero().reshape(-1)              # (one sync per new panel)

@@ -181,15 +181,29 @@ def broadcast_arrays(d: Dist, arrays: Optional[dict], src: int = 0, as_tensors: 
 
 
 def broadcast_batches(d: Dist, batches: Optional[dict], src: int = 0) -> dict:
-    """Split dicts ``{split: {key: array/tensor}}`` read on ``src`` only, delivered to every
-    rank as tensors on its collective device (one RCCL broadcast per array over xGMI)."""
-    flat = None
+    """Split dicts ``{split: {key: array/tensor}}`` held on ``src`` only, delivered to every
+    rank as tensors on its collective device: one metadata broadcast, then one RCCL broadcast
+    per array over xGMI. A tensor already on ``src``'s collective device (a panel generated or
+    loaded on its GPU) is broadcast in place -- no host round trip on any rank."""
+    if not d.active:
+        return batches
+    meta = [None]
     if d.rank == src:
-        flat = {f"{sp}/{k}": (v.cpu().numpy() if isinstance(v, torch.Tensor) else np.asarray(v))
-                for sp, b in batches.items() for k, v in b.items() if v is not None}
-    got = broadcast_arrays(d, flat, src, as_tensors=True)
+        meta = [{f"{sp}/{k}": (tuple(v.shape), str(v.dtype).replace("torch.", "") if isinstance(v, torch.Tensor)
+                               else str(np.asarray(v).dtype))
+                 for sp, b in batches.items() for k, v in b.items() if v is not None}]
+    tdist.broadcast_object_list(meta, src=src)
+    dev = d.comm_device()
     out: dict = {}
-    for key, t in got.items():
+    for key, (shape, dt) in meta[0].items():
         sp, k = key.split("/", 1)
+        if d.rank == src:
+            v = batches[sp][k]
+            t = v if isinstance(v, torch.Tensor) else torch.from_numpy(np.ascontiguousarray(v))
+            t = t.to(dev).contiguous()
+        else:
+            tdt = getattr(torch, dt) if hasattr(torch, dt) else torch.from_numpy(np.empty(0, np.dtype(dt))).dtype
+            t = torch.empty(shape, dtype=tdt, device=dev)
+        tdist.broadcast(t, src=src)
         out.setdefault(sp, {})[k] = t
     return out

@@ -78,7 +78,7 @@ def train_members(config: Dict, batches: Dict[str, Dict], seeds: Sequence[int], 
                 config, tr, va, te, device=device, num_epochs_unc=n1, num_epochs_moment=n2,
                 num_epochs=n3, lr=lr, print_freq=print_freq, ignore_epoch=ignore_epoch,
                 selection_sign=selection_sign, verbose=verbose, models=models,
-                seeds=[seeds[i] for i in todo], save_dirs=[dirs[i] for i in todo])
+                seeds=[seeds[i] for i in todo], save_dirs=[dirs[i] for i in todo], final_weights_device=True)
             if len(todo) == 1:
                 res_m, res_h = [res_m], [res_h]
             tm = dict(train_3phase_gpu.last_timers.total)
@@ -87,8 +87,9 @@ def train_members(config: Dict, batches: Dict[str, Dict], seeds: Sequence[int], 
                 recs[i]["timing"] = tm
             for k, i in enumerate(todo):
                 fe = res_m[k].engine_final_eval
+                # (CUDA tensors: the members' weights never leave the GPU before the all-gather)
                 recs[i].update(ok=True, history=res_h[k],
-                               weights={sp: fe[j]["weights"].numpy() for j, sp in enumerate(SPLITS)})
+                               weights={sp: fe[j]["weights"] for j, sp in enumerate(SPLITS)})
                 if dirs[i]:
                     save_history(res_h[k], dirs[i])
         except Exception as e:          # whole batch failed (e.g. OOM): isolate, do not hang peers
@@ -145,7 +146,7 @@ def run_ensemble(config: Dict, batches: Dict[str, Dict], seeds: Sequence[int] = 
             loc_t = torch.full((len(recs), T, N), float("nan"), dtype=torch.float32, device=d.device)
             for k, r in enumerate(recs):
                 if r["ok"]:
-                    loc_t[k].copy_(torch.from_numpy(r["weights"][sp]), non_blocking=True)
+                    loc_t[k].copy_(torch.as_tensor(r["weights"][sp]), non_blocking=True)
             allt = comm.all_gather_rows_tensor(d, loc_t, len(seeds), mine)
             wdev[sp] = allt.to(d.device)    # (a gloo rehearsal gathers on the host)
             continue

@@ -19,10 +19,10 @@ CHU only for the hidden layer. Which mapping the paper's code used is parity-unp
 num_moments, with SMV doubling it to 384): HL {2,3,4} x LR {4 values} x dropout {0, 0.05, 0.1,
 0.2} x moments {4, 8, 16, 32} x SMV {4, 8}, no conditional hidden layer.
 
-Execution: configurations that build the same network form a *bucket* (LR and the no-op CSMV
-vary inside it); a bucket is trained as ONE batched native-engine run, one member per config
-(per-member learning rates, ``Engine.set_lr``), so the paper grid's 384 configs are 48 engine
-runs. Buckets are assigned to ranks longest-processing-time first (``comm.assign_lpt``) by
+Execution: configurations that build the same network form a *bucket* (LR, dropout and the
+no-op CSMV vary inside it); a bucket is trained as ONE batched native-engine run, one member per
+config (per-member learning rates and dropout rates, ``Engine.set_lr`` / ``Engine.set_dropout``),
+so the paper grid's 384 configs are 48 engine runs and the baseline grid's 24 runs of 16. Buckets are assigned to ranks longest-processing-time first (``comm.assign_lpt``) by
 ``bucket_cost``: the measured per-epoch time of that architecture's 8-member engine on the
 600 x 3000 panel (``sweep_costs.json``, written by ``tools/sweep_costs.py`` on an MI355X) or,
 for architectures it does not list, an analytic estimate. A bucket that raises marks its
@@ -33,6 +33,7 @@ validation Sharpe of the paper-sign SDF factor by default). Per-rank wall-clocks
 from __future__ import annotations
 
 import argparse
+import dataclasses
 import itertools
 import json
 import os
@@ -120,13 +121,14 @@ def bucket_cost(spec: ModelSpec, members: int = 8, table: Optional[Dict[str, flo
 def buckets(entries: Sequence[Tuple[Dict, float, Dict]]) -> List[List[int]]:
     """Group config indices that build the same network (one batched engine run each).
 
-    The key is the ``ModelSpec`` the config produces, so configs that differ only in lr or in
-    keys the model ignores -- CSMV (``num_units_rnn_moment``) is such a no-op in the reference
+    The key is the ``ModelSpec`` the config produces without its dropout rate, so configs that
+    differ only in lr, in dropout (a per-member rate of the batched engine) or in keys the model
+    ignores -- CSMV (``num_units_rnn_moment``) is such a no-op in the reference
     (`/root/reference/src/model.py:309-311`) -- share a bucket: the paper grid's 384 configs
-    are 48 architectures x 8 members."""
+    are 48 architectures x 8 members, the baseline grid's 24 x 16."""
     groups: Dict[object, List[int]] = {}
     for i, (cfg, _, _) in enumerate(entries):
-        groups.setdefault(ModelSpec.from_config(cfg), []).append(i)
+        groups.setdefault(dataclasses.replace(ModelSpec.from_config(cfg), dropout=0.0), []).append(i)
     return list(groups.values())
 
 
@@ -143,6 +145,7 @@ def run_bucket(entries, idx: List[int], batches: Dict[str, Dict], device: torch.
     out[:, 0] = 0.0
     cfg = entries[idx[0]][0]
     lrs = [entries[i][1] for i in idx]
+    drops = [float(entries[i][0].get("dropout", 0.05)) for i in idx]
     t0 = time.time()
     n1, n2, n3 = epochs
     tr, va, te = (batches[s] for s in SPLITS)
@@ -153,7 +156,7 @@ def run_bucket(entries, idx: List[int], batches: Dict[str, Dict], device: torch.
         ms, hs = train_3phase_gpu(cfg, tr, va, te, device=device, num_epochs_unc=n1, num_epochs_moment=n2,
                                   num_epochs=n3, lr=lrs[0], print_freq=10 ** 9, ignore_epoch=ignore_epoch,
                                   selection_sign=selection_sign, verbose=False, models=models,
-                                  seeds=[seed + 17 * k for k in range(len(idx))], lrs=lrs)
+                                  seeds=[seed + 17 * k for k in range(len(idx))], lrs=lrs, dropouts=drops)
         if len(idx) == 1:
             ms = [ms]
         tm = dict(train_3phase_gpu.last_timers.total)
@@ -166,7 +169,7 @@ def run_bucket(entries, idx: List[int], batches: Dict[str, Dict], device: torch.
         from ..train.trainer import evaluate, train_3phase
         for k, lr in enumerate(lrs):
             torch.manual_seed(seed)
-            model, _ = train_3phase(cfg, tr, va, te, device=torch.device("cpu"), num_epochs_unc=n1,
+            model, _ = train_3phase(entries[idx[k]][0], tr, va, te, device=torch.device("cpu"), num_epochs_unc=n1,
                                     num_epochs_moment=n2, num_epochs=n3, lr=lr, print_freq=10 ** 9,
                                     ignore_epoch=ignore_epoch, selection_sign=selection_sign, verbose=False)
             ev = [evaluate(model, b, "cpu") for b in (tr, va, te)]

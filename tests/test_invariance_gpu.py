@@ -1,0 +1,175 @@
+"""Batching / sharding invariance and the fused forward's safety guarantees on a real MI355X.
+
+* A member's trajectory is a function of its seed and hyperparameters only: the same seed trained
+  alone or batched with 1, 2 or 8 other models (at any position) gives bitwise-identical
+  parameters, history and snapshots (the backward's fine-slab partition and the
+  Gram split-K partition depend on R / T only). The reference's ensemble is defined by its seeds
+  (`/root/reference/src/evaluate_ensemble.py:112-157`), so the same 9 seeds must give the same
+  ensemble on 1, 2, 4 or 8 GPUs.
+* Per-member dropout: a batched member with rate p equals a solo engine built with p
+  (`/root/reference/src/model.py:314`; BASELINE config 4's dropout axis).
+* The fused LSTM + tower launch only runs when its whole grid is co-resident (occupancy query),
+  and a wait that gives up poisons the model on the device: no update, NaN epochs, the host raises.
+
+Panel: the bench size (T = 240 / 60 / 300, N = 3000, F = 46, M = 178), large enough that no grid
+cap of the engine binds (256 fine slabs per model)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from deeplearninginassetpricing_paperreplication_amd.config import default_cli_config
+from deeplearninginassetpricing_paperreplication_amd.models.gan import AssetPricingGAN
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PHASES = ((1, 5), (2, 3), (3, 5))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from deeplearninginassetpricing_paperreplication_amd.ops import native
+    native.load(required=True)
+
+
+@pytest.fixture(scope="module")
+def big():
+    sys.path.insert(0, ROOT)
+    from bench import make_panel
+    tr, va, te = make_panel(seed=3, device="cuda", keep_on_device=True)
+    return tr, va, te
+
+
+def _train(data, cfg, seeds, G, phases=PHASES, dropouts=None, pipeline=True):
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import GANEngine
+    eng = GANEngine(AssetPricingGAN(cfg).spec, G, max_epochs=64)
+    eng.set_data(*data)
+    eng.eng.set_pipeline(pipeline)
+    for g in range(G):
+        torch.manual_seed(1000 + seeds[g])             # init weights follow the seed, not the slot
+        eng.set_model(g, AssetPricingGAN(cfg), seeds[g])
+        if dropouts is not None:
+            eng.eng.set_dropout(g, dropouts[g])
+    for ph, n in phases:
+        eng.eng.begin_phase(ph)
+        eng.run(ph, n, 1e-3, 1, 1.0, True)
+    eng.eng.sync()
+    assert eng.eng.prog_timeouts() == 0
+    out = {seeds[g]: (eng.params(g), np.nan_to_num(eng.history_rows(g), nan=-7.0), eng.params(g, "sharpe"),
+                      eng.params(g, "loss")) for g in range(G)}
+    return eng, out
+
+
+def _same(a, b):
+    for x, y in zip(a, b):
+        np.testing.assert_array_equal(x, y)
+
+
+def test_member_is_bitwise_independent_of_batch_size_and_position(big):
+    cfg = default_cli_config(178, 46)
+    _, solo = _train(big, cfg, [123], 1)
+    layouts = {2: [7, 123], 3: [7, 8, 123], 9: [0, 1, 2, 3, 123, 5, 6, 7, 8]}
+    for G, seeds in layouts.items():
+        eng, res = _train(big, cfg, seeds, G)
+        _same(solo[123], res[123])
+        info = eng.eng.fused_info()
+        for ph in (1, 3):            # a fused launch never asks for more than is resident at once
+            gx = info[f"train_gx_p{ph}"]
+            assert gx == 0 or (1 + gx) * G <= info["cap_train"], info
+        del eng
+
+
+def test_nine_seeds_same_members_on_any_sharding(big):
+    """The 9-seed ensemble split 9 / 5+4 / 3+2+2+2 over engines (what 1, 2 or 4 ranks run):
+    identical member trajectories."""
+    cfg = default_cli_config(178, 46)
+    seeds = list(range(9))
+    _, whole = _train(big, cfg, seeds, 9)
+    for parts in ((seeds[:5], seeds[5:]), (seeds[:3], seeds[3:5], seeds[5:7], seeds[7:])):
+        for p in parts:
+            _, res = _train(big, cfg, p, len(p))
+            for s in p:
+                _same(whole[s], res[s])
+
+
+def test_per_member_dropout_equals_solo_engines(big):
+    rates = [0.0, 0.05, 0.2]
+    seeds = [31, 32, 33]
+    cfg = default_cli_config(178, 46, dropout=0.05)
+    eng, res = _train(big, cfg, seeds, 3, dropouts=rates)
+    assert [eng.eng.get_dropout(g) for g in range(3)] == pytest.approx(rates)
+    for s, p in zip(seeds, rates):
+        _, solo = _train(big, default_cli_config(178, 46, dropout=p), [s], 1)
+        _same(solo[s], res[s])
+    # the rates matter: the 0.2 member differs from the same seed at 0.05
+    _, other = _train(big, cfg, [33], 1)
+    assert not np.array_equal(other[33][0], res[33][0])
+
+
+def test_fused_forward_capped_grid_equals_two_launches(big, monkeypatch):
+    """A co-residency capacity smaller than the tuned grid caps the fused launch (bitwise the
+    same results: the forward is per row); below a minimum grid the engine uses two launches."""
+    cfg = default_cli_config(178, 46)
+    monkeypatch.setenv("DLAP_RNN_OVERLAP", "0")
+    _, ref = _train(big, cfg, [5, 6], 2)
+    monkeypatch.setenv("DLAP_RNN_OVERLAP", "1")
+    monkeypatch.setenv("DLAP_FUSED_CAP", "80")           # 2 jobs x (1 + 39)
+    eng, res = _train(big, cfg, [5, 6], 2)
+    info = eng.eng.fused_info()
+    assert info["train_gx_p1"] == 39 and info["train_gx_p3"] == 39, info
+    for s in (5, 6):
+        _same(ref[s], res[s])
+    monkeypatch.setenv("DLAP_FUSED_CAP", "20")           # 2 x (1 + 9): below the minimum grid
+    eng, _ = _train(big, cfg, [5, 6], 2, phases=())
+    assert not eng.eng.fused_forward(1) and not eng.eng.fused_forward(3)
+
+
+def test_fused_phase2_under_the_guarantee_equals_two_launches(big, monkeypatch):
+    """Phase 2's fused forward (opt-in, DLAP_FUSED_PHASE2=1) runs on the capped grid and gives the
+    same bits as the two-launch path."""
+    cfg = default_cli_config(178, 46)
+    _, ref = _train(big, cfg, [9], 1)
+    monkeypatch.setenv("DLAP_FUSED_PHASE2", "1")
+    eng, res = _train(big, cfg, [9], 1)
+    assert eng.eng.fused_forward(2)
+    gx = eng.eng.fused_info()["train_gx_p2"]
+    assert 0 < gx and 1 + gx <= eng.eng.fused_info()["cap_train"]
+    _same(ref[9], res[9])
+
+
+def test_fused_wait_give_up_poisons_the_model(monkeypatch):
+    """Force every fused wait to give up (spin limit 0): the launch writes nothing, the model is
+    never updated (parameters bit-identical to the initial ones), every epoch is recorded as NaN
+    with no snapshot taken, and the GPU trainer raises at its next synchronisation."""
+    from deeplearninginassetpricing_paperreplication_amd.data.synthetic import generate_panel_fast
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import GANEngine, train_3phase_gpu
+    ret, feats, mask, mac = generate_panel_fast(96, 600, 46, 8, seed=1)
+    mac = (mac - mac.mean(0)) / (mac.std(0, unbiased=False) + 1e-8)
+    b = {"returns": ret, "individual_features": feats, "mask": mask, "macro_features": mac}
+    cfg = default_cli_config(8, 46)
+    monkeypatch.setenv("DLAP_PROG_SPIN_LIMIT", "0")
+    torch.manual_seed(0)
+    eng = GANEngine(AssetPricingGAN(cfg).spec, 1, max_epochs=16)
+    eng.set_data(b, b, b)
+    eng.set_model(0, AssetPricingGAN(cfg), 3)
+    assert eng.eng.fused_forward(1)
+    p0 = eng.params(0).copy()
+    eng.eng.begin_phase(1)
+    eng.run(1, 4, 1e-3, 0, 1.0, True)
+    eng.eng.sync()
+    assert eng.eng.prog_timeouts() > 0
+    np.testing.assert_array_equal(eng.params(0), p0)
+    h = eng.history_rows(0)
+    # every metric NaN, no best-model flag (columns 21, 22) raised
+    assert h.shape[0] == 4 and np.isnan(h[:, 1:21]).all() and (h[:, 21:23] == 0).all()
+    assert list(eng.eng.snap_flags(0)) == [0, 0]
+    eng.eng.reset_prog_errors()
+    assert eng.eng.prog_timeouts() == 0
+    with pytest.raises(RuntimeError, match="spin wait gave up"):
+        train_3phase_gpu(cfg, b, b, b, num_epochs_unc=4, num_epochs_moment=1, num_epochs=2, print_freq=2,
+                         ignore_epoch=0, verbose=False, seed=3)

@@ -157,6 +157,18 @@ def test_paper_grid_is_384_configs_in_48_buckets():
     assert {len(b) for b in buckets(e)} == {8}
 
 
+def test_baseline_grid_is_384_configs_in_24_buckets_of_16():
+    """BASELINE config 4's literal axes (hidden_dim x lr x dropout x moments, x SMV): dropout is a
+    per-member rate of the batched engine (``Engine.set_dropout``), so it varies inside a bucket
+    like lr -- 3 HL x 2 SMV x 4 K architectures of 4 lr x 4 dropout members."""
+    from deeplearninginassetpricing_paperreplication_amd.parallel.sweep import baseline_grid, buckets
+    e = baseline_grid(178, 46)
+    bks = buckets(e)
+    assert len(e) == 384 and len(bks) == 24 and {len(b) for b in bks} == {16}
+    for b in bks:
+        assert len({(e[i][1], e[i][0]["dropout"]) for i in b}) == 16
+
+
 def test_rank0_load_and_broadcast_equals_local_loading(tmp_path):
     (tmp_path / "a").mkdir()
     (tmp_path / "b").mkdir()
