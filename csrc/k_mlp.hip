@@ -1088,9 +1088,12 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
     RowInfo ri;
     if constexpr (ZIN) ri = finish_ztile<1>(J, tile, zcur);
     else ri = finish_tile<P, KS1>(J, D, tile, cur, xf, spp);
+    // SDF backward launches always read pre-generated keep words (k_dropmask runs ahead of every
+    // phase-1/3 step that trains with dropout), so no hash path is compiled into the tile loop
+    DLAP_ASSERT(pre || !dc.on);
     uint32_t kw[NL];
 #pragma unroll
-    for (int j = 0; j < NL; ++j) kw[j] = (pre || !dc.on) ? kw_cur[j] : hash_keep<4>(dc, j, ri);
+    for (int j = 0; j < NL; ++j) kw[j] = kw_cur[j];
     // ---- forward recompute: packed activations of every hidden layer ----
     Frag act[NL][2][2];
     f32x4 a[2][4];

@@ -156,7 +156,8 @@ def run_bucket(entries, idx: List[int], batches: Dict[str, Dict], device: torch.
         ms, hs = train_3phase_gpu(cfg, tr, va, te, device=device, num_epochs_unc=n1, num_epochs_moment=n2,
                                   num_epochs=n3, lr=lrs[0], print_freq=10 ** 9, ignore_epoch=ignore_epoch,
                                   selection_sign=selection_sign, verbose=False, models=models,
-                                  seeds=[seed + 17 * k for k in range(len(idx))], lrs=lrs, dropouts=drops)
+                                  seeds=[seed + 17 * k for k in range(len(idx))], lrs=lrs, dropouts=drops,
+                                  final_weights_device=True)      # (metrics only: no [T, N] host copies)
         if len(idx) == 1:
             ms = [ms]
         tm = dict(train_3phase_gpu.last_timers.total)

@@ -439,10 +439,17 @@ def train_epoch(model: XSectionGAN, optimizer, data: Dict, device, phase: str = 
             off += g.numel()
     gn = torch.nn.utils.clip_grad_norm_(params, max_norm=grad_clip)
     optimizer.step()
-    return {"loss": out["loss"].item(), "loss_unc": out["loss_unconditional"].item(),
-            "loss_cond": out["loss_conditional"].item(), "loss_residual": out["loss_residual"].item(),
-            "sharpe": compute_sharpe(out["portfolio_returns"].detach()),
-            "grad_norm": gn.item() if isinstance(gn, torch.Tensor) else gn}
+    # the six scalars in ONE device-to-host read (the reference: six .item() syncs)
+    dev = out["loss"].device
+    p = out["portfolio_returns"].detach().float()
+    sd = p.std()
+    sharpe = torch.where(sd < 1e-8, torch.zeros_like(sd), p.mean() / sd)
+    v = torch.stack([out["loss"].detach().float().reshape(()), out["loss_unconditional"].detach().float().reshape(()),
+                     out["loss_conditional"].detach().float().reshape(()),
+                     out["loss_residual"].detach().float().reshape(()), sharpe,
+                     torch.as_tensor(gn, device=dev).detach().float().reshape(())]).tolist()
+    return {"loss": v[0], "loss_unc": v[1], "loss_cond": v[2], "loss_residual": v[3], "sharpe": v[4],
+            "grad_norm": v[5]}
 
 
 @torch.no_grad()
@@ -453,12 +460,16 @@ def evaluate(model: XSectionGAN, data: Dict, device, normalized: bool = True) ->
     macro, x, r, m = _args(data, device)
     w, _ = model.get_weights(macro, x, m, normalized=normalized)
     pr = all_reduce_sum((w * r * m.float()).sum(1), model.dist)
-    port = pr.cpu().numpy()
     out = model(macro, x, r, m, phase="conditional", n_total=data.get("n_total"))
-    return {"loss": out["loss"].item(), "loss_unc": out["loss_unconditional"].item(),
-            "loss_cond": out["loss_conditional"].item(), "sharpe": compute_sharpe(pr.cpu()),
+    # portfolio returns and the three losses in ONE device-to-host read
+    v = torch.cat([pr.float(), torch.stack([out["loss"].float().reshape(()),
+                                            out["loss_unconditional"].float().reshape(()),
+                                            out["loss_conditional"].float().reshape(())])]).cpu()
+    port = v[:-3].numpy()
+    loss, loss_unc, loss_cond = (float(x) for x in v[-3:])
+    return {"loss": loss, "loss_unc": loss_unc, "loss_cond": loss_cond, "sharpe": compute_sharpe(v[:-3]),
             "max_drawdown": compute_max_drawdown(port), "mean_return": port.mean(),
-            "std_return": port.std(), "weights": w.cpu()}
+            "std_return": port.std(), "weights": w}      # (the rank's stocks, on its device)
 
 
 def train_3phase_xsection(config: Dict, train_data: Dict, valid_data: Dict, test_data: Optional[Dict],
