@@ -253,6 +253,7 @@ class Engine {
     rnn_overlap_eval_ = env_int("DLAP_RNN_OVERLAP_EVAL", 0) != 0;
     prog_mode_ = env_int("DLAP_PROG_MODE", 1);
     prog_limit_ = (unsigned)env_int("DLAP_PROG_SPIN_LIMIT", 1 << 22);
+    graph_copies_ = env_int("DLAP_GRAPH_COPIES", 1);
     fused_p2_ = env_int("DLAP_FUSED_PHASE2", 0) != 0;
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
                residual, fp32);
@@ -666,23 +667,32 @@ class Engine {
       for (int e = 0; e < n; ++e) enqueue_epoch(phase, lr, ignore_epoch, sel);
       return;
     }
+    // DLAP_GRAPH_COPIES: several executors of the same epoch graph, launched in turn. Every
+    // hipGraphLaunch of these multi-branch graphs blocks the host ~one epoch (HIP API trace,
+    // profiles/r4_hostgaps_short.txt); alternating executors did not remove that (the wait is
+    // not per executor) and measured 2-3% slower, so the default is one.
+    const int C = std::max(1, std::min(8, graph_copies_));
     if (!pipe) {
-      hipGraphExec_t g = graph_for(graph_key(phase, lr, ignore_epoch, sel, 0),
-                                   [&] { enqueue_epoch(phase, lr, ignore_epoch, sel); });
-      for (int e = 0; e < n; ++e) HIP_OK(hipGraphLaunch(g, st_));
+      std::vector<hipGraphExec_t> gs;
+      for (int c = 0; c < C; ++c)            // (all C always: a later run never captures)
+        gs.push_back(graph_for(graph_key(phase, lr, ignore_epoch, sel, 200 + c),
+                               [&] { enqueue_epoch(phase, lr, ignore_epoch, sel); }));
+      for (int e = 0; e < n; ++e) HIP_OK(hipGraphLaunch(gs[e % gs.size()], st_));
       return;
     }
     hipGraphExec_t head = graph_for(graph_key(phase, lr, ignore_epoch, sel, 1), [&] { enqueue_head(phase, lr); });
-    hipGraphExec_t body = graph_for(graph_key(phase, lr, ignore_epoch, sel, 2),
-                                    [&] { enqueue_pipe(phase, lr, ignore_epoch, sel); });
+    std::vector<hipGraphExec_t> bodies;
+    for (int c = 0; c < C; ++c)
+      bodies.push_back(graph_for(graph_key(phase, lr, ignore_epoch, sel, c ? 300 + c : 2),
+                                 [&] { enqueue_pipe(phase, lr, ignore_epoch, sel); }));
     hipGraphExec_t tail = graph_for(graph_key(phase, lr, ignore_epoch, sel, 3),
                                     [&] { enqueue_tail(phase, ignore_epoch, sel); });
     // U pipelined epochs per graph launch: no launch gap between the epochs of one graph
     const int U = unroll_;
     hipGraphExec_t bodyU = nullptr;
-    if (U > 1 && n - 1 >= U)
-      bodyU = graph_for(graph_key(phase, lr, ignore_epoch, sel, 100 + U), [&] {
-        for (int u = 0; u < U; ++u) enqueue_pipe(phase, lr, ignore_epoch, sel);
+    if (U > 1)                            // (captured even when this run is short: a later run
+      bodyU = graph_for(graph_key(phase, lr, ignore_epoch, sel, 100 + U), [&] {   // never captures
+        for (int u = 0; u < U; ++u) enqueue_pipe(phase, lr, ignore_epoch, sel);  // inside a timed run)
       });
     HTRACE("launch head");
     HIP_OK(hipGraphLaunch(head, st_));
@@ -690,7 +700,7 @@ class Engine {
     int e = 1;
     if (bodyU)
       for (; e + U <= n; e += U) HIP_OK(hipGraphLaunch(bodyU, st_));
-    for (; e < n; ++e) HIP_OK(hipGraphLaunch(body, st_));
+    for (int k = 0; e < n; ++e, ++k) HIP_OK(hipGraphLaunch(bodies[k % bodies.size()], st_));
     HTRACE("launch tail");
     HIP_OK(hipGraphLaunch(tail, st_));
     HTRACE("run_epochs done");
@@ -762,10 +772,11 @@ class Engine {
       launch_mlp_fwd_zx(as<MlpJob>(j_mlp_train_[phase]), G_, std::max(1, zx_gx_ / G_), md_.md, md_.WMB, st_, true);
     else if (fused)
       launch_mlp_fwd_rnn(as<MlpJob>(j_mlp_train_[phase]), as<RnnJob>(j_rnn_train_), dd(), G_,
-                         fused_train_gx(phase), md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, D.T, st_);
+                         fused_train_gx(phase), md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, D.T, st_,
+                         !train_mom(phase));
     else
       launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, phase == 2 ? gx_fwd_[0] : gx_fwd13_, md_.md, md_.KS1,
-                     md_.WMB, st_);
+                     md_.WMB, st_, !train_mom(phase));
     for (int g = 0; g < G_; ++g) {
       ModelSplitWS& W = ws(g, 0);
       if (phase == 2 && dh) {
@@ -1034,6 +1045,7 @@ class Engine {
   int prog_mode_ = 1;                        // DLAP_PROG_MODE (see MlpJob::prog_mode)
   unsigned prog_limit_ = 1u << 22;           // DLAP_PROG_SPIN_LIMIT (see MlpJob::prog_limit)
   bool fused_p2_ = false;                    // DLAP_FUSED_PHASE2: fused training forward in phase 2 too
+  int graph_copies_ = 1;                     // executors per epoch graph, launched in turn (run_epochs)
   DevBuf<int> prog_;
   // Co-residency guarantee of the fused LSTM + tower launches: resident workgroups of the fused
   // kernel on the device (occupancy query, rebuild_jobs) for the train split / the evaluation
@@ -1085,6 +1097,10 @@ class Engine {
     d["cap_train"] = cap_train_; d["cap_eval"] = cap_eval_;
     for (int ph = 1; ph <= 3; ++ph) d[("train_gx_p" + std::to_string(ph)).c_str()] = fused_fwd(ph) ? fused_train_gx(ph) : 0;
     d["eval_gx_solo"] = fused_grid(eval_grid(), n_eval_jobs_, cap_eval_);
+    // backward launch shape: fine slabs per model (R-only partition), fine slabs per workgroup
+    d["bwd_nfine"] = nfine_; d["bwd_fpw"] = fpw_;
+    d["bwd_lds_fpw1"] = (long)mlp_bwd_lds_bytes(md_.md, slab_stride(), 1);
+    d["bwd_lds_fpw4"] = (long)mlp_bwd_lds_bytes(md_.md, slab_stride(), 4);
     return d;
   }
   // spin waits of the fused forward that gave up (0 unless the dispatch-order argument failed)
@@ -1265,10 +1281,11 @@ class Engine {
     for (int j = 1; j < d.nl_s; ++j, ++t)
       d.tile_s[t] = GradTile{d.s[j].w_off, d.s[j].ld, 0, d.s[j].out, d.s[j].in, 0, t, j, 0};
     d.ntile_s = t;
-    // two gradient tiles per slice share one forward recompute (fits the 512-register
-    // budget of a single wave per SIMD); DLAP_TPS=1 forces one tile per slice
+    // one gradient tile per slice (the slices recompute the forward each, but the kernel fits
+    // two waves per SIMD: DLAP_BWD1_WPS) measured faster than two tiles sharing one recompute at
+    // one wave per SIMD (profiles/r4_bwd_shape.log); DLAP_TPS=2 selects the latter
     const char* tps_env = std::getenv("DLAP_TPS");
-    const bool tps2 = (wide || d.KS1 == 2) && d.ntile_s == 2 && !(tps_env && std::atoi(tps_env) == 1);
+    const bool tps2 = (wide || d.KS1 == 2) && d.ntile_s == 2 && tps_env && std::atoi(tps_env) == 2;
     d.tps_s = tps2 ? 2 : 1;
     // at least one slice: slice 0 also produces the bias / output / per-period gradients
     d.nslice_s = std::max(1, (d.ntile_s + d.tps_s - 1) / d.tps_s);
@@ -1557,11 +1574,14 @@ class Engine {
     fwd_tables_.clear();
     j_mlp_bwd_dh_.free();
     {   // backward launch shape over the fixed fine-slab partition: one workgroup per fine slab
-        // for one or two models (the tuned single-model grid), four fine slabs per workgroup
-        // from three models on (about the round-3 per-model grids: fewer weight stagings and
-        // a quarter of the slabs for k_finalize), if the coarse accumulator fits in LDS
-      const int want = env_int("DLAP_BWD_FPW", G_ >= 3 ? 4 : 1);
-      fpw_ = (want == 4 && mlp_bwd_lds_bytes(md_.md, slab_stride(), 4) <= 160 * 1024) ? 4 : 1;
+        // (the compile-time one-slab kernel). DLAP_BWD_FPW=4 walks four fine slabs per
+        // workgroup (weights staged once, fine + coarse LDS images, a quarter of the slabs for
+        // k_finalize) if the images fit without losing a workgroup per CU -- measured slower at
+        // G = 3 and 9 (the runtime slab loop spills more and every fine slab still pays its
+        // reduction: 10.58k vs 10.72k model-epochs/s at G = 9, profiles/r4_bwd_shape.log)
+      const int want = env_int("DLAP_BWD_FPW", 1);
+      const int tps = std::max(md_.tps_s, md_.tps_m);
+      fpw_ = (want == 4 && mlp_bwd_fpw_fits(md_.md, md_.KS1, slab_stride(), tps, 4)) ? 4 : 1;
       gx_bwd_ = nfine_ / fpw_;
     }
     std::vector<RnnJob> rt, re;
@@ -1757,10 +1777,11 @@ class Engine {
       launch_mlp_fwd_zx(as<MlpJob>(j_mlp_train_[phase]), G_, std::max(1, zx_gx_ / G_), md_.md, md_.WMB, st_, true);
     else if (fused)
       launch_mlp_fwd_rnn(as<MlpJob>(j_mlp_train_[phase]), as<RnnJob>(j_rnn_train_), dd(), G_,
-                         fused_train_gx(phase), md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, D.T, st_);
+                         fused_train_gx(phase), md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, D.T, st_,
+                         !train_mom(phase));
     else
       launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, phase == 2 ? gx_fwd_[0] : gx_fwd13_, md_.md, md_.KS1,
-                     md_.WMB, st_);
+                     md_.WMB, st_, !train_mom(phase));
     if (mark == 2) HIP_OK(hipEventRecord(ev_a_, st_));
     HTRACE("launch_period_fwd");
     launch_period_fwd(lj, G_, D.T, st_);
@@ -1866,9 +1887,9 @@ class Engine {
       HTRACE("launch_mlp_fwd");
       if (fused_eval())
         launch_mlp_fwd_rnn(as<MlpJob>(j_mlp_eval_), as<RnnJob>(j_rnn_eval_), dd(), n_eval_jobs_, fused_eval_gx(),
-                           md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, tmax_eval_, st);
+                           md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, tmax_eval_, st, h_cache_);
       else
-        launch_mlp_fwd(as<MlpJob>(j_mlp_eval_), n_eval_jobs_, gx, md_.md, md_.KS1, md_.WMB, st);
+        launch_mlp_fwd(as<MlpJob>(j_mlp_eval_), n_eval_jobs_, gx, md_.md, md_.KS1, md_.WMB, st, h_cache_);
     }
     const bool eg = eval_gram_now();
     const LossJob* le = as<LossJob>(eg ? j_loss_eval_ : j_loss_eval_dense_);

@@ -49,9 +49,11 @@ DLAP_DEV int opaque_zero() {
 #define DLAP_FWD_WPS 2
 #endif
 
-// Waves per SIMD of the one-tile-per-slice SDF backward (TPS = 1): 2 halves its register budget.
+// Waves per SIMD of the one-tile-per-slice SDF backward (TPS = 1): 2 halves its register budget
+// and lets two waves hide each other's MFMA / LDS latency (600x3000x46: 0.1983 vs 0.2041 ms
+// per epoch for the two-tiles-per-slice kernel at one wave, profiles/r4_bwd_shape.log).
 #ifndef DLAP_BWD1_WPS
-#define DLAP_BWD1_WPS 1
+#define DLAP_BWD1_WPS 2
 #endif
 
 // In-kernel timestamps (wall clock, 100 MHz) of k_mlp_fwd's first / last workgroup, wave 0:
@@ -576,7 +578,11 @@ DLAP_DEV int prog_wait(const int* prog, int* err, int need, int seen, bool fence
 // fused k_mlp_fwd_rnn: grid.x - 1, its workgroup 0 runs the LSTM). WAIT: the per-period inputs
 // are produced concurrently by that LSTM -- before a tile is finished, the wave waits until the
 // periods of its rows are published (J.prog) and reads them from global memory.
-template <class P, int KS1, int WMB, bool ZIN, bool WAIT>
+// SO: the SDF tower only, with its dropout masks pre-generated (or no dropout) -- the phase-1/3
+// training forward and the evaluation forward of the epoch graphs. The moment tower and the
+// in-kernel mask hash are compiled out, so the tile loop carries neither their branches nor
+// their registers (the host picks SO only when every job qualifies: launch_mlp_fwd*).
+template <class P, int KS1, int WMB, bool ZIN, bool WAIT, bool SO = false>
 DLAP_DEV void mlp_fwd_body(const MlpJob& J, const MlpDims& D, char* smem, const int bx, const int gxw) {
   using Frag = typename P::Frag;
   Frag* lds = reinterpret_cast<Frag*>(smem);
@@ -593,7 +599,7 @@ DLAP_DEV void mlp_fwd_body(const MlpJob& J, const MlpDims& D, char* smem, const 
   ZTile<WMB> zcur, znxt;                 // ZIN: layer-0 pre-activations instead of X rows
   AbPre<WMB> ab_cur, ab_nxt;
   int2 ti_ahead[2];                      // periods of the tile after next (for the abias prefetch)
-  const bool mom = J.do_mom;
+  const bool mom = !SO && J.do_mom;
   // prologue: the step counter, the first tile's panel rows and keep words (both parity
   // halves: the step is not known yet) are all in flight with the weight staging
   const uint32_t stp = load_step(J);
@@ -657,10 +663,16 @@ DLAP_DEV void mlp_fwd_body(const MlpJob& J, const MlpDims& D, char* smem, const 
     if constexpr (ZIN) ri = finish_ztile<WMB>(J, tile, zcur);
     else if (WAIT && J.prog_mode != 0) ri = finish_tile<P, KS1, true, true>(J, D, tile, cur, xf, spp);
     else ri = finish_tile<P, KS1>(J, D, tile, cur, xf, spp);
-    if (J.do_sdf) {
+    if (SO || J.do_sdf) {
       float w[2];
       uint32_t kw[4];
-      sdf_keep_words(pre, kw_cur, dc, ri, Dt.nl_sdf, kw);
+      if constexpr (SO) {
+        DLAP_ASSERT(pre || !dc.on);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) kw[j] = pre ? kw_cur[j] : 0xFFFFFFFFu;
+      } else {
+        sdf_keep_words(pre, kw_cur, dc, ri, Dt.nl_sdf, kw);
+      }
       auto l0 = [&](f32x4 (&a)[2][4]) {
         if constexpr (ZIN) {
           if (D.pp_lds_floats > 0) zin_sdf0(zcur.zs, ri, spp, pst, auxt, D, a);
@@ -679,7 +691,7 @@ DLAP_DEV void mlp_fwd_body(const MlpJob& J, const MlpDims& D, char* smem, const 
         if (q == 0 && r < J.R) gp(J.w_out)[r] = w[b];
       }
     }
-    if (J.do_mom) {
+    if (!SO && J.do_mom) {
       auto l0 = [&](f32x4 (&a)[2][WMB]) {
         if constexpr (ZIN) {
 #pragma unroll
@@ -702,10 +714,10 @@ DLAP_DEV void mlp_fwd_body(const MlpJob& J, const MlpDims& D, char* smem, const 
   MLP_TS(3);
 }
 
-template <class P, int KS1, int WMB, bool ZIN>
+template <class P, int KS1, int WMB, bool ZIN, bool SO = false>
 __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __restrict__ jobs, MlpDims D) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  mlp_fwd_body<P, KS1, WMB, ZIN, false>(jobs[blockIdx.y], D, smem, blockIdx.x, gridDim.x);
+  mlp_fwd_body<P, KS1, WMB, ZIN, false, SO>(jobs[blockIdx.y], D, smem, blockIdx.x, gridDim.x);
 }
 
 // ============================== fused LSTM + training tower forward =======================
@@ -745,7 +757,7 @@ DLAP_DEV void lstm_publish(const RnnJob& J, const ModelDesc* __restrict__ md, co
   }
 }
 
-template <class P, int KS1, int WMB, int HM, bool DPPG>
+template <class P, int KS1, int WMB, int HM, bool DPPG, bool SO = false>
 __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd_rnn(const MlpJob* __restrict__ jobs, MlpDims D,
                                                                   const RnnJob* __restrict__ rjobs,
                                                                   const ModelDesc* __restrict__ md) {
@@ -772,7 +784,7 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd_rnn(const MlpJob*
     }
     return;
   }
-  mlp_fwd_body<P, KS1, WMB, false, true>(jobs[blockIdx.y], D, smem, blockIdx.x - 1, gridDim.x - 1);
+  mlp_fwd_body<P, KS1, WMB, false, true, SO>(jobs[blockIdx.y], D, smem, blockIdx.x - 1, gridDim.x - 1);
 }
 
 // ============================== wide evaluation forward ==================================
@@ -944,6 +956,10 @@ DLAP_DEV void x_rows_k(const typename P::Frag& x0, const typename P::Frag& x1, i
   out = P::pack(P::mma(x0, sel, zero4()), P::mma(x1, sel, zero4()));
 }
 
+// Fine slabs per workgroup: FPW = 1 compiled in (the one-slab launch: no slab loop state in the
+// register budget of the two-waves-per-SIMD kernel, ~2% faster at 600x3000x46) or 0 = J.fpw
+#define BWD_FPW(J) (FPW ? FPW : (J).fpw)
+
 // One slab per workgroup: zero an LDS image (reusing the weight staging area), let the
 // waves add into it one after another (fixed order = deterministic), then store it.
 DLAP_DEV float* wg_slab_begin(char* smem, int slab_stride) {
@@ -975,26 +991,30 @@ DLAP_DEV int slab_lds(int e) {
 }
 
 // Fine slab k (of J.fpw) of this workgroup is complete in `red` (after the wave loop's final
-// barrier). fpw == 1: store it as fine slab blockIdx.x of the slice. Else add it, in order, to
-// the coarse accumulator red_c (natural layout, LDS beyond the staging area; each thread
-// touches the same elements every time, so no barrier is needed between the passes) and store
-// the coarse slab after the last one: ((s0 + s1) + s2) + s3 -- exactly the grouping k_finalize
-// applies to stored fine slabs, so either launch shape gives the same gradient bits.
-template <int TPS>
-DLAP_DEV void wg_slab_finish(const MlpJob& J, const float* red, float* red_c, int slab_stride, int k) {
-  if (J.fpw == 1) {
-    const auto slab = gp(J.slab) + (size_t)(J.slab_base + blockIdx.z * J.nslab + blockIdx.x) * slab_stride;
+// barrier). fpw == 1: store it as fine slab blockIdx.x of the slice. Else accumulate it, in
+// order, into the workgroup's coarse image in LDS right after `red` (same swizzled layout, each
+// thread adds only its own elements): ((s0 + s1) + s2) + s3 -- exactly the grouping k_finalize
+// applies to stored fine slabs, so either launch shape gives the same gradient bits -- and store
+// the coarse slab after the last one. (A global read-modify-write per fine slab cost ~20 us per
+// flush at G = 9: the loads of the loop serialise behind the stores they may alias.)
+template <int TPS, int FPW>
+DLAP_DEV void wg_slab_finish(const MlpJob& J, float* red, int slab_stride, int k) {
+  const int fpw = BWD_FPW(J);
+  const int nst = J.nslab / fpw;                   // slabs stored per slice
+  const auto slab = gp(J.slab) + (size_t)(J.slab_base + blockIdx.z * nst + blockIdx.x) * slab_stride;
+  if (fpw == 1) {
     for (int i = threadIdx.x; i < slab_stride; i += blockDim.x) slab[i] = red[slab_lds<TPS>(i)];
     return;
   }
-  for (int i = threadIdx.x; i < slab_stride; i += blockDim.x) {
-    const float v = red[slab_lds<TPS>(i)];
-    red_c[i] = k ? red_c[i] + v : v;
+  float* coarse = red + slab_stride;
+  if (k == 0) {
+    for (int i = threadIdx.x; i < slab_stride; i += blockDim.x) coarse[i] = red[i];
+  } else {
+    for (int i = threadIdx.x; i < slab_stride; i += blockDim.x) coarse[i] = coarse[i] + red[i];
   }
-  if (k + 1 < J.fpw) return;
-  const int ncoarse = J.nslab / J.fpw;
-  const auto slab = gp(J.slab) + (size_t)(J.slab_base + blockIdx.z * ncoarse + blockIdx.x) * slab_stride;
-  for (int i = threadIdx.x; i < slab_stride; i += blockDim.x) slab[i] = red_c[i];
+  if (k + 1 < fpw) return;
+  __syncthreads();
+  for (int i = threadIdx.x; i < slab_stride; i += blockDim.x) slab[i] = coarse[slab_lds<TPS>(i)];
 }
 
 // SDF backward. NL = number of hidden (MFMA) layers, all 64 wide.
@@ -1009,14 +1029,16 @@ DLAP_DEV void wg_slab_finish(const MlpJob& J, const float* red, float* red_c, in
 // in place across the tile loop; else -1 (runtime tile map). A slice of layer TLC > 0 stops
 // its backward chain at that layer and leaves the bias / output-layer / per-period input
 // gradients to slice 0, so its live state (and register budget) is that of its own role.
-template <class P, int KS1, int NL, int TPS, bool ZIN, int TLC>
+template <class P, int KS1, int NL, int TPS, bool ZIN, int TLC, int FPW>
 DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, char* smem, int slice, int C0,
                            int red_off) {
   using Frag = typename P::Frag;
   Frag* lds = reinterpret_cast<Frag*>(smem);
   float* aux = aux_lds_ptr(smem, D);
   float* spp = pp_lds_ptr(smem, D);
-  float* red_c = reinterpret_cast<float*>(smem + red_off);
+  // fine slab image: over the staging area (one fine slab per workgroup) or, walking several,
+  // beyond it (red_off > 0), so the staged weights stay valid for the next fine slab
+  char* const sred = smem + red_off;
   const int lane = lane_id(), q = lane >> 4, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   const int ntiles = (J.R + 31) >> 5;
   const bool s0 = TLC <= 0 && slice == 0;      // the slice that owns the extra gradients (-2: slice 0)
@@ -1036,7 +1058,7 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
   const int stride = J.nslab * nwaves;
   const uint32_t stp = load_step(J);
   const bool pre = J.gbits && J.train && J.dropout > 0.f;   // keep words of this step (k_dropmask)
-  for (int kf = 0; kf < J.fpw; ++kf) {
+  for (int kf = 0; kf < BWD_FPW(J); ++kf) {
   if (kf) __syncthreads();                      // the previous slab's LDS reads are done
   f32x4 dW[TPS][4][4];
 #pragma unroll
@@ -1049,7 +1071,7 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
 #pragma unroll
   for (int u = 0; u < 4; ++u) { gbias[u] = zero4(); gwo[u] = zero4(); }
   float gbo = 0.f;
-  int tile = (blockIdx.x * J.fpw + kf) * nwaves + wave;
+  int tile = (blockIdx.x * BWD_FPW(J) + kf) * nwaves + wave;
   TileIn<P, KS1> cur, nxt;
   ZTile<1> zcur, znxt;
   // prologue as k_mlp_fwd: step, first tile and its keep words of both parities in flight with
@@ -1064,7 +1086,7 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
       kw_alt[j] = pre ? gp(J.gbits)[J.gb_half + ((size_t)tile * NL + j) * 64 + lane] : 0xFFFFFFFFu;
     }
   }
-  stage_weights<P>(J, D, lds, aux, spp);       // first tile's loads are already in flight
+  if (kf == 0) stage_weights<P>(J, D, lds, aux, spp);   // first tile's loads are already in flight
   const DropCtx dc = drop_ctx(J, D, stp);
   const auto gbase = pre ? gp(J.gbits) + (size_t)(dc.step & 1u) * J.gb_half : nullptr;
   if (dc.step & 1u) {
@@ -1223,7 +1245,7 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
     for (int j = 0; j < NL; ++j) kw_cur[j] = kw_nxt[j];
   }
   // ---- workgroup slab: waves add their partials into LDS in a fixed order ----
-  float* red = wg_slab_begin(smem, slab_stride);
+  float* red = wg_slab_begin(sred, slab_stride);
   for (int w = 0; w < nwaves; ++w) {
     if (wave == w) {
 #pragma unroll
@@ -1254,11 +1276,11 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
     }
     __syncthreads();
   }
-  wg_slab_finish<TPS>(J, red, red_c, slab_stride, kf);
+  wg_slab_finish<TPS, FPW>(J, red, slab_stride, kf);
   }
 }
 
-template <class P, int KS1, int NL, int TPS, bool ZIN>
+template <class P, int KS1, int NL, int TPS, bool ZIN, int FPW>
 __global__ __launch_bounds__(256, TPS == 1 ? DLAP_BWD1_WPS : 1) void k_mlp_bwd_sdf(const MlpJob* __restrict__ jobs, MlpDims D,
                                                         int slab_stride, int red_off) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1269,14 +1291,14 @@ __global__ __launch_bounds__(256, TPS == 1 ? DLAP_BWD1_WPS : 1) void k_mlp_bwd_s
   const int C0 = ZIN ? (D.Dm + 63) / 64 : KS1 / 2;
   if constexpr (TPS == 1) {
     const int tl = slice < C0 ? 0 : slice - C0 + 1;     // block-uniform: one role per slice
-    if (tl == 0) bwd_sdf_body<P, KS1, NL, 1, ZIN, 0>(J, D, slab_stride, smem, slice, C0, red_off);
-    if constexpr (NL > 1) if (tl == 1) bwd_sdf_body<P, KS1, NL, 1, ZIN, 1>(J, D, slab_stride, smem, slice, C0, red_off);
-    if constexpr (NL > 2) if (tl == 2) bwd_sdf_body<P, KS1, NL, 1, ZIN, 2>(J, D, slab_stride, smem, slice, C0, red_off);
-    if constexpr (NL > 3) if (tl == 3) bwd_sdf_body<P, KS1, NL, 1, ZIN, 3>(J, D, slab_stride, smem, slice, C0, red_off);
+    if (tl == 0) bwd_sdf_body<P, KS1, NL, 1, ZIN, 0, FPW>(J, D, slab_stride, smem, slice, C0, red_off);
+    if constexpr (NL > 1) if (tl == 1) bwd_sdf_body<P, KS1, NL, 1, ZIN, 1, FPW>(J, D, slab_stride, smem, slice, C0, red_off);
+    if constexpr (NL > 2) if (tl == 2) bwd_sdf_body<P, KS1, NL, 1, ZIN, 2, FPW>(J, D, slab_stride, smem, slice, C0, red_off);
+    if constexpr (NL > 3) if (tl == 3) bwd_sdf_body<P, KS1, NL, 1, ZIN, 3, FPW>(J, D, slab_stride, smem, slice, C0, red_off);
   } else if (TPS == 2 && C0 == 1) {     // the engine's TPS = 2 case: tiles (layer 0, layer 1)
-    bwd_sdf_body<P, KS1, NL, TPS, ZIN, -2>(J, D, slab_stride, smem, slice, C0, red_off);
+    bwd_sdf_body<P, KS1, NL, TPS, ZIN, -2, FPW>(J, D, slab_stride, smem, slice, C0, red_off);
   } else {
-    bwd_sdf_body<P, KS1, NL, TPS, ZIN, -1>(J, D, slab_stride, smem, slice, C0, red_off);
+    bwd_sdf_body<P, KS1, NL, TPS, ZIN, -1, FPW>(J, D, slab_stride, smem, slice, C0, red_off);
   }
 }
 
@@ -1293,7 +1315,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
   const MlpJob& J = jobs[blockIdx.y];
   Frag* lds = reinterpret_cast<Frag*>(smem);
   float* aux = aux_lds_ptr(smem, D);
-  float* red_c = reinterpret_cast<float*>(smem + red_off);
+  char* const sred = smem + red_off;         // fine slab image (see bwd_sdf_body)
   const int lane = lane_id(), q = lane >> 4, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
   const int ntiles = (J.R + 31) >> 5;
   const int slice = blockIdx.z;
@@ -1332,7 +1354,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
     if (tile + stride < ntiles) issue_rowti(J, tile + stride, ti_ahead);
   }
   const uint32_t stp = load_step(J);
-  stage_weights<P>(J, D, lds, aux);
+  if (kf == 0) stage_weights<P>(J, D, lds, aux);
   const DropCtx dc = drop_ctx(J, D, stp);
   if (tile < ntiles) {
     if constexpr (ZIN) issue_abias<WMB>(J, zcur.ti, ab_cur);
@@ -1461,7 +1483,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
     else cur = nxt;
     ab_cur = ab_nxt;
   }
-  float* red = wg_slab_begin(smem, slab_stride);
+  float* red = wg_slab_begin(sred, slab_stride);
   for (int w = 0; w < nwaves; ++w) {
     if (wave == w) {
 #pragma unroll
@@ -1485,7 +1507,7 @@ __global__ __launch_bounds__(256, 1) void k_mlp_bwd_mom(const MlpJob* __restrict
     }
     __syncthreads();
   }
-  wg_slab_finish<TPS>(J, red, red_c, slab_stride, kf);
+  wg_slab_finish<TPS, 0>(J, red, slab_stride, kf);
   }
 }
 
@@ -1524,19 +1546,31 @@ void launch_dropmask(const MlpJob* jobs, int njobs, int ntiles, const MlpDims& D
 
 // ---- host launchers -------------------------------------------------------------------
 size_t mlp_lds_bytes(const MlpDims& D) { return lds_bytes_of(D); }
-// backward LDS: the staging area (reused by the fine slab reduction), then with fpw > 1 the
-// coarse accumulator at red_off
-static size_t bwd_red_off(const MlpDims& D, int slab_stride) {
-  const size_t a = mlp_lds_bytes(D), b = (size_t)slab_stride * 4;
-  return ((a > b ? a : b) + 15) & ~(size_t)15;
+// backward LDS: the staging area, reused by the fine slab image when a workgroup walks one
+// fine slab; walking several (fpw > 1) the fine and coarse images go beyond it (red_off), so
+// the weights are staged once
+static size_t bwd_red_off(const MlpDims& D, int /*slab_stride*/) {
+  return (mlp_lds_bytes(D) + 15) & ~(size_t)15;
+}
+// a launch walking fpw fine slabs keeps the per-CU workgroup count of the one-slab launch (two
+// for the one-tile-per-slice kernel at DLAP_BWD1_WPS = 2)
+bool mlp_bwd_fpw_fits(const MlpDims& D, int KS1, int slab_stride, int tps, int fpw) {
+  if (fpw > 1 && !D.wide && !(KS1 == 2 && tps == 1)) return false;     // not instantiated
+  const size_t per_cu = 160 * 1024 / (tps == 1 ? DLAP_BWD1_WPS : 1);
+  return mlp_bwd_lds_bytes(D, slab_stride, fpw) <= per_cu;
 }
 size_t mlp_bwd_lds_bytes(const MlpDims& D, int slab_stride, int fpw) {
-  return bwd_red_off(D, slab_stride) + (fpw > 1 ? (size_t)slab_stride * 4 : 0);
+  const size_t a = mlp_lds_bytes(D), b = (size_t)slab_stride * 4;
+  return fpw > 1 ? bwd_red_off(D, slab_stride) + 2 * b : (a > b ? a : b);
 }
 
 template <class P>
 static bool launch_mlp_fwd_p(const MlpJob* jobs, dim3 grid, dim3 block, size_t sh, const MlpDims& D, int KS1,
-                             int WMB, hipStream_t st) {
+                             int WMB, hipStream_t st, bool so) {
+  if (so && !P::kF32) {      // (SDF-only: the moment width is irrelevant)
+    if (KS1 == 2) { hipLaunchKernelGGL((k_mlp_fwd<P, 2, 1, false, true>), grid, block, sh, st, jobs, D); HIP_OK(hipGetLastError()); return true; }
+    if (KS1 == 4) { hipLaunchKernelGGL((k_mlp_fwd<P, 4, 1, false, true>), grid, block, sh, st, jobs, D); HIP_OK(hipGetLastError()); return true; }
+  }
 #define F_CASE(K, W) if (KS1 == K && WMB == W) { hipLaunchKernelGGL((k_mlp_fwd<P, K, W, false>), grid, block, sh, st, jobs, D); HIP_OK(hipGetLastError()); return true; }
   F_CASE(2, 1) F_CASE(2, 2) F_CASE(2, 4) F_CASE(4, 1) F_CASE(4, 2) F_CASE(4, 4)
 #undef F_CASE
@@ -1544,7 +1578,7 @@ static bool launch_mlp_fwd_p(const MlpJob* jobs, dim3 grid, dim3 block, size_t s
 }
 
 void launch_mlp_fwd(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int KS1, int WMB,
-                    hipStream_t st) {
+                    hipStream_t st, bool so) {
   dim3 grid(gx, njobs), block(256);
   size_t sh = mlp_lds_bytes(D);
   if (D.wide) {      // layer 0 from k_proj0's z (bf16, or fp32 reference precision)
@@ -1553,8 +1587,8 @@ void launch_mlp_fwd(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int
     else { FZ_CASE(PrecBF16, 1) FZ_CASE(PrecBF16, 2) FZ_CASE(PrecBF16, 4) }
 #undef FZ_CASE
   }
-  const bool ok = D.fp32 ? launch_mlp_fwd_p<PrecF32>(jobs, grid, block, sh, D, KS1, WMB, st)
-                         : launch_mlp_fwd_p<PrecBF16>(jobs, grid, block, sh, D, KS1, WMB, st);
+  const bool ok = D.fp32 ? launch_mlp_fwd_p<PrecF32>(jobs, grid, block, sh, D, KS1, WMB, st, so)
+                         : launch_mlp_fwd_p<PrecBF16>(jobs, grid, block, sh, D, KS1, WMB, st, so);
   if (!ok) dlap_throw_hip(hipErrorInvalidValue, "mlp_fwd: unsupported (KS1, WMB)", __FILE__, __LINE__);
 }
 
@@ -1597,13 +1631,21 @@ int mlp_fwd_rnn_capacity(const MlpDims& D0, int KS1, int WMB, int H, int nrnn, i
 }
 
 bool launch_mlp_fwd_rnn(const MlpJob* jobs, const RnnJob* rjobs, const ModelDesc* md, int njobs, int gx,
-                        const MlpDims& D0, int KS1, int WMB, int H, int nrnn, int tmax, hipStream_t st) {
+                        const MlpDims& D0, int KS1, int WMB, int H, int nrnn, int tmax, hipStream_t st, bool so) {
   if (!mlp_fwd_rnn_supported(D0, KS1, WMB, H, nrnn, tmax))
     dlap_throw_hip(hipErrorInvalidValue, "mlp_fwd_rnn: unsupported shape", __FILE__, __LINE__);
   MlpDims D = D0;
   D.pp_lds_floats = 0;                 // the per-period inputs are read as they are published
   const size_t sh = fwd_rnn_lds(D0, H, tmax);
   dim3 grid(gx + 1, njobs), block(256);
+  if (so && !D.fp32) {
+#define RS_CASE(K, HM, DP) \
+    if (KS1 == K && H == HM) { \
+      hipLaunchKernelGGL((k_mlp_fwd_rnn<PrecBF16, K, 1, HM, DP, true>), grid, block, sh, st, jobs, D, rjobs, md); \
+      HIP_OK(hipGetLastError()); return true; }
+    RS_CASE(2, 4, true) RS_CASE(4, 4, true) RS_CASE(2, 8, false) RS_CASE(4, 8, false)
+#undef RS_CASE
+  }
 #define R_CASE(PR, K, W, HM, DP) \
   if (KS1 == K && WMB == W && H == HM) { \
     hipLaunchKernelGGL((k_mlp_fwd_rnn<PR, K, W, HM, DP>), grid, block, sh, st, jobs, D, rjobs, md); \
@@ -1630,12 +1672,17 @@ void launch_mlp_fwd_zx(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, 
 
 template <class P>
 static bool launch_bwd_sdf_p(const MlpJob* jobs, dim3 grid, dim3 block, size_t sh, int tps, const MlpDims& D,
-                             int KS1, int slab_stride, int roff, hipStream_t st) {
-#define S_CASE(K, N, T) if (KS1 == K && D.nl_sdf == N && tps == T) { hipLaunchKernelGGL((k_mlp_bwd_sdf<P, K, N, T, false>), grid, block, sh, st, jobs, D, slab_stride, roff); HIP_OK(hipGetLastError()); return true; }
+                             int KS1, int slab_stride, int roff, int fpw, hipStream_t st) {
+#define S_CASE(K, N, T) if (fpw == 1 && KS1 == K && D.nl_sdf == N && tps == T) { hipLaunchKernelGGL((k_mlp_bwd_sdf<P, K, N, T, false, 1>), grid, block, sh, st, jobs, D, slab_stride, roff); HIP_OK(hipGetLastError()); return true; }
   S_CASE(2, 1, 1) S_CASE(2, 2, 1) S_CASE(2, 3, 1) S_CASE(2, 4, 1)
   S_CASE(2, 2, 2)
   S_CASE(4, 1, 1) S_CASE(4, 2, 1) S_CASE(4, 3, 1) S_CASE(4, 4, 1)
 #undef S_CASE
+  // several fine slabs per workgroup (batched models): the one-tile-per-slice tower of the
+  // 64-column X (mlp_bwd_fpw_supported)
+#define SF_CASE(N) if (fpw > 1 && KS1 == 2 && D.nl_sdf == N && tps == 1) { hipLaunchKernelGGL((k_mlp_bwd_sdf<P, 2, N, 1, false, 0>), grid, block, sh, st, jobs, D, slab_stride, roff); HIP_OK(hipGetLastError()); return true; }
+  SF_CASE(1) SF_CASE(2) SF_CASE(3) SF_CASE(4)
+#undef SF_CASE
   return false;
 }
 
@@ -1645,14 +1692,14 @@ void launch_mlp_bwd_sdf(const MlpJob* jobs, int njobs, int gx, int nslice, int t
   const size_t sh = mlp_bwd_lds_bytes(D, slab_stride, fpw);
   const int roff = fpw > 1 ? (int)bwd_red_off(D, slab_stride) : 0;
   if (D.wide) {
-#define SZ_CASE(PR, N, T) if (D.nl_sdf == N && tps == T) { hipLaunchKernelGGL((k_mlp_bwd_sdf<PR, 2, N, T, true>), grid, block, sh, st, jobs, D, slab_stride, roff); HIP_OK(hipGetLastError()); return; }
+#define SZ_CASE(PR, N, T) if (D.nl_sdf == N && tps == T) { hipLaunchKernelGGL((k_mlp_bwd_sdf<PR, 2, N, T, true, 0>), grid, block, sh, st, jobs, D, slab_stride, roff); HIP_OK(hipGetLastError()); return; }
     if (D.fp32) { SZ_CASE(PrecF32, 1, 1) SZ_CASE(PrecF32, 2, 1) SZ_CASE(PrecF32, 3, 1) SZ_CASE(PrecF32, 4, 1) SZ_CASE(PrecF32, 2, 2) }
     else { SZ_CASE(PrecBF16, 1, 1) SZ_CASE(PrecBF16, 2, 1) SZ_CASE(PrecBF16, 3, 1) SZ_CASE(PrecBF16, 4, 1) SZ_CASE(PrecBF16, 2, 2) }
 #undef SZ_CASE
     dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_sdf: unsupported depth (wide)", __FILE__, __LINE__);
   }
-  const bool ok = D.fp32 ? launch_bwd_sdf_p<PrecF32>(jobs, grid, block, sh, tps, D, KS1, slab_stride, roff, st)
-                         : launch_bwd_sdf_p<PrecBF16>(jobs, grid, block, sh, tps, D, KS1, slab_stride, roff, st);
+  const bool ok = D.fp32 ? launch_bwd_sdf_p<PrecF32>(jobs, grid, block, sh, tps, D, KS1, slab_stride, roff, fpw, st)
+                         : launch_bwd_sdf_p<PrecBF16>(jobs, grid, block, sh, tps, D, KS1, slab_stride, roff, fpw, st);
   if (!ok) dlap_throw_hip(hipErrorInvalidValue, "mlp_bwd_sdf: unsupported depth/tiling", __FILE__, __LINE__);
 }
 

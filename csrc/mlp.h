@@ -97,8 +97,9 @@ struct WideJob {
 #define SLAB_EXTRA (DLAP_MAXL * 64 + 64 + 64)
 
 size_t mlp_lds_bytes(const MlpDims& D);
+// so: every job runs the SDF tower only with pre-generated (or no) dropout masks
 void launch_mlp_fwd(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int KS1, int WMB,
-                    hipStream_t st);
+                    hipStream_t st, bool so = false);
 // wide path, evaluation forward: layer 0 streamed from X inside the tower kernel (no z)
 void launch_mlp_fwd_zx(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int WMB, hipStream_t st,
                        bool train = false);
@@ -107,6 +108,7 @@ void launch_mlp_bwd_sdf(const MlpJob* jobs, int njobs, int gx, int nslice, int t
                         int KS1, int slab_stride, int fpw, hipStream_t st);
 // LDS bytes of a backward launch walking fpw fine slabs per workgroup (> 160 KiB: use fpw = 1)
 size_t mlp_bwd_lds_bytes(const MlpDims& D, int slab_stride, int fpw);
+bool mlp_bwd_fpw_fits(const MlpDims& D, int KS1, int slab_stride, int tps, int fpw);
 struct RnnJob;
 struct ModelDesc;
 // fused LSTM + training tower forward; false = not instantiated for this shape (see k_mlp.hip)
@@ -114,7 +116,8 @@ bool mlp_fwd_rnn_supported(const MlpDims& D, int KS1, int WMB, int H, int nrnn, 
 // resident workgroups of the fused kernel on the device (0: not instantiated for this shape)
 int mlp_fwd_rnn_capacity(const MlpDims& D, int KS1, int WMB, int H, int nrnn, int tmax);
 bool launch_mlp_fwd_rnn(const MlpJob* jobs, const RnnJob* rjobs, const ModelDesc* md, int njobs, int gx,
-                        const MlpDims& D, int KS1, int WMB, int H, int nrnn, int tmax, hipStream_t st);
+                        const MlpDims& D, int KS1, int WMB, int H, int nrnn, int tmax, hipStream_t st,
+                        bool so = false);
 void launch_dropmask(const MlpJob* jobs, int njobs, int ntiles, const MlpDims& D, int step_offset,
                      hipStream_t st);
 void launch_mlp_bwd_mom(const MlpJob* jobs, int njobs, int gx, int nslice, int tps, const MlpDims& D,
