@@ -1507,6 +1507,7 @@ class Engine {
     J.h = cond ? W.h.p : nullptr;
     J.Rm = D.Rm.p; J.invT = D.invT.p; J.G = W.gram.p;
     J.T = D.T; J.N = D.N; J.K = md_.K;
+    if ((long)D.N * std::max(md_.K, 1) >= (1l << 31) - 16) throw std::runtime_error("gram: N * K exceeds the 32-bit inner index");
     return J;
   }
   // Gram build job tables of every split (rebuild_jobs): the train split's conditional matrix

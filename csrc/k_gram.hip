@@ -36,7 +36,7 @@ DLAP_DEV f64x4 mfma_f64(double a, double b, f64x4 c) {
 DLAP_DEV int gram_tiles(int T) { return (T + 31) >> 5; }
 
 #define GB_WAVES 8      // waves per workgroup: one tile, GB_WAVES inner-axis slices
-#define GB_U 4          // 16-element chunks whose loads are issued together
+#define GB_U 2          // 16-element chunks per register batch (two batches in flight)
 
 __global__ __launch_bounds__(64 * GB_WAVES) void k_gram_build(const GramJob* __restrict__ jobs, int nsb) {
   const GramJob& J = jobs[blockIdx.y];
@@ -68,41 +68,50 @@ __global__ __launch_bounds__(64 * GB_WAVES) void k_gram_build(const GramJob* __r
   const auto invT = gp(J.invT);
   if (cond) {
     // inner axis: e = i*K + k in 16-element chunks, split evenly over the slices
-    const long E = (long)N * K;
-    const long nch = (E + 15) / 16;
-    const long c0 = nch * sl / nslice, c1 = nch * (sl + 1) / nslice;
+    // (32-bit index math: N * K < 2^31, checked by the launcher; a 64-bit division per chunk
+    // was a large share of the VALU work)
+    const int E = N * K;
+    const int nch = (E + 15) / 16;
+    const int c0 = (int)((long)nch * sl / nslice), c1 = (int)((long)nch * (sl + 1) / nslice);
+    const unsigned uK = (unsigned)K;
     const auto h = gp(J.h);
-    for (long cb = c0; cb < c1; cb += GB_U) {
-      // every operand of GB_U chunks requested before any is used
+    // two register batches of GB_U chunks: the loads of the next batch are in flight while the
+    // MFMAs of this one run (the single-batch loop spent ~40% of its cycles waiting on memory:
+    // SQ_WAIT_INST_ANY, profiles/r4_pmc_summary.txt). Same accumulation order as one batch.
+    struct Batch {
       f32x4 hv[GB_U][4];
       float rm[GB_U][4], iv[GB_U];
       bool first[GB_U];
+    };
+    auto load = [&](int cb, Batch& B) {
 #pragma unroll
       for (int u = 0; u < GB_U; ++u) {
-        const long e = (cb + u) * 16 + 4 * q;
+        const int e = (cb + u) * 16 + 4 * q;
         const bool eok = cb + u < c1 && e < E;
-        const long ec = eok ? e : 0;
-        const int i = (int)(ec / K);
-        first[u] = eok && (ec - (long)i * K) == 0;
-        iv[u] = eok ? invT[i] : 0.f;
+        const unsigned ec = eok ? (unsigned)e : 0u;
+        const int i = (int)(ec / uK);
+        B.first[u] = eok && (ec - (unsigned)i * uK) == 0u;
+        B.iv[u] = eok ? invT[i] : 0.f;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
-          hv[u][s] = ld4(h + (size_t)row[s] * E + ec);
-          rm[u][s] = rok[s] ? Rm[(size_t)row[s] * N + i] : 0.f;
+          B.hv[u][s] = ld4(h + (size_t)row[s] * E + ec);
+          B.rm[u][s] = rok[s] ? Rm[(size_t)row[s] * N + i] : 0.f;
         }
       }
+    };
+    auto comp = [&](const Batch& B) {
 #pragma unroll
       for (int u = 0; u < GB_U; ++u) {
         double a[4];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) a[s] = (double)rm[u][s] * (double)iv[u];
+        for (int s = 0; s < 4; ++s) a[s] = (double)B.rm[u][s] * (double)B.iv[u];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           double va[2], vb[2];
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
-            va[s] = (double)hv[u][s][j] * a[s];
-            vb[s] = (double)hv[u][2 + s][j] * a[2 + s];
+            va[s] = (double)B.hv[u][s][j] * a[s];
+            vb[s] = (double)B.hv[u][2 + s][j] * a[2 + s];
           }
 #pragma unroll
           for (int x = 0; x < 2; ++x)
@@ -113,8 +122,17 @@ __global__ __launch_bounds__(64 * GB_WAVES) void k_gram_build(const GramJob* __r
         for (int x = 0; x < 2; ++x)
 #pragma unroll
           for (int y = 0; y < 2; ++y)
-            gu[x][y] = mfma_f64(first[u] ? a[x] : 0.0, first[u] ? a[2 + y] : 0.0, gu[x][y]);
+            gu[x][y] = mfma_f64(B.first[u] ? a[x] : 0.0, B.first[u] ? a[2 + y] : 0.0, gu[x][y]);
       }
+    };
+    Batch b0, b1;
+    if (c0 < c1) load(c0, b0);
+    for (int cb = c0; cb < c1; cb += 2 * GB_U) {
+      if (cb + GB_U < c1) load(cb + GB_U, b1);
+      comp(b0);
+      if (cb + GB_U >= c1) break;
+      if (cb + 2 * GB_U < c1) load(cb + 2 * GB_U, b0);
+      comp(b1);
     }
   } else {
     // unconditional only: inner axis = stocks, 4 per MFMA (k-slot q <-> stock 4c + q)

@@ -6,6 +6,8 @@ set -o pipefail
 TAG=${1:-rh}
 mkdir -p gpurun_out
 export TMPDIR=/tmp DLAP_DIST_BACKEND=gloo DLAP_SHARE_GPU=1
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/${TAG}_n1.log 2>&1 || { tail -20 gpurun_out/${TAG}_n1.log; exit 3; }
+grep -o '"test_sharpe": [0-9.-]*\|"valid_sharpe": [0-9.-]*\|"panel_setup_s": [0-9.]*\|"fused_wait_timeouts": [0-9]*' gpurun_out/${TAG}_n1.log | tr '\n' ' '; echo
 for n in 2 4; do
   timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node $n --master-addr 127.0.0.1 \
     --master-port $((29600 + n)) bench.py --gpus $n --steps 20 --warmup 5 > gpurun_out/${TAG}_n$n.log 2>&1 || { tail -20 gpurun_out/${TAG}_n$n.log; exit 3; }
