@@ -454,9 +454,54 @@ void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* m
 // on wave 0 from LDS (next step prefetched), then all threads form the small gradients
 // (W_hh, biases, W_ih of layers > 0, d input of the layer below). The layer-0 W_ih
 // gradient (T x 4H x M) is left to k_wgrad, which has many workgroups.
+// Dense-state BPTT (H = 4, `scan`): the backward recurrence is LINEAR in the carried state
+// y_t = (dh_t, dc_next_t) in R^8 (dh_t = dout_t + dh_next, the cell gradient arriving from t+1):
+//   y_t = M_{t+1} y_{t+1} + (dout_t, 0),   M_t = [[Pc diag(A) + Qo, Pc], [diag(F A), diag(F)]],
+//   Pc[j][k] = sum_{q = i,f,g} W_hh[4q+k][j] B_q[k],  Qo[j][k] = W_hh[12+k][j] Bo[k]
+// (A, B_q, F: the pre-pass coefficients of step t). All M_t are formed in parallel, and the
+// serial chain is one 8x8 mat-vec per step on one wave, lane (i, j) = 8 i + j holding M[i][j]:
+// the product is reduced over j inside 8-lane groups (DPP quad perms + half mirror, "R layout":
+// every lane of group i holds y[i]) on even steps and over i across the wave (DPP row_ror 8 +
+// v_permlane16_swap + v_permlane32_swap, "C layout": lane (i, j) holds y[j]) on odd steps --
+// each layout is the other's input layout, so no lane permutation is on the chain. ~6 VALU per
+// step instead of the gate-per-lane step's ~25 (one dependent 4-unit cell update + a 16-lane
+// reduce-scatter). The gate gradients then follow from the recorded y_t in parallel.
+// m * y rounded once and hidden from the combiner: p + dpp(p) must not become fma(m, y, dpp(p))
+// (the lanes of a group would then round differently and disagree on y)
+DLAP_DEV float rmul(float m, float y) {
+  float p = m * y;
+  asm volatile("" : "+v"(p));
+  return p;
+}
+DLAP_DEV float red8_j(float p) {         // sum over the 8 lanes of a group (lanes 8i .. 8i+7)
+  p += dppf<0xB1>(p);                    // quad_perm [1,0,3,2]
+  p += dppf<0x4E>(p);                    // quad_perm [2,3,0,1]
+  p += dppf<0x141>(p);                   // row_half_mirror: lane j <-> 7 - j (the other quad)
+  return p;
+}
+DLAP_DEV float red8_i(float p) {         // sum over lanes j, j+8, ..., j+56
+  p += dppf<0x128>(p);                   // row_ror:8 = lane ^ 8 inside a 16-lane row
+  {
+    const auto s = __builtin_amdgcn_permlane16_swap(__float_as_uint(p), __float_as_uint(p), false, false);
+    p = __uint_as_float(s[0]) + __uint_as_float(s[1]);      // lane ^ 16
+  }
+  {
+    const auto s = __builtin_amdgcn_permlane32_swap(__float_as_uint(p), __float_as_uint(p), false, false);
+    p = __uint_as_float(s[0]) + __uint_as_float(s[1]);      // lane ^ 32
+  }
+  return p;
+}
+// weight-gradient partials: segment sums [S][nout], or the four MFMA tiles of the H = 4 path
+__host__ __device__ inline size_t lstm_gpart_floats(int H) {
+  const size_t a = 256 + (size_t)16 * H * (2 * H + 1);
+  return a > 1024 ? a : 1024;
+}
+// LDS floats of the dense-state path: M_t [T][64], y_t [T][8], W_hh [64], pair maps N_t / v_t
+__host__ __device__ inline size_t lstm_bwd_scan_floats(int T) { return (size_t)T * 72 + 64 + (size_t)((T - 1) / 2) * 72; }
+
 template <int HM>
 __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ jobs,
-                                                  const ModelDesc* __restrict__ md) {
+                                                  const ModelDesc* __restrict__ md, int scan) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const UpdJob& J = jobs[blockIdx.x];
   if (md->nrnn == 0) return;
@@ -480,27 +525,214 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
     const auto scg = gp(J.sc) + (size_t)l * T * H;
     const auto shg = gp(J.sh) + (size_t)l * T * H;
     __syncthreads();
-    // parallel pre-pass: everything of the backward step that does not depend on dh_next
-    for (int i = threadIdx.x; i < T * H; i += 256) {
-      const int t = i / H, k = i - t * H;
-      const float gi = sgg[(size_t)t * G4 + k], gf = sgg[(size_t)t * G4 + H + k];
-      const float gg = sgg[(size_t)t * G4 + 2 * H + k], go = sgg[(size_t)t * G4 + 3 * H + k];
-      const float c = scg[i], cp = t > 0 ? scg[i - H] : (J.c0 ? gp(J.c0)[l * H + k] : 0.f);
-      const float tc = ftanh(c);
-      float* q = s_cf + t * LSTM_NCOEF * H + k;
-      q[0 * H] = go * (1.f - tc * tc);
-      q[1 * H] = gg * gi * (1.f - gi);
-      q[2 * H] = cp * gf * (1.f - gf);
-      q[3 * H] = gi * (1.f - gg * gg);
-      q[4 * H] = tc * go * (1.f - go);
-      q[5 * H] = gf;
-      s_h[i] = shg[i];
-      s_d[i] = dout[i];
+    // parallel pre-pass: everything of the backward step that does not depend on dh_next.
+    // PU elements per thread with every global load issued before the first use (one memory
+    // round trip instead of one per element)
+    constexpr int PU = 4;
+    for (int i0 = threadIdx.x; i0 < T * H; i0 += 256 * PU) {
+      float gi[PU], gf[PU], gg[PU], go[PU], c[PU], cp[PU], hv[PU], dv[PU];
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        const int i = min(i0 + 256 * u, T * H - 1);
+        const int t = i / H, k = i - t * H;
+        gi[u] = sgg[(size_t)t * G4 + k];
+        gf[u] = sgg[(size_t)t * G4 + H + k];
+        gg[u] = sgg[(size_t)t * G4 + 2 * H + k];
+        go[u] = sgg[(size_t)t * G4 + 3 * H + k];
+        c[u] = scg[i];
+        cp[u] = t > 0 ? scg[i - H] : (J.c0 ? gp(J.c0)[l * H + k] : 0.f);
+        hv[u] = shg[i];
+        dv[u] = dout[i];
+      }
+#pragma unroll
+      for (int u = 0; u < PU; ++u) {
+        const int i = i0 + 256 * u;
+        if (i >= T * H) break;
+        const int t = i / H, k = i - t * H;
+        const float tc = ftanh(c[u]);
+        float* q = s_cf + t * LSTM_NCOEF * H + k;
+        q[0 * H] = go[u] * (1.f - tc * tc);
+        q[1 * H] = gg[u] * gi[u] * (1.f - gi[u]);
+        q[2 * H] = cp[u] * gf[u] * (1.f - gf[u]);
+        q[3 * H] = gi[u] * (1.f - gg[u] * gg[u]);
+        q[4 * H] = tc * go[u] * (1.f - go[u]);
+        q[5 * H] = gf[u];
+        s_h[i] = hv[u];
+        s_d[i] = dv[u];
+      }
     }
     __syncthreads();
     if (l == 0) RNN_TS(9, tsm);
     if (wave == 0) __builtin_amdgcn_s_setprio(3);     // serial chain: see k_lstm_gls
-    if (wave == 0 && HM == 4 && H == 4) {
+    if (HM == 4 && H == 4 && scan) {
+      // ---- dense-state BPTT (header comment): step matrices, chain on wave 0, gate gradients
+      float* s_M = dgs + T * G4 + 64 + lstm_gpart_floats(H);        // after the gpart region
+      float* s_y = s_M + T * 64;
+      float* s_W = s_y + T * 8;
+      float* s_N = s_W + 64;                          // [(T-1)/2][64] pair maps N_t
+      float* s_v = s_N + ((T - 1) / 2) * 64;          // [(T-1)/2][8]  pair offsets v_t
+      const auto Whh = params + md->lstm_w_hh[l];
+      if (threadIdx.x < 64) s_W[threadIdx.x] = Whh[threadIdx.x];
+      __syncthreads();
+      // one thread per (t, row i): the step's 24 coefficients as six 16-byte reads, the row's
+      // W_hh column in registers, two 16-byte stores
+      {
+        const int i = threadIdx.x & 7;
+        float wc[16];                                  // wc[r] = W_hh[r][i] (rows r = 4q + k)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) wc[r] = s_W[r * 4 + (i & 3)];
+        for (int t = threadIdx.x >> 3; t < T; t += 32) {
+          const f32x4* q4 = reinterpret_cast<const f32x4*>(s_cf + t * (LSTM_NCOEF * 4));
+          const f32x4 A = q4[0], Bi = q4[1], Bf = q4[2], Bg = q4[3], Bo = q4[4], F = q4[5];
+          f32x4 lo, hi;
+          if (i < 4) {                                 // row i of dh_next' (= unit j = i)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const float pc = wc[k] * Bi[k] + wc[4 + k] * Bf[k] + wc[8 + k] * Bg[k];
+              lo[k] = fmaf(pc, A[k], wc[12 + k] * Bo[k]);
+              hi[k] = pc;
+            }
+          } else {                                     // row of dc_next' (unit k = i - 4)
+            const int k = i - 4;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+              lo[c] = c == k ? F[c] * A[c] : 0.f;
+              hi[c] = c == k ? F[c] : 0.f;
+            }
+          }
+          f32x4* dst = reinterpret_cast<f32x4*>(s_M + t * 64 + 8 * i);
+          dst[0] = lo;
+          dst[1] = hi;
+        }
+      }
+      __syncthreads();
+      // pair maps: the chain advances two steps per link, y_t = N_t y_{t+2} + v_t for the chain
+      // points t = T-1-2p (p = 1 .. np), N_t = M_{t+1} M_{t+2}, v_t = M_{t+1} (dout_{t+1}, 0) +
+      // (dout_t, 0); one thread per (link, row), fixed summation order
+      const int npair = (T - 1) / 2;
+      for (int task = threadIdx.x; task < npair * 8; task += 256) {
+        const int p = 1 + (task >> 3), i = task & 7, t = T - 1 - 2 * p;
+        const f32x4* ra = reinterpret_cast<const f32x4*>(s_M + (t + 1) * 64 + 8 * i);
+        const f32x4 a0 = ra[0], a1 = ra[1];
+        const float a[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+        const f32x4* mb = reinterpret_cast<const f32x4*>(s_M + (t + 2) * 64);
+        f32x4 lo = zero4(), hi = zero4();
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          lo = lo + a[k] * mb[2 * k];
+          hi = hi + a[k] * mb[2 * k + 1];
+        }
+        f32x4* dn = reinterpret_cast<f32x4*>(s_N + (p - 1) * 64 + 8 * i);
+        dn[0] = lo;
+        dn[1] = hi;
+        const f32x4 du = *reinterpret_cast<const f32x4*>(s_d + (t + 1) * 4);
+        float v = a[0] * du[0] + a[1] * du[1] + a[2] * du[2] + a[3] * du[3];
+        if (i < 4) v += s_d[t * 4 + i];
+        s_v[(p - 1) * 8 + i] = v;
+      }
+      __syncthreads();
+      if (l == 0) RNN_TS(13, tsm);
+      if (wave == 0) {
+        const int i = lane >> 3, j = lane & 7;
+        const int offA = 8 * i + j, offB = 8 * j + i;
+        // per-link state records without exec-mask changes: the owner lanes of a layout (j == 0
+        // in R, i == 0 in C) store y_t, the others write a junk slot (the old path's)
+        float* junk = dgs + T * G4;
+        float* dstR = j == 0 ? s_y + i : junk + lane;
+        float* dstC = i == 0 ? s_y + j : junk + lane;
+        const int strR = j == 0 ? 16 : 0, strC = i == 0 ? 16 : 0;     // two steps per link
+        // y_{T-1} = (dout_{T-1}, 0) in the C layout
+        float y = j < 4 ? s_d[(T - 1) * 4 + j] : 0.f;
+        if (i == 0) s_y[(T - 1) * 8 + j] = y;
+        float* yR = dstR + (T - 1) * (j == 0 ? 8 : 0);   // record of link p at yR - p * strR
+        float* yC = dstC + (T - 1) * (i == 0 ? 8 : 0);
+        // links in blocks of U (even: every block starts from the C layout), the next block's
+        // operands loaded a whole block ahead
+        constexpr int U = 8;
+        float mA[U], uA[U], mB[U], uB[U];
+        auto load_block = [&](int p0, float (&m)[U], float (&u)[U]) {
+#pragma unroll
+          for (int k = 0; k < U; ++k) {
+            const int pp = min(p0 + k, npair) - 1;
+            const bool ev = (k & 1) == 0;
+            m[k] = s_N[pp * 64 + (ev ? offA : offB)];
+            u[k] = s_v[pp * 8 + (ev ? i : j)];
+          }
+        };
+        auto run_block = [&](int p0, const float (&m)[U], const float (&u)[U]) {
+#pragma unroll
+          for (int k = 0; k < U; ++k) {
+            const int pp = p0 + k;
+            const float pr = rmul(m[k], y);
+            if ((k & 1) == 0) {
+              y = red8_j(pr) + u[k];
+              yR[-pp * strR] = y;
+            } else {
+              y = red8_i(pr) + u[k];
+              yC[-pp * strC] = y;
+            }
+          }
+        };
+        const int nfull = npair / U;
+        int p = 1;
+        if (nfull > 0) load_block(p, mA, uA);
+        for (int b = 0; b < nfull; b += 2) {
+          if (b + 1 < nfull) load_block(p + U, mB, uB);
+          run_block(p, mA, uA);
+          p += U;
+          if (b + 1 < nfull) {
+            if (b + 2 < nfull) load_block(p + U, mA, uA);
+            run_block(p, mB, uB);
+            p += U;
+          }
+        }
+        bool cl = true;                                // C layout after an even number of links
+        for (; p <= npair; ++p) {
+          const float m = s_N[(p - 1) * 64 + (cl ? offA : offB)];
+          const float u = s_v[(p - 1) * 8 + (cl ? i : j)];
+          const float pr = rmul(m, y);
+          y = (cl ? red8_j(pr) : red8_i(pr)) + u;
+          if (cl) yR[-p * strR] = y;
+          else yC[-p * strC] = y;
+          cl = !cl;
+        }
+      }
+      __syncthreads();
+      // the steps between chain points, in parallel: y_t = M_{t+1} y_{t+1} + (dout_t, 0)
+      for (int task = threadIdx.x; task < (T / 2) * 8; task += 256) {
+        const int t = T - 2 - 2 * (task >> 3), i = task & 7;
+        const f32x4* ra = reinterpret_cast<const f32x4*>(s_M + (t + 1) * 64 + 8 * i);
+        const f32x4* yb = reinterpret_cast<const f32x4*>(s_y + (t + 1) * 8);
+        const f32x4 a0 = ra[0], a1 = ra[1], y0 = yb[0], y1 = yb[1];
+        float v = a0[0] * y0[0] + a0[1] * y0[1] + a0[2] * y0[2] + a0[3] * y0[3] +
+                  (a1[0] * y1[0] + a1[1] * y1[1] + a1[2] * y1[2] + a1[3] * y1[3]);
+        if (i < 4) v += s_d[t * 4 + i];
+        s_y[t * 8 + i] = v;
+      }
+      __syncthreads();
+      // dL/d(initial state): the state leaving step 0, M_0 y_0
+      if (J.dh0 && threadIdx.x < 8) {
+        const int i = threadIdx.x;
+        float v = 0.f;
+        for (int k = 0; k < 8; ++k) v += s_M[8 * i + k] * s_y[k];
+        if (i < 4) gp(J.dh0)[l * 4 + i] = v;
+        else gp(J.dc0)[l * 4 + (i - 4)] = v;
+      }
+      __syncthreads();
+      if (l == 0) RNN_TS(15, tsm);
+      // gate gradients from the recorded states: dh = y_h, dc = A dh + y_c
+      for (int idx = threadIdx.x; idx < T * 4; idx += 256) {
+        const int t = idx >> 2, k = idx & 3;
+        const float* q = s_cf + t * (LSTM_NCOEF * 4);
+        const float dh = s_y[t * 8 + k];
+        const float dc = fmaf(dh, q[k], s_y[t * 8 + 4 + k]);
+        float* d = dgs + t * 16 + k;
+        d[0] = dc * q[4 + k];
+        d[4] = dc * q[8 + k];
+        d[8] = dc * q[12 + k];
+        d[12] = dh * q[16 + k];
+      }
+    } else if (wave == 0 && HM == 4 && H == 4) {
       // Gate-per-lane BPTT (H = 4): lane L (mod 16) owns gate row L = 4q + k and keeps the
       // recurrent state of unit k replicated, so d_L = (q == 3 ? dh : dc) * coef is lane-local
       // and dh_next_j = sum_L W_hh[L][j] d_L is ONE reduce-scatter over the 16 lanes: two DPP
@@ -648,6 +880,43 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
     const int nout = G4 * ncol;
     const int S = max(1, min(LSTM_GSEG, 256 / max(nout, 1)));
     float* gpart = dgs + T * G4 + 64;                 // [S][nout] (after the junk slots)
+    if (HM == 4 && H == 4) {
+      // H = 4: [ncol x 16 gates] = sum_t x[t][col] dG[t][g] on v_mfma_f32_16x16x4f32 (exact
+      // fp32 products) -- x = (h_{t-1} (the initial state at t = 0), 1 for the biases, the layer
+      // input of a deeper layer). Wave w takes the 4-period k-steps w, w + 4, ...; the four
+      // partial tiles are summed in wave order (fixed order: deterministic).
+      //   A lane l -> x[t0 + (l >> 4)][col = l & 15],  B lane l -> dG[t0 + (l >> 4)][g = l & 15]
+      //   C lane l, r -> (col = 4 (l >> 4) + r, g = l & 15)
+      const int lc = lane & 15, lk = lane >> 4;
+      const float h0c = (lc < 4 && J.h0) ? gp(J.h0)[l * 4 + lc] : 0.f;
+      f32x4 acc = zero4();
+      for (int kb = wave; kb * 4 < T; kb += 4) {
+        const int t = kb * 4 + lk;
+        const bool ok = t < T;
+        const int tc = ok ? t : T - 1;
+        float a = 0.f;
+        if (lc < 4) a = tc > 0 ? s_h[(tc - 1) * 4 + lc] : h0c;
+        else if (lc == 4) a = 1.f;
+        else if (lc < 9 && l > 0) {
+          const int m = lc - 5;
+          a = hb[(size_t)tc * 4 + m];
+          if (drop) a = dropout_keep(key_below, (uint32_t)tc, (uint32_t)m, thr) ? a * scale : 0.f;
+        }
+        const float b = dgs[tc * 16 + lc];
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(ok ? a : 0.f, ok ? b : 0.f, acc, 0, 0, 0);
+      }
+      *reinterpret_cast<f32x4*>(gpart + wave * 256 + lane * 4) = acc;
+      __syncthreads();
+      for (int o = threadIdx.x; o < ncol * 16; o += 256) {
+        const int col = o >> 4, g = o & 15;
+        const int li = 16 * (col >> 2) + g, r = col & 3;
+        const float v = ((gpart[li * 4 + r] + gpart[256 + li * 4 + r]) + gpart[512 + li * 4 + r]) + gpart[768 + li * 4 + r];
+        if (col < 4) grads[md->lstm_w_hh[l] + g * 4 + col] = v;
+        else if (col == 4) { grads[md->lstm_b_ih[l] + g] = v; grads[md->lstm_b_hh[l] + g] = v; }
+        else grads[md->lstm_w_ih[l] + g * in_dim + (col - 5)] = v;
+      }
+      __syncthreads();
+    } else
     for (int idx0 = 0; idx0 < nout; idx0 += 256 / S) {
       const int lt = (int)threadIdx.x % (256 / S), seg = (int)threadIdx.x / (256 / S);
       const int idx = idx0 + lt;
@@ -775,13 +1044,20 @@ __global__ __launch_bounds__(256) void k_wgrad(const UpdJob* __restrict__ jobs,
 void launch_lstm_bwd(const UpdJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
                      int T, int phase, hipStream_t st) {
   if (phase != 2 && mh.nrnn > 0) {
-    // coef, h, d, dgates, junk, weight-gradient segment partials
-    const size_t sh = ((size_t)T * (LSTM_NCOEF + 2 + 4) * mh.H + 64 + 256 + 16 * mh.H * (2 * mh.H + 1)) * sizeof(float);
+    // coef, h, d, dgates, junk, weight-gradient segment partials (+ the dense-state path's
+    // step matrices / states when H = 4 and they fit; DLAP_LSTM_SCAN=0 keeps the gate-per-lane
+    // chain)
+    size_t sh = ((size_t)T * (LSTM_NCOEF + 2 + 4) * mh.H + 64 + lstm_gpart_floats(mh.H)) * sizeof(float);
     if (sh > 160 * 1024) dlap_throw_hip(hipErrorInvalidValue, "lstm_bwd: T*H too large for LDS", __FILE__, __LINE__);
-    if (mh.H <= 4) hipLaunchKernelGGL((k_lstm_bwd<4>), dim3(njobs), dim3(256), sh, st, jobs, md);
-    else if (mh.H <= 8) hipLaunchKernelGGL((k_lstm_bwd<8>), dim3(njobs), dim3(256), sh, st, jobs, md);
-    else if (mh.H <= 16) hipLaunchKernelGGL((k_lstm_bwd<16>), dim3(njobs), dim3(256), sh, st, jobs, md);
-    else hipLaunchKernelGGL((k_lstm_bwd<32>), dim3(njobs), dim3(256), sh, st, jobs, md);
+    const char* scan_env = std::getenv("DLAP_LSTM_SCAN");
+    const bool scan_on = !(scan_env && std::atoi(scan_env) == 0);
+    const size_t sh_scan = sh + lstm_bwd_scan_floats(T) * sizeof(float);
+    const int scan = scan_on && mh.H == 4 && T >= 2 && sh_scan <= 160 * 1024 ? 1 : 0;
+    if (scan) sh = sh_scan;
+    if (mh.H <= 4) hipLaunchKernelGGL((k_lstm_bwd<4>), dim3(njobs), dim3(256), sh, st, jobs, md, scan);
+    else if (mh.H <= 8) hipLaunchKernelGGL((k_lstm_bwd<8>), dim3(njobs), dim3(256), sh, st, jobs, md, 0);
+    else if (mh.H <= 16) hipLaunchKernelGGL((k_lstm_bwd<16>), dim3(njobs), dim3(256), sh, st, jobs, md, 0);
+    else hipLaunchKernelGGL((k_lstm_bwd<32>), dim3(njobs), dim3(256), sh, st, jobs, md, 0);
     HIP_OK(hipGetLastError());
   }
   if (mh.M == 0) return;

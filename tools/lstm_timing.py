@@ -35,6 +35,8 @@ def main():
         print(f"  k_lstm_gl train: stage {us(0, 1):7.1f}  recur {us(1, 2):7.1f}  tail {us(2, 3):7.1f}  total {us(0, 3):7.1f}")
         print(f"  k_lstm_gl eval : stage {us(4, 5):7.1f}  recur {us(5, 6):7.1f}  tail {us(6, 7):7.1f}  total {us(4, 7):7.1f}")
         print(f"  k_lstm_bwd     : stage {us(8, 9):7.1f}  bptt  {us(9, 10):7.1f}  grads {us(10, 11):7.1f} total {us(8, 11):7.1f}")
+        if ts[13] > ts[9] and ts[15] > ts[13]:     # dense-state path: step matrices | chain | gates
+            print(f"    dense-state  : matrices {us(9, 13):7.1f}  chain {us(13, 15):7.1f}  gates {us(15, 10):7.1f}")
         print(f"  k_proj tile0   : total {us(12, 14):7.1f}")
         m = np.array(mod.Engine.mlp_timestamps(), dtype=np.int64)
         um = lambda a, b: (m[b] - m[a]) / 100.0  # noqa: E731
