@@ -412,6 +412,92 @@ class XSectionGAN(AssetPricingGAN):
         return w, None
 
 
+class _Bundle:
+    """Device scalars of one epoch read back to the host in ONE transfer. ``train_epoch`` and
+    ``evaluate`` register their results (valid / test evaluations follow the step without a host
+    read in between) and return ``_Deferred`` mappings; the first key access of any of them copies
+    every pending tensor at once (the step and the two evaluations used to
+    cost a device-to-host read each)."""
+    pending: list = []
+
+    @classmethod
+    def add(cls, vec: torch.Tensor, post) -> "_Deferred":
+        d = _Deferred(vec.detach().float().reshape(-1), post)
+        cls.pending.append(d)
+        return d
+
+    @classmethod
+    def flush(cls):
+        todo, cls.pending = cls.pending, []
+        live = [d for d in todo if d._vals is None]
+        if not live:
+            return
+        host = torch.cat([d._vec for d in live]).cpu().numpy()
+        off = 0
+        for d in live:
+            n = d._vec.numel()
+            d._vals = d._post(host[off:off + n])
+            d._vec = None
+            off += n
+
+
+class _Deferred(dict):
+    """A result dict whose scalar entries arrive with the epoch's bundle read; device tensors
+    (``weights``) are available at once."""
+
+    def __init__(self, vec, post, **eager):
+        super().__init__(**eager)
+        self._vec, self._post, self._vals = vec, post, None
+
+    def _ready(self):
+        if self._vals is None:
+            _Bundle.flush()
+        if self._vals is not None and not self._merged:
+            super().update(self._vals)
+            self._merged = True
+
+    _merged = False
+
+    def __getitem__(self, k):
+        if not dict.__contains__(self, k):
+            self._ready()
+        return super().__getitem__(k)
+
+    def get(self, k, default=None):
+        try:
+            return self[k]
+        except KeyError:
+            return default
+
+    def __contains__(self, k):
+        self._ready()
+        return super().__contains__(k)
+
+    def keys(self):
+        self._ready()
+        return super().keys()
+
+    def items(self):
+        self._ready()
+        return super().items()
+
+    def values(self):
+        self._ready()
+        return super().values()
+
+    def __iter__(self):            # (also keeps {**d} / dict(d) off the raw-storage fast path)
+        self._ready()
+        return super().__iter__()
+
+    def __len__(self):
+        self._ready()
+        return super().__len__()
+
+    def __repr__(self):
+        self._ready()
+        return super().__repr__()
+
+
 def _args(data: Dict, device):
     macro = data.get("macro_features")
     return (None if macro is None else macro.to(device), data["individual_features"].to(device),
@@ -439,7 +525,8 @@ def train_epoch(model: XSectionGAN, optimizer, data: Dict, device, phase: str = 
             off += g.numel()
     gn = torch.nn.utils.clip_grad_norm_(params, max_norm=grad_clip)
     optimizer.step()
-    # the six scalars in ONE device-to-host read (the reference: six .item() syncs)
+    # the six scalars stay on the device until the epoch's bundle is read (no host sync here;
+    # the reference: six .item() syncs per step)
     dev = out["loss"].device
     p = out["portfolio_returns"].detach().float()
     sd = p.std()
@@ -447,9 +534,9 @@ def train_epoch(model: XSectionGAN, optimizer, data: Dict, device, phase: str = 
     v = torch.stack([out["loss"].detach().float().reshape(()), out["loss_unconditional"].detach().float().reshape(()),
                      out["loss_conditional"].detach().float().reshape(()),
                      out["loss_residual"].detach().float().reshape(()), sharpe,
-                     torch.as_tensor(gn, device=dev).detach().float().reshape(())]).tolist()
-    return {"loss": v[0], "loss_unc": v[1], "loss_cond": v[2], "loss_residual": v[3], "sharpe": v[4],
-            "grad_norm": v[5]}
+                     torch.as_tensor(gn, device=dev).detach().float().reshape(())])
+    keys = ("loss", "loss_unc", "loss_cond", "loss_residual", "sharpe", "grad_norm")
+    return _Bundle.add(v, lambda h: {k: float(x) for k, x in zip(keys, h)})
 
 
 @torch.no_grad()
@@ -461,15 +548,19 @@ def evaluate(model: XSectionGAN, data: Dict, device, normalized: bool = True) ->
     w, _ = model.get_weights(macro, x, m, normalized=normalized)
     pr = all_reduce_sum((w * r * m.float()).sum(1), model.dist)
     out = model(macro, x, r, m, phase="conditional", n_total=data.get("n_total"))
-    # portfolio returns and the three losses in ONE device-to-host read
+    # portfolio returns and the three losses join the epoch's bundle read (train_epoch)
     v = torch.cat([pr.float(), torch.stack([out["loss"].float().reshape(()),
                                             out["loss_unconditional"].float().reshape(()),
-                                            out["loss_conditional"].float().reshape(())])]).cpu()
-    port = v[:-3].numpy()
-    loss, loss_unc, loss_cond = (float(x) for x in v[-3:])
-    return {"loss": loss, "loss_unc": loss_unc, "loss_cond": loss_cond, "sharpe": compute_sharpe(v[:-3]),
-            "max_drawdown": compute_max_drawdown(port), "mean_return": port.mean(),
-            "std_return": port.std(), "weights": w}      # (the rank's stocks, on its device)
+                                            out["loss_conditional"].float().reshape(())])])
+
+    def post(h):
+        port = np.asarray(h[:-3], dtype=np.float32)
+        return {"loss": float(h[-3]), "loss_unc": float(h[-2]), "loss_cond": float(h[-1]),
+                "sharpe": compute_sharpe(torch.from_numpy(port)), "max_drawdown": compute_max_drawdown(port),
+                "mean_return": port.mean(), "std_return": port.std()}
+    d = _Bundle.add(v, post)
+    dict.__setitem__(d, "weights", w)                    # (the rank's stocks, on its device)
+    return d
 
 
 def train_3phase_xsection(config: Dict, train_data: Dict, valid_data: Dict, test_data: Optional[Dict],
@@ -545,7 +636,10 @@ def main(argv: Optional[Sequence[str]] = None):
                                         ignore_epoch=args.ignore_epoch, seed=args.seed,
                                         engine=False if args.torch_towers else None)
     ev = {k: evaluate(model, b[k], d.device) for k in SPLITS}
-    res = {"world_size": d.world, "n_stocks": tr["n_total"], "wall_s": time.time() - t0,
+    wall = time.time() - t0
+    n_ep = sum(args.epochs)
+    res = {"world_size": d.world, "n_stocks": tr["n_total"], "wall_s": wall, "epochs": n_ep,
+           "ms_per_epoch": 1e3 * wall / max(n_ep, 1),        # incl. the valid / test evaluations
            **{f"{k}_sharpe": float(ev[k]["sharpe"]) for k in SPLITS}}
     if d.is_main:
         print(json.dumps(res))

@@ -211,3 +211,23 @@ def test_param_cache_sees_data_edits_after_invalidation():
         out_g = gpu(*_args(bc), phase="conditional")
         out_c = cpu(*_args(b), phase="conditional")
     _close_out(out_g["weights"], out_c["weights"])
+
+
+def test_new_panel_at_a_reused_address_is_uploaded():
+    """a loop that moves a new host batch of the same shape to the GPU every step gets
+    the freed block back at the same address with version 0. The panel cache key holds weak
+    references to the tensor objects (``ops.fused._PanelKey``), so the second batch is uploaded
+    and the outputs follow it (checked against the CPU module on each batch)."""
+    cpu, gpu = _pair()
+    outs = []
+    for seed in (4, 5):
+        b = _batch(seed=seed)
+        bc = _cuda(b)
+        with torch.no_grad():
+            out_g = gpu(*_args(bc), phase="conditional")
+            out_c = cpu(*_args(b), phase="conditional")
+        _close_out(out_g["weights"], out_c["weights"])
+        outs.append((bc["individual_features"].data_ptr(), out_g["weights"].detach().cpu()))
+        del bc, out_g
+        torch.cuda.synchronize()
+    assert not torch.equal(outs[0][1], outs[1][1])
