@@ -32,6 +32,17 @@ typedef unsigned short u16;
 #endif
 template <typename T>
 DLAP_DEV DLAP_GLOBAL T* gp(T* p) { return (DLAP_GLOBAL T*)p; }
+// Element `off` of a uniform base with a 32-bit unsigned BYTE offset (the caller guarantees the
+// array is < 4 GiB): lowers to the global_load/store SGPR-base + 32-bit VGPR-offset form instead
+// of a 64-bit address add per access (v_lshl_add_u64 + moves in the tower tile loops).
+template <typename T>
+DLAP_DEV DLAP_GLOBAL T* gp32(T* base, uint32_t off) {
+  return (DLAP_GLOBAL T*)((DLAP_GLOBAL char*)gp(base) + off * (uint32_t)sizeof(T));
+}
+template <typename T>
+DLAP_DEV DLAP_GLOBAL T* at32(DLAP_GLOBAL T* base, uint32_t off) {
+  return (DLAP_GLOBAL T*)((DLAP_GLOBAL char*)base + off * (uint32_t)sizeof(T));
+}
 #define DLAP_MAXL 6   // max MFMA layers per tower
 
 #define HIP_OK(expr)                                                                        \

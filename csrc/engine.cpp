@@ -357,6 +357,7 @@ class Engine {
     if ((int)row_ptr.size() != T + 1) throw std::invalid_argument("row_ptr must be [T+1]");
     if (md_.M > 0 && (long)macro.size() != (long)T * md_.M) throw std::invalid_argument("macro must be [T][M]");
     D.T = T; D.N = N; D.R = R;
+    check_x32(R);
     const size_t nx = (size_t)R * md_.KP * xw();
     if (x_on_device) {
       D.X.alloc(nx, false);
@@ -445,6 +446,7 @@ class Engine {
     int R = 0;
     finish_stats(D, &R);
     D.R = R;
+    check_x32(R);
     D.rowti.alloc((size_t)2 * std::max(R, 1), false);
     D.Rc.alloc(std::max(R, 1), false);
     D.X.alloc(std::max<size_t>((size_t)R * md_.KP * xw(), 1), false);
@@ -1310,6 +1312,12 @@ class Engine {
       for (int o = 0; o < d.m[j].out; ++o) d.extra_m[j * 64 + o] = d.m[j].b_off + o;
   }
 
+  // the tower tile loops address the compact panel with 32-bit byte offsets (gp32): fused-path
+  // panels must stay below 4 GiB (the wide path streams layer 0 through other kernels)
+  void check_x32(int R) const {
+    if (!md_.md.wide && (size_t)R * md_.KP * xw() * sizeof(uint16_t) >= (size_t(1) << 32) - 256)
+      throw std::invalid_argument("compact panel exceeds 4 GiB on the fused layer-0 path");
+  }
   int slab_stride() const { return std::max(md_.tps_s, md_.tps_m) * 4096 + SLAB_EXTRA; }
 
   void alloc_ws(int s) {

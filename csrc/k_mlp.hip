@@ -243,11 +243,13 @@ DLAP_DEV void issue_tile(const MlpJob& J, int tile, TileIn<P, KS1>& in) {
 #pragma unroll
   for (int b = 0; b < 2; ++b) {
     const int r = min(tile * 32 + 16 * b + (l & 15), J.R - 1);   // clamp: no divergent loads
-    in.ti[b] = gp(J.rowti)[r];
-    const auto row = xrows<P>(J) + (size_t)r * (4 * KS1);
+    in.ti[b] = *gp32(J.rowti, (uint32_t)r);
+    // (32-bit element offsets: the compact panel is < 4 GiB -- R * KP bf16 / fp32, checked on
+    // the host when the split is set)
 #pragma unroll
-    for (int s = 0; s < KS1; ++s) in.x[b][s] = row[4 * s + q];
-    if (DW) in.dw[b] = gp(J.dw)[r];
+    for (int s = 0; s < KS1; ++s)
+      in.x[b][s] = *gp32(reinterpret_cast<const typename P::Frag*>(J.X), (uint32_t)r * (4 * KS1) + 4 * s + q);
+    if (DW) in.dw[b] = *gp32(J.dw, (uint32_t)r);
   }
 }
 
@@ -945,6 +947,10 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
 template <class P, int UB>
 DLAP_DEV void to_rows_k(const typename P::Frag (&pf)[2][(UB + 1) / 2], int blk, const typename P::Frag& s0,
                         const typename P::Frag& s1, typename P::Frag& out) {
+#ifdef DLAP_FAKE_TRANSPOSE      // timing experiment only: wrong results
+  out = (blk & 1) ? pf[1][blk >> 1] : pf[0][blk >> 1];
+  return;
+#endif
   const typename P::Frag sel = (blk & 1) ? s1 : s0;
   out = P::pack(P::mma(pf[0][blk >> 1], sel, zero4()), P::mma(pf[1][blk >> 1], sel, zero4()));
 }
@@ -952,6 +958,10 @@ DLAP_DEV void to_rows_k(const typename P::Frag (&pf)[2][(UB + 1) / 2], int blk, 
 template <class P>
 DLAP_DEV void x_rows_k(const typename P::Frag& x0, const typename P::Frag& x1, int blk,
                        const typename P::Frag& s0, const typename P::Frag& s1, typename P::Frag& out) {
+#ifdef DLAP_FAKE_TRANSPOSE
+  out = (blk & 1) ? x1 : x0;
+  return;
+#endif
   const typename P::Frag sel = (blk & 1) ? s1 : s0;
   out = P::pack(P::mma(x0, sel, zero4()), P::mma(x1, sel, zero4()));
 }
@@ -1082,8 +1092,8 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
     else issue_tile<P, KS1, true>(J, tile, cur);
 #pragma unroll
     for (int j = 0; j < NL; ++j) {
-      kw_cur[j] = pre ? gp(J.gbits)[((size_t)tile * NL + j) * 64 + lane] : 0xFFFFFFFFu;
-      kw_alt[j] = pre ? gp(J.gbits)[J.gb_half + ((size_t)tile * NL + j) * 64 + lane] : 0xFFFFFFFFu;
+      kw_cur[j] = pre ? *gp32(J.gbits, (uint32_t)((tile * NL + j) * 64 + lane)) : 0xFFFFFFFFu;
+      kw_alt[j] = pre ? *gp32(J.gbits, (uint32_t)(J.gb_half + (tile * NL + j) * 64 + lane)) : 0xFFFFFFFFu;
     }
   }
   if (kf == 0) stage_weights<P>(J, D, lds, aux, spp);   // first tile's loads are already in flight
@@ -1104,7 +1114,7 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
       else issue_tile<P, KS1, true>(J, tile + stride, nxt);
 #pragma unroll
       for (int j = 0; j < NL; ++j)
-        kw_nxt[j] = pre ? gbase[((size_t)(tile + stride) * NL + j) * 64 + lane] : 0xFFFFFFFFu;
+        kw_nxt[j] = pre ? *at32(gbase, (uint32_t)(((tile + stride) * NL + j) * 64 + lane)) : 0xFFFFFFFFu;
     }
     Frag xf[2][KS1];
     RowInfo ri;
@@ -1233,7 +1243,7 @@ DLAP_DEV void bwd_sdf_body(const MlpJob& J, const MlpDims& D, int slab_stride, c
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
               const int d = 16 * ub + 4 * q + r;
-              if (d < D.Dm && row < J.R) gp(J.u_out)[(size_t)row * D.Dm + d] = c[r];
+              if (d < D.Dm && row < J.R) *gp32(J.u_out, (uint32_t)(row * D.Dm + d)) = c[r];
             }
           }
         }
