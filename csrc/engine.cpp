@@ -1140,6 +1140,7 @@ class Engine {
   DevBuf<char> j_mlp_bwd_dh_;                                   // moment backward from an external dL/dh
   DevBuf<char> j_loss_eval_dense_;                              // evaluation loss jobs, dense passes
   int n_mom_jobs_ = 0, tmax_all_ = 0, gx_mom_ = 1;
+  int n_mom_tr_ = 0, tmax_mom_tr_ = 0, tmax_mom_ev_ = 0;   // train-split jobs lead the tables
   int n_eval_jobs_ = 0;
   int tmax_eval_ = 0, nmax_eval_ = 0;
 
@@ -1652,16 +1653,21 @@ class Engine {
       std::vector<RnnJob> rm;
       std::vector<MlpJob> mm;
       std::vector<WideJob> wm;
-      tmax_all_ = 0; gx_mom_ = 1;
-      for (int g = 0; g < G_; ++g)
-        for (int s = 0; s < 3; ++s) {
-          if (!splits_[s].set) continue;
-          rm.push_back(rnn_job(g, s, false));
-          mm.push_back(mlp_job(g, s, false, false, true));
-          wm.push_back(wide_job(g, s, false, true));
-          tmax_all_ = std::max(tmax_all_, splits_[s].T);
-          gx_mom_ = std::max(gx_mom_, gx_fwd_[s]);
-        }
+      // the train split's jobs first, then the evaluation splits' (ensure_moments may run the
+      // latter on the evaluation stream)
+      tmax_all_ = 0; gx_mom_ = 1; n_mom_tr_ = 0; tmax_mom_tr_ = 0; tmax_mom_ev_ = 0;
+      for (int grp = 0; grp < 2; ++grp)
+        for (int g = 0; g < G_; ++g)
+          for (int s = grp ? 1 : 0; s < (grp ? 3 : 1); ++s) {
+            if (!splits_[s].set) continue;
+            rm.push_back(rnn_job(g, s, false));
+            mm.push_back(mlp_job(g, s, false, false, true));
+            wm.push_back(wide_job(g, s, false, true));
+            tmax_all_ = std::max(tmax_all_, splits_[s].T);
+            (grp ? tmax_mom_ev_ : tmax_mom_tr_) = std::max(grp ? tmax_mom_ev_ : tmax_mom_tr_, splits_[s].T);
+            gx_mom_ = std::max(gx_mom_, gx_fwd_[s]);
+            if (!grp) ++n_mom_tr_;
+          }
       n_mom_jobs_ = (int)mm.size();
       upload(j_rnn_mom_, rm); upload(j_mlp_mom_, mm); upload(j_wide_mom_, wm);
     }
@@ -1732,6 +1738,24 @@ class Engine {
       return;
     }
     HTRACE("ensure_moments jobs=%d tmax=%d gx=%d", n_mom_jobs_, tmax_all_, gx_mom_);
+    const int n_ev = n_mom_jobs_ - n_mom_tr_;
+    if (defer_eval_gram && gram_on_ && !md_.md.wide && n_mom_tr_ > 0 && n_ev > 0) {
+      // the evaluation splits' moments (and then their Gram builds, build_gram) on the
+      // evaluation stream: only the train split's refresh + Gram precede the head epoch (which
+      // trains only); the first graph that evaluates joins them (join_eval_gram)
+      HIP_OK(hipEventRecord(ev_fork_, st_));
+      HIP_OK(hipStreamWaitEvent(st2_, ev_fork_, 0));
+      eval_gram_pending_ = true;
+      HTRACE("launch_prologue (moments, split)");
+      launch_prologue(as<RnnJob>(j_rnn_mom_), n_mom_tr_, tmax_mom_tr_, dd(), md_, st_, true, false);
+      launch_mlp_fwd(as<MlpJob>(j_mlp_mom_), n_mom_tr_, gx_mom_, md_.md, md_.KS1, md_.WMB, st_);
+      launch_prologue(as<RnnJob>(j_rnn_mom_) + n_mom_tr_, n_ev, tmax_mom_ev_, dd(), md_, st2_, true, false);
+      launch_mlp_fwd(as<MlpJob>(j_mlp_mom_) + n_mom_tr_, n_ev, gx_mom_, md_.md, md_.KS1, md_.WMB, st2_);
+      h_valid_ = true;
+      for (bool& v : gram_valid_) v = false;
+      build_gram(true);
+      return;
+    }
     HTRACE("launch_prologue");
     launch_prologue(as<RnnJob>(j_rnn_mom_), n_mom_jobs_, tmax_all_, dd(), md_, st_, true, false);
     if (md_.md.wide && zx_eval_) {

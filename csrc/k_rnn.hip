@@ -524,6 +524,9 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
     const auto sgg = gp(J.sg) + (size_t)l * T * G4;
     const auto scg = gp(J.sc) + (size_t)l * T * H;
     const auto shg = gp(J.sh) + (size_t)l * T * H;
+    // W_hh of the layer for the dense-state path's step matrices: loaded with the pre-pass
+    // (its latency hides behind the pre-pass loads), stored after the pre-pass barrier
+    const float whh_l = threadIdx.x < 64 ? params[md->lstm_w_hh[l] + (threadIdx.x < 4 * H * H ? threadIdx.x : 0)] : 0.f;
     __syncthreads();
     // parallel pre-pass: everything of the backward step that does not depend on dh_next.
     // PU elements per thread with every global load issued before the first use (one memory
@@ -571,8 +574,7 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
       float* s_W = s_y + T * 8;
       float* s_N = s_W + 64;                          // [(T-1)/2][64] pair maps N_t
       float* s_v = s_N + ((T - 1) / 2) * 64;          // [(T-1)/2][8]  pair offsets v_t
-      const auto Whh = params + md->lstm_w_hh[l];
-      if (threadIdx.x < 64) s_W[threadIdx.x] = Whh[threadIdx.x];
+      if (threadIdx.x < 64) s_W[threadIdx.x] = whh_l;
       __syncthreads();
       // one thread per (t, row i): the step's 24 coefficients as six 16-byte reads, the row's
       // W_hh column in registers, two 16-byte stores
