@@ -154,12 +154,18 @@ def measure_ensemble(d, cfg, pc, seed_panel: int = 0):
     comm.barrier(d)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    batches = None
-    if d.rank == 0:
-        tr, va, te = make_panel(seed=seed_panel, device=f"cuda:{d.local_rank}", cfg=pc, keep_on_device=True)
-        batches = {"train": tr, "valid": va, "test": te}
+    # the synthetic panel is generated on every rank's GPU from the same seed (bit-exact: the
+    # same kernels and generator stream), so no rank waits for a broadcast; one small all-gather
+    # of per-split checksums proves the copies identical (comm.broadcast_batches is the path for
+    # panels read from disk, parallel/ensemble.py)
+    tr, va, te = make_panel(seed=seed_panel, device=f"cuda:{d.local_rank}", cfg=pc, keep_on_device=True)
+    batches = {"train": tr, "valid": va, "test": te}
     if d.active:
-        batches = comm.broadcast_batches(d, batches)            # RCCL broadcast over xGMI
+        ck = np.array([[float(torch.nan_to_num(b[k].double()).sum()) for b in (tr, va, te)
+                        for k in ("returns", "individual_features")]])
+        allck = comm.all_gather_rows(d, ck, d.world, [d.rank])
+        if not (allck == allck[0:1]).all():
+            raise RuntimeError("bench.py: ranks generated different synthetic panels")
     t_panel = time.perf_counter() - t0
     res = run_ensemble(cfg, batches, ENSEMBLE_SEEDS, d, epochs=(256, 64, 1024), lr=1e-3, ignore_epoch=64,
                        print_freq=1024)
