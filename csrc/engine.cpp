@@ -192,7 +192,6 @@ class Engine {
          float residual, int G, int max_epochs, bool fp32)
       : G_(G), max_epochs_(max_epochs) {
     g_live_engines.fetch_add(1);
-    unroll_ = std::max(1, env_int("DLAP_UNROLL", 1));
     prio_ = env_int("DLAP_PRIO", 0) != 0;
     if (prio_) {   // the training chain (critical path) ahead of the evaluation branch
       int lo = 0, hi = 0;
@@ -253,7 +252,6 @@ class Engine {
     rnn_overlap_eval_ = env_int("DLAP_RNN_OVERLAP_EVAL", 0) != 0;
     prog_mode_ = env_int("DLAP_PROG_MODE", 1);
     prog_limit_ = (unsigned)env_int("DLAP_PROG_SPIN_LIMIT", 1 << 22);
-    graph_copies_ = env_int("DLAP_GRAPH_COPIES", 1);
     fused_p2_ = env_int("DLAP_FUSED_PHASE2", 0) != 0;
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
                residual, fp32);
@@ -669,40 +667,25 @@ class Engine {
       for (int e = 0; e < n; ++e) enqueue_epoch(phase, lr, ignore_epoch, sel);
       return;
     }
-    // DLAP_GRAPH_COPIES: several executors of the same epoch graph, launched in turn. Every
-    // hipGraphLaunch of these multi-branch graphs blocks the host ~one epoch (HIP API trace,
-    // profiles/r4_hostgaps_short.txt); alternating executors did not remove that (the wait is
-    // not per executor) and measured 2-3% slower, so the default is one.
-    const int C = std::max(1, std::min(8, graph_copies_));
+    // One executor per epoch graph. (Measured and dropped in round 4: alternating several
+    // executors of the same graph -- every hipGraphLaunch of these multi-branch graphs blocks the
+    // host ~one epoch, and the wait is not per executor, profiles/r4_hostgaps_short.txt -- and
+    // unrolling several pipelined epochs into one graph: both 2-5% slower.)
     if (!pipe) {
-      std::vector<hipGraphExec_t> gs;
-      for (int c = 0; c < C; ++c)            // (all C always: a later run never captures)
-        gs.push_back(graph_for(graph_key(phase, lr, ignore_epoch, sel, 200 + c),
-                               [&] { enqueue_epoch(phase, lr, ignore_epoch, sel); }));
-      for (int e = 0; e < n; ++e) HIP_OK(hipGraphLaunch(gs[e % gs.size()], st_));
+      hipGraphExec_t g = graph_for(graph_key(phase, lr, ignore_epoch, sel, 200),
+                                   [&] { enqueue_epoch(phase, lr, ignore_epoch, sel); });
+      for (int e = 0; e < n; ++e) HIP_OK(hipGraphLaunch(g, st_));
       return;
     }
     hipGraphExec_t head = graph_for(graph_key(phase, lr, ignore_epoch, sel, 1), [&] { enqueue_head(phase, lr); });
-    std::vector<hipGraphExec_t> bodies;
-    for (int c = 0; c < C; ++c)
-      bodies.push_back(graph_for(graph_key(phase, lr, ignore_epoch, sel, c ? 300 + c : 2),
-                                 [&] { enqueue_pipe(phase, lr, ignore_epoch, sel); }));
+    hipGraphExec_t body = graph_for(graph_key(phase, lr, ignore_epoch, sel, 2),
+                                    [&] { enqueue_pipe(phase, lr, ignore_epoch, sel); });
     hipGraphExec_t tail = graph_for(graph_key(phase, lr, ignore_epoch, sel, 3),
                                     [&] { enqueue_tail(phase, ignore_epoch, sel); });
-    // U pipelined epochs per graph launch: no launch gap between the epochs of one graph
-    const int U = unroll_;
-    hipGraphExec_t bodyU = nullptr;
-    if (U > 1)                            // (captured even when this run is short: a later run
-      bodyU = graph_for(graph_key(phase, lr, ignore_epoch, sel, 100 + U), [&] {   // never captures
-        for (int u = 0; u < U; ++u) enqueue_pipe(phase, lr, ignore_epoch, sel);  // inside a timed run)
-      });
     HTRACE("launch head");
     HIP_OK(hipGraphLaunch(head, st_));
     join_eval_gram();                     // the next graphs evaluate
-    int e = 1;
-    if (bodyU)
-      for (; e + U <= n; e += U) HIP_OK(hipGraphLaunch(bodyU, st_));
-    for (int k = 0; e < n; ++e, ++k) HIP_OK(hipGraphLaunch(bodies[k % bodies.size()], st_));
+    for (int e = 1; e < n; ++e) HIP_OK(hipGraphLaunch(body, st_));
     HTRACE("launch tail");
     HIP_OK(hipGraphLaunch(tail, st_));
     HTRACE("run_epochs done");
@@ -981,7 +964,6 @@ class Engine {
   DevBuf<char> j_pack_;                      // per-model re-pack jobs
   struct FwdTables { DevBuf<char> r, m, l, w; bool built = false; };
   std::map<int, FwdTables> fwd_tables_;      // module-API forward job tables (per split / mode)
-  int unroll_ = 1;                           // pipelined epochs per graph launch (DLAP_UNROLL)
   bool prio_ = false;                        // stream/node priorities (DLAP_PRIO)
   hipStream_t st2_ = nullptr;                // evaluation branch of the pipelined epoch graph
   hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr, ev_mid_ = nullptr, ev_a_ = nullptr;
@@ -1047,7 +1029,6 @@ class Engine {
   int prog_mode_ = 1;                        // DLAP_PROG_MODE (see MlpJob::prog_mode)
   unsigned prog_limit_ = 1u << 22;           // DLAP_PROG_SPIN_LIMIT (see MlpJob::prog_limit)
   bool fused_p2_ = false;                    // DLAP_FUSED_PHASE2: fused training forward in phase 2 too
-  int graph_copies_ = 1;                     // executors per epoch graph, launched in turn (run_epochs)
   DevBuf<int> prog_;
   // Co-residency guarantee of the fused LSTM + tower launches: resident workgroups of the fused
   // kernel on the device (occupancy query, rebuild_jobs) for the train split / the evaluation

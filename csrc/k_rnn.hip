@@ -342,37 +342,15 @@ __global__ __launch_bounds__(64) void k_lstm_gl(const RnnJob* __restrict__ jobs,
 
 // ---------------------------------------------------------------------- k_lstm_gls -----
 // k_lstm_gl with every per-step output kept in LDS (lstm_gls.h): one wave per job.
-// FUSE: the workgroup (LSTM_FUSE_THREADS) first computes the layer-0 input projections of its
-// job straight into the LDS staging area with all its waves (k_proj + the staging copy in one
-// launch), then waves 1.. exit and wave 0 runs the recurrence (see launch_prologue).
-#define LSTM_FUSE_THREADS 1024
-template <int HM, bool DPPG, bool FUSE>
-__global__ __launch_bounds__(FUSE ? LSTM_FUSE_THREADS : 64) void k_lstm_gls(const RnnJob* __restrict__ jobs,
-                                                                            const ModelDesc* __restrict__ md) {
+template <int HM, bool DPPG>
+__global__ __launch_bounds__(64) void k_lstm_gls(const RnnJob* __restrict__ jobs, const ModelDesc* __restrict__ md) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const RnnJob& J = jobs[blockIdx.x];
   if (md->nrnn == 0) return;
   const int tsb = J.sc != nullptr ? 0 : 4;
   const bool tsm = J.sc != nullptr || blockIdx.x == gridDim.x - 1;
   RNN_TS(tsb + 0, tsm);
-  if constexpr (FUSE) {
-    const int T = J.T, G4 = 4 * (DPPG ? HM : md->H);
-    const int w = threadIdx.x >> 6, nw = blockDim.x >> 6, l = threadIdx.x & 63;
-    const int nto = (G4 + 15) >> 4, ntiles = ((T + 15) >> 4) * nto;
-    for (int tile = w; tile < ntiles; tile += nw) {
-      const int t0 = (tile / nto) * 16, o0 = (tile % nto) * 16;
-      const f32x4 acc = proj_tile(J, md, t0, o0);
-      const int o = o0 + (l & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int t = t0 + 4 * (l >> 4) + r;
-        if (t < T && o < G4) sm[t * G4 + o] = acc[r];
-      }
-    }
-    __syncthreads();
-    if (w > 0) return;
-  }
-  lstm_gls_body<HM, DPPG, !FUSE, false>(J, md, sm, nullptr, tsm ? g_rnn_ts : nullptr, tsb);
+  lstm_gls_body<HM, DPPG, true, false>(J, md, sm, nullptr, tsm ? g_rnn_ts : nullptr, tsb);
 }
 
 static const bool g_rtrace = [] { const char* v = std::getenv("DLAP_TRACE_HOST"); return v && *v == '1'; }();
@@ -390,24 +368,16 @@ void launch_proj(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* md, c
 
 void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* md, const ModelDesc& mh,
                      hipStream_t st, bool abias, bool lstm) {
-  // DLAP_LSTM_FUSE_PROJ=1: the LSTM workgroup projects its own inputs (k_lstm_gls<.., FUSE>) and
-  // k_proj only builds the moment network's per-period bias table. Off by default: one
-  // workgroup streams the whole macro panel through one CU (15 us at T = 240, M = 178, against
-  // 6 us for k_proj's T/16 workgroups plus the 3.5 us staging copy). The bias table is built
-  // only when a tower launched after this prologue reads it.
-  const char* fz_env = std::getenv("DLAP_LSTM_FUSE_PROJ");
-  const char* ul_env0 = std::getenv("DLAP_LSTM_UNIT_LANES");
-  const char* gls_env0 = std::getenv("DLAP_LSTM_GLS");
-  const bool fuse = mh.nrnn > 0 && (fz_env && std::atoi(fz_env) == 1) && !(ul_env0 && std::atoi(ul_env0) == 1) &&
-                    !(gls_env0 && std::atoi(gls_env0) == 0) && mh.H <= 16 &&
-                    gls_lds_floats(tmax, mh.H) * sizeof(float) <= 64 * 1024;
+  // k_proj: the layer-0 gate projections (unless only the moment bias is asked for) and, with
+  // abias, the moment network's per-period bias table; then the recurrence: the gate-per-lane
+  // form with its outputs in LDS (k_lstm_gls) when they fit in 64 KiB, the same form with
+  // global outputs (k_lstm_gl: long splits) otherwise, and the unit-per-lane form (k_lstm) for
+  // H > 16
   const int G4 = mh.nrnn > 0 ? 4 * mh.H : 0;
-  // column tiles for k_proj: all (abias, unfused), the moment ones only (abias, fused; a tile
-  // shared by the last gates and the first moment columns stays), the gates only, or none
-  const int y0 = abias && (fuse || !lstm) ? G4 / 16 : 0;
-  const int ny = abias ? mh.proj_np / 16 - y0 : (fuse || !lstm ? 0 : (G4 + 15) / 16);
-  RTRACE("prologue jobs=%p njobs=%d tmax=%d H=%d nrnn=%d proj_np=%d y0=%d ny=%d fuse=%d st=%p", (const void*)jobs,
-         njobs, tmax, mh.H, mh.nrnn, mh.proj_np, y0, ny, (int)fuse, (void*)st);
+  const int y0 = abias && !lstm ? G4 / 16 : 0;
+  const int ny = abias ? mh.proj_np / 16 - y0 : (lstm ? (G4 + 15) / 16 : 0);
+  RTRACE("prologue jobs=%p njobs=%d tmax=%d H=%d nrnn=%d proj_np=%d y0=%d ny=%d st=%p", (const void*)jobs,
+         njobs, tmax, mh.H, mh.nrnn, mh.proj_np, y0, ny, (void*)st);
   if (ny > 0) {
     hipLaunchKernelGGL(k_proj, dim3((tmax + 15) / 16, ny, njobs), dim3(64), 0, st, jobs, md, y0);
     HIP_OK(hipGetLastError());
@@ -416,31 +386,21 @@ void launch_prologue(const RnnJob* jobs, int njobs, int tmax, const ModelDesc* m
   if (mh.nrnn > 0 && lstm) {
     const bool stage = tmax * 4 * mh.H <= 12288;     // 48 KiB of LDS
     const size_t sh = stage ? (size_t)tmax * 4 * mh.H * sizeof(float) : 0;
-#define L_CASE(HM) \
-    if (stage) hipLaunchKernelGGL((k_lstm<HM, true>), dim3(njobs), dim3(64), sh, st, jobs, md); \
-    else hipLaunchKernelGGL((k_lstm<HM, false>), dim3(njobs), dim3(64), sh, st, jobs, md);
+    const bool gls = mh.H <= 16 && gls_lds_floats(tmax, mh.H) * sizeof(float) <= 64 * 1024;
+    const size_t shg = gls_lds_floats(tmax, mh.H) * sizeof(float);
 #define G_CASE(HM, DP) \
     if (stage) hipLaunchKernelGGL((k_lstm_gl<HM, DP, true>), dim3(njobs), dim3(64), sh, st, jobs, md); \
     else hipLaunchKernelGGL((k_lstm_gl<HM, DP, false>), dim3(njobs), dim3(64), sh, st, jobs, md);
-    const char* ul_env = std::getenv("DLAP_LSTM_UNIT_LANES");
-    const char* gls_env = std::getenv("DLAP_LSTM_GLS");
-    const bool gls = !(gls_env && std::atoi(gls_env) == 0) && mh.H <= 16 &&
-                     gls_lds_floats(tmax, mh.H) * sizeof(float) <= 64 * 1024;
-    const size_t shg = gls_lds_floats(tmax, mh.H) * sizeof(float);
-#define S_CASE(HM, DP) \
-    if (fuse) hipLaunchKernelGGL((k_lstm_gls<HM, DP, true>), dim3(njobs), dim3(LSTM_FUSE_THREADS), shg, st, jobs, md); \
-    else hipLaunchKernelGGL((k_lstm_gls<HM, DP, false>), dim3(njobs), dim3(64), shg, st, jobs, md);
-    if (ul_env && std::atoi(ul_env) == 1) {       // unit-per-lane form (reference for tests)
-      if (mh.H <= 4) { L_CASE(4) } else if (mh.H <= 8) { L_CASE(8) } else if (mh.H <= 16) { L_CASE(16) } else { L_CASE(32) }
-    } else if (gls) {
+#define S_CASE(HM, DP) hipLaunchKernelGGL((k_lstm_gls<HM, DP>), dim3(njobs), dim3(64), shg, st, jobs, md);
+    if (gls) {
       if (mh.H == 1) { S_CASE(1, true) } else if (mh.H == 2) { S_CASE(2, true) }
       else if (mh.H == 3) { S_CASE(3, true) } else if (mh.H == 4) { S_CASE(4, true) }
       else if (mh.H <= 8) { S_CASE(8, false) } else { S_CASE(16, false) }
     } else if (mh.H == 1) { G_CASE(1, true) } else if (mh.H == 2) { G_CASE(2, true) }
     else if (mh.H == 3) { G_CASE(3, true) } else if (mh.H == 4) { G_CASE(4, true) }
     else if (mh.H <= 8) { G_CASE(8, false) } else if (mh.H <= 16) { G_CASE(16, false) }
-    else { L_CASE(32) }
-#undef L_CASE
+    else if (stage) hipLaunchKernelGGL((k_lstm<32, true>), dim3(njobs), dim3(64), sh, st, jobs, md);
+    else hipLaunchKernelGGL((k_lstm<32, false>), dim3(njobs), dim3(64), sh, st, jobs, md);
 #undef G_CASE
 #undef S_CASE
     HIP_OK(hipGetLastError());
