@@ -835,7 +835,8 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
       }
     }
   };
-  bf16x8 xc[2][4], xn[2][4];
+  // panel chunks streamed two ahead (xn, xn2): 16 KiB per wave in flight
+  bf16x8 xc[2][4], xn[2][4], xn2[2][4];
   f32x4 acc[2][NU];
 #pragma unroll
   for (int b = 0; b < 2; ++b)
@@ -845,11 +846,19 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
   issue_rowti(J, tile, ti);
   issue(tile, 0, xc);
   int ch = 0;
+  auto advance = [&](int tl, int c, int& t2, int& c2) {
+    t2 = tl; c2 = c + 1;
+    if (c2 == nch) { c2 = 0; t2 += stride; }
+  };
+  int ntl, nc;
+  advance(tile, ch, ntl, nc);
+  bool more = ntl < ntiles;
+  if (more) issue(ntl, nc, xn);
   for (;;) {
-    int ntl = tile, nc = ch + 1;
-    if (nc == nch) { nc = 0; ntl += stride; }
-    const bool more = ntl < ntiles;
-    if (more) issue(ntl, nc, xn);
+    int ntl2, nc2;
+    advance(ntl, nc, ntl2, nc2);
+    const bool more2 = more && ntl2 < ntiles;
+    if (more2) issue(ntl2, nc2, xn2);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int ks = 4 * ch + s;
@@ -936,10 +945,16 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
     if (!more) break;
     tile = ntl;
     ch = nc;
+    ntl = ntl2;
+    nc = nc2;
+    more = more2;
 #pragma unroll
     for (int b = 0; b < 2; ++b)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) xc[b][s] = xn[b][s];
+      for (int s = 0; s < 4; ++s) {
+        xc[b][s] = xn[b][s];
+        xn[b][s] = xn2[b][s];
+      }
   }
 }
 

@@ -31,10 +31,12 @@ template <int J>
 DLAP_DEV float row_bcast(float v) {
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x150 + J, 0xF, 0xF, true));
 }
+// acc + sum_j w[j] h_j: the accumulator (the step's input projection) enters the first FMA, so the
+// chain is FMA | FMA | add (three dependent levels) instead of mul | fma | add | add
 template <int HM>
-DLAP_DEV float bcast_dot_row(const float (&w)[HM], float v) {
+DLAP_DEV float bcast_dot_row(const float (&w)[HM], float v, float acc = 0.f) {
   static_assert(HM >= 1 && HM <= 4, "row-broadcast dot: 1..4 units");
-  float p0 = w[0] * row_bcast<0>(v);
+  float p0 = fmaf(w[0], row_bcast<0>(v), acc);
   if constexpr (HM == 1) return p0;
   float p1 = w[1] * row_bcast<1>(v);
   if constexpr (HM == 2) return p0 + p1;
@@ -152,7 +154,7 @@ DLAP_DEV void lstm_gls_body(const RnnJob& J, const ModelDesc* __restrict__ md, f
     // lanes H <= j < HM carry zero weights
     float h = ul && J.h0 ? gp(J.h0)[l * H + L] : 0.f, c = ul && J.c0 ? gp(J.c0)[l * H + L] * KC : 0.f;
     auto cell = [&](int t, float pre) {
-      if constexpr (DPPG) pre += bcast_dot_row<HM>(whh, h);
+      if constexpr (DPPG) pre = bcast_dot_row<HM>(whh, h, pre);
       else pre += bcast_dot<HM>(whh, h);
       const float y = kb * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(pre)) + kc;
       const float gf = gl_gather<HM, DPPG>(y, H, 1);
