@@ -19,6 +19,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned short u16;
 
 #define DLAP_DEV __device__ __forceinline__
+#define DLAP_HD __host__ __device__ __forceinline__
 
 // Pointers loaded from job records are generic (flat) to the compiler. A flat access counts
 // against both vmcnt and lgkmcnt, so every LDS wait would also wait for outstanding global

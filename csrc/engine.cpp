@@ -156,7 +156,7 @@ struct ModelSplitWS {   // per (model, split)
 
 struct ModelState {
   DevBuf<float> params, grads, m, v, snap_loss, snap_sharpe, gnorm, best, aux, hist, wproj;
-  DevBuf<int> adam_step, drop_step, snap_flags, ep;
+  DevBuf<int> adam_step, drop_step, snap_flags, ep, upd_ctr;
   DevBuf<uint16_t> blob, blob0;
   unsigned seed = 0;
   unsigned tower_salt = 0;  // XOR-ed (mixed) into the towers' dropout seed only (N-sharding: per rank)
@@ -270,13 +270,32 @@ class Engine {
       // packed weights: evaluation copy, then the training copy (dropout scale folded in)
       S.gnorm.alloc(1); S.best.alloc(3); S.aux.alloc((size_t)2 * md_.md.aux_floats);
       S.hist.alloc((size_t)max_epochs_ * HIST_W);
-      S.adam_step.alloc(2); S.drop_step.alloc(1); S.snap_flags.alloc(2); S.ep.alloc(2);
+      S.adam_step.alloc(2); S.drop_step.alloc(1); S.snap_flags.alloc(2); S.ep.alloc(2); S.upd_ctr.alloc(1);
       S.blob.alloc((size_t)2 * md_.md.blob_frags * 512 * xw());   // bf16 (or fp32: 2 u16 each)
       S.blob0.alloc((size_t)std::max(1, md_.md.b0_frags) * 512 * xw());
-      S.wproj.alloc((size_t)(md_.proj_mp + 1) * md_.proj_np);
+      S.wproj.alloc((size_t)(md_.proj_mp + 2) * md_.proj_np);
     }
     ws_.resize((size_t)G * 3);
+    build_pack_inverse();
     upload_pack_jobs();
+  }
+  // Scatter lists of the fused re-pack: pack_index_host names the parameter behind every packed
+  // element (from the same gathers k_pack uses), inverted here into
+  // fixed-width lists per parameter (PACK_FAN slots). Without them (DLAP_FUSED_PACK=0, indices
+  // past fp32's exact integers, or a parameter with more copies) k_pack runs after k_adam.
+  void build_pack_inverse() {
+    if (env_int("DLAP_FUSED_PACK", 1) == 0 || md_.P >= (1 << 24)) return;
+    const int total = pack_total(md_);
+    std::vector<int> h(total);
+    pack_index_host(md_, h.data());
+    std::vector<int> code((size_t)md_.P * PACK_FAN, -1), fan(md_.P, 0);
+    for (int e = 0; e < total; ++e) {
+      if (h[e] < -1 || h[e] >= md_.P) throw std::runtime_error("pack_index_host: parameter index out of range");
+      if (h[e] < 0) continue;
+      if (fan[h[e]] == PACK_FAN) return;             // a parameter with more copies: separate k_pack
+      code[(size_t)h[e] * PACK_FAN + fan[h[e]]++] = e;
+    }
+    up(inv_code_, code.data(), code.size());
   }
   // per-model re-pack jobs (buffers allocated in the constructor, never reallocated)
   void upload_pack_jobs() {
@@ -962,6 +981,7 @@ class Engine {
   hipStream_t own_st_ = nullptr;             // the engine's stream (st_ may be an external one)
   bool ext_stream_ = false;
   DevBuf<char> j_pack_;                      // per-model re-pack jobs
+  DevBuf<int> inv_code_;                     // parameter -> packed elements (k_adam's fused re-pack)
   struct FwdTables { DevBuf<char> r, m, l, w; bool built = false; };
   std::map<int, FwdTables> fwd_tables_;      // module-API forward job tables (per split / mode)
   bool prio_ = false;                        // stream/node priorities (DLAP_PRIO)
@@ -1082,6 +1102,7 @@ class Engine {
     d["eval_gx_solo"] = fused_grid(eval_grid(), n_eval_jobs_, cap_eval_);
     // backward launch shape: fine slabs per model (R-only partition), fine slabs per workgroup
     d["bwd_nfine"] = nfine_; d["bwd_fpw"] = fpw_;
+    d["fused_pack"] = inv_code_.p != nullptr;
     d["bwd_lds_fpw1"] = (long)mlp_bwd_lds_bytes(md_.md, slab_stride(), 1);
     d["bwd_lds_fpw4"] = (long)mlp_bwd_lds_bytes(md_.md, slab_stride(), 4);
     return d;
@@ -1615,6 +1636,7 @@ class Engine {
       U.dg = W.dg.p; U.dx = W.dx.p; U.dab = W.dab.p; U.scal = W.scal.p; U.scal_prev = W.scal_prev.p;
       U.h0 = W.h0.p; U.c0 = W.c0.p; U.dh0 = W.dh0.p; U.dc0 = W.dc0.p;
       U.T = splits_[0].T; U.seed = S.seed; U.lr = S.lr; U.prog = prog_ptr(g, 0); U.dropout = S.dropout;
+      U.inv_code = inv_code_.p; U.upd_ctr = S.upd_ctr.p;
       uj.push_back(U);
     }
     n_eval_jobs_ = (int)le.size();
@@ -1876,7 +1898,7 @@ class Engine {
   void enqueue_train(int phase, float lr) {
     enqueue_train_grads(phase);
     HTRACE("launch_update");
-    launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);
+    launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_, inv_code_.p != nullptr);
   }
   void enqueue_eval(hipStream_t st) {
     enqueue_eval_prologue(st);
@@ -1928,7 +1950,7 @@ class Engine {
   void enqueue_epoch(int phase, float lr, int ignore_epoch, float sel) {
     enqueue_train_grads(phase);
     HTRACE("launch_update");
-    launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);
+    launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_, inv_code_.p != nullptr);
     if (phase != 2) { SoloScope solo(eval_solo_); enqueue_eval(st_); }
     enqueue_epoch_end(phase, ignore_epoch, sel, st_);
   }
@@ -1936,7 +1958,7 @@ class Engine {
     enqueue_train_grads(phase);
     enqueue_dropmask(phase, 1, st_);                     // masks of the first pipelined epoch
     HTRACE("launch_update");
-    launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);
+    launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_, inv_code_.p != nullptr);
   }
   void enqueue_pipe(int phase, float lr, int ignore_epoch, float sel) {
     HIP_OK(hipEventRecord(ev_fork_, st_));
@@ -1967,7 +1989,7 @@ class Engine {
         HIP_OK(hipEventRecord(ev_join_, st2_));
         HIP_OK(hipStreamWaitEvent(st_, ev_join_, 0));
         HTRACE("launch_update");
-        launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);
+        launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_, inv_code_.p != nullptr);
         return;
       }
       if (mark) HIP_OK(hipStreamWaitEvent(st2_, ev_a_, 0));
@@ -2001,7 +2023,7 @@ class Engine {
     HIP_OK(hipEventRecord(ev_join_, st2_));               // (train monitor ran on st2_ too)
     HIP_OK(hipStreamWaitEvent(st_, ev_join_, 0));
     HTRACE("launch_update");
-    launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_);
+    launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_, inv_code_.p != nullptr);
   }
   struct SoloScope {
     bool& f;

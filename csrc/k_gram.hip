@@ -18,9 +18,8 @@
 //   inner index e of Gc = i * K + k (h is [T][N][K], so a row of the operand is contiguous):
 //   lane (r = l & 15, q = l >> 4) loads elements e0 + 4q .. +3 of row t0 + r as one 16-byte
 //   load; MFMA j of the chunk takes element j (k-slot q <-> e0 + 4q + j), so the four MFMAs of
-//   a 16-element chunk cover it once. Gu's inner index is the stock: a lane whose quad starts a
-//   stock (e % K == 0, K % 4 == 0) contributes a_{t,i}, the others 0 -- one more MFMA per chunk.
-//   Unconditional-only jobs (h == nullptr) run the inner axis over stocks directly.
+//   a 16-element chunk cover it once. Gu runs its own inner axis over stocks (4 per MFMA) in
+//   both modes; unconditional-only jobs (h == nullptr) run that loop alone.
 //   Block partials go to part[job][block-slice][2][T][T] (upper-triangle tiles only).
 // k_gram_reduce: fixed-order sum over the slices, mirrored to the full symmetric matrices.
 #include <cstdlib>
@@ -81,7 +80,6 @@ __global__ __launch_bounds__(64 * GB_WAVES) void k_gram_build(const GramJob* __r
     struct Batch {
       f32x4 hv[GB_U][4];
       float rm[GB_U][4], iv[GB_U];
-      bool first[GB_U];
     };
     auto load = [&](int cb, Batch& B) {
 #pragma unroll
@@ -90,7 +88,6 @@ __global__ __launch_bounds__(64 * GB_WAVES) void k_gram_build(const GramJob* __r
         const bool eok = cb + u < c1 && e < E;
         const unsigned ec = eok ? (unsigned)e : 0u;
         const int i = (int)(ec / uK);
-        B.first[u] = eok && (ec - (unsigned)i * uK) == 0u;
         B.iv[u] = eok ? invT[i] : 0.f;
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -118,11 +115,6 @@ __global__ __launch_bounds__(64 * GB_WAVES) void k_gram_build(const GramJob* __r
 #pragma unroll
             for (int y = 0; y < 2; ++y) gc[x][y] = mfma_f64(va[x], vb[y], gc[x][y]);
         }
-#pragma unroll
-        for (int x = 0; x < 2; ++x)
-#pragma unroll
-          for (int y = 0; y < 2; ++y)
-            gu[x][y] = mfma_f64(B.first[u] ? a[x] : 0.0, B.first[u] ? a[2 + y] : 0.0, gu[x][y]);
       }
     };
     Batch b0, b1;
@@ -134,8 +126,10 @@ __global__ __launch_bounds__(64 * GB_WAVES) void k_gram_build(const GramJob* __r
       if (cb + 2 * GB_U < c1) load(cb + 2 * GB_U, b0);
       comp(b1);
     }
-  } else {
-    // unconditional only: inner axis = stocks, 4 per MFMA (k-slot q <-> stock 4c + q)
+  }
+  {
+    // Gu (both modes): inner axis = stocks, 4 per MFMA (k-slot q <-> stock 4c + q) -- dense
+    // operands, an eighth of the MFMAs of riding along Gc's (stock, moment) chunks
     const int nch = (N + 3) / 4;
     const int c0 = (int)((long)nch * sl / nslice), c1 = (int)((long)nch * (sl + 1) / nslice);
     for (int cb = c0; cb < c1; cb += GB_U) {
@@ -203,9 +197,23 @@ __global__ __launch_bounds__(256) void k_gram_reduce(const GramJob* __restrict__
   const size_t T2 = (size_t)T * T, src = (size_t)a * T + b;
   const auto part = gp(J.part);
   double sc = 0.0, su = 0.0;
-  for (int s = 0; s < nslice; ++s) {
-    sc += part[(size_t)s * 2 * T2 + src];
-    su += part[(size_t)s * 2 * T2 + T2 + src];
+  // RB slices' loads in flight before the (in-order) adds: one memory round trip per RB slices
+  // instead of one per slice (same summation order)
+  constexpr int RB = 16;
+  for (int s0 = 0; s0 < nslice; s0 += RB) {
+    double pc[RB], pu[RB];
+#pragma unroll
+    for (int k = 0; k < RB; ++k) {
+      const size_t o = (size_t)min(s0 + k, nslice - 1) * 2 * T2 + src;
+      pc[k] = part[o];
+      pu[k] = part[o + T2];
+    }
+#pragma unroll
+    for (int k = 0; k < RB; ++k)
+      if (s0 + k < nslice) {
+        sc += pc[k];
+        su += pu[k];
+      }
   }
   gp(J.G)[e] = sc;
   gp(J.G)[T2 + e] = su;

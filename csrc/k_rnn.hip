@@ -48,8 +48,8 @@ DLAP_DEV float ftanh(float x) {
 // (moment layer-0 per-period bias, zero-padded to 64): a [T x MP] . [MP x NP] fp32 GEMM on
 // the matrix cores. grid (ceil(T/16), NP/16, jobs), one wave per 16x16 output tile, K = 4 per
 // v_mfma_f32_16x16x4f32 (full fp32 products / accumulation). Operands come straight from
-// global memory (macro rows, and the k_pack-produced wproj [MP+1][NP] whose last row holds
-// the biases): all loads of a tile are independent, so the tile costs ~one memory round trip.
+// global memory (macro rows, and the k_pack-produced wproj [MP+2][NP] whose last two rows
+// hold the biases): all loads of a tile are independent, so the tile costs ~one memory round trip.
 //   A (16x4): lane l -> A[t = l&15][k = l>>4];  B (4x16): lane l -> B[k = l>>4][o = l&15]
 //   C (16x16): lane l -> C[t = 4*(l>>4) + r][o = l&15]
 // One 16 (periods) x 16 (outputs) tile of the projection on one wave: returns lane l's
@@ -77,7 +77,7 @@ DLAP_DEV f32x4 proj_tile(const RnnJob& J, const ModelDesc* md, int t0, int o0) {
 #pragma unroll
     for (int s = 0; s < PROJ_KC; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
   }
-  const float bias = wcol[(size_t)MP * NP];
+  const float bias = wcol[(size_t)MP * NP] + wcol[(size_t)(MP + 1) * NP];   // b_ih + b_hh (b_m0 + 0)
   return acc + bias;
 }
 
@@ -543,28 +543,41 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
         float wc[16];                                  // wc[r] = W_hh[r][i] (rows r = 4q + k)
 #pragma unroll
         for (int r = 0; r < 16; ++r) wc[r] = s_W[r * 4 + (i & 3)];
-        for (int t = threadIdx.x >> 3; t < T; t += 32) {
-          const f32x4* q4 = reinterpret_cast<const f32x4*>(s_cf + t * (LSTM_NCOEF * 4));
-          const f32x4 A = q4[0], Bi = q4[1], Bf = q4[2], Bg = q4[3], Bo = q4[4], F = q4[5];
-          f32x4 lo, hi;
-          if (i < 4) {                                 // row i of dh_next' (= unit j = i)
+        // SU steps per pass with every coefficient read issued before the first store (the stores
+        // may alias the reads as far as the compiler knows: one LDS round trip per pass, not per step)
+        constexpr int SU = 4;
+        for (int t0 = threadIdx.x >> 3; t0 < T; t0 += 32 * SU) {
+          f32x4 A[SU], Bi[SU], Bf[SU], Bg[SU], Bo[SU], F[SU];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-              const float pc = wc[k] * Bi[k] + wc[4 + k] * Bf[k] + wc[8 + k] * Bg[k];
-              lo[k] = fmaf(pc, A[k], wc[12 + k] * Bo[k]);
-              hi[k] = pc;
-            }
-          } else {                                     // row of dc_next' (unit k = i - 4)
-            const int k = i - 4;
-#pragma unroll
-            for (int c = 0; c < 4; ++c) {
-              lo[c] = c == k ? F[c] * A[c] : 0.f;
-              hi[c] = c == k ? F[c] : 0.f;
-            }
+          for (int u = 0; u < SU; ++u) {
+            const int t = min(t0 + 32 * u, T - 1);
+            const f32x4* q4 = reinterpret_cast<const f32x4*>(s_cf + t * (LSTM_NCOEF * 4));
+            A[u] = q4[0]; Bi[u] = q4[1]; Bf[u] = q4[2]; Bg[u] = q4[3]; Bo[u] = q4[4]; F[u] = q4[5];
           }
-          f32x4* dst = reinterpret_cast<f32x4*>(s_M + t * 64 + 8 * i);
-          dst[0] = lo;
-          dst[1] = hi;
+#pragma unroll
+          for (int u = 0; u < SU; ++u) {
+            const int t = t0 + 32 * u;
+            if (t >= T) break;
+            f32x4 lo, hi;
+            if (i < 4) {                               // row i of dh_next' (= unit j = i)
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                const float pc = wc[k] * Bi[u][k] + wc[4 + k] * Bf[u][k] + wc[8 + k] * Bg[u][k];
+                lo[k] = fmaf(pc, A[u][k], wc[12 + k] * Bo[u][k]);
+                hi[k] = pc;
+              }
+            } else {                                   // row of dc_next' (unit k = i - 4)
+              const int k = i - 4;
+#pragma unroll
+              for (int c = 0; c < 4; ++c) {
+                lo[c] = c == k ? F[u][c] * A[u][c] : 0.f;
+                hi[c] = c == k ? F[u][c] : 0.f;
+              }
+            }
+            f32x4* dst = reinterpret_cast<f32x4*>(s_M + t * 64 + 8 * i);
+            dst[0] = lo;
+            dst[1] = hi;
+          }
         }
       }
       __syncthreads();
@@ -572,25 +585,42 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
       // points t = T-1-2p (p = 1 .. np), N_t = M_{t+1} M_{t+2}, v_t = M_{t+1} (dout_{t+1}, 0) +
       // (dout_t, 0); one thread per (link, row), fixed summation order
       const int npair = (T - 1) / 2;
-      for (int task = threadIdx.x; task < npair * 8; task += 256) {
-        const int p = 1 + (task >> 3), i = task & 7, t = T - 1 - 2 * p;
-        const f32x4* ra = reinterpret_cast<const f32x4*>(s_M + (t + 1) * 64 + 8 * i);
-        const f32x4 a0 = ra[0], a1 = ra[1];
-        const float a[8] = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-        const f32x4* mb = reinterpret_cast<const f32x4*>(s_M + (t + 2) * 64);
-        f32x4 lo = zero4(), hi = zero4();
+      constexpr int PU2 = 2;                           // links per pass, reads hoisted (as above)
+      for (int task0 = threadIdx.x; task0 < npair * 8; task0 += 256 * PU2) {
+        f32x4 a0[PU2], a1[PU2], mb[PU2][16], du[PU2];
+        float dt[PU2];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          lo = lo + a[k] * mb[2 * k];
-          hi = hi + a[k] * mb[2 * k + 1];
+        for (int u = 0; u < PU2; ++u) {
+          const int task = min(task0 + 256 * u, npair * 8 - 1);
+          const int p = 1 + (task >> 3), i = task & 7, t = T - 1 - 2 * p;
+          const f32x4* ra = reinterpret_cast<const f32x4*>(s_M + (t + 1) * 64 + 8 * i);
+          a0[u] = ra[0];
+          a1[u] = ra[1];
+          const f32x4* m4 = reinterpret_cast<const f32x4*>(s_M + (t + 2) * 64);
+#pragma unroll
+          for (int k = 0; k < 16; ++k) mb[u][k] = m4[k];
+          du[u] = *reinterpret_cast<const f32x4*>(s_d + (t + 1) * 4);
+          dt[u] = s_d[t * 4 + (i & 3)];
         }
-        f32x4* dn = reinterpret_cast<f32x4*>(s_N + (p - 1) * 64 + 8 * i);
-        dn[0] = lo;
-        dn[1] = hi;
-        const f32x4 du = *reinterpret_cast<const f32x4*>(s_d + (t + 1) * 4);
-        float v = a[0] * du[0] + a[1] * du[1] + a[2] * du[2] + a[3] * du[3];
-        if (i < 4) v += s_d[t * 4 + i];
-        s_v[(p - 1) * 8 + i] = v;
+#pragma unroll
+        for (int u = 0; u < PU2; ++u) {
+          const int task = task0 + 256 * u;
+          if (task >= npair * 8) break;
+          const int p = 1 + (task >> 3), i = task & 7;
+          const float a[8] = {a0[u][0], a0[u][1], a0[u][2], a0[u][3], a1[u][0], a1[u][1], a1[u][2], a1[u][3]};
+          f32x4 lo = zero4(), hi = zero4();
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            lo = lo + a[k] * mb[u][2 * k];
+            hi = hi + a[k] * mb[u][2 * k + 1];
+          }
+          f32x4* dn = reinterpret_cast<f32x4*>(s_N + (p - 1) * 64 + 8 * i);
+          dn[0] = lo;
+          dn[1] = hi;
+          float v = a[0] * du[u][0] + a[1] * du[u][1] + a[2] * du[u][2] + a[3] * du[u][3];
+          if (i < 4) v += dt[u];
+          s_v[(p - 1) * 8 + i] = v;
+        }
       }
       __syncthreads();
       if (l == 0) RNN_TS(13, tsm);

@@ -125,11 +125,11 @@ void launch_finalize(const FinJob* jobs, int njobs, const ModelDesc* md, const M
 }
 
 // ============================================================ packing ===================
-DLAP_DEV int perm_u(int q, int j) { return j < 4 ? 4 * q + j : 16 + 4 * q + (j - 4); }
+DLAP_HD int perm_u(int q, int j) { return j < 4 ? 4 * q + j : 16 + 4 * q + (j - 4); }
 
 // Pack one blob element / aux float of a model from its flat parameter vector.
 template <typename PP>
-DLAP_DEV float pack_blob_elem(const ModelDesc* __restrict__ md, PP P, int e) {
+DLAP_HD float pack_blob_elem(const ModelDesc* __restrict__ md, PP P, int e) {
   const MlpDims& D = md->md;
   const int KS1 = md->KSB, WMB = md->WMB, KSM = (WMB + 1) / 2;   // (no layer-0 range if KSB = 0)
   const int frag = e >> 9, lane = (e >> 3) & 63, j = e & 7;
@@ -182,17 +182,17 @@ DLAP_DEV float pack_blob_elem(const ModelDesc* __restrict__ md, PP P, int e) {
 }
 // whether blob fragment `frag` / aux float `e` belongs to a layer whose training copy carries
 // the dropout scale (hidden layers >= 1 of both towers, forward and transposed, and wo)
-DLAP_DEV bool blob_scaled(const ModelDesc* __restrict__ md, int frag) {
+DLAP_HD bool blob_scaled(const ModelDesc* __restrict__ md, int frag) {
   const MlpDims& D = md->md;
   return (frag >= D.s_fwd && frag < D.m_fwd0) || (frag >= D.m_fwd && frag < D.s_upp) ||
          (frag >= D.s_wo && frag < D.s_wo + 2);
 }
-DLAP_DEV bool aux_scaled(const ModelDesc* __restrict__ md, int e) {
+DLAP_HD bool aux_scaled(const ModelDesc* __restrict__ md, int e) {
   return e >= md->md.a_wo && e < md->md.a_bo;
 }
 
 template <typename PP>
-DLAP_DEV float pack_aux_elem(const ModelDesc* __restrict__ md, PP P, int e) {
+DLAP_HD float pack_aux_elem(const ModelDesc* __restrict__ md, PP P, int e) {
   const MlpDims& D = md->md;
   float val = 0.f;
   if (e < D.a_wo) {
@@ -217,16 +217,17 @@ DLAP_DEV float pack_aux_elem(const ModelDesc* __restrict__ md, PP P, int e) {
 // Input-projection matrix for k_proj (ModelDesc::proj_mp): transposed, zero padded, biases in
 // the last row, so k_proj can stage it with plain coalesced 16-byte loads.
 template <typename PP>
-DLAP_DEV float pack_proj_elem(const ModelDesc* __restrict__ md, PP P, int f) {
+DLAP_HD float pack_proj_elem(const ModelDesc* __restrict__ md, PP P, int f) {
   const int NP = md->proj_np, M = md->M;
   const int m = f / NP, o = f - m * NP;
   const int G4 = md->nrnn > 0 ? 4 * md->H : 0;
   const PackLayer& L0 = md->m[0];
   const int om = o - G4;
-  if (m == md->proj_mp) {                       // bias row
-    if (o < G4) return P[md->lstm_b_ih[0] + o] + P[md->lstm_b_hh[0] + o];
-    return om < md->cm1 ? P[L0.b_off + om] : 0.f;
+  if (m == md->proj_mp) {                       // bias rows: b_ih | b_m0, then b_hh | 0 (every
+    if (o < G4) return P[md->lstm_b_ih[0] + o]; // packed element is one parameter, so the fused
+    return om < md->cm1 ? P[L0.b_off + om] : 0.f;   // Adam can scatter each update itself)
   }
+  if (m == md->proj_mp + 1) return o < G4 ? P[md->lstm_b_hh[0] + o] : 0.f;
   if (m >= M) return 0.f;
   if (o < G4) return P[md->lstm_w_ih[0] + o * M + m];
   return om < md->cm1 ? P[L0.w_off + om * L0.ld + m] : 0.f;
@@ -236,7 +237,7 @@ DLAP_DEV float pack_proj_elem(const ModelDesc* __restrict__ md, PP P, int f) {
 // fragment (u, s) with u < 4 the SDF W0[16u + n][32s + 8q + j], u >= 4 the moment layer 0's
 // x columns; columns >= F and units beyond the layer width are zero.
 template <typename PP>
-DLAP_DEV float pack_blob0_elem(const ModelDesc* __restrict__ md, PP P, int e) {
+DLAP_HD float pack_blob0_elem(const ModelDesc* __restrict__ md, PP P, int e) {
   const int KSX = md->md.KSX;
   const int frag = e >> 9, lane = (e >> 3) & 63, j = e & 7;
   const int q = lane >> 4, n = lane & 15;
@@ -257,41 +258,72 @@ DLAP_DEV float pack_blob0_elem(const ModelDesc* __restrict__ md, PP P, int e) {
 // grid (ceil(elements / 256), models): one packed element per thread, gathered straight from
 // the (L2-resident) parameter vector -- a single memory round trip per launch.
 // Block 0 also advances the step counters (after every Adam block has read them).
-__global__ __launch_bounds__(256) void k_pack(const UpdJob* __restrict__ jobs,
-                                              const ModelDesc* __restrict__ md, int bump) {
-  const UpdJob& J = jobs[blockIdx.y];
-  const int nel = md->md.blob_frags * 512, naux = nel + md->md.aux_floats;
-  const int NP = md->proj_np, MP = md->proj_mp;
-  const int nproj = naux + (MP + 1) * NP;
-  const int total = nproj + md->md.b0_frags * 512;
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  const auto src = gp(static_cast<const float*>(J.params));
-  // two copies: evaluation weights, then the training weights with the dropout scale 1/(1-p)
-  // folded into every layer fed by dropped-out activations (the towers then apply the bare
-  // keep mask; k_finalize scales those gradients back)
-  const float dscale = J.dropout > 0.f ? 1.f / (1.f - J.dropout) : 1.f;
-  if (e < nel) {
-    const float v = pack_blob_elem(md, src, e);
+// The packed element space of a model, in order: blob (eval copy; the train copy sits nel
+// further), aux (ditto), the input-projection matrix, the wide path's layer-0 fragments.
+struct PackSpace {
+  int nel, naux, nproj, total;
+  DLAP_HD explicit PackSpace(const ModelDesc* __restrict__ md)
+      : nel(md->md.blob_frags * 512), naux(nel + md->md.aux_floats),
+        nproj(naux + (md->proj_mp + 2) * md->proj_np), total(nproj + md->md.b0_frags * 512) {}
+};
+
+// Value of packed element e gathered from the parameter vector (any P with operator[]).
+template <typename PP>
+DLAP_HD float pack_value(const ModelDesc* __restrict__ md, const PackSpace& S, PP P, int e) {
+  if (e < S.nel) return pack_blob_elem(md, P, e);
+  if (e < S.naux) return pack_aux_elem(md, P, e - S.nel);
+  if (e < S.nproj) return pack_proj_elem(md, P, e - S.naux);
+  return pack_blob0_elem(md, P, e - S.nproj);
+}
+
+// Store packed element e with value v: two copies of the blob / aux elements -- evaluation
+// weights, then the training weights with the dropout scale 1/(1-p) folded into every layer fed
+// by dropped-out activations (the towers then apply the bare keep mask; k_finalize scales those
+// gradients back).
+DLAP_DEV void pack_store(const UpdJob& J, const ModelDesc* __restrict__ md, const PackSpace& S, int e,
+                         float v, float dscale) {
+  if (e < S.nel) {
     const float vt = blob_scaled(md, e >> 9) ? v * dscale : v;
     if (md->md.fp32) {                                                // reference-precision towers
       ((DLAP_GLOBAL float*)(J.blob))[e] = v;
-      ((DLAP_GLOBAL float*)(J.blob))[nel + e] = vt;
+      ((DLAP_GLOBAL float*)(J.blob))[S.nel + e] = vt;
     } else {
       ((DLAP_GLOBAL __bf16*)(J.blob))[e] = (__bf16)v;
-      ((DLAP_GLOBAL __bf16*)(J.blob))[nel + e] = (__bf16)vt;
+      ((DLAP_GLOBAL __bf16*)(J.blob))[S.nel + e] = (__bf16)vt;
     }
-  } else if (e < naux) {
-    const int a = e - nel;
-    const float v = pack_aux_elem(md, src, a);
+  } else if (e < S.naux) {
+    const int a = e - S.nel;
     gp(J.aux)[a] = v;
     gp(J.aux)[md->md.aux_floats + a] = aux_scaled(md, a) ? v * dscale : v;
+  } else if (e < S.nproj) {
+    gp(J.wproj)[e - S.naux] = v;
+  } else {
+    if (md->md.fp32) ((DLAP_GLOBAL float*)(J.blob0))[e - S.nproj] = v;
+    else ((DLAP_GLOBAL __bf16*)(J.blob0))[e - S.nproj] = (__bf16)v;
   }
-  else if (e < nproj) gp(J.wproj)[e - naux] = pack_proj_elem(md, src, e - naux);
-  else if (e < total) {
-    const float v = pack_blob0_elem(md, src, e - nproj);
-    if (md->md.fp32) ((DLAP_GLOBAL float*)(J.blob0))[e - nproj] = v;
-    else ((DLAP_GLOBAL __bf16*)(J.blob0))[e - nproj] = (__bf16)v;
-  }
+}
+
+// Index mode of the gathers: P[i] -> i + 1 (exact in fp32 below 2^24), padding stays 0.
+struct PackIdx {
+  DLAP_HD float operator[](int i) const { return (float)(i + 1); }
+};
+
+// src[e] = the parameter packed element e holds (-1: constant zero padding), evaluated on the
+// host from the same gathers k_pack runs (once per engine; the engine inverts it into the
+// scatter lists of k_adam).
+void pack_index_host(const ModelDesc& mh, int* src) {
+  const PackSpace S(&mh);
+  for (int e = 0; e < S.total; ++e) src[e] = (int)pack_value(&mh, S, PackIdx{}, e) - 1;
+}
+
+__global__ __launch_bounds__(256) void k_pack(const UpdJob* __restrict__ jobs,
+                                              const ModelDesc* __restrict__ md, int bump) {
+  const UpdJob& J = jobs[blockIdx.y];
+  const PackSpace S(md);
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  const auto src = gp(static_cast<const float*>(J.params));
+  const float dscale = J.dropout > 0.f ? 1.f / (1.f - J.dropout) : 1.f;
+  if (e < S.total) pack_store(J, md, S, e, pack_value(md, S, src, e), dscale);
   if (bump && blockIdx.x == 0 && threadIdx.x == 0) {
     gp(J.adam_step)[bump - 1] = gp(J.adam_step)[bump - 1] + 1;
     gp(J.drop_step)[0] = gp(J.drop_step)[0] + 1;
@@ -311,9 +343,13 @@ void launch_set_int(int* p, int v, hipStream_t st) {
 }
 
 static int pack_blocks_of(const ModelDesc& mh) {
-  return (mh.md.blob_frags * 512 + mh.md.aux_floats + (mh.proj_mp + 1) * mh.proj_np + mh.md.b0_frags * 512 +
-          255) / 256;
+  return (pack_total(mh) + 255) / 256;
 }
+
+int pack_total(const ModelDesc& mh) {
+  return mh.md.blob_frags * 512 + mh.md.aux_floats + (mh.proj_mp + 2) * mh.proj_np + mh.md.b0_frags * 512;
+}
+
 
 void launch_pack(float* const*, const UpdJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
                  hipStream_t st) {
@@ -347,6 +383,11 @@ __global__ __launch_bounds__(256) void k_adam(const UpdJob* __restrict__ jobs,
   // scope norm: the block's whole share of loads is issued before any use (register blocks of
   // ADAM_NB per thread), so the reduction costs ~one memory round trip per block of 256*ADAM_NB
   constexpr int ADAM_NB = 48;
+  // bias corrections in double like torch's Python-float scalars, evaluated by every wave from
+  // the (uniform) step count while the first norm loads are in flight
+  const int step = gp(J.adam_step)[mom ? 1 : 0] + 1;
+  const float lr_g = J.lr > 0.f ? J.lr : lr;
+  float step_size = 0.f, bc2s = 1.f;
   float ss = 0.f;
   for (int b0 = p0; b0 < p1; b0 += 256 * ADAM_NB) {
     float gv[ADAM_NB];
@@ -355,53 +396,81 @@ __global__ __launch_bounds__(256) void k_adam(const UpdJob* __restrict__ jobs,
       const int i = b0 + k * 256 + threadIdx.x;
       gv[k] = grads[i < p1 ? i : p0];
     }
+    if (b0 == p0) {
+      const double bc1 = 1.0 - pow(0.9, (double)step);
+      const double bc2 = 1.0 - pow(0.999, (double)step);
+      step_size = (float)(lr_g / bc1);
+      bc2s = (float)sqrt(bc2);
+    }
 #pragma unroll
     for (int k = 0; k < ADAM_NB; ++k) ss += (b0 + k * 256 + (int)threadIdx.x < p1) ? gv[k] * gv[k] : 0.f;
   }
   ss = block_sum<256>(ss, red);
   const float norm = sqrtf(ss);
   const float coef = fminf(1.f / (norm + 1e-6f), 1.f);
-  // bias corrections in double like torch's Python-float scalars; one thread evaluates the
-  // (slow) double pow and shares the two fp32 scalars through LDS
-  __shared__ float sc2[2];
-  if (threadIdx.x == 0) {
-    const int step = gp(J.adam_step)[mom ? 1 : 0] + 1;
-    const double bc1 = 1.0 - pow(0.9, (double)step);
-    const double bc2 = 1.0 - pow(0.999, (double)step);
-    const float lr_g = J.lr > 0.f ? J.lr : lr;
-    sc2[0] = (float)(lr_g / bc1);
-    sc2[1] = (float)sqrt(bc2);
-  }
-  __syncthreads();
-  const float step_size = sc2[0];
-  const float bc2s = sc2[1];
   const int i = p0 + blockIdx.x * ADAM_PB;
   float* __restrict__ pm = gp(J.m);
   float* __restrict__ pv = gp(J.v);
   float* __restrict__ pp = gp(J.params);
+  // fused re-pack: every packed element holds exactly one parameter (pack_index_host), so the
+  // thread that updates a parameter also writes its packed copies -- no second pass over the
+  // parameter vector, no separate launch
+  const bool fused = J.inv_code != nullptr;
+  const PackSpace S(md);
+  const float dscale = J.dropout > 0.f ? 1.f / (1.f - J.dropout) : 1.f;
+  // every operand of the thread's ADAM_PB / 256 parameters (and their scatter lists) is requested
+  // before the first use: one memory round trip
+  constexpr int KPT = ADAM_PB / 256;
+  float gq[KPT], mq[KPT], vq[KPT], pq[KPT];
+  int cq[KPT][PACK_FAN];
 #pragma unroll
-  for (int k = 0; k < ADAM_PB / 256; ++k) {
+  for (int k = 0; k < KPT; ++k) {
+    const int e = i + k * 256 + threadIdx.x, ec = e < p1 ? e : p0;
+    gq[k] = grads[ec];
+    mq[k] = pm[ec];
+    vq[k] = pv[ec];
+    pq[k] = pp[ec];
+#pragma unroll
+    for (int j = 0; j < PACK_FAN; ++j) cq[k][j] = fused ? gp(J.inv_code)[(size_t)ec * PACK_FAN + j] : -1;
+  }
+#pragma unroll
+  for (int k = 0; k < KPT; ++k) {
     const int e = i + k * 256 + threadIdx.x;
     if (e < p1) {
-      const float g = grads[e] * coef;
-      float m = pm[e];
+      const float g = gq[k] * coef;
+      float m = mq[k];
       m = m + 0.1f * (g - m);
-      const float v = 0.999f * pv[e] + 0.001f * g * g;
+      const float v = 0.999f * vq[k] + 0.001f * g * g;
       pm[e] = m;
       pv[e] = v;
       const float denom = sqrtf(v) / bc2s + 1e-8f;
-      pp[e] = pp[e] - step_size * (m / denom);
+      const float pn = pq[k] - step_size * (m / denom);
+      pp[e] = pn;
+#pragma unroll
+      for (int j = 0; j < PACK_FAN; ++j)
+        if (cq[k][j] >= 0) pack_store(J, md, S, cq[k][j], pn, dscale);
     }
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) gp(J.gnorm)[0] = norm;
+  // the last block to finish advances the step counters: every block has read them (above,
+  // consumed before its increment), so no block of this launch can see the new values
+  if (fused && threadIdx.x == 0) {
+    const int done = __hip_atomic_fetch_add(J.upd_ctr, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (done == (int)gridDim.x - 1) {
+      gp(J.upd_ctr)[0] = 0;
+      gp(J.adam_step)[mom ? 1 : 0] = gp(J.adam_step)[mom ? 1 : 0] + 1;
+      gp(J.drop_step)[0] = gp(J.drop_step)[0] + 1;
+    }
+  }
 }
 
 void launch_update(const UpdJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh, int phase,
-                   float lr, hipStream_t st) {
+                   float lr, hipStream_t st, bool fused) {
   const int n = phase == 2 ? mh.P - mh.P_sdf : mh.P_sdf;
   hipLaunchKernelGGL(k_adam, dim3((n + ADAM_PB - 1) / ADAM_PB, njobs), dim3(256), 0, st, jobs, md, phase,
                      lr);
   HIP_OK(hipGetLastError());
+  if (fused) return;
   hipLaunchKernelGGL(k_pack, dim3(pack_blocks_of(mh), njobs), dim3(256), 0, st, jobs, md,
                      phase == 2 ? 2 : 1);
   HIP_OK(hipGetLastError());

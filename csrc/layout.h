@@ -56,8 +56,8 @@ struct ModelDesc {
   // gradient reduction tables (phase-specific tower)
   int ntile_s, ntile_m, nslice_s, nslice_m;
   int tps_s, tps_m;        // gradient tiles accumulated per backward slice
-  // input-projection matrix re-packed by k_pack for k_proj: wproj[MP + 1][NP] fp32, row m < M =
-  // column m of [W_ih(layer 0) ; W_m0[:, :M]], row MP = biases (b_ih + b_hh ; b_m0), zero pad
+  // input-projection matrix re-packed by k_pack for k_proj: wproj[MP + 2][NP] fp32, row m < M =
+  // column m of [W_ih(layer 0) ; W_m0[:, :M]], row MP = (b_ih ; b_m0), row MP + 1 = (b_hh ; 0)
   int proj_mp, proj_np;
   GradTile tile_s[DLAP_MAX_TILES], tile_m[DLAP_MAX_TILES];
   int extra_s[SLAB_EXTRA], extra_m[SLAB_EXTRA];   // slab extra slot -> flat index (-1 unused)

@@ -4,6 +4,8 @@
 
 struct ModelDesc;
 
+#define PACK_FAN 4         // max packed copies of one parameter for k_adam's fused re-pack
+
 struct FinJob {            // one model
   const float* slab;       // first slab of this model (slices contiguous, gx slabs each)
   float* grads;            // flat gradient vector [P]
@@ -52,6 +54,9 @@ struct UpdJob {            // one model
   const int* prog;         // the model's fused-forward progress records (3 splits, 16 ints each;
                            // [16 s + 1] = spin waits that gave up): non-zero poisons the model --
                            // k_adam skips every later update, k_epoch_end records NaN epochs
+  const int* inv_code;     // [P][PACK_FAN] scatter lists: the packed elements holding parameter p
+                           // (-1 padded; nullptr: a separate k_pack re-packs after k_adam)
+  int* upd_ctr;            // [1] k_adam blocks finished (the last one advances the step counters)
 };
 
 // History row written per epoch by k_epoch_end (HIST_W floats).
@@ -80,12 +85,15 @@ struct EpochJob {          // one model
 
 void launch_finalize(const FinJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
                      int phase, int slab_stride, int tmax, hipStream_t st, int part = 0);
+// fused: the jobs carry scatter lists (UpdJob::inv_code) -- k_adam re-packs, no k_pack launch
 void launch_update(const UpdJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh, int phase,
-                   float lr, hipStream_t st);
+                   float lr, hipStream_t st, bool fused);
 void launch_lstm_bwd(const UpdJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
                      int T, int phase, hipStream_t st);
 void launch_pack(float* const* params_unused, const UpdJob* jobs, int njobs, const ModelDesc* md,
                  const ModelDesc& mh, hipStream_t st);
+int pack_total(const ModelDesc& mh);   // packed elements per model (k_pack's element space)
+void pack_index_host(const ModelDesc& mh, int* src);   // packed element -> parameter (-1: padding)
 void launch_set_int(int* p, int v, hipStream_t st);
 void launch_begin_phase(const EpochJob* jobs, int njobs, hipStream_t st);
 void launch_epoch_end(const EpochJob* jobs, int njobs, int phase, int ignore_epoch, float sel,

@@ -142,6 +142,26 @@ def test_fused_phase2_under_the_guarantee_equals_two_launches(big, monkeypatch):
     _same(ref[9], res[9])
 
 
+def test_adam_fused_repack_equals_separate_pack(big, monkeypatch):
+    """k_adam writing every updated parameter's packed copies itself (scatter lists built from
+    k_pack_index) gives the bits of Adam followed by a full k_pack: parameters, history,
+    snapshots, Adam moments and step counters, with per-member dropout scales in the blob."""
+    cfg = default_cli_config(178, 46, dropout=0.05)
+    monkeypatch.setenv("DLAP_FUSED_PACK", "0")
+    e0, ref = _train(big, cfg, [41, 42], 2, dropouts=[0.0, 0.1])
+    assert not e0.eng.fused_info()["fused_pack"]
+    monkeypatch.setenv("DLAP_FUSED_PACK", "1")
+    e1, res = _train(big, cfg, [41, 42], 2, dropouts=[0.0, 0.1])
+    assert e1.eng.fused_info()["fused_pack"]
+    for g, s in enumerate((41, 42)):
+        _same(ref[s], res[s])
+        a, b = e0.eng.get_opt_state(g), e1.eng.get_opt_state(g)
+        for k in ("m", "v"):
+            np.testing.assert_array_equal(a[k], b[k])
+        assert [a[k] for k in ("step_sdf", "step_moment", "drop_step")] == \
+            [b[k] for k in ("step_sdf", "step_moment", "drop_step")] == [10, 3, 13]
+
+
 def test_fused_wait_give_up_poisons_the_model(monkeypatch):
     """Force every fused wait to give up (spin limit 0): the launch writes nothing, the model is
     never updated (parameters bit-identical to the initial ones), every epoch is recorded as NaN
