@@ -91,7 +91,7 @@ static void retire_graph_exec(hipGraphExec_t e, hipStream_t st) {
   }
   std::lock_guard<std::mutex> g(g_retired_mu);
   g_retired.push_back({e, ev, g_retire_seq++});
-  if (g_retired.size() < 2 * RETIRE_LAG) return;
+  if (g_retired.size() < 2 * RETIRE_LAG) { (void)hipGetLastError(); return; }
   std::vector<RetiredExec> keep;
   keep.reserve(g_retired.size());
   for (const RetiredExec& r : g_retired) {
@@ -105,6 +105,9 @@ static void retire_graph_exec(hipGraphExec_t e, hipStream_t st) {
     }
   }
   g_retired.swap(keep);
+  // the statuses above are ignored on purpose (a query of a still-pending event, a destroy the
+  // runtime refuses): do not leave one as the thread's sticky error for the next launch check
+  (void)hipGetLastError();
 }
 
 namespace {
@@ -329,6 +332,7 @@ class Engine {
     if (st2_) (void)hipStreamDestroy(st2_);
     if (st3_) (void)hipStreamDestroy(st3_);
     if (own_st_) (void)hipStreamDestroy(own_st_);
+    (void)hipGetLastError();      // (ignored statuses above must not fail the next launch check)
   }
 
   // ---------------------------------------------------------------- description ----------

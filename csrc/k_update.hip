@@ -453,11 +453,13 @@ __global__ __launch_bounds__(256) void k_adam(const UpdJob* __restrict__ jobs,
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) gp(J.gnorm)[0] = norm;
   // the last block to finish advances the step counters: every block has read them (above,
-  // consumed before its increment), so no block of this launch can see the new values
+  // consumed before its increment), so no block of this launch can see the new values. Relaxed:
+  // only that read must precede the increment (it has returned -- its value was used), and an
+  // acquire / release at agent scope would write back and invalidate the XCD's L2.
   if (fused && threadIdx.x == 0) {
-    const int done = __hip_atomic_fetch_add(J.upd_ctr, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const int done = __hip_atomic_fetch_add(J.upd_ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (done == (int)gridDim.x - 1) {
-      gp(J.upd_ctr)[0] = 0;
+      __hip_atomic_store(J.upd_ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       gp(J.adam_step)[mom ? 1 : 0] = gp(J.adam_step)[mom ? 1 : 0] + 1;
       gp(J.drop_step)[0] = gp(J.drop_step)[0] + 1;
     }

@@ -3,7 +3,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 400 python -u -m pytest tests/test_invariance_gpu.py::test_adam_fused_repack_equals_separate_pack tests/test_engine_gpu.py -x -v --timeout 200 --timeout-method thread > gpurun_out/r4_fp_tests.log 2>&1 \
+timeout -k 10 400 python -u -m pytest tests/test_invariance_gpu.py tests/test_engine_gpu.py -x -v --timeout 200 --timeout-method thread > gpurun_out/r4_fp_tests.log 2>&1 \
   || { echo "tests FAILED"; grep -E "FAILED|Error|assert" gpurun_out/r4_fp_tests.log | tail -20; tail -5 gpurun_out/r4_fp_tests.log; exit 3; }
 tail -2 gpurun_out/r4_fp_tests.log
 for i in 1 2; do
