@@ -159,7 +159,8 @@ struct ModelSplitWS {   // per (model, split)
 
 struct ModelState {
   DevBuf<float> params, grads, m, v, snap_loss, snap_sharpe, gnorm, best, aux, hist, wproj;
-  DevBuf<int> adam_step, drop_step, snap_flags, ep, upd_ctr;
+  DevBuf<int> adam_step, drop_step, snap_flags, ep, upd_ctr, tail_ctr;
+  DevBuf<float> mscr;       // fused backward tail: LSTM step-matrix scratch [T][64]
   DevBuf<uint16_t> blob, blob0;
   unsigned seed = 0;
   unsigned tower_salt = 0;  // XOR-ed (mixed) into the towers' dropout seed only (N-sharding: per rank)
@@ -181,6 +182,7 @@ static int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
   return v && *v ? std::atoi(v) : dflt;
 }
+static const int g_skip = env_int("DLAP_SKIP", 0);   // TEMPORARY knock-out timing experiment
 
 static void install_crash_handler();
 // DLAP_TRACE_HOST=1: one stderr line per host-side engine step (crash localisation on boxes
@@ -256,6 +258,8 @@ class Engine {
     prog_mode_ = env_int("DLAP_PROG_MODE", 1);
     prog_limit_ = (unsigned)env_int("DLAP_PROG_SPIN_LIMIT", 1 << 22);
     fused_p2_ = env_int("DLAP_FUSED_PHASE2", 0) != 0;
+    eval_in_fwd_ = env_int("DLAP_EVAL_IN_FWD", 1) != 0;
+    fused_tail_ = env_int("DLAP_FUSED_TAIL", 1) != 0;
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
                residual, fp32);
     // fp32 wide path: layer 0 through k_proj0 + the ZIN towers (the fused-layer-0 k_mlp_fwd_zx
@@ -274,6 +278,7 @@ class Engine {
       S.gnorm.alloc(1); S.best.alloc(3); S.aux.alloc((size_t)2 * md_.md.aux_floats);
       S.hist.alloc((size_t)max_epochs_ * HIST_W);
       S.adam_step.alloc(2); S.drop_step.alloc(1); S.snap_flags.alloc(2); S.ep.alloc(2); S.upd_ctr.alloc(1);
+      S.tail_ctr.alloc(16);
       S.blob.alloc((size_t)2 * md_.md.blob_frags * 512 * xw());   // bf16 (or fp32: 2 u16 each)
       S.blob0.alloc((size_t)std::max(1, md_.md.b0_frags) * 512 * xw());
       S.wproj.alloc((size_t)(md_.proj_mp + 2) * md_.proj_np);
@@ -561,6 +566,8 @@ class Engine {
     float mx = 0.f;
     for (const ModelState& S : models_) mx = std::max(mx, S.dropout);
     md_.dropout = md_.md.dropout = mx;          // structural switches: any model with dropout
+    // (queued graphs and kernels read the descriptor: the synchronous copy must not overtake them)
+    sync();
     HIP_LEGACY(hipMemcpy(d_desc_.p, &md_, sizeof(ModelDesc), hipMemcpyHostToDevice));
     upload_pack_jobs();
     pack(g);                                     // its train blob carries the new scale
@@ -1053,6 +1060,13 @@ class Engine {
   int prog_mode_ = 1;                        // DLAP_PROG_MODE (see MlpJob::prog_mode)
   unsigned prog_limit_ = 1u << 22;           // DLAP_PROG_SPIN_LIMIT (see MlpJob::prog_limit)
   bool fused_p2_ = false;                    // DLAP_FUSED_PHASE2: fused training forward in phase 2 too
+  // pipelined phase-1/3 epochs: the evaluation splits' recurrences run inside the fused training
+  // forward (k_mlp_fwd_rnn, ne > 0) and their input projections inside its k_proj launch
+  // (one job table: j_rnn_all_ = train jobs, then evaluation jobs); DLAP_EVAL_IN_FWD=0: the
+  // evaluation branch runs its own prologue beside the training chain (the round-4 graph)
+  bool eval_in_fwd_ = true;
+  DevBuf<char> j_rnn_all_;
+  int cap_all_ = 0;                          // co-residency capacity at the longest split's LDS
   DevBuf<int> prog_;
   // Co-residency guarantee of the fused LSTM + tower launches: resident workgroups of the fused
   // kernel on the device (occupancy query, rebuild_jobs) for the train split / the evaluation
@@ -1091,6 +1105,20 @@ class Engine {
   // the capped grids of the fused launches (valid when fused_fwd / fused_eval)
   int fused_train_gx(int phase) const { return fused_grid(train_fwd_grid(phase), G_, cap_train_); }
   int fused_eval_gx() const { return fused_grid(eval_grid(), n_eval_jobs_, cap_eval_); }
+  // evaluation recurrences per model inside the fused training forward, and its grid
+  int ne_per_model() const { return G_ > 0 && n_eval_jobs_ % G_ == 0 ? n_eval_jobs_ / G_ : 0; }
+  int tmax_fwd_all() const { return std::max(splits_[0].T, tmax_eval_); }
+  int fused_all_gx(int phase) const {
+    const int ne = ne_per_model();
+    if (cap_all_ <= 0 || ne <= 0) return 0;
+    const int gx = std::min(train_fwd_grid(phase), cap_all_ / G_ - 1 - ne);
+    return gx >= 16 ? gx : 0;
+  }
+  bool eval_rnn_in_fwd(int phase) const {
+    if (!eval_in_fwd_ || phase == 2 || n_eval_jobs_ == 0 || ne_per_model() == 0 || !fused_fwd(phase)) return false;
+    if (!mlp_fwd_rnn_supported(md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, tmax_fwd_all())) return false;
+    return fused_all_gx(phase) > 0;
+  }
   // zero the spin-timeout counters (tests: the device poison is permanent otherwise)
   void reset_prog_errors() {
     sync();
@@ -1098,12 +1126,25 @@ class Engine {
     HIP_LEGACY(hipMemcpy(h.data(), prog_.p, h.size() * sizeof(int), hipMemcpyDeviceToHost));
     for (int k = 0; k < 3 * G_; ++k) h[16 * k + 1] = 0;
     HIP_LEGACY(hipMemcpy(prog_.p, h.data(), h.size() * sizeof(int), hipMemcpyHostToDevice));
+    // a wait that gave up leaves its launch's counters behind: rearm them (and Adam's)
+    for (ModelState& S : models_) {
+      HIP_LEGACY(hipMemset(S.tail_ctr.p, 0, S.tail_ctr.n * sizeof(int)));
+      HIP_LEGACY(hipMemset(S.upd_ctr.p, 0, S.upd_ctr.n * sizeof(int)));
+    }
   }
   py::dict fused_info() const {
     py::dict d;
     d["cap_train"] = cap_train_; d["cap_eval"] = cap_eval_;
     for (int ph = 1; ph <= 3; ++ph) d[("train_gx_p" + std::to_string(ph)).c_str()] = fused_fwd(ph) ? fused_train_gx(ph) : 0;
     d["eval_gx_solo"] = fused_grid(eval_grid(), n_eval_jobs_, cap_eval_);
+    // pipelined epochs with the evaluation recurrences inside the fused training forward
+    d["cap_all"] = cap_all_;
+    for (int ph = 1; ph <= 3; ph += 2) {
+      d[("eval_in_fwd_p" + std::to_string(ph)).c_str()] = eval_rnn_in_fwd(ph);
+      d[("all_gx_p" + std::to_string(ph)).c_str()] = eval_rnn_in_fwd(ph) ? fused_all_gx(ph) : 0;
+    }
+    d["eval_per_model"] = ne_per_model();
+    d["fused_tail"] = tail_fused(1);
     // backward launch shape: fine slabs per model (R-only partition), fine slabs per workgroup
     d["bwd_nfine"] = nfine_; d["bwd_fpw"] = fpw_;
     d["fused_pack"] = inv_code_.p != nullptr;
@@ -1641,9 +1682,16 @@ class Engine {
       U.h0 = W.h0.p; U.c0 = W.c0.p; U.dh0 = W.dh0.p; U.dc0 = W.dc0.p;
       U.T = splits_[0].T; U.seed = S.seed; U.lr = S.lr; U.prog = prog_ptr(g, 0); U.dropout = S.dropout;
       U.inv_code = inv_code_.p; U.upd_ctr = S.upd_ctr.p;
+      if (splits_[0].set && (S.mscr.n < (size_t)splits_[0].T * 64)) S.mscr.alloc((size_t)std::max(splits_[0].T, 1) * 64, false);
+      U.tail_ctr = S.tail_ctr.p; U.mscr = S.mscr.p; U.spin_limit = prog_limit_;
       uj.push_back(U);
     }
     n_eval_jobs_ = (int)le.size();
+    {
+      std::vector<RnnJob> ra = rt;
+      ra.insert(ra.end(), re.begin(), re.end());
+      upload(j_rnn_all_, ra);
+    }
     {   // co-residency capacity of the fused launches (no GPU query when they cannot run)
       const int force = env_int("DLAP_FUSED_CAP", -1);
       const bool can = rnn_overlap_ && md_.nrnn > 0 && !md_.md.wide;
@@ -1651,6 +1699,8 @@ class Engine {
                    : force >= 0 ? force : mlp_fwd_rnn_capacity(md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, splits_[0].T);
       cap_eval_ = !can || n_eval_jobs_ == 0 ? 0
                   : force >= 0 ? force : mlp_fwd_rnn_capacity(md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, tmax_eval_);
+      cap_all_ = !can || n_eval_jobs_ == 0 || !splits_[0].set ? 0
+                 : force >= 0 ? force : mlp_fwd_rnn_capacity(md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, tmax_fwd_all());
     }
     if (gram_on_) build_gram_jobs();
     for (bool& v : gram_valid_) v = false;
@@ -1781,7 +1831,7 @@ class Engine {
   bool dropmask_on(int phase) const { return md_.dropout > 0.f && phase != 2; }
   // keep masks of the step *drop_step + offset* (phases 1/3: the SDF tower's dropout)
   void enqueue_dropmask(int phase, int offset, hipStream_t st) {
-    if (!dropmask_on(phase)) return;
+    if (!dropmask_on(phase) || (g_skip & 32)) return;
     HTRACE("launch_dropmask");
     launch_dropmask(as<MlpJob>(j_mlp_train_[phase]), G_, (splits_[0].R + 31) / 32, md_.md, offset, st);
   }
@@ -1793,8 +1843,10 @@ class Engine {
   // part1_only: stop before the gradient finalisation (the caller enqueues the tail).
   // defer_metrics: the train split's metrics are left to the caller (it records ev_mid_ after the
   // asset pass; the pipelined epoch runs them on the evaluation branch, off the critical chain).
+  // eval_rnn: the evaluation splits' projections and recurrences ride in the training prologue
+  // and fused forward (eval_rnn_in_fwd; the caller's evaluation branch starts at its towers)
   void enqueue_train_grads(int phase, hipStream_t side = nullptr, bool premasked = false, int mark = 0,
-                           bool part1_only = false, bool defer_metrics = false) {
+                           bool part1_only = false, bool defer_metrics = false, bool eval_rnn = false) {
     const SplitDev& D = splits_[0];
     const bool gram = use_gram(phase);
     const LossJob* lj = loss_tab(phase, gram);
@@ -1802,8 +1854,9 @@ class Engine {
     // the latency-bound LSTM first, before the streaming projection loads the memory system
     // (fused: only its input projection here, the recurrence runs inside the tower launch)
     const bool fused = fused_fwd(phase);
-    HTRACE("launch_prologue fused=%d", (int)fused);
-    if (fused) launch_proj(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_, train_mom(phase));
+    HTRACE("launch_prologue fused=%d eval_rnn=%d", (int)fused, (int)eval_rnn);
+    if (eval_rnn) launch_proj(as<RnnJob>(j_rnn_all_), G_ + n_eval_jobs_, tmax_fwd_all(), dd(), md_, st_, train_mom(phase));
+    else if (fused) launch_proj(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_, train_mom(phase));
     else launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_, train_mom(phase));
     // pipelined epoch, train_first_ == 2: the evaluation branch's LSTM prologue is enqueued right
     // behind the training one, so its (serial, few-CU) recurrence starts at the epoch start
@@ -1815,6 +1868,10 @@ class Engine {
     if (mark == 3) HIP_OK(hipEventRecord(ev_a_, st_));
     if (zx_train)      // layer 0 streamed inside the training towers, z stored for the backward
       launch_mlp_fwd_zx(as<MlpJob>(j_mlp_train_[phase]), G_, std::max(1, zx_gx_ / G_), md_.md, md_.WMB, st_, true);
+    else if (eval_rnn)
+      launch_mlp_fwd_rnn(as<MlpJob>(j_mlp_train_[phase]), as<RnnJob>(j_rnn_all_), dd(), G_, fused_all_gx(phase),
+                         md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, tmax_fwd_all(), st_, !train_mom(phase),
+                         ne_per_model());
     else if (fused)
       launch_mlp_fwd_rnn(as<MlpJob>(j_mlp_train_[phase]), as<RnnJob>(j_rnn_train_), dd(), G_,
                          fused_train_gx(phase), md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, D.T, st_,
@@ -1824,8 +1881,8 @@ class Engine {
                      md_.WMB, st_, !train_mom(phase));
     if (mark == 2) HIP_OK(hipEventRecord(ev_a_, st_));
     HTRACE("launch_period_fwd");
-    launch_period_fwd(lj, G_, D.T, st_);
-    if (!gram) {
+    if (!(g_skip & 128)) launch_period_fwd(lj, G_, D.T, st_);
+    if (g_skip & 128) {} else if (!gram) {
       HTRACE("launch_asset");
       launch_asset(lj, G_, D.N, md_.K, st_, asset_full_default());
     } else {
@@ -1859,7 +1916,7 @@ class Engine {
         launch_period_bwd(lj, G_, D.T, st_);
       }
       HTRACE("launch_mlp_bwd_sdf");
-      launch_mlp_bwd_sdf(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_s, md_.tps_s, md_.md, md_.KS1,
+      if (!(g_skip & 4)) launch_mlp_bwd_sdf(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_s, md_.tps_s, md_.md, md_.KS1,
                          slab_stride(), fpw_, st_);
     }
     if (md_.md.wide)   // layer-0 weight gradient from the tower's dz fragments
@@ -1868,8 +1925,20 @@ class Engine {
     if (part1_only) return;
     enqueue_train_tail(phase);
   }
+  // k_finalize -> k_lstm_bwd -> k_wgrad as one launch (k_lstm_tail) where it applies
+  bool fused_tail_ = true;                   // DLAP_FUSED_TAIL
+  bool tail_fused(int phase) const {
+    return fused_tail_ && !split_tail_ && phase != 2 && splits_[0].set && lstm_tail_supported(md_, splits_[0].T);
+  }
   void enqueue_train_tail(int phase) {
     const SplitDev& D = splits_[0];
+    if (g_skip & 1) { join_side(); return; }
+    if (tail_fused(phase)) {
+      HTRACE("launch_lstm_tail");
+      launch_lstm_tail(as<UpdJob>(j_upd_), as<FinJob>(j_fin_), G_, dd(), md_, D.T, slab_stride(), st_);
+      join_side();
+      return;
+    }
     if (split_tail_) {
       // slab sums beside the LSTM backward (which reads only the per-period sums)
       HIP_OK(hipEventRecord(ev_b3_, st_));
@@ -1909,14 +1978,14 @@ class Engine {
     enqueue_eval_towers(st);
   }
   void enqueue_eval_prologue(hipStream_t st) {
-    if (n_eval_jobs_ == 0) return;
+    if (n_eval_jobs_ == 0 || (g_skip & 2)) return;
     HTRACE("launch_prologue");
     // fused: the input projections only, the recurrences run inside the tower launch
     if (fused_eval()) launch_proj(as<RnnJob>(j_rnn_eval_), n_eval_jobs_, tmax_eval_, dd(), md_, st, !h_cache_);
     else launch_prologue(as<RnnJob>(j_rnn_eval_), n_eval_jobs_, tmax_eval_, dd(), md_, st, !h_cache_);
   }
   void enqueue_eval_towers(hipStream_t st) {
-    if (n_eval_jobs_ == 0) return;
+    if (n_eval_jobs_ == 0 || (g_skip & 2)) return;
     const int gx = eval_grid();
     if (md_.md.wide && zx_eval_) {     // layer 0 streamed inside the evaluation towers
       HTRACE("launch_mlp_fwd_zx");
@@ -1931,6 +2000,7 @@ class Engine {
       else
         launch_mlp_fwd(as<MlpJob>(j_mlp_eval_), n_eval_jobs_, gx, md_.md, md_.KS1, md_.WMB, st, h_cache_);
     }
+    if (g_skip & 16) return;
     const bool eg = eval_gram_now();
     const LossJob* le = as<LossJob>(eg ? j_loss_eval_ : j_loss_eval_dense_);
     HTRACE("launch_period_fwd");
@@ -1947,6 +2017,7 @@ class Engine {
   }
   void enqueue_epoch_end(int phase, int ignore_epoch, float sel, hipStream_t st) {
     HTRACE("launch_epoch_end");
+    if (g_skip & 64) return;
     launch_epoch_end(as<EpochJob>(j_epoch_[phase]), G_, phase, ignore_epoch, sel, md_.residual_factor,
                      md_.P, st);
   }
@@ -1967,6 +2038,27 @@ class Engine {
   void enqueue_pipe(int phase, float lr, int ignore_epoch, float sel) {
     HIP_OK(hipEventRecord(ev_fork_, st_));
     HIP_OK(hipStreamWaitEvent(st2_, ev_fork_, 0));
+    if (b_wait_ == 0 && !side_metrics_ && eval_rnn_in_fwd(phase)) {
+      // the evaluation recurrences run inside this epoch's fused training forward; the
+      // evaluation branch forks after it: towers, losses, this epoch's train metrics (after its
+      // loss pass), the bookkeeping and the next epoch's dropout masks, beside the training
+      // backward and its tail
+      const bool defer = defer_metrics_;
+      enqueue_train_grads(phase, nullptr, true, 2, false, defer, true);
+      HIP_OK(hipStreamWaitEvent(st2_, ev_a_, 0));
+      enqueue_eval_towers(st2_);
+      if (defer && phase != 2) {
+        HIP_OK(hipStreamWaitEvent(st2_, ev_mid_, 0));
+        launch_job_metrics(loss_tab(phase, use_gram(phase)), G_, st2_);
+      }
+      enqueue_epoch_end(phase, ignore_epoch, sel, st2_);
+      enqueue_dropmask(phase, 1, st2_);
+      HIP_OK(hipEventRecord(ev_join_, st2_));
+      HIP_OK(hipStreamWaitEvent(st_, ev_join_, 0));
+      HTRACE("launch_update");
+      if (!(g_skip & 8)) launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_, inv_code_.p != nullptr);
+      return;
+    }
     if (b_wait_ == 0 && train_first_) {
       // same graph topology, training-chain nodes first (they land on the graph's first queue)
       const bool defer = !side_metrics_ && defer_metrics_;
@@ -2027,7 +2119,7 @@ class Engine {
     HIP_OK(hipEventRecord(ev_join_, st2_));               // (train monitor ran on st2_ too)
     HIP_OK(hipStreamWaitEvent(st_, ev_join_, 0));
     HTRACE("launch_update");
-    launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_, inv_code_.p != nullptr);
+    if (!(g_skip & 8)) launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_, inv_code_.p != nullptr);
   }
   struct SoloScope {
     bool& f;

@@ -731,9 +731,14 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd(const MlpJob* __r
 // workgroup runs the tower forward, waiting per tile for the periods of its rows. Tiles are
 // visited in period order (tile index = bx * waves + wave, strided by the grid), so the
 // towers trail the recurrence period by period instead of starting after it.
-// Forward progress: workgroups are dispatched in linear-ID order on every XCD and each tower
-// workgroup depends only on workgroup (0, its job), whose ID is lower, so the lowest unfinished
-// workgroup can always run; the spin is bounded anyway (prog_wait).
+// Forward progress: each tower workgroup depends only on workgroup (0, its job). The engine
+// launches the fused kernel only when its whole grid fits the device at once (occupancy query of
+// the instantiation that runs, mlp_fwd_rnn_capacity), so on an otherwise idle device every
+// workgroup is resident. Beside the evaluation branch of the pipelined epoch some workgroups may
+// wait for CUs, but every kernel of that branch runs to completion without waiting on anything,
+// so the CUs it holds are released and the fused grid becomes resident; only one fused (spinning)
+// launch runs at a time. The spin is bounded anyway (prog_wait): a wait that gives up poisons the
+// model instead of hanging the device.
 DLAP_DEV void lstm_publish(const RnnJob& J, const ModelDesc* __restrict__ md, const float* sm, const int* sprog) {
   const int T = J.T, H = md->H, lane = threadIdx.x & 63;
   const float* shb = sm + gls_out_offset(T, H, md->nrnn);
@@ -759,11 +764,26 @@ DLAP_DEV void lstm_publish(const RnnJob& J, const ModelDesc* __restrict__ md, co
   }
 }
 
+// ne > 0 (the pipelined phase-1/3 epoch): workgroups 1 .. ne of each job run the recurrences of
+// that model's evaluation splits as well (rjobs[gridDim.y + job * ne + e], outputs flushed to
+// their pp at the end; nothing waits for them inside this launch), so the evaluation branch
+// starts at its tower forward right after this kernel instead of running its own LSTM launch
+// beside the training chain (where it waited for CUs the spinning tower workgroups held).
 template <class P, int KS1, int WMB, int HM, bool DPPG, bool SO = false>
 __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd_rnn(const MlpJob* __restrict__ jobs, MlpDims D,
                                                                   const RnnJob* __restrict__ rjobs,
-                                                                  const ModelDesc* __restrict__ md) {
+                                                                  const ModelDesc* __restrict__ md, int ne) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  if (blockIdx.x >= 1 && (int)blockIdx.x <= ne) {
+    const RnnJob& R = rjobs[gridDim.y + blockIdx.y * ne + (blockIdx.x - 1)];
+    float* sx = reinterpret_cast<float*>(smem);
+    const auto xg = gp(R.xg);
+    const int n = md->nrnn > 0 ? R.T * 4 * md->H : 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) sx[i] = xg[i];
+    __syncthreads();
+    if (threadIdx.x < 64 && md->nrnn > 0) lstm_gls_body<HM, DPPG, false, false>(R, md, sx, nullptr, nullptr, 0);
+    return;
+  }
   if (blockIdx.x == 0) {
     __shared__ int s_prog;
     const RnnJob& R = rjobs[blockIdx.y];
@@ -786,7 +806,7 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd_rnn(const MlpJob*
     }
     return;
   }
-  mlp_fwd_body<P, KS1, WMB, false, true, SO>(jobs[blockIdx.y], D, smem, blockIdx.x - 1, gridDim.x - 1);
+  mlp_fwd_body<P, KS1, WMB, false, true, SO>(jobs[blockIdx.y], D, smem, blockIdx.x - 1 - ne, gridDim.x - 1 - ne);
 }
 
 // ============================== wide evaluation forward ==================================
@@ -1648,6 +1668,17 @@ int mlp_fwd_rnn_capacity(const MlpDims& D0, int KS1, int WMB, int H, int nrnn, i
   else { O_KW(PrecBF16, 4, true) O_KW(PrecBF16, 8, false) }
 #undef O_KW
 #undef O_CASE
+  // the SDF-only instantiation (launch_mlp_fwd_rnn, so = true: the phase-1/3 training and
+  // evaluation forwards) has its own register footprint: the capacity is the smaller of the two
+  if (!D0.fp32 && per_cu > 0) {
+    int per_so = per_cu;
+#define OS_CASE(K, HM, DP) \
+    if (KS1 == K && H == HM) \
+      HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_so, k_mlp_fwd_rnn<PrecBF16, K, 1, HM, DP, true>, 256, sh));
+    OS_CASE(2, 4, true) OS_CASE(4, 4, true) OS_CASE(2, 8, false) OS_CASE(4, 8, false)
+#undef OS_CASE
+    per_cu = std::min(per_cu, per_so);
+  }
   int dev = 0;
   HIP_OK(hipGetDevice(&dev));
   int ncu = 0;
@@ -1656,24 +1687,25 @@ int mlp_fwd_rnn_capacity(const MlpDims& D0, int KS1, int WMB, int H, int nrnn, i
 }
 
 bool launch_mlp_fwd_rnn(const MlpJob* jobs, const RnnJob* rjobs, const ModelDesc* md, int njobs, int gx,
-                        const MlpDims& D0, int KS1, int WMB, int H, int nrnn, int tmax, hipStream_t st, bool so) {
+                        const MlpDims& D0, int KS1, int WMB, int H, int nrnn, int tmax, hipStream_t st, bool so,
+                        int ne) {
   if (!mlp_fwd_rnn_supported(D0, KS1, WMB, H, nrnn, tmax))
     dlap_throw_hip(hipErrorInvalidValue, "mlp_fwd_rnn: unsupported shape", __FILE__, __LINE__);
   MlpDims D = D0;
   D.pp_lds_floats = 0;                 // the per-period inputs are read as they are published
   const size_t sh = fwd_rnn_lds(D0, H, tmax);
-  dim3 grid(gx + 1, njobs), block(256);
+  dim3 grid(gx + 1 + ne, njobs), block(256);
   if (so && !D.fp32) {
 #define RS_CASE(K, HM, DP) \
     if (KS1 == K && H == HM) { \
-      hipLaunchKernelGGL((k_mlp_fwd_rnn<PrecBF16, K, 1, HM, DP, true>), grid, block, sh, st, jobs, D, rjobs, md); \
+      hipLaunchKernelGGL((k_mlp_fwd_rnn<PrecBF16, K, 1, HM, DP, true>), grid, block, sh, st, jobs, D, rjobs, md, ne); \
       HIP_OK(hipGetLastError()); return true; }
     RS_CASE(2, 4, true) RS_CASE(4, 4, true) RS_CASE(2, 8, false) RS_CASE(4, 8, false)
 #undef RS_CASE
   }
 #define R_CASE(PR, K, W, HM, DP) \
   if (KS1 == K && WMB == W && H == HM) { \
-    hipLaunchKernelGGL((k_mlp_fwd_rnn<PR, K, W, HM, DP>), grid, block, sh, st, jobs, D, rjobs, md); \
+    hipLaunchKernelGGL((k_mlp_fwd_rnn<PR, K, W, HM, DP>), grid, block, sh, st, jobs, D, rjobs, md, ne); \
     HIP_OK(hipGetLastError()); return true; }
 #define R_KW(PR, HM, DP) R_CASE(PR, 2, 1, HM, DP) R_CASE(PR, 2, 2, HM, DP) R_CASE(PR, 2, 4, HM, DP) \
   R_CASE(PR, 4, 1, HM, DP) R_CASE(PR, 4, 2, HM, DP) R_CASE(PR, 4, 4, HM, DP)

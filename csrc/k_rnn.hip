@@ -26,13 +26,14 @@
 #include "rnn.h"
 #include "update.h"
 #include "lstm_gls.h"
+#include "finalize.h"
 
 #define DLAP_MAX_M 1024
 
 // In-kernel phase timestamps (wall clock, 100 MHz) for profiling the serial kernels, read by
 // Engine.rnn_timestamps(). Slots: [0..3] k_lstm_gl train launch, [4..7] its eval launch (last
 // block = longest split), [8..12] k_lstm_bwd.
-__device__ long long g_rnn_ts[16];
+__device__ long long g_rnn_ts[24];   // [16]: fused tail, dpp in LDS; [17]: W_ih start
 #define RNN_TS(slot, cond) do { if ((cond) && threadIdx.x == 0) g_rnn_ts[slot] = wall_clock64(); } while (0)
 
 // Fast activations (v_exp + v_rcp): |err| < 1e-6 relative in the ranges that matter; tanh
@@ -459,11 +460,43 @@ __host__ __device__ inline size_t lstm_gpart_floats(int H) {
 // LDS floats of the dense-state path: M_t [T][64], y_t [T][8], W_hh [64], pair maps N_t / v_t
 __host__ __device__ inline size_t lstm_bwd_scan_floats(int T) { return (size_t)T * 72 + 64 + (size_t)((T - 1) / 2) * 72; }
 
-template <int HM>
-__global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ jobs,
-                                                  const ModelDesc* __restrict__ md, int scan) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const UpdJob& J = jobs[blockIdx.x];
+// LDS map of the LSTM backward (float offsets). k_lstm_bwd: coefficients, layer outputs,
+// incoming gradient, gate gradients, junk slots, weight-gradient partials, then (dense-state
+// path) M_t, y_t, W_hh, the pair maps. The fused tail (k_lstm_tail, `fused`): the step matrices
+// M_t live in global scratch (UpdJob::mscr) and the pair maps share one region with the gate
+// gradients + partials (dead before those are formed), so the block fits two per CU beside
+// the finalisation blocks of the same launch.
+struct LstmBwdLds { size_t cf, h, d, dgs, junk, gpart, M, y, W, N, v, total; };
+__host__ __device__ inline LstmBwdLds lstm_bwd_lds(int T, int H, bool scan, bool fused) {
+  LstmBwdLds L{};
+  const size_t G4 = 4 * (size_t)H, np = (size_t)((T - 1) / 2);
+  L.cf = 0; L.h = L.cf + (size_t)T * 6 * H; L.d = L.h + (size_t)T * H;
+  if (!fused) {
+    L.dgs = L.d + (size_t)T * H; L.junk = L.dgs + T * G4; L.gpart = L.junk + 64;
+    L.total = L.gpart + lstm_gpart_floats(H);
+    if (scan) {
+      L.M = L.total; L.y = L.M + (size_t)T * 64; L.W = L.y + (size_t)T * 8; L.N = L.W + 64; L.v = L.N + np * 64;
+      L.total = L.v + np * 8;
+    }
+    return L;
+  }
+  L.y = L.d + (size_t)T * H; L.W = L.y + (size_t)T * 8; L.junk = L.W + 64;
+  const size_t u = L.junk + 64;
+  L.N = u; L.v = L.N + np * 64;
+  L.dgs = u; L.gpart = L.dgs + T * G4;
+  const size_t a = np * 72, b = T * G4 + lstm_gpart_floats(H);
+  L.total = u + (a > b ? a : b);
+  L.M = 0;                                        // global (UpdJob::mscr)
+  return L;
+}
+
+// FUSED (the tail launch k_lstm_tail, single layer, H = 4, dense-state path): the incoming
+// gradient dpp is produced by the period blocks of the same launch -- the block waits for their
+// count (J.tail_ctr) only right before the pair maps, after the pre-pass and the step matrices;
+// the step matrices go to global scratch (LDS map above); the layer-0 W_ih gradient (k_wgrad's
+// sum, same order) is formed here from the gate gradients in LDS.
+template <int HM, bool FUSED>
+DLAP_DEV void lstm_bwd_body(const UpdJob& J, const ModelDesc* __restrict__ md, int scan, float* sm, bool tsm) {
   if (md->nrnn == 0) return;
   const int T = J.T, M = md->M, H = md->H, G4 = 4 * H;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -473,13 +506,17 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
   const uint32_t step = (uint32_t)*gp(J.drop_step);
   const auto params = gp(J.params);
   const auto grads = gp(J.grads);
-  const bool tsm = blockIdx.x == 0;
   RNN_TS(8, tsm);
-  float* s_cf = sm;                           // [T][6][H] BPTT coefficients (pre-pass)
-  float* s_h = s_cf + T * LSTM_NCOEF * H;      // [T][H]  layer outputs
-  float* s_d = s_h + T * H;                    // [T][H]  incoming gradient
-  float* dgs = s_d + T * H;                    // [T][4H] gate pre-activation gradients
-  for (int l = md->nrnn - 1; l >= 0; --l) {
+  const LstmBwdLds LL = lstm_bwd_lds(T, H, HM == 4 && H == 4 && scan, FUSED);
+  float* s_cf = sm + LL.cf;                    // [T][6][H] BPTT coefficients (pre-pass)
+  float* s_h = sm + LL.h;                      // [T][H]  layer outputs
+  float* s_d = sm + LL.d;                      // [T][H]  incoming gradient
+  float* dgs = sm + LL.dgs;                    // [T][4H] gate pre-activation gradients
+  float* junk0 = sm + LL.junk;                 // 64 junk slots (stores of non-owner lanes)
+  __shared__ int s_bad;                        // FUSED: the wait for dpp gave up
+  if (FUSED && threadIdx.x == 0) s_bad = 0;
+  if (FUSED) __syncthreads();
+  for (int l = FUSED ? 0 : md->nrnn - 1; l >= 0; --l) {
     const auto dout = l == md->nrnn - 1 ? gp(J.dpp) : gp(J.dx);
     const auto sgg = gp(J.sg) + (size_t)l * T * G4;
     const auto scg = gp(J.sc) + (size_t)l * T * H;
@@ -505,7 +542,7 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
         c[u] = scg[i];
         cp[u] = t > 0 ? scg[i - H] : (J.c0 ? gp(J.c0)[l * H + k] : 0.f);
         hv[u] = shg[i];
-        dv[u] = dout[i];
+        dv[u] = FUSED ? 0.f : dout[i];
       }
 #pragma unroll
       for (int u = 0; u < PU; ++u) {
@@ -521,19 +558,19 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
         q[4 * H] = tc * go[u] * (1.f - go[u]);
         q[5 * H] = gf[u];
         s_h[i] = hv[u];
-        s_d[i] = dv[u];
+        if (!FUSED) s_d[i] = dv[u];
       }
     }
     __syncthreads();
     if (l == 0) RNN_TS(9, tsm);
     if (wave == 0) __builtin_amdgcn_s_setprio(3);     // serial chain: see k_lstm_gls
-    if (HM == 4 && H == 4 && scan) {
+    if (FUSED || (HM == 4 && H == 4 && scan)) {
       // ---- dense-state BPTT (header comment): step matrices, chain on wave 0, gate gradients
-      float* s_M = dgs + T * G4 + 64 + lstm_gpart_floats(H);        // after the gpart region
-      float* s_y = s_M + T * 64;
-      float* s_W = s_y + T * 8;
-      float* s_N = s_W + 64;                          // [(T-1)/2][64] pair maps N_t
-      float* s_v = s_N + ((T - 1) / 2) * 64;          // [(T-1)/2][8]  pair offsets v_t
+      float* s_M = FUSED ? gp(J.mscr) : sm + LL.M;   // [T][64] step matrices
+      float* s_y = sm + LL.y;
+      float* s_W = sm + LL.W;
+      float* s_N = sm + LL.N;                         // [(T-1)/2][64] pair maps N_t
+      float* s_v = sm + LL.v;                         // [(T-1)/2][8]  pair offsets v_t
       if (threadIdx.x < 64) s_W[threadIdx.x] = whh_l;
       __syncthreads();
       // one thread per (t, row i): the step's 24 coefficients as six 16-byte reads, the row's
@@ -579,6 +616,31 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
             dst[1] = hi;
           }
         }
+      }
+      if constexpr (FUSED) {
+        // the incoming gradient: every period block of this launch has published dpp[t]
+        // (write-through stores, drained, then one agent-scope add each). Wave 0 polls the count
+        // (relaxed, s_sleep between polls, bounded), ONE agent acquire, then every wave loads.
+        if (threadIdx.x < 64) {
+          const int* ctr = J.tail_ctr;
+          int v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          unsigned spins = 0;
+          while (v < T) {
+            if (spins++ >= J.spin_limit) {         // never on a resident grid: poison the model
+              if (threadIdx.x == 0) { atomicAdd(const_cast<int*>(J.prog) + 1, 1); s_bad = 1; }
+              break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+            v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          }
+          asm volatile("" ::: "memory");
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        __syncthreads();
+        if (s_bad) return;                           // block-uniform; nothing written
+        for (int i = threadIdx.x; i < T * H; i += 256) s_d[i] = dout[i];
+        RNN_TS(16, tsm);
       }
       __syncthreads();
       // pair maps: the chain advances two steps per link, y_t = N_t y_{t+2} + v_t for the chain
@@ -629,7 +691,7 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
         const int offA = 8 * i + j, offB = 8 * j + i;
         // per-link state records without exec-mask changes: the owner lanes of a layout (j == 0
         // in R, i == 0 in C) store y_t, the others write a junk slot (the old path's)
-        float* junk = dgs + T * G4;
+        float* junk = junk0;
         float* dstR = j == 0 ? s_y + i : junk + lane;
         float* dstC = i == 0 ? s_y + j : junk + lane;
         const int strR = j == 0 ? 16 : 0, strC = i == 0 ? 16 : 0;     // two steps per link
@@ -724,7 +786,7 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
         d[8] = dc * q[12 + k];
         d[12] = dh * q[16 + k];
       }
-    } else if (wave == 0 && HM == 4 && H == 4) {
+    } else if (!FUSED && wave == 0 && HM == 4 && H == 4) {
       // Gate-per-lane BPTT (H = 4): lane L (mod 16) owns gate row L = 4q + k and keeps the
       // recurrent state of unit k replicated, so d_L = (q == 3 ? dh : dc) * coef is lane-local
       // and dh_next_j = sum_L W_hh[L][j] d_L is ONE reduce-scatter over the 16 lanes: two DPP
@@ -737,7 +799,7 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
       float w[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) w[j] = Whh[L16 * 4 + j];
-      float* junk = dgs + T * G4;
+      float* junk = junk0;
       float* ddst = lane < 16 ? dgs + L16 : junk + lane;
       const int dstride = lane < 16 ? 16 : 0;
       const int ci = (1 + kq) * 4 + ku;
@@ -791,7 +853,7 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
       }
       // dL/d(initial state) of the layer: the gradients carried past t = 0
       if (J.dh0 && lane < 4) { gp(J.dh0)[l * 4 + lane] = dh_next; gp(J.dc0)[l * 4 + lane] = dc_next; }
-    } else if (wave == 0) {
+    } else if (!FUSED && wave == 0) {
       const int k = lane < H ? lane : 0;
       const bool act = lane < H;
       const auto Whh = params + md->lstm_w_hh[l];
@@ -858,7 +920,7 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
     }
     __syncthreads();
     if (l == 0) RNN_TS(10, tsm);
-    if (l == 0) {
+    if (l == 0 && !FUSED) {
       const auto dg = gp(J.dg);
       for (int i = threadIdx.x; i < T * G4; i += 256) dg[i] = dgs[i];   // for k_wgrad
     }
@@ -871,8 +933,8 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
     const int ncol = H + 1 + (l > 0 ? H : 0);
     const int nout = G4 * ncol;
     const int S = max(1, min(LSTM_GSEG, 256 / max(nout, 1)));
-    float* gpart = dgs + T * G4 + 64;                 // [S][nout] (after the junk slots)
-    if (HM == 4 && H == 4) {
+    float* gpart = sm + LL.gpart;                     // [S][nout] (after the gate gradients)
+    if (FUSED || (HM == 4 && H == 4)) {
       // H = 4: [ncol x 16 gates] = sum_t x[t][col] dG[t][g] on v_mfma_f32_16x16x4f32 (exact
       // fp32 products) -- x = (h_{t-1} (the initial state at t = 0), 1 for the biases, the layer
       // input of a deeper layer). Wave w takes the 4-period k-steps w, w + 4, ...; the four
@@ -944,7 +1006,7 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
       }
       __syncthreads();
     }
-    if (l > 0) {
+    if (!FUSED && l > 0) {
       const auto Wih = params + md->lstm_w_ih[l];
       const auto dx = gp(J.dx);
       for (int idx = threadIdx.x; idx < T * H; idx += 256) {
@@ -958,7 +1020,108 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
     }
   }
   __syncthreads();
+  if constexpr (FUSED) {
+    // layer-0 W_ih gradient, k_wgrad<1>'s sums in k_wgrad's order: per 16-column tile, wave w
+    // takes the time quarter [T w / 4, T (w + 1) / 4) as one MFMA chain (A = macro columns,
+    // B = the gate gradients, here from LDS), the four partial tiles summed in wave order.
+    // Column tiles in batches of WB, every macro load of a batch issued before its MFMAs.
+    const int lk = lane >> 4, n = lane & 15;
+    const int ta = (T * wave) / 4, tb = (T * (wave + 1)) / 4;
+    const auto X = gp(J.macro);
+    float* red = sm + LL.gpart;                     // [4][64][4] per tile (gate partials dead)
+    RNN_TS(17, tsm);
+    constexpr int WB = 4, KC = 16;
+    const int ntc = (M + 1 + 15) / 16;
+    for (int c0t = 0; c0t < ntc; c0t += WB) {
+      f32x4 acc[WB];
+#pragma unroll
+      for (int c = 0; c < WB; ++c) acc[c] = zero4();
+      for (int t0 = ta; t0 < tb; t0 += 4 * KC) {
+        float a[WB][KC], bq[KC];
+#pragma unroll
+        for (int s2 = 0; s2 < KC; ++s2) {
+          const int t = t0 + 4 * s2 + lk;
+          const bool ok = t < tb;
+          const int tc = ok ? t : ta;
+          bq[s2] = ok ? dgs[tc * G4 + n] : 0.f;
+#pragma unroll
+          for (int c = 0; c < WB; ++c) {
+            const int col = (c0t + c) * 16 + n;
+            const float x = X[(size_t)tc * M + (col < M ? col : 0)];
+            a[c][s2] = ok ? (col < M ? x : (col == M ? 1.f : 0.f)) : 0.f;
+          }
+        }
+#pragma unroll
+        for (int s2 = 0; s2 < KC; ++s2)
+#pragma unroll
+          for (int c = 0; c < WB; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c][s2], bq[s2], acc[c], 0, 0, 0);
+      }
+#pragma unroll
+      for (int c = 0; c < WB; ++c) {
+        if (c0t + c >= ntc) break;                   // block-uniform
+        *reinterpret_cast<f32x4*>(red + (wave * 64 + lane) * 4) = acc[c];
+        __syncthreads();
+        if (wave == 0) {
+          const f32x4* r4 = reinterpret_cast<const f32x4*>(red);
+          const f32x4 v = r4[lane] + r4[64 + lane] + r4[128 + lane] + r4[192 + lane];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int cc = (c0t + c) * 16 + 4 * lk + r;
+            if (cc < M) grads[md->lstm_w_ih[0] + (size_t)n * M + cc] = v[r];
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // every period block has added to the count (the wait saw all T): rearm it for the next launch
+    if (threadIdx.x == 0) __hip_atomic_store(J.tail_ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   RNN_TS(11, tsm);
+}
+
+template <int HM>
+__global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ jobs,
+                                                  const ModelDesc* __restrict__ md, int scan) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  lstm_bwd_body<HM, false>(jobs[blockIdx.x], md, scan, sm, blockIdx.x == 0);
+}
+
+// Fused backward tail of phases 1 / 3 (one launch instead of k_finalize -> k_lstm_bwd -> k_wgrad):
+// grid (1 + T + slab blocks, models). Block 0 runs the LSTM backward (lstm_bwd_body<4, true>:
+// pre-pass and step matrices first, then it waits for the per-period gradient), blocks 1 .. T
+// form the per-period sums dpp[t] and publish them, the rest sum the weight-gradient slabs --
+// all three the same arithmetic as the separate kernels, so the results are bitwise equal.
+// The LSTM block is dispatched first and is the only one that waits; the others never wait, so
+// the launch drains on any residency.
+__global__ __launch_bounds__(256, 2) void k_lstm_tail(const UpdJob* __restrict__ ujobs, const FinJob* __restrict__ fjobs,
+                                                   const ModelDesc* __restrict__ md, int slab_stride, int nslab_blocks) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const UpdJob& U = ujobs[blockIdx.y];
+  if (blockIdx.x == 0) {
+    lstm_bwd_body<4, true>(U, md, 1, sm, blockIdx.y == 0);
+    return;
+  }
+  const FinJob& F = fjobs[blockIdx.y];
+  const int b = blockIdx.x - 1;
+  if (b < U.T) finalize_block(F, md, 1, slab_stride, nslab_blocks + b, U.tail_ctr);
+  else finalize_block(F, md, 1, slab_stride, b - U.T);
+}
+
+// whether the fused tail applies (single LSTM layer of width 4 on the dense-state BPTT path,
+// phases 1 / 3); its LDS bytes
+size_t lstm_tail_lds_bytes(int T, int H) { return lstm_bwd_lds(T, H, true, true).total * sizeof(float); }
+bool lstm_tail_supported(const ModelDesc& mh, int T) {
+  if (mh.nrnn != 1 || mh.H != 4 || mh.M <= 0 || T < 2) return false;
+  const char* scan_env = std::getenv("DLAP_LSTM_SCAN");
+  if (scan_env && std::atoi(scan_env) == 0) return false;
+  return lstm_tail_lds_bytes(T, mh.H) <= 80 * 1024;     // two per CU beside the finalisation blocks
+}
+void launch_lstm_tail(const UpdJob* ujobs, const FinJob* fjobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
+                      int T, int slab_stride, hipStream_t st) {
+  const int nslab_blocks = mh.ntile_s * 64 + (SLAB_EXTRA + 63) / 64;
+  hipLaunchKernelGGL(k_lstm_tail, dim3(1 + T + nslab_blocks, njobs), dim3(256), lstm_tail_lds_bytes(T, mh.H), st,
+                     ujobs, fjobs, md, slab_stride, nslab_blocks);
+  HIP_OK(hipGetLastError());
 }
 
 // --------------------------------------------------------------------------- k_wgrad ---
@@ -1064,7 +1227,7 @@ void launch_lstm_bwd(const UpdJob* jobs, int njobs, const ModelDesc* md, const M
 }
 
 std::vector<long long> rnn_timestamps() {
-  std::vector<long long> v(16);
-  HIP_OK(hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(g_rnn_ts), sizeof(long long) * 16));
+  std::vector<long long> v(24);
+  HIP_OK(hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(g_rnn_ts), sizeof(long long) * 24));
   return v;
 }

@@ -12,101 +12,16 @@
 #include "layout.h"
 #include "update.h"
 #include "loss.h"
+#include "finalize.h"
 
 // ============================================================ finalize ==================
-// Sums the per-workgroup slabs of the MLP backward into the flat gradient vector and the
-// per-row LSTM / moment-bias gradients into per-period sums. grid (nblocks, models).
+// The per-workgroup slab sums and per-period segment sums of the MLP backward (finalize.h),
+// one block per element group / period. grid (nblocks, models).
 __global__ __launch_bounds__(256) void k_finalize(const FinJob* __restrict__ jobs,
                                                   const ModelDesc* __restrict__ md, int phase,
                                                   int slab_stride, int b0) {
-  const FinJob& J = jobs[blockIdx.y];
-  const bool mom = phase == 2;
-  const int ntile = mom ? md->ntile_m : md->ntile_s;
-  const int tps = mom ? md->tps_m : md->tps_s;
-  const int nb_tiles = ntile * 64;                    // 64 elements per block
-  const int nb_extra = (SLAB_EXTRA + 63) / 64;
-  __shared__ float red[4][64];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  int b = blockIdx.x + b0;       // b0: first block of a partial launch (see launch_finalize)
-  // slab sums: lane = element, the 4 waves split the slabs (each sums its quarter in order,
-  // 16 independent loads in flight), then a fixed-order LDS combine
-  // (group 4: the stored slabs are fine slabs, summed in groups ((s0 + s1) + s2) + s3 first --
-  // the coarse slabs a launch with 4 fine slabs per workgroup stores; see wg_slab_finish)
-  auto slab_sum = [&](const float* src) {
-    const auto s0 = gp(src);
-    float acc = 0.f;
-    if (J.group == 4) {
-      const int nc = J.nslab >> 2;
-#pragma unroll 4
-      for (int k = wave; k < nc; k += 4) {
-        const size_t b = (size_t)4 * k * slab_stride;
-        float c = s0[b] + s0[b + slab_stride];
-        c += s0[b + 2 * (size_t)slab_stride];
-        c += s0[b + 3 * (size_t)slab_stride];
-        acc += c;
-      }
-    } else {
-#pragma unroll 16
-      for (int k = wave; k < J.nslab; k += 4) acc += s0[(size_t)k * slab_stride];
-    }
-    red[wave][lane] = acc;
-    __syncthreads();
-    return red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-  };
-  // the packed training weights of layers >= 1 and the SDF output row carry the dropout scale
-  // 1/(1-p) (k_pack), so their slab sums are gradients w.r.t. the scaled weights: scale back
-  const float dscale = J.dropout > 0.f ? 1.f / (1.f - J.dropout) : 1.f;
-  if (b < nb_tiles) {
-    const int ti = b >> 6, e = ((b & 63) << 6) + lane;
-    const GradTile& G = mom ? md->tile_m[ti] : md->tile_s[ti];
-    const int o = e >> 6, i = (e & 63) + 64 * G.chunk;
-    const int tpos = ti - G.slice * tps;
-    const float v = slab_sum(J.slab + (size_t)G.slice * J.nslab * slab_stride + tpos * 4096 + e);
-    bool ok = o < G.out && i < G.in;
-    int col = G.col0 + i;
-    if (G.xmap) {                                   // fused SDF layer 0: panel column -> W0 column
-      const int F = md->F, ppc = md->md.ppc;
-      if (i < F) col = i;
-      else if (i >= ppc && i < ppc + md->Dm) col = F + (i - ppc);
-      else ok = false;
-    }
-    if (wave == 0 && ok) gp(J.grads)[G.w_off + o * G.ld + col] = G.layer > 0 ? v * dscale : v;
-    return;
-  }
-  b -= nb_tiles;
-  if (b < nb_extra) {
-    const int e = b * 64 + lane;
-    const int ec = e < SLAB_EXTRA ? e : SLAB_EXTRA - 1;
-    const float v = slab_sum(J.slab + tps * 4096 + ec);     // slice-0 slabs
-    const int dst = e < SLAB_EXTRA ? (mom ? md->extra_m[e] : md->extra_s[e]) : -1;
-    const bool wo = !mom && e >= DLAP_MAXL * 64 && e < DLAP_MAXL * 64 + 64;   // SDF output row
-    if (wave == 0 && dst >= 0) gp(J.grads)[dst] = wo ? v * dscale : v;
-    return;
-  }
-  b -= nb_extra;
-  // per-period segment sums: one block per period, threads = (column d, row group)
-  const int D = mom ? 64 : (md->nrnn > 0 ? md->Dm : 0);
-  const int t = b;
-  if (D == 0 || t >= J.T) return;
-  __shared__ float seg[256];
-  int Dp = 1;
-  while (Dp < D) Dp <<= 1;
-  const int nrg = 256 / Dp, d = threadIdx.x % Dp, rg = threadIdx.x / Dp;
-  const auto src = gp(mom ? J.v : J.u);
-  const int r0 = gp(J.row_ptr)[t], r1 = gp(J.row_ptr)[t + 1];
-  float s = 0.f;
-  if (d < D) {
-#pragma unroll 8
-    for (int r = r0 + rg; r < r1; r += nrg) s += src[(size_t)r * D + d];
-  }
-  seg[threadIdx.x] = s;
-  __syncthreads();
-  if (rg == 0 && d < D) {
-    float tot = 0.f;
-    for (int g = 0; g < nrg; ++g) tot += seg[g * Dp + d];
-    if (mom) gp(J.dab)[t * 64 + d] = tot;
-    else gp(J.dpp)[t * D + d] = tot;
-  }
+  // b0: first block of a partial launch (see launch_finalize)
+  finalize_block(jobs[blockIdx.y], md, phase, slab_stride, blockIdx.x + b0);
 }
 
 void launch_finalize(const FinJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
@@ -122,6 +37,12 @@ void launch_finalize(const FinJob* jobs, int njobs, const ModelDesc* md, const M
   if (nb == 0) return;
   hipLaunchKernelGGL(k_finalize, dim3(nb, njobs), dim3(256), 0, st, jobs, md, phase, slab_stride, b0);
   HIP_OK(hipGetLastError());
+}
+
+DLAP_DEV bool prog_poisoned(const int* prog) {
+  if (!prog) return false;
+  const auto p = gp(prog);
+  return (p[1] | p[16 + 1] | p[32 + 1]) != 0;
 }
 
 // ============================================================ packing ===================
@@ -324,7 +245,8 @@ __global__ __launch_bounds__(256) void k_pack(const UpdJob* __restrict__ jobs,
   const auto src = gp(static_cast<const float*>(J.params));
   const float dscale = J.dropout > 0.f ? 1.f / (1.f - J.dropout) : 1.f;
   if (e < S.total) pack_store(J, md, S, e, pack_value(md, S, src, e), dscale);
-  if (bump && blockIdx.x == 0 && threadIdx.x == 0) {
+  // (a poisoned model's counters stay put, as in the fused k_adam, which returns early)
+  if (bump && blockIdx.x == 0 && threadIdx.x == 0 && !prog_poisoned(J.prog)) {
     gp(J.adam_step)[bump - 1] = gp(J.adam_step)[bump - 1] + 1;
     gp(J.drop_step)[0] = gp(J.drop_step)[0] + 1;
   }
@@ -358,11 +280,6 @@ void launch_pack(float* const*, const UpdJob* jobs, int njobs, const ModelDesc* 
 }
 
 // ============================================================ update ====================
-DLAP_DEV bool prog_poisoned(const int* prog) {
-  if (!prog) return false;
-  const auto p = gp(prog);
-  return (p[1] | p[16 + 1] | p[32 + 1]) != 0;
-}
 
 // Clip-by-global-norm + Adam over the phase's scope. grid (blocks, models): every block
 // reduces the full scope norm itself (fixed order -> identical in all blocks, no grid

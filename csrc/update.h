@@ -57,6 +57,10 @@ struct UpdJob {            // one model
   const int* inv_code;     // [P][PACK_FAN] scatter lists: the packed elements holding parameter p
                            // (-1 padded; nullptr: a separate k_pack re-packs after k_adam)
   int* upd_ctr;            // [1] k_adam blocks finished (the last one advances the step counters)
+  int* tail_ctr;           // fused backward tail (k_lstm_tail): per-period sums published so far
+                           //   (zero between launches: the LSTM block rearms it)
+  float* mscr;             // fused backward tail: [T][64] LSTM step-matrix scratch (train split)
+  unsigned spin_limit;     // fused backward tail: polls before the wait for dpp gives up
 };
 
 // History row written per epoch by k_epoch_end (HIST_W floats).
@@ -90,6 +94,10 @@ void launch_update(const UpdJob* jobs, int njobs, const ModelDesc* md, const Mod
                    float lr, hipStream_t st, bool fused);
 void launch_lstm_bwd(const UpdJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
                      int T, int phase, hipStream_t st);
+// fused backward tail of phases 1 / 3: k_finalize + k_lstm_bwd + k_wgrad as one launch (k_rnn.hip)
+bool lstm_tail_supported(const ModelDesc& mh, int T);
+void launch_lstm_tail(const UpdJob* ujobs, const FinJob* fjobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
+                      int T, int slab_stride, hipStream_t st);
 void launch_pack(float* const* params_unused, const UpdJob* jobs, int njobs, const ModelDesc* md,
                  const ModelDesc& mh, hipStream_t st);
 int pack_total(const ModelDesc& mh);   // packed elements per model (k_pack's element space)

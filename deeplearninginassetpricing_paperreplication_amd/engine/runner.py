@@ -92,13 +92,30 @@ class GANEngine:
         self.splits: Dict[int, object] = {}
 
     # ---- data -----------------------------------------------------------------------
+    # host splits whose dense fp32 features exceed this are compacted on the host and only the
+    # compact bf16 rows are uploaded (a dense device copy of the scaled 600x30000x512 panel would
+    # be ~37 GB of temporaries); smaller host splits take the device path (faster, same bits:
+    # tests/test_panel_gpu.py)
+    HOST_COMPACT_BYTES = 1 << 31
+
     def set_data(self, train: Dict, valid: Optional[Dict] = None, test: Optional[Dict] = None):
         """Upload the splits. The engine builds its compacted layout on the GPU from the dense
         split (``Engine.set_split_dense``, k_panel.hip): CUDA tensors are read in place, host
-        arrays are copied to the device once; nothing comes back to the host but the row count."""
+        arrays are copied to the device once (large host splits are compacted on the host
+        instead, ``HOST_COMPACT_BYTES``); nothing comes back to the host but the row count."""
+        from .panel import prepare_split
         dev = torch.device("cuda", torch.cuda.current_device())
         for s, b in enumerate((train, valid, test)):
             if b is None:
+                continue
+            f0 = b["individual_features"]
+            on_dev = isinstance(f0, torch.Tensor) and f0.is_cuda
+            if not on_dev and int(np.prod(tuple(f0.shape))) * 4 > self.HOST_COMPACT_BYTES:
+                ps = prepare_split(b, self.KP, fp32=self.fp32)
+                self.eng.set_split(s, ps.X, ps.rowti, ps.row_ptr, ps.Rm, ps.mask, ps.macro.reshape(-1),
+                                   int(ps.T), int(ps.N))
+                self.splits[s] = SplitInfo(self.eng, s, int(ps.T), int(ps.N), int(self.eng.split_rows(s)))
+                del ps
                 continue
             feats = _on_device(b["individual_features"], torch.float32, dev)
             ret = _on_device(b["returns"], torch.float32, dev)
@@ -113,6 +130,9 @@ class GANEngine:
             self.eng.set_split_dense(s, feats.data_ptr(), ret.data_ptr(), mask.data_ptr(), True, mptr,
                                      int(T), int(N), int(F), torch.cuda.current_stream(dev).cuda_stream)
             self.splits[s] = SplitInfo(self.eng, s, int(T), int(N), int(self.eng.split_rows(s)))
+            if not on_dev:              # the dense device copies were temporaries: release them
+                del feats, ret, mask, macro
+                torch.cuda.empty_cache()
 
     # ---- parameters -----------------------------------------------------------------
     def set_model(self, g: int, model, seed: int):

@@ -125,10 +125,17 @@ def buckets(entries: Sequence[Tuple[Dict, float, Dict]]) -> List[List[int]]:
     differ only in lr, in dropout (a per-member rate of the batched engine) or in keys the model
     ignores -- CSMV (``num_units_rnn_moment``) is such a no-op in the reference
     (`/root/reference/src/model.py:309-311`) -- share a bucket: the paper grid's 384 configs
-    are 48 architectures x 8 members, the baseline grid's 24 x 16."""
+    are 48 architectures x 8 members, the baseline grid's 24 x 16.
+
+    With hidden moment layers the engine's structural switch "the train split's moments can be
+    cached in phase 3" depends on whether ANY batched member drops out (their keep masks change
+    the moments), so there the key also carries ``dropout > 0``: a p = 0 member then trains in a
+    bucket of p = 0 members, exactly as it would alone."""
     groups: Dict[object, List[int]] = {}
     for i, (cfg, _, _) in enumerate(entries):
-        groups.setdefault(dataclasses.replace(ModelSpec.from_config(cfg), dropout=0.0), []).append(i)
+        spec = ModelSpec.from_config(cfg)
+        key = (dataclasses.replace(spec, dropout=0.0), len(spec.moment_hidden) > 0 and spec.dropout > 0)
+        groups.setdefault(key, []).append(i)
     return list(groups.values())
 
 

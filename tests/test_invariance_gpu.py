@@ -129,6 +129,40 @@ def test_fused_forward_capped_grid_equals_two_launches(big, monkeypatch):
     assert not eng.eng.fused_forward(1) and not eng.eng.fused_forward(3)
 
 
+def test_eval_recurrences_in_fused_forward_equal_separate_branch(big, monkeypatch):
+    """The pipelined epoch with the evaluation splits' projections and recurrences inside the
+    training prologue / fused forward (one launch, workgroups 1 .. 2 of each model) gives the bits
+    of the round-4 graph whose evaluation branch ran its own LSTM launches."""
+    cfg = default_cli_config(178, 46)
+    monkeypatch.setenv("DLAP_EVAL_IN_FWD", "0")
+    e0, ref = _train(big, cfg, [21, 22], 2)
+    assert not e0.eng.fused_info()["eval_in_fwd_p3"]
+    monkeypatch.setenv("DLAP_EVAL_IN_FWD", "1")
+    e1, res = _train(big, cfg, [21, 22], 2)
+    info = e1.eng.fused_info()
+    assert info["eval_in_fwd_p1"] and info["eval_in_fwd_p3"], info
+    for ph in (1, 3):       # (1 recurrence + 2 evaluation recurrences + towers) per model, resident
+        assert (1 + info["eval_per_model"] + info[f"all_gx_p{ph}"]) * 2 <= info["cap_all"], info
+    for s in (21, 22):
+        _same(ref[s], res[s])
+
+
+def test_fused_backward_tail_equals_separate_kernels(big, monkeypatch):
+    """k_lstm_tail (the per-period sums, the LSTM BPTT with its weight gradients, the layer-0
+    W_ih gradient and the weight-slab sums in ONE launch; the LSTM block waits for the period
+    blocks in-kernel) gives the bits of k_finalize -> k_lstm_bwd -> k_wgrad, batched models
+    included."""
+    cfg = default_cli_config(178, 46)
+    monkeypatch.setenv("DLAP_FUSED_TAIL", "0")
+    e0, ref = _train(big, cfg, [51, 52], 2)
+    assert not e0.eng.fused_info()["fused_tail"]
+    monkeypatch.setenv("DLAP_FUSED_TAIL", "1")
+    e1, res = _train(big, cfg, [51, 52], 2)
+    assert e1.eng.fused_info()["fused_tail"]
+    for s in (51, 52):
+        _same(ref[s], res[s])
+
+
 def test_fused_phase2_under_the_guarantee_equals_two_launches(big, monkeypatch):
     """Phase 2's fused forward (opt-in, DLAP_FUSED_PHASE2=1) runs on the capped grid and gives the
     same bits as the two-launch path."""
