@@ -260,6 +260,8 @@ class Engine {
     fused_p2_ = env_int("DLAP_FUSED_PHASE2", 0) != 0;
     eval_in_fwd_ = env_int("DLAP_EVAL_IN_FWD", 1) != 0;
     fused_tail_ = env_int("DLAP_FUSED_TAIL", 1) != 0;
+    self_proj_ = env_int("DLAP_SELF_PROJ", 1) != 0;
+    rotate_ = env_int("DLAP_ROTATE", 0) != 0;
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
                residual, fp32);
     // fp32 wide path: layer 0 through k_proj0 + the ZIN towers (the fused-layer-0 k_mlp_fwd_zx
@@ -278,7 +280,7 @@ class Engine {
       S.gnorm.alloc(1); S.best.alloc(3); S.aux.alloc((size_t)2 * md_.md.aux_floats);
       S.hist.alloc((size_t)max_epochs_ * HIST_W);
       S.adam_step.alloc(2); S.drop_step.alloc(1); S.snap_flags.alloc(2); S.ep.alloc(2); S.upd_ctr.alloc(1);
-      S.tail_ctr.alloc(16);
+      S.tail_ctr.alloc(lstm_tail_words());
       S.blob.alloc((size_t)2 * md_.md.blob_frags * 512 * xw());   // bf16 (or fp32: 2 u16 each)
       S.blob0.alloc((size_t)std::max(1, md_.md.b0_frags) * 512 * xw());
       S.wproj.alloc((size_t)(md_.proj_mp + 2) * md_.proj_np);
@@ -707,11 +709,21 @@ class Engine {
       for (int e = 0; e < n; ++e) HIP_OK(hipGraphLaunch(g, st_));
       return;
     }
-    hipGraphExec_t head = graph_for(graph_key(phase, lr, ignore_epoch, sel, 1), [&] { enqueue_head(phase, lr); });
-    hipGraphExec_t body = graph_for(graph_key(phase, lr, ignore_epoch, sel, 2),
-                                    [&] { enqueue_pipe(phase, lr, ignore_epoch, sel); });
-    hipGraphExec_t tail = graph_for(graph_key(phase, lr, ignore_epoch, sel, 3),
-                                    [&] { enqueue_tail(phase, ignore_epoch, sel); });
+    // rotated graphs (the eval-in-forward epoch): each graph STARTS with the previous epoch's
+    // Adam and ends at the join of its two branches, so no kernel of the graph waits on the other
+    // branch -- the join coincides with the graph boundary. head = first epoch's training (no
+    // Adam); body = Adam(e-1) | training(e) || evaluation(e-1) + bookkeeping; tail = Adam(last) |
+    // evaluation(last) + bookkeeping. The same kernels in the same dependency order per buffer.
+    const bool rot = rotate_ && b_wait_ == 0 && !side_metrics_ && eval_rnn_in_fwd(phase);
+    const int k0 = rot ? 10 : 0;
+    hipGraphExec_t head = graph_for(graph_key(phase, lr, ignore_epoch, sel, k0 + 1),
+                                    [&] { if (rot) enqueue_head_rot(phase); else enqueue_head(phase, lr); });
+    hipGraphExec_t body = graph_for(graph_key(phase, lr, ignore_epoch, sel, k0 + 2),
+                                    [&] { if (rot) enqueue_pipe_rot(phase, lr, ignore_epoch, sel);
+                                          else enqueue_pipe(phase, lr, ignore_epoch, sel); });
+    hipGraphExec_t tail = graph_for(graph_key(phase, lr, ignore_epoch, sel, k0 + 3),
+                                    [&] { if (rot) enqueue_tail_rot(phase, lr, ignore_epoch, sel);
+                                          else enqueue_tail(phase, ignore_epoch, sel); });
     HTRACE("launch head");
     HIP_OK(hipGraphLaunch(head, st_));
     join_eval_gram();                     // the next graphs evaluate
@@ -1065,6 +1077,7 @@ class Engine {
   // (one job table: j_rnn_all_ = train jobs, then evaluation jobs); DLAP_EVAL_IN_FWD=0: the
   // evaluation branch runs its own prologue beside the training chain (the round-4 graph)
   bool eval_in_fwd_ = true;
+  bool self_proj_ = true;                    // DLAP_SELF_PROJ: recurrences project their own inputs
   DevBuf<char> j_rnn_all_;
   int cap_all_ = 0;                          // co-residency capacity at the longest split's LDS
   DevBuf<int> prog_;
@@ -1550,6 +1563,7 @@ class Engine {
     J.dE = (phase == 2 || phase == 3) ? W.dE.p : nullptr;
     J.dEu = phase == 1 ? W.dEu.p : nullptr;
     J.part = W.part.p; J.pe = W.pe.p; J.pu = W.pu.p; J.dw = W.dw.p; J.rstat = W.rstat.p; J.scal = W.scal.p;
+    if (s == 0 && phase > 0) J.prog_reset = prog_ptr(g, 0);
     if (gram) {
       J.gram = 1; J.G = W.gram.p; J.gpart = W.gpart.p;
       J.asset_full = 0;
@@ -1854,8 +1868,12 @@ class Engine {
     // the latency-bound LSTM first, before the streaming projection loads the memory system
     // (fused: only its input projection here, the recurrence runs inside the tower launch)
     const bool fused = fused_fwd(phase);
-    HTRACE("launch_prologue fused=%d eval_rnn=%d", (int)fused, (int)eval_rnn);
-    if (eval_rnn) launch_proj(as<RnnJob>(j_rnn_all_), G_ + n_eval_jobs_, tmax_fwd_all(), dd(), md_, st_, train_mom(phase));
+    // the recurrences project their own inputs inside the fused launch unless the towers need the
+    // moment network's per-period bias table (k_proj's other output)
+    const bool selfproj = fused && self_proj_ && !train_mom(phase) && !md_.md.wide;
+    HTRACE("launch_prologue fused=%d eval_rnn=%d selfproj=%d", (int)fused, (int)eval_rnn, (int)selfproj);
+    if (selfproj) {}
+    else if (eval_rnn) launch_proj(as<RnnJob>(j_rnn_all_), G_ + n_eval_jobs_, tmax_fwd_all(), dd(), md_, st_, train_mom(phase));
     else if (fused) launch_proj(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_, train_mom(phase));
     else launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_, train_mom(phase));
     // pipelined epoch, train_first_ == 2: the evaluation branch's LSTM prologue is enqueued right
@@ -1871,11 +1889,11 @@ class Engine {
     else if (eval_rnn)
       launch_mlp_fwd_rnn(as<MlpJob>(j_mlp_train_[phase]), as<RnnJob>(j_rnn_all_), dd(), G_, fused_all_gx(phase),
                          md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, tmax_fwd_all(), st_, !train_mom(phase),
-                         ne_per_model());
+                         ne_per_model(), selfproj);
     else if (fused)
       launch_mlp_fwd_rnn(as<MlpJob>(j_mlp_train_[phase]), as<RnnJob>(j_rnn_train_), dd(), G_,
                          fused_train_gx(phase), md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, D.T, st_,
-                         !train_mom(phase));
+                         !train_mom(phase), 0, selfproj);
     else
       launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, phase == 2 ? gx_fwd_[0] : gx_fwd13_, md_.md, md_.KS1,
                      md_.WMB, st_, !train_mom(phase));
@@ -1891,7 +1909,9 @@ class Engine {
       HTRACE("launch_period_bwd(gram)");
       launch_period_bwd(lj, G_, D.T, st_);
     }
-    if (defer_metrics && phase != 2) {
+    if (tail_metrics_ && phase != 2) {
+      // the train split's metrics are computed by the backward tail (enqueue_train_tail)
+    } else if (defer_metrics && phase != 2) {
       HIP_OK(hipEventRecord(ev_mid_, st_));
     } else if (side) {
       HIP_OK(hipEventRecord(ev_mid_, st_));
@@ -1927,18 +1947,24 @@ class Engine {
   }
   // k_finalize -> k_lstm_bwd -> k_wgrad as one launch (k_lstm_tail) where it applies
   bool fused_tail_ = true;                   // DLAP_FUSED_TAIL
+  // the pipelined eval-in-forward epoch: the train split's job metrics run in the backward tail
+  // (one more block of k_lstm_tail; a launch after the tail where it is not fused) instead of on
+  // the evaluation branch, so the training chain forks only once (after the fused forward)
+  bool tail_metrics_ = false;
   bool tail_fused(int phase) const {
     return fused_tail_ && !split_tail_ && phase != 2 && splits_[0].set && lstm_tail_supported(md_, splits_[0].T);
   }
   void enqueue_train_tail(int phase) {
     const SplitDev& D = splits_[0];
     if (g_skip & 1) { join_side(); return; }
+    const LossJob* lm = tail_metrics_ && phase != 2 ? loss_tab(phase, use_gram(phase)) : nullptr;
     if (tail_fused(phase)) {
       HTRACE("launch_lstm_tail");
-      launch_lstm_tail(as<UpdJob>(j_upd_), as<FinJob>(j_fin_), G_, dd(), md_, D.T, slab_stride(), st_);
+      launch_lstm_tail(as<UpdJob>(j_upd_), as<FinJob>(j_fin_), G_, dd(), md_, D.T, slab_stride(), st_, lm);
       join_side();
       return;
     }
+    if (lm) launch_job_metrics(lm, G_, st_);
     if (split_tail_) {
       // slab sums beside the LSTM backward (which reads only the per-period sums)
       HIP_OK(hipEventRecord(ev_b3_, st_));
@@ -2035,6 +2061,31 @@ class Engine {
     HTRACE("launch_update");
     launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_, inv_code_.p != nullptr);
   }
+  // rotated pipeline (run_epochs): see there
+  bool rotate_ = true;                       // DLAP_ROTATE
+  void enqueue_head_rot(int phase) {
+    enqueue_train_grads(phase);
+    enqueue_dropmask(phase, 1, st_);                     // masks of the first pipelined epoch
+  }
+  void enqueue_pipe_rot(int phase, float lr, int ignore_epoch, float sel) {
+    HTRACE("launch_update");
+    if (!(g_skip & 8)) launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_, inv_code_.p != nullptr);
+    tail_metrics_ = true;
+    enqueue_train_grads(phase, nullptr, true, 2, false, false, true);
+    tail_metrics_ = false;
+    HIP_OK(hipStreamWaitEvent(st2_, ev_a_, 0));          // after the fused forward (evaluation LSTMs)
+    enqueue_eval_towers(st2_);
+    enqueue_epoch_end(phase, ignore_epoch, sel, st2_);
+    enqueue_dropmask(phase, 1, st2_);
+    HIP_OK(hipEventRecord(ev_join_, st2_));             // (capture end: the branches join here)
+    HIP_OK(hipStreamWaitEvent(st_, ev_join_, 0));
+  }
+  void enqueue_tail_rot(int phase, float lr, int ignore_epoch, float sel) {
+    HTRACE("launch_update");
+    launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_, inv_code_.p != nullptr);
+    { SoloScope solo(eval_solo_); enqueue_eval(st_); }
+    enqueue_epoch_end(phase, ignore_epoch, sel, st_);
+  }
   void enqueue_pipe(int phase, float lr, int ignore_epoch, float sel) {
     HIP_OK(hipEventRecord(ev_fork_, st_));
     HIP_OK(hipStreamWaitEvent(st2_, ev_fork_, 0));
@@ -2043,14 +2094,11 @@ class Engine {
       // evaluation branch forks after it: towers, losses, this epoch's train metrics (after its
       // loss pass), the bookkeeping and the next epoch's dropout masks, beside the training
       // backward and its tail
-      const bool defer = defer_metrics_;
-      enqueue_train_grads(phase, nullptr, true, 2, false, defer, true);
+      tail_metrics_ = true;
+      enqueue_train_grads(phase, nullptr, true, 2, false, false, true);
+      tail_metrics_ = false;
       HIP_OK(hipStreamWaitEvent(st2_, ev_a_, 0));
       enqueue_eval_towers(st2_);
-      if (defer && phase != 2) {
-        HIP_OK(hipStreamWaitEvent(st2_, ev_mid_, 0));
-        launch_job_metrics(loss_tab(phase, use_gram(phase)), G_, st2_);
-      }
       enqueue_epoch_end(phase, ignore_epoch, sel, st2_);
       enqueue_dropmask(phase, 1, st2_);
       HIP_OK(hipEventRecord(ev_join_, st2_));

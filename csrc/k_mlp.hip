@@ -769,40 +769,59 @@ DLAP_DEV void lstm_publish(const RnnJob& J, const ModelDesc* __restrict__ md, co
 // their pp at the end; nothing waits for them inside this launch), so the evaluation branch
 // starts at its tower forward right after this kernel instead of running its own LSTM launch
 // beside the training chain (where it waited for CUs the spinning tower workgroups held).
+// selfproj: the recurrences' layer-0 input projections are computed inside their workgroups
+// (proj_into_lds on the spare waves, tile by tile ahead of the recurrence) instead of being staged
+// from k_proj's output -- no k_proj launch before this one. (The train split's progress counter,
+// which k_proj used to zero, is zeroed by the k_period_fwd that follows every fused forward.)
 template <class P, int KS1, int WMB, int HM, bool DPPG, bool SO = false>
 __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd_rnn(const MlpJob* __restrict__ jobs, MlpDims D,
                                                                   const RnnJob* __restrict__ rjobs,
-                                                                  const ModelDesc* __restrict__ md, int ne) {
+                                                                  const ModelDesc* __restrict__ md, int ne,
+                                                                  int selfproj) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int w = threadIdx.x >> 6;
   if (blockIdx.x >= 1 && (int)blockIdx.x <= ne) {
     const RnnJob& R = rjobs[gridDim.y + blockIdx.y * ne + (blockIdx.x - 1)];
     float* sx = reinterpret_cast<float*>(smem);
+    if (md->nrnn == 0) return;
+    if (selfproj) {
+      int* ready = reinterpret_cast<int*>(sx + gls_ready_offset(R.T, md->H));
+      for (int i = threadIdx.x; i < (R.T + 15) / 16; i += blockDim.x) ready[i] = 0;
+      __syncthreads();
+      if (w == 0) lstm_gls_body<HM, DPPG, false, false>(R, md, sx, nullptr, nullptr, 0, ready);
+      else proj_into_lds(R, md, sx, ready, w - 1, 3);
+      return;
+    }
     const auto xg = gp(R.xg);
-    const int n = md->nrnn > 0 ? R.T * 4 * md->H : 0;
+    const int n = R.T * 4 * md->H;
     for (int i = threadIdx.x; i < n; i += blockDim.x) sx[i] = xg[i];
     __syncthreads();
-    if (threadIdx.x < 64 && md->nrnn > 0) lstm_gls_body<HM, DPPG, false, false>(R, md, sx, nullptr, nullptr, 0);
+    if (w == 0) lstm_gls_body<HM, DPPG, false, false>(R, md, sx, nullptr, nullptr, 0);
     return;
   }
   if (blockIdx.x == 0) {
     __shared__ int s_prog;
     const RnnJob& R = rjobs[blockIdx.y];
     const bool tsm = blockIdx.y == 0 && jobs[0].gbits;
+    float* sx = reinterpret_cast<float*>(smem);
+    int* ready = selfproj ? reinterpret_cast<int*>(sx + gls_ready_offset(R.T, md->H)) : nullptr;
     if (threadIdx.x == 0) s_prog = 0;
     if (tsm && threadIdx.x == 0) g_mlp_ts[8] = wall_clock64();
-    {   // layer-0 input projections (k_proj) into the LDS staging area with all four waves
-      float* sx = reinterpret_cast<float*>(smem);
+    if (selfproj) {
+      for (int i = threadIdx.x; i < (R.T + 15) / 16; i += blockDim.x) ready[i] = 0;
+    } else {   // layer-0 input projections (k_proj) into the LDS staging area with all four waves
       const auto xg = gp(R.xg);
       const int n = md->nrnn > 0 ? R.T * 4 * md->H : 0;
       for (int i = threadIdx.x; i < n; i += blockDim.x) sx[i] = xg[i];
     }
     __syncthreads();
-    const int w = threadIdx.x >> 6;
     if (w == 0) {
-      lstm_gls_body<HM, DPPG, false, true>(R, md, reinterpret_cast<float*>(smem), &s_prog, tsm ? g_mlp_ts : nullptr, 8);
+      lstm_gls_body<HM, DPPG, false, true>(R, md, sx, &s_prog, tsm ? g_mlp_ts : nullptr, 8, ready);
     } else if (w == 1) {
-      lstm_publish(R, md, reinterpret_cast<const float*>(smem), &s_prog);
+      lstm_publish(R, md, sx, &s_prog);
       if (tsm && threadIdx.x == 64) g_mlp_ts[12] = wall_clock64();
+    } else if (selfproj) {
+      proj_into_lds(R, md, sx, ready, w - 2, 2);
     }
     return;
   }
@@ -1643,7 +1662,7 @@ void launch_mlp_fwd(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int
 static size_t fwd_rnn_lds(const MlpDims& D0, int H, int tmax) {
   MlpDims D = D0;
   D.pp_lds_floats = 0;
-  return std::max(lds_bytes_of(D), gls_lds_floats(tmax, H) * sizeof(float));
+  return std::max(lds_bytes_of(D), gls_lds_floats_ready(tmax, H) * sizeof(float));
 }
 bool mlp_fwd_rnn_supported(const MlpDims& D, int KS1, int WMB, int H, int nrnn, int tmax) {
   if (D.wide || nrnn <= 0 || D.Dm != H || tmax <= 0) return false;
@@ -1688,7 +1707,7 @@ int mlp_fwd_rnn_capacity(const MlpDims& D0, int KS1, int WMB, int H, int nrnn, i
 
 bool launch_mlp_fwd_rnn(const MlpJob* jobs, const RnnJob* rjobs, const ModelDesc* md, int njobs, int gx,
                         const MlpDims& D0, int KS1, int WMB, int H, int nrnn, int tmax, hipStream_t st, bool so,
-                        int ne) {
+                        int ne, bool selfproj) {
   if (!mlp_fwd_rnn_supported(D0, KS1, WMB, H, nrnn, tmax))
     dlap_throw_hip(hipErrorInvalidValue, "mlp_fwd_rnn: unsupported shape", __FILE__, __LINE__);
   MlpDims D = D0;
@@ -1698,14 +1717,14 @@ bool launch_mlp_fwd_rnn(const MlpJob* jobs, const RnnJob* rjobs, const ModelDesc
   if (so && !D.fp32) {
 #define RS_CASE(K, HM, DP) \
     if (KS1 == K && H == HM) { \
-      hipLaunchKernelGGL((k_mlp_fwd_rnn<PrecBF16, K, 1, HM, DP, true>), grid, block, sh, st, jobs, D, rjobs, md, ne); \
+      hipLaunchKernelGGL((k_mlp_fwd_rnn<PrecBF16, K, 1, HM, DP, true>), grid, block, sh, st, jobs, D, rjobs, md, ne, (int)selfproj); \
       HIP_OK(hipGetLastError()); return true; }
     RS_CASE(2, 4, true) RS_CASE(4, 4, true) RS_CASE(2, 8, false) RS_CASE(4, 8, false)
 #undef RS_CASE
   }
 #define R_CASE(PR, K, W, HM, DP) \
   if (KS1 == K && WMB == W && H == HM) { \
-    hipLaunchKernelGGL((k_mlp_fwd_rnn<PR, K, W, HM, DP>), grid, block, sh, st, jobs, D, rjobs, md, ne); \
+    hipLaunchKernelGGL((k_mlp_fwd_rnn<PR, K, W, HM, DP>), grid, block, sh, st, jobs, D, rjobs, md, ne, (int)selfproj); \
     HIP_OK(hipGetLastError()); return true; }
 #define R_KW(PR, HM, DP) R_CASE(PR, 2, 1, HM, DP) R_CASE(PR, 2, 2, HM, DP) R_CASE(PR, 2, 4, HM, DP) \
   R_CASE(PR, 4, 1, HM, DP) R_CASE(PR, 4, 2, HM, DP) R_CASE(PR, 4, 4, HM, DP)

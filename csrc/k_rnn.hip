@@ -27,6 +27,7 @@
 #include "update.h"
 #include "lstm_gls.h"
 #include "finalize.h"
+#include "loss_dev.h"
 
 #define DLAP_MAX_M 1024
 
@@ -45,43 +46,7 @@ DLAP_DEV float ftanh(float x) {
 }
 
 // ------------------------------------------------------------------------ k_proj -------
-// xg[t] = W_ih x_t + b_ih + b_hh (layer-0 LSTM gates) and abias[t] = W_m0[:, :M] x_t + b_m0
-// (moment layer-0 per-period bias, zero-padded to 64): a [T x MP] . [MP x NP] fp32 GEMM on
-// the matrix cores. grid (ceil(T/16), NP/16, jobs), one wave per 16x16 output tile, K = 4 per
-// v_mfma_f32_16x16x4f32 (full fp32 products / accumulation). Operands come straight from
-// global memory (macro rows, and the k_pack-produced wproj [MP+2][NP] whose last two rows
-// hold the biases): all loads of a tile are independent, so the tile costs ~one memory round trip.
-//   A (16x4): lane l -> A[t = l&15][k = l>>4];  B (4x16): lane l -> B[k = l>>4][o = l&15]
-//   C (16x16): lane l -> C[t = 4*(l>>4) + r][o = l&15]
-// One 16 (periods) x 16 (outputs) tile of the projection on one wave: returns lane l's
-// accumulator C[t0 + 4*(l>>4) + r][o0 + (l&15)] with the bias added.
-DLAP_DEV f32x4 proj_tile(const RnnJob& J, const ModelDesc* md, int t0, int o0) {
-  const int T = J.T, M = md->M, MP = md->proj_mp, NP = md->proj_np;
-  const int l = threadIdx.x & 63, n = l & 15, kq = l >> 4;
-  const int ta = min(t0 + n, T - 1);
-  const auto xrow = gp(J.macro) + (size_t)ta * M;
-  const auto wcol = gp(J.wproj) + o0 + n;
-  f32x4 acc = zero4();
-  // all operand loads of a K chunk are issued before the first MFMA consumes them: one
-  // memory round trip per PROJ_KC * 4 columns instead of one per unrolled group
-  constexpr int PROJ_KC = 48;
-  for (int kb = 0; kb < MP; kb += 4 * PROJ_KC) {
-    float a[PROJ_KC], b[PROJ_KC];
-#pragma unroll
-    for (int s = 0; s < PROJ_KC; ++s) {
-      const int m = kb + 4 * s + kq;
-      const float x = xrow[m < M ? m : M - 1];
-      const float w = wcol[(size_t)(m < MP ? m : MP - 1) * NP];
-      a[s] = m < M ? x : 0.f;
-      b[s] = m < MP ? w : 0.f;
-    }
-#pragma unroll
-    for (int s = 0; s < PROJ_KC; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], b[s], acc, 0, 0, 0);
-  }
-  const float bias = wcol[(size_t)MP * NP] + wcol[(size_t)(MP + 1) * NP];   // b_ih + b_hh (b_m0 + 0)
-  return acc + bias;
-}
-
+// (proj_tile: lstm_gls.h)
 // grid (ceil(T/16), column tiles, jobs); blockIdx.y counts from column tile y0 (y0 = G4/16 when
 // the LSTM projects its own inputs: only the moment table is left here).
 __global__ __launch_bounds__(64) void k_proj(const RnnJob* __restrict__ jobs,
@@ -467,6 +432,12 @@ __host__ __device__ inline size_t lstm_bwd_scan_floats(int T) { return (size_t)T
 // gradients + partials (dead before those are formed), so the block fits two per CU beside
 // the finalisation blocks of the same launch.
 struct LstmBwdLds { size_t cf, h, d, dgs, junk, gpart, M, y, W, N, v, total; };
+// hand-off words of the fused tail (UpdJob::tail_ctr, one 128-byte line each): periods published,
+// gate gradients published, W_ih helper blocks done
+#define TAIL_CNT 0
+#define TAIL_FLAG 32
+#define TAIL_DONE 64
+#define TAIL_WORDS 96
 __host__ __device__ inline LstmBwdLds lstm_bwd_lds(int T, int H, bool scan, bool fused) {
   LstmBwdLds L{};
   const size_t G4 = 4 * (size_t)H, np = (size_t)((T - 1) / 2);
@@ -924,6 +895,17 @@ DLAP_DEV void lstm_bwd_body(const UpdJob& J, const ModelDesc* __restrict__ md, i
       const auto dg = gp(J.dg);
       for (int i = threadIdx.x; i < T * G4; i += 256) dg[i] = dgs[i];   // for k_wgrad
     }
+    if (l == 0 && FUSED) {
+      // hand the gate gradients to the W_ih helper blocks of the launch (R1: write-through stores,
+      // every wave drains, barrier, one flag store); they run k_wgrad's sums while this block forms
+      // the W_hh / bias gradients
+      const auto dg = gp(J.dg);
+      for (int i = threadIdx.x; i < T * G4; i += 256)
+        __hip_atomic_store(dg + i, dgs[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_store(J.tail_ctr + TAIL_FLAG, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     // W_hh [4H][H] and the biases: (gate, column) outputs x S time segments over the 256
     // threads (S = 3 at H = 4: 240 of them busy instead of 80), segment partials summed in
     // segment order from LDS (fixed order: deterministic)
@@ -1021,60 +1003,8 @@ DLAP_DEV void lstm_bwd_body(const UpdJob& J, const ModelDesc* __restrict__ md, i
   }
   __syncthreads();
   if constexpr (FUSED) {
-    // layer-0 W_ih gradient, k_wgrad<1>'s sums in k_wgrad's order: per 16-column tile, wave w
-    // takes the time quarter [T w / 4, T (w + 1) / 4) as one MFMA chain (A = macro columns,
-    // B = the gate gradients, here from LDS), the four partial tiles summed in wave order.
-    // Column tiles in batches of WB, every macro load of a batch issued before its MFMAs.
-    const int lk = lane >> 4, n = lane & 15;
-    const int ta = (T * wave) / 4, tb = (T * (wave + 1)) / 4;
-    const auto X = gp(J.macro);
-    float* red = sm + LL.gpart;                     // [4][64][4] per tile (gate partials dead)
-    RNN_TS(17, tsm);
-    constexpr int WB = 4, KC = 16;
-    const int ntc = (M + 1 + 15) / 16;
-    for (int c0t = 0; c0t < ntc; c0t += WB) {
-      f32x4 acc[WB];
-#pragma unroll
-      for (int c = 0; c < WB; ++c) acc[c] = zero4();
-      for (int t0 = ta; t0 < tb; t0 += 4 * KC) {
-        float a[WB][KC], bq[KC];
-#pragma unroll
-        for (int s2 = 0; s2 < KC; ++s2) {
-          const int t = t0 + 4 * s2 + lk;
-          const bool ok = t < tb;
-          const int tc = ok ? t : ta;
-          bq[s2] = ok ? dgs[tc * G4 + n] : 0.f;
-#pragma unroll
-          for (int c = 0; c < WB; ++c) {
-            const int col = (c0t + c) * 16 + n;
-            const float x = X[(size_t)tc * M + (col < M ? col : 0)];
-            a[c][s2] = ok ? (col < M ? x : (col == M ? 1.f : 0.f)) : 0.f;
-          }
-        }
-#pragma unroll
-        for (int s2 = 0; s2 < KC; ++s2)
-#pragma unroll
-          for (int c = 0; c < WB; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a[c][s2], bq[s2], acc[c], 0, 0, 0);
-      }
-#pragma unroll
-      for (int c = 0; c < WB; ++c) {
-        if (c0t + c >= ntc) break;                   // block-uniform
-        *reinterpret_cast<f32x4*>(red + (wave * 64 + lane) * 4) = acc[c];
-        __syncthreads();
-        if (wave == 0) {
-          const f32x4* r4 = reinterpret_cast<const f32x4*>(red);
-          const f32x4 v = r4[lane] + r4[64 + lane] + r4[128 + lane] + r4[192 + lane];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int cc = (c0t + c) * 16 + 4 * lk + r;
-            if (cc < M) grads[md->lstm_w_ih[0] + (size_t)n * M + cc] = v[r];
-          }
-        }
-        __syncthreads();
-      }
-    }
     // every period block has added to the count (the wait saw all T): rearm it for the next launch
-    if (threadIdx.x == 0) __hip_atomic_store(J.tail_ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) __hip_atomic_store(J.tail_ctr + TAIL_CNT, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   RNN_TS(11, tsm);
 }
@@ -1086,44 +1016,6 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
   lstm_bwd_body<HM, false>(jobs[blockIdx.x], md, scan, sm, blockIdx.x == 0);
 }
 
-// Fused backward tail of phases 1 / 3 (one launch instead of k_finalize -> k_lstm_bwd -> k_wgrad):
-// grid (1 + T + slab blocks, models). Block 0 runs the LSTM backward (lstm_bwd_body<4, true>:
-// pre-pass and step matrices first, then it waits for the per-period gradient), blocks 1 .. T
-// form the per-period sums dpp[t] and publish them, the rest sum the weight-gradient slabs --
-// all three the same arithmetic as the separate kernels, so the results are bitwise equal.
-// The LSTM block is dispatched first and is the only one that waits; the others never wait, so
-// the launch drains on any residency.
-__global__ __launch_bounds__(256, 2) void k_lstm_tail(const UpdJob* __restrict__ ujobs, const FinJob* __restrict__ fjobs,
-                                                   const ModelDesc* __restrict__ md, int slab_stride, int nslab_blocks) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const UpdJob& U = ujobs[blockIdx.y];
-  if (blockIdx.x == 0) {
-    lstm_bwd_body<4, true>(U, md, 1, sm, blockIdx.y == 0);
-    return;
-  }
-  const FinJob& F = fjobs[blockIdx.y];
-  const int b = blockIdx.x - 1;
-  if (b < U.T) finalize_block(F, md, 1, slab_stride, nslab_blocks + b, U.tail_ctr);
-  else finalize_block(F, md, 1, slab_stride, b - U.T);
-}
-
-// whether the fused tail applies (single LSTM layer of width 4 on the dense-state BPTT path,
-// phases 1 / 3); its LDS bytes
-size_t lstm_tail_lds_bytes(int T, int H) { return lstm_bwd_lds(T, H, true, true).total * sizeof(float); }
-bool lstm_tail_supported(const ModelDesc& mh, int T) {
-  if (mh.nrnn != 1 || mh.H != 4 || mh.M <= 0 || T < 2) return false;
-  const char* scan_env = std::getenv("DLAP_LSTM_SCAN");
-  if (scan_env && std::atoi(scan_env) == 0) return false;
-  return lstm_tail_lds_bytes(T, mh.H) <= 80 * 1024;     // two per CU beside the finalisation blocks
-}
-void launch_lstm_tail(const UpdJob* ujobs, const FinJob* fjobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
-                      int T, int slab_stride, hipStream_t st) {
-  const int nslab_blocks = mh.ntile_s * 64 + (SLAB_EXTRA + 63) / 64;
-  hipLaunchKernelGGL(k_lstm_tail, dim3(1 + T + nslab_blocks, njobs), dim3(256), lstm_tail_lds_bytes(T, mh.H), st,
-                     ujobs, fjobs, md, slab_stride, nslab_blocks);
-  HIP_OK(hipGetLastError());
-}
-
 // --------------------------------------------------------------------------- k_wgrad ---
 // out[g][col] = sum_t dG[t][g] * x[t][col] (x = macro, or 1 for the bias column col = M) for the
 // layer-0 LSTM input weights (phases 1/3, dG = gate gradients) or the moment layer-0 macro
@@ -1133,11 +1025,16 @@ void launch_lstm_tail(const UpdJob* ujobs, const FinJob* fjobs, int njobs, const
 //   C lane l -> (col = c0 + 4(l>>4) + r, g = g0 + (l&15)).
 // grid (ceil((M+1)/16), models), 4 waves split the time axis, every operand of a wave's 16
 // k-steps is requested before the first MFMA; the 4 partial tiles are summed in LDS in wave order.
-template <int GT>
-__global__ __launch_bounds__(256) void k_wgrad(const UpdJob* __restrict__ jobs,
-                                               const ModelDesc* __restrict__ md, int phase) {
+// done: the fused tail's helper form -- after every wave has read its operands, one lane counts
+// the block on *done (agent scope); the last of ndone rearms the hand-off words for the next launch
+// before_dg: called by every thread once, after the first k-chunk's macro operands are requested
+// and before any gate-gradient load (the fused tail's helpers wait for the hand-off there, with
+// their constant operands already in flight); returns false to abandon the block (block-uniform).
+struct NoWait { DLAP_DEV bool operator()() const { return true; } };
+template <int GT, typename BeforeDG = NoWait>
+DLAP_DEV void wgrad_block(const UpdJob& J, const ModelDesc* __restrict__ md, int phase, int cblk,
+                          int* done = nullptr, int ndone = 0, BeforeDG before_dg = NoWait{}) {
   __shared__ f32x4 red[4][GT][64];
-  const UpdJob& J = jobs[blockIdx.y];
   const int T = J.T, M = md->M;
   const bool mom = phase == 2;
   const int G = mom ? md->m[0].out : 4 * md->H;
@@ -1145,14 +1042,14 @@ __global__ __launch_bounds__(256) void k_wgrad(const UpdJob* __restrict__ jobs,
   const auto dG = gp(mom ? J.dab : J.dg);
   const auto X = gp(J.macro);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, n = lane & 15, kq = lane >> 4;
-  const int c0 = blockIdx.x * 16, col = c0 + n;
+  const int c0 = cblk * 16, col = c0 + n;
   const int ta = (T * wave) / 4, tb = (T * (wave + 1)) / 4;
   f32x4 acc[GT];
 #pragma unroll
   for (int gt = 0; gt < GT; ++gt) acc[gt] = zero4();
   constexpr int KC = 16;
-  for (int t0 = ta; t0 < tb; t0 += 4 * KC) {
-    float a[KC], b[KC][GT];
+  float a[KC], b[KC][GT];
+  auto load_x = [&](int t0) {
 #pragma unroll
     for (int s = 0; s < KC; ++s) {
       const int t = t0 + 4 * s + kq;
@@ -1160,6 +1057,17 @@ __global__ __launch_bounds__(256) void k_wgrad(const UpdJob* __restrict__ jobs,
       const int tc = ok ? t : ta;
       const float x = X[(size_t)tc * M + (col < M ? col : 0)];
       a[s] = ok ? (col < M ? x : (col == M ? 1.f : 0.f)) : 0.f;
+    }
+  };
+  load_x(ta);                                   // (harmless when this wave's range is empty)
+  if (!before_dg()) return;
+  for (int t0 = ta; t0 < tb; t0 += 4 * KC) {
+    if (t0 != ta) load_x(t0);
+#pragma unroll
+    for (int s = 0; s < KC; ++s) {
+      const int t = t0 + 4 * s + kq;
+      const bool ok = t < tb;
+      const int tc = ok ? t : ta;
 #pragma unroll
       for (int gt = 0; gt < GT; ++gt) {
         const int g = gt * 16 + n;
@@ -1175,6 +1083,13 @@ __global__ __launch_bounds__(256) void k_wgrad(const UpdJob* __restrict__ jobs,
 #pragma unroll
   for (int gt = 0; gt < GT; ++gt) red[wave][gt][lane] = acc[gt];
   __syncthreads();
+  if (done && threadIdx.x == 0) {
+    const int prev = __hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (prev == ndone - 1) {               // every helper has read dg: rearm flag and counter
+      __hip_atomic_store(done - (TAIL_DONE - TAIL_FLAG), 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   if (wave != 0) return;
 #pragma unroll
   for (int gt = 0; gt < GT; ++gt) {
@@ -1194,6 +1109,90 @@ __global__ __launch_bounds__(256) void k_wgrad(const UpdJob* __restrict__ jobs,
       }
     }
   }
+}
+
+template <int GT>
+__global__ __launch_bounds__(256) void k_wgrad(const UpdJob* __restrict__ jobs,
+                                               const ModelDesc* __restrict__ md, int phase) {
+  wgrad_block<GT>(jobs[blockIdx.y], md, phase, blockIdx.x);
+}
+
+// Fused backward tail of phases 1 / 3 (one launch instead of k_finalize -> k_lstm_bwd -> k_wgrad):
+// grid (1 + T + slab blocks + W_ih blocks, models). Block 0 runs the LSTM backward
+// (lstm_bwd_body<4, true>: pre-pass and step matrices first, then it waits for the per-period
+// gradient); blocks 1 .. T form the per-period sums dpp[t] and publish them; the slab blocks sum
+// the weight-gradient slabs; the last (M + 16) / 16 blocks wait for block 0's gate gradients
+// and form the layer-0 W_ih gradient (wgrad_block) while block 0 forms W_hh and the biases.
+// Every block runs the same arithmetic as the separate kernels, so the results are bitwise equal.
+// Blocks 0 and the W_ih blocks are the only ones that wait; the blocks they wait for never wait,
+// and the launch (under 400 blocks at the bench size) is resident at once on an idle device.
+// ljobs (optional): the train split's loss jobs of the step -- one more block per model computes
+// its job metrics (k_job_metrics' body; the loss passes finished before this launch), so the
+// pipelined epoch needs no fork to the evaluation branch for them.
+__global__ __launch_bounds__(256, 2) void k_lstm_tail(const UpdJob* __restrict__ ujobs, const FinJob* __restrict__ fjobs,
+                                                   const ModelDesc* __restrict__ md, int slab_stride, int nslab_blocks,
+                                                   const LossJob* __restrict__ ljobs) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const UpdJob& U = ujobs[blockIdx.y];
+  if (blockIdx.x == 0) {
+    lstm_bwd_body<4, true>(U, md, 1, sm, blockIdx.y == 0);
+    return;
+  }
+  const FinJob& F = fjobs[blockIdx.y];
+  const int b = blockIdx.x - 1;
+  if (b < U.T) { finalize_block(F, md, 1, slab_stride, nslab_blocks + b, U.tail_ctr + TAIL_CNT); return; }
+  if (b < U.T + nslab_blocks) { finalize_block(F, md, 1, slab_stride, b - U.T); return; }
+  const int nwg = (md->M + 1 + 15) / 16;
+  if (b >= U.T + nslab_blocks + nwg) {            // the train split's job metrics
+    if (ljobs) job_metrics_body<256>(ljobs[blockIdx.y], sm + DLAP_MAX_T, sm);
+    return;
+  }
+  // W_ih helper: k_wgrad's block, its macro operands requested first, then the wait for the gate
+  // gradients (relaxed poll, one agent acquire, barrier) before their loads
+  const int cblk = b - U.T - nslab_blocks;
+  __shared__ int bad;
+  auto wait_dg = [&]() -> bool {
+    if (threadIdx.x < 64) {
+      const int* flag = U.tail_ctr + TAIL_FLAG;
+      int v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      unsigned spins = 0;
+      bool ok = true;
+      while (v == 0) {
+        if (spins++ >= U.spin_limit) { ok = false; break; }   // block 0 gave up (and poisoned the model)
+        __builtin_amdgcn_s_sleep(2);
+        v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      }
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (threadIdx.x == 0) bad = ok ? 0 : 1;
+    }
+    __syncthreads();
+    return bad == 0;
+  };
+  wgrad_block<1>(U, md, 1, cblk, U.tail_ctr + TAIL_DONE, nwg, wait_dg);
+  if (blockIdx.y == 0 && cblk == nwg - 1 && threadIdx.x == 0) g_rnn_ts[17] = wall_clock64();
+}
+
+// whether the fused tail applies (single LSTM layer of width 4 on the dense-state BPTT path,
+// phases 1 / 3); its LDS bytes
+size_t lstm_tail_lds_bytes(int T, int H) { return lstm_bwd_lds(T, H, true, true).total * sizeof(float); }
+bool lstm_tail_supported(const ModelDesc& mh, int T) {
+  if (mh.nrnn != 1 || mh.H != 4 || mh.M <= 0 || T < 2) return false;
+  const char* scan_env = std::getenv("DLAP_LSTM_SCAN");
+  if (scan_env && std::atoi(scan_env) == 0) return false;
+  return lstm_tail_lds_bytes(T, mh.H) + 6400 <= 80 * 1024;   // (+ static LDS) two per CU
+}
+int lstm_tail_words() { return TAIL_WORDS; }
+void launch_lstm_tail(const UpdJob* ujobs, const FinJob* fjobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
+                      int T, int slab_stride, hipStream_t st, const LossJob* ljobs) {
+  const int nslab_blocks = mh.ntile_s * 64 + (SLAB_EXTRA + 63) / 64;
+  const int nwg = (mh.M + 1 + 15) / 16;
+  // (the metrics block keeps its scratch in the dynamic LDS: DLAP_MAX_T + 4 floats)
+  const size_t sh = std::max(lstm_tail_lds_bytes(T, mh.H), (size_t)(DLAP_MAX_T + 4) * sizeof(float));
+  hipLaunchKernelGGL(k_lstm_tail, dim3(1 + T + nslab_blocks + nwg + (ljobs ? 1 : 0), njobs), dim3(256), sh, st,
+                     ujobs, fjobs, md, slab_stride, nslab_blocks, ljobs);
+  HIP_OK(hipGetLastError());
 }
 
 void launch_lstm_bwd(const UpdJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,

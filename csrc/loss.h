@@ -56,6 +56,8 @@ struct LossJob {
   int gram;              // 1: Gram mode
   const double* G;       // [2][T][T] Gc, Gu
   double* gpart;         // [T][2] per-period s_t (G s)_t of Gc and Gu
+  int* prog_reset;       // train jobs: the fused forward's progress counter of this (model, split),
+                         //   zeroed by k_period_fwd (it follows every fused forward; nullptr: none)
 };
 
 // One (model, split) of the Gram build (k_gram.hip).

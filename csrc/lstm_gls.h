@@ -13,6 +13,7 @@
 // sum_j w[j] * v(lane j) as a balanced tree (dependency depth log2 HM + 1)
 template <int HM>
 DLAP_DEV float bcast_dot(const float (&w)[HM], float v) {
+#pragma clang fp contract(off)
   float p[HM];
 #pragma unroll
   for (int j = 0; j < HM; ++j) p[j] = w[j] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
@@ -60,6 +61,89 @@ DLAP_DEV float gl_gather(float y, int off_units, int q) {
   }
 }
 
+// ---- layer-0 input projection (k_proj in k_rnn.hip, and the fused forward's in-kernel form) ----
+// xg[t] = W_ih x_t + b_ih + b_hh (layer-0 LSTM gates) and abias[t] = W_m0[:, :M] x_t + b_m0
+// (moment layer-0 per-period bias, zero-padded to 64): a [T x MP] . [MP x NP] fp32 GEMM on
+// the matrix cores. grid (ceil(T/16), NP/16, jobs), one wave per 16x16 output tile, K = 4 per
+// v_mfma_f32_16x16x4f32 (full fp32 products / accumulation). Operands come straight from
+// global memory (macro rows, and the k_pack-produced wproj [MP+2][NP] whose last two rows
+// hold the biases): all loads of a tile are independent, so the tile costs ~one memory round trip.
+//   A (16x4): lane l -> A[t = l&15][k = l>>4];  B (4x16): lane l -> B[k = l>>4][o = l&15]
+//   C (16x16): lane l -> C[t = 4*(l>>4) + r][o = l&15]
+// One 16 (periods) x 16 (outputs) tile of the projection on one wave: returns lane l's
+// accumulator C[t0 + 4*(l>>4) + r][o0 + (l&15)] with the bias added.
+// Operands through raw buffer loads: one 32-bit per-lane offset per operand stream with the
+// K step in the instruction's immediate (x) or a scalar offset (w), so a chunk's 2 x PROJ_KC
+// loads cost their data registers only and stay in flight together even inside a kernel at its
+// register limit (the fused forward's in-kernel projection; with 64-bit per-load addresses the
+// compiler there serialised them, one memory round trip per load). Reads past a row end are
+// masked to zero; reads past the buffer return zero (the descriptors' num_records).
+DLAP_DEV f32x4 proj_tile(const RnnJob& J, const ModelDesc* md, int t0, int o0) {
+  const int T = J.T, M = md->M, MP = md->proj_mp, NP = md->proj_np;
+  const int l = threadIdx.x & 63, n = l & 15, kq = l >> 4;
+  const int ta = min(t0 + n, T - 1);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)J.macro, (short)0, T * M * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)J.wproj, (short)0, (MP + 2) * NP * 4, 0x00020000);
+  const int xo = (ta * M + kq) * 4, wo = (kq * NP + o0 + n) * 4;
+  f32x4 acc = zero4();
+  // all operand loads of a K chunk are issued before the first MFMA consumes them: one
+  // memory round trip per PROJ_KC * 4 columns instead of one per unrolled group
+  constexpr int PROJ_KC = 48;
+  for (int kb = 0; kb < MP; kb += 4 * PROJ_KC) {
+    float a[PROJ_KC], b[PROJ_KC];
+#pragma unroll
+    for (int s = 0; s < PROJ_KC; ++s) {
+      a[s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, xo + 4 * kb + 16 * s, 0, 0));
+      b[s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(wr, wo, (kb + 4 * s) * NP * 4, 0));
+    }
+#pragma unroll
+    for (int s = 0; s < PROJ_KC; ++s) {
+      const int m = kb + 4 * s + kq;
+      acc = __builtin_amdgcn_mfma_f32_16x16x4f32(m < M ? a[s] : 0.f, m < MP ? b[s] : 0.f, acc, 0, 0, 0);
+    }
+  }
+  const auto wcol = gp(J.wproj) + o0 + n;
+  const float bias = wcol[(size_t)MP * NP] + wcol[(size_t)(MP + 1) * NP];   // b_ih + b_hh (b_m0 + 0)
+  return acc + bias;
+}
+
+
+// The fused forward's in-kernel projection (k_mlp_fwd_rnn, selfproj): waves w0 .. w0 + nw - 1 of
+// the recurrence's workgroup take the 16-period tiles of xg round-robin -- proj_tile, the bits of
+// k_proj -- write them to the LDS staging area and raise each tile's ready flag once the wave's
+// LDS stores have completed; the recurrence (lstm_gls_body, `ready`) polls a tile's flag (plain
+// LDS reads: no fence -- a wave's LDS operations complete in order) only when it reaches a tile
+// it has not seen ready yet.
+DLAP_DEV void proj_into_lds(const RnnJob& J, const ModelDesc* __restrict__ md, float* sx, int* ready, int w, int nw) {
+  const int T = J.T, G4 = 4 * md->H;
+  const int l = threadIdx.x & 63, n = l & 15, kq = l >> 4;
+  for (int j = w; j * 16 < T; j += nw) {
+    for (int o0 = 0; o0 < G4; o0 += 16) {
+      const f32x4 acc = proj_tile(J, md, 16 * j, o0);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = 16 * j + 4 * kq + r;
+        if (t < T && o0 + n < G4) sx[t * G4 + o0 + n] = acc[r];
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (l == 0) __hip_atomic_store(ready + j, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  }
+}
+// the recurrence waits for the projected tile holding period t (one wave; bounded). `have`:
+// tiles 0 .. have - 1 are known to be ready (the recurrence reaches the tiles in order)
+DLAP_DEV void wait_xtile(const int* ready, int t, int& have) {
+  if (!ready || (t >> 4) < have) return;
+  const int j = t >> 4;
+  unsigned spins = 0;
+  while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(ready + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) == 0) {
+    __builtin_amdgcn_s_sleep(1);
+    if (++spins > (1u << 24)) break;         // (never: the producing waves always finish)
+  }
+  asm volatile("" ::: "memory");
+  have = j + 1;
+}
+
 // LDS ordering among the lanes of ONE wave (the recurrence runs on a single wave; the fused
 // kernel's publisher wave never takes part in a workgroup barrier, so none is used here).
 DLAP_DEV void wave_lds_sync() {
@@ -70,6 +154,9 @@ DLAP_DEV void wave_lds_sync() {
 
 // LDS (floats): xg [T][4H] | gates [T][4H] | cells [T][H] | outputs 2 x [T][H] | junk [64].
 __host__ __device__ inline size_t gls_lds_floats(int T, int H) { return (size_t)T * (8 * H + 3 * H) + 64; }
+// ready flags after the recurrence's LDS image (one per 16-period tile)
+__host__ __device__ inline size_t gls_ready_offset(int T, int H) { return gls_lds_floats(T, H); }
+__host__ __device__ inline size_t gls_lds_floats_ready(int T, int H) { return gls_lds_floats(T, H) + (T + 15) / 16 + 4; }
 // the last layer's output ring inside that image
 __host__ __device__ inline size_t gls_out_offset(int T, int H, int nrnn) {
   return (size_t)T * (8 * H + H) + (size_t)((nrnn - 1) & 1) * T * H;
@@ -87,9 +174,15 @@ __host__ __device__ inline size_t gls_out_offset(int T, int H, int nrnn) {
 //           (LDS, workgroup-scope release); the output flush to J.out is left to the
 //           publisher wave (lstm_publish in k_mlp.hip).
 //   ts:     optional in-kernel timestamps (slots tsb + 1, tsb + 2, tsb + 3).
+//   ready:  (fused forward, in-kernel projection) per-tile flags of the staged projections: the
+//           layer-0 loop waits for a tile before it reads its steps (nullptr: all staged).
 template <int HM, bool DPPG, bool STAGEX, bool PUB>
 DLAP_DEV void lstm_gls_body(const RnnJob& J, const ModelDesc* __restrict__ md, float* sm, int* sprog,
-                            long long* ts, int tsb) {
+                            long long* ts, int tsb, const int* ready = nullptr) {
+  // every multiply-add of the recurrence is written out (fmaf) and nothing else is contracted: the
+  // stand-alone kernel and the fused forward compile this body in different contexts and must
+  // produce the same bits (tests/test_invariance_gpu.py, fused vs two launches)
+#pragma clang fp contract(off)
   const int nrnn = md->nrnn;
   const int T = J.T, H = DPPG ? HM : md->H, G4 = 4 * H;
   const int L = threadIdx.x & 63;
@@ -156,12 +249,12 @@ DLAP_DEV void lstm_gls_body(const RnnJob& J, const ModelDesc* __restrict__ md, f
     auto cell = [&](int t, float pre) {
       if constexpr (DPPG) pre = bcast_dot_row<HM>(whh, h, pre);
       else pre += bcast_dot<HM>(whh, h);
-      const float y = kb * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(pre)) + kc;
+      const float y = fmaf(kb, __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(pre)), kc);
       const float gf = gl_gather<HM, DPPG>(y, H, 1);
       const float gg = gl_gather<HM, DPPG>(y, 2 * H, 2);
       const float go = gl_gather<HM, DPPG>(y, 3 * H, 3);
-      c = gf * c + y * gg;                                  // y = i on the unit lanes
-      h = go * (2.f * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(c)) - 1.f);
+      c = fmaf(gf, c, y * gg);                              // y = i on the unit lanes
+      h = go * fmaf(2.f, __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(c)), -1.f);
       gdst[t * gstride] = y * ysave;
       udst_c[t * ustride] = c * (1.f / KC);
       udst_h[t * ustride] = h;
@@ -177,8 +270,11 @@ DLAP_DEV void lstm_gls_body(const RnnJob& J, const ModelDesc* __restrict__ md, f
         for (int k = 0; k < CH; ++k) x[k] = sx[min(t0 + k, T - 1) * G4 + row];
       };
       const int tfull = T / CH * CH;
+      int have = 0;                                     // projected tiles known to be in LDS
+      wait_xtile(ready, 0, have);
       ldch(0, xa);
       for (int t0 = 0; t0 < tfull; t0 += CH) {
+        if (t0 + CH < T) wait_xtile(ready, t0 + CH, have);   // (CH divides 16: one tile per chunk)
         ldch(t0 + CH, xb);
 #pragma unroll
         for (int k = 0; k < CH; ++k) cell(t0 + k, xa[k] * kx);
@@ -186,7 +282,10 @@ DLAP_DEV void lstm_gls_body(const RnnJob& J, const ModelDesc* __restrict__ md, f
         for (int k = 0; k < CH; ++k) xa[k] = xb[k];
         if (PUB && last) publish(t0 + CH);
       }
-      for (int t = tfull; t < T; ++t) cell(t, sx[t * G4 + row] * kx);
+      for (int t = tfull; t < T; ++t) {
+        wait_xtile(ready, t, have);
+        cell(t, sx[t * G4 + row] * kx);
+      }
     } else {
       const uint32_t key_in = dropout_key(J.seed, step, 32 + (l - 1));
       float nx = ul ? sin[L] : 0.f;
@@ -197,7 +296,7 @@ DLAP_DEV void lstm_gls_body(const RnnJob& J, const ModelDesc* __restrict__ md, f
         float pre = bias;
 #pragma unroll
         for (int j = 0; j < HM; ++j)
-          pre += wih[j] * __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), j));
+          pre = fmaf(wih[j], __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), j)), pre);
         cell(t, pre);
         if (PUB && last && (t & 7) == 7) publish(t + 1);
       }

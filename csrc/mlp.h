@@ -117,9 +117,11 @@ bool mlp_fwd_rnn_supported(const MlpDims& D, int KS1, int WMB, int H, int nrnn, 
 int mlp_fwd_rnn_capacity(const MlpDims& D, int KS1, int WMB, int H, int nrnn, int tmax);
 // ne: evaluation-split recurrences per job run in the same launch (rjobs = [njobs train jobs]
 // [njobs * ne evaluation jobs], tmax over both)
+// selfproj: the recurrences project their own layer-0 inputs (no k_proj launch before; no moment
+// bias table -- only when the towers skip the moment network)
 bool launch_mlp_fwd_rnn(const MlpJob* jobs, const RnnJob* rjobs, const ModelDesc* md, int njobs, int gx,
                         const MlpDims& D, int KS1, int WMB, int H, int nrnn, int tmax, hipStream_t st,
-                        bool so = false, int ne = 0);
+                        bool so = false, int ne = 0, bool selfproj = false);
 void launch_dropmask(const MlpJob* jobs, int njobs, int ntiles, const MlpDims& D, int step_offset,
                      hipStream_t st);
 void launch_mlp_bwd_mom(const MlpJob* jobs, int njobs, int gx, int nslice, int tps, const MlpDims& D,

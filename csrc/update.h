@@ -96,8 +96,11 @@ void launch_lstm_bwd(const UpdJob* jobs, int njobs, const ModelDesc* md, const M
                      int T, int phase, hipStream_t st);
 // fused backward tail of phases 1 / 3: k_finalize + k_lstm_bwd + k_wgrad as one launch (k_rnn.hip)
 bool lstm_tail_supported(const ModelDesc& mh, int T);
+int lstm_tail_words();     // ints of UpdJob::tail_ctr (hand-off words, 128 bytes apart)
+struct LossJob;
+// ljobs: the train split's loss jobs whose job metrics one more block per model computes (or nullptr)
 void launch_lstm_tail(const UpdJob* ujobs, const FinJob* fjobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
-                      int T, int slab_stride, hipStream_t st);
+                      int T, int slab_stride, hipStream_t st, const LossJob* ljobs = nullptr);
 void launch_pack(float* const* params_unused, const UpdJob* jobs, int njobs, const ModelDesc* md,
                  const ModelDesc& mh, hipStream_t st);
 int pack_total(const ModelDesc& mh);   // packed elements per model (k_pack's element space)

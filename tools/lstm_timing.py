@@ -39,7 +39,7 @@ def main():
             print(f"    dense-state  : matrices {us(9, 13):7.1f}  chain {us(13, 15):7.1f}  gates {us(15, 10):7.1f}")
         if eng.eng.fused_info()["fused_tail"] and ts[16] > ts[9]:    # k_lstm_tail: dpp wait, W_ih
             print(f"    fused tail   : pre-pass->dpp in LDS {us(9, 16):7.1f}  pair maps {us(16, 13):7.1f}  "
-                  f"W_hh grads {us(10, 17):7.1f}  W_ih {us(17, 11):7.1f}")
+                  f"W_hh grads {us(10, 11):7.1f}  last W_ih block done {us(10, 17):7.1f} after the gates")
         print(f"  k_proj tile0   : total {us(12, 14):7.1f}")
         m = np.array(mod.Engine.mlp_timestamps(), dtype=np.int64)
         um = lambda a, b: (m[b] - m[a]) / 100.0  # noqa: E731

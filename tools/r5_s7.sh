@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round-5 session 7: buffer-load projection operands (in-kernel projection no longer serialised) -- tests, timing, A/B benches
+set -o pipefail
+mkdir -p gpurun_out
+T="timeout -k 10"
+$T 500 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_invariance_gpu.py -k "capped or self_projecting or rotated or fused_backward_tail or eval_recurrences" > gpurun_out/r5_s7_t1.log 2>&1 || { tail -40 gpurun_out/r5_s7_t1.log; exit 1; }
+tail -3 gpurun_out/r5_s7_t1.log
+$T 200 python3 tools/lstm_timing.py > gpurun_out/r5_s7_lstm_timing.txt 2>&1 || { cat gpurun_out/r5_s7_lstm_timing.txt; exit 1; }
+grep -A9 "pipeline=True" gpurun_out/r5_s7_lstm_timing.txt
+OUT=gpurun_out/r5_s7_bench.log; : > $OUT
+b() { local tag=$1; shift; local a="$1"; shift
+  line=$($T 200 env "$@" python3 bench.py $a --no-ensemble9 2>>gpurun_out/r5_s7.err | tail -1) || { echo "[$tag] FAILED" >> $OUT; cat $OUT; exit 1; }
+  echo "[$tag] $(echo "$line" | python3 -c 'import sys,json; d=json.loads(sys.stdin.read()); print(d["ms_per_step"], d["ms_per_epoch_phase"])')" >> $OUT; }
+L="--steps 210 --warmup 21"
+b long_new "$L"
+b long_noself "$L" DLAP_SELF_PROJ=0
+b long_rot "$L" DLAP_ROTATE=1
+
+b short_new "--steps 20 --warmup 5"
+b short_noself "--steps 20 --warmup 5" DLAP_SELF_PROJ=0
+b long_new2 "$L"
+b long_noself2 "$L" DLAP_SELF_PROJ=0
+b g2 "--steps 60 --warmup 10 --models-per-gpu 2"
+cat $OUT

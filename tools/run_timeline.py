@@ -21,6 +21,12 @@ def main():
     rows = []
     for f in Path(a.dir).glob("**/*kernel_trace.csv"):
         rows += list(csv.DictReader(open(f)))
+    for f in Path(a.dir).glob("**/*results.db"):          # rocpd SQLite output
+        import sqlite3
+        q = ("select s.kernel_name, d.start, d.end, d.queue_id from rocpd_kernel_dispatch d "
+             "join rocpd_info_kernel_symbol s on d.kernel_id = s.id")
+        rows += [{"Kernel_Name": n, "Start_Timestamp": b, "End_Timestamp": e, "Queue_Id": str(qid)}
+                 for n, b, e, qid in sqlite3.connect(str(f)).execute(q)]
     from kernel_stats import demangle
     dm = demangle({r["Kernel_Name"] for r in rows})
     for r in rows:
