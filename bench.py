@@ -261,6 +261,8 @@ def main():
         eng.eng.begin_phase(ph)
         eng.run(ph, k, 1e-3, 64, 1.0, use_graph)
         evs[i + 1].record(est)
+    t_enq = time.perf_counter() - t0      # host time to enqueue the timed region (vs dt: host-bound?)
+    launch_us = float(eng.eng.fused_info().get("host_launch_us_per_epoch", 0.0))
     eng.eng.sync()
     torch.cuda.synchronize()
     comm.barrier(d)
@@ -304,6 +306,8 @@ def main():
             "hipgraph": use_graph, "finite": finite, "fused_wait_timeouts": fused_timeouts,
             "gram_plan": [list(map(bool, eng_plan[ph])) for ph in (1, 3)],
             "panel_setup_s": round(t_gen, 2),
+            "host_enqueue_ms_per_step": round(t_enq / K * 1e3, 4),
+            "host_launch_us_per_epoch": round(launch_us, 1),
             "ensemble9": ens,
         }
         print(json.dumps(out), flush=True)

@@ -301,6 +301,12 @@ DLAP_DEV float block_sum(float v, float* red) {
   return s;
 }
 
+// Write-through (sc1) store: visible at agent scope once the storing wave has drained it
+// (s_waitcnt vmcnt(0)) -- no L2 writeback -- for payloads read later in the same launch by
+// other workgroups (the fused backward tail's gradients and job scalars).
+template <class T>
+DLAP_DEV void st_wt(T* p, float v) { __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
 DLAP_DEV float sigmoidf_(float x) { return 1.f / (1.f + __expf(-x)); }
 DLAP_DEV float tanhf_(float x) { return tanhf(x); }
 

@@ -261,6 +261,9 @@ class Engine {
     eval_in_fwd_ = env_int("DLAP_EVAL_IN_FWD", 1) != 0;
     fused_tail_ = env_int("DLAP_FUSED_TAIL", 1) != 0;
     self_proj_ = env_int("DLAP_SELF_PROJ", 1) != 0;
+    tail_adam_ = env_int("DLAP_TAIL_ADAM", 1) != 0;
+    split_graphs_ = env_int("DLAP_SPLIT_GRAPHS", 1) != 0;
+    unroll_ = std::max(1, env_int("DLAP_UNROLL", 4));
     rotate_ = env_int("DLAP_ROTATE", 0) != 0;
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
                residual, fp32);
@@ -268,6 +271,7 @@ class Engine {
     // is bf16 only)
     if (fp32) zx_eval_ = zx_train_ = false;
     prog_.alloc((size_t)G * 3 * 16);      // per (model, split): [0] published periods, [1] spin timeouts
+    esync_.alloc(64);                      // split epoch graphs: [0] evaluation recurrences done, [32] consumed
     d_desc_.alloc(sizeof(ModelDesc));
     HIP_LEGACY(hipMemcpy(d_desc_.p, &md_, sizeof(ModelDesc), hipMemcpyHostToDevice));
     models_.resize(G);
@@ -714,6 +718,51 @@ class Engine {
     // branch -- the join coincides with the graph boundary. head = first epoch's training (no
     // Adam); body = Adam(e-1) | training(e) || evaluation(e-1) + bookkeeping; tail = Adam(last) |
     // evaluation(last) + bookkeeping. The same kernels in the same dependency order per buffer.
+    if (split_graphs(phase)) {
+      hipGraphExec_t head = graph_for(graph_key(phase, lr, ignore_epoch, sel, 1), [&] { enqueue_head(phase, lr); });
+      // the body epochs in graphs of `unroll_` epochs each (the rest one by one): a graph boundary
+      // costs ~5-9 us (the last node's system-scope release, the first one's acquire); inside a
+      // graph consecutive kernels of one queue follow each other directly
+      // (both graphs are captured on the first call, whatever n: the bench's warmup captures
+      // what its timed region launches)
+      const int nbody = n - 1, ku = unroll_;
+      hipGraphExec_t chain = graph_for(graph_key(phase, lr, ignore_epoch, sel, 21),
+                                       [&] { enqueue_chain_split(phase, lr); });
+      hipGraphExec_t evalg = graph_for(graph_key(phase, lr, ignore_epoch, sel, 22),
+                                       [&] { enqueue_eval_split(phase, ignore_epoch, sel); }, st2_);
+      hipGraphExec_t chaink = chain, evalk = evalg;
+      if (ku > 1) {
+        chaink = graph_for(graph_key(phase, lr, ignore_epoch, sel, 1000 + ku),
+                           [&] { for (int i = 0; i < ku; ++i) enqueue_chain_split(phase, lr); });
+        evalk = graph_for(graph_key(phase, lr, ignore_epoch, sel, 2000 + ku),
+                          [&] { for (int i = 0; i < ku; ++i) enqueue_eval_split(phase, ignore_epoch, sel); }, st2_);
+      }
+      hipGraphExec_t tail = graph_for(graph_key(phase, lr, ignore_epoch, sel, 3),
+                                      [&] { enqueue_tail(phase, ignore_epoch, sel); });
+      HIP_OK(hipGraphLaunch(head, st_));
+      join_eval_gram();
+      // the evaluation graphs follow the head on st2_ (its masks / step counters, its weights)
+      HIP_OK(hipEventRecord(ev_fork_, st_));
+      HIP_OK(hipStreamWaitEvent(st2_, ev_fork_, 0));
+      const auto t_l = std::chrono::steady_clock::now();
+      int e = 0;
+      for (; e + ku <= nbody; e += ku) {
+        HIP_OK(hipGraphLaunch(chaink, st_));
+        HIP_OK(hipGraphLaunch(evalk, st2_));
+      }
+      for (; e < nbody; ++e) {
+        HIP_OK(hipGraphLaunch(chain, st_));
+        HIP_OK(hipGraphLaunch(evalg, st2_));
+      }
+      host_launch_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t_l).count();
+      host_launch_n_ += n - 1;
+      // (the last evaluation graph finished before the last chain's update: one event for the
+      // stream order the host and later launches rely on)
+      HIP_OK(hipEventRecord(ev_join_, st2_));
+      HIP_OK(hipStreamWaitEvent(st_, ev_join_, 0));
+      HIP_OK(hipGraphLaunch(tail, st_));
+      return;
+    }
     const bool rot = rotate_ && b_wait_ == 0 && !side_metrics_ && eval_rnn_in_fwd(phase);
     const int k0 = rot ? 10 : 0;
     hipGraphExec_t head = graph_for(graph_key(phase, lr, ignore_epoch, sel, k0 + 1),
@@ -727,7 +776,10 @@ class Engine {
     HTRACE("launch head");
     HIP_OK(hipGraphLaunch(head, st_));
     join_eval_gram();                     // the next graphs evaluate
+    const auto t_l = std::chrono::steady_clock::now();
     for (int e = 1; e < n; ++e) HIP_OK(hipGraphLaunch(body, st_));
+    host_launch_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t_l).count();
+    host_launch_n_ += n - 1;
     HTRACE("launch tail");
     HIP_OK(hipGraphLaunch(tail, st_));
     HTRACE("run_epochs done");
@@ -1081,6 +1133,7 @@ class Engine {
   DevBuf<char> j_rnn_all_;
   int cap_all_ = 0;                          // co-residency capacity at the longest split's LDS
   DevBuf<int> prog_;
+  DevBuf<int> esync_;                        // see split_graphs()
   // Co-residency guarantee of the fused LSTM + tower launches: resident workgroups of the fused
   // kernel on the device (occupancy query, rebuild_jobs) for the train split / the evaluation
   // splits; DLAP_FUSED_CAP overrides (tests of the fallback).
@@ -1144,6 +1197,7 @@ class Engine {
       HIP_LEGACY(hipMemset(S.tail_ctr.p, 0, S.tail_ctr.n * sizeof(int)));
       HIP_LEGACY(hipMemset(S.upd_ctr.p, 0, S.upd_ctr.n * sizeof(int)));
     }
+    HIP_LEGACY(hipMemset(esync_.p, 0, esync_.n * sizeof(int)));
   }
   py::dict fused_info() const {
     py::dict d;
@@ -1158,6 +1212,9 @@ class Engine {
     }
     d["eval_per_model"] = ne_per_model();
     d["fused_tail"] = tail_fused(1);
+    d["adam_in_tail"] = adam_in_tail(1) && pipeline_ && eval_rnn_in_fwd(1);
+    d["split_graphs"] = split_graphs(1) && pipeline_;
+    d["host_launch_us_per_epoch"] = host_launch_n_ ? 1e6 * host_launch_s_ / host_launch_n_ : 0.0;
     // backward launch shape: fine slabs per model (R-only partition), fine slabs per workgroup
     d["bwd_nfine"] = nfine_; d["bwd_fpw"] = fpw_;
     d["fused_pack"] = inv_code_.p != nullptr;
@@ -1772,6 +1829,7 @@ class Engine {
         E.snap_loss = S.snap_loss.p; E.snap_sharpe = S.snap_sharpe.p;
         E.max_ep = max_epochs_;
         E.prog = prog_ptr(g, 0);
+        E.eval_gen = S.tail_ctr.p + TAIL_EVGEN;
         ej.push_back(E);
       }
       upload(j_mlp_train_[phase], mt); upload(j_mlp_bwd_[phase], mb); upload(j_loss_train_[phase], lt);
@@ -1889,7 +1947,7 @@ class Engine {
     else if (eval_rnn)
       launch_mlp_fwd_rnn(as<MlpJob>(j_mlp_train_[phase]), as<RnnJob>(j_rnn_all_), dd(), G_, fused_all_gx(phase),
                          md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, tmax_fwd_all(), st_, !train_mom(phase),
-                         ne_per_model(), selfproj);
+                         ne_per_model(), selfproj, fwd_esig_);
     else if (fused)
       launch_mlp_fwd_rnn(as<MlpJob>(j_mlp_train_[phase]), as<RnnJob>(j_rnn_train_), dd(), G_,
                          fused_train_gx(phase), md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, D.T, st_,
@@ -1954,13 +2012,54 @@ class Engine {
   bool tail_fused(int phase) const {
     return fused_tail_ && !split_tail_ && phase != 2 && splits_[0].set && lstm_tail_supported(md_, splits_[0].T);
   }
+  // the pipelined eval-in-forward epoch: the clip + Adam update runs in the backward tail's last
+  // blocks (k_lstm_tail, adam 2) after the evaluation branch's bookkeeping signalled, so the
+  // training chain has no join edge and no k_adam launch (the branches join at the graph end)
+  bool tail_adam_ = true;                    // DLAP_TAIL_ADAM
+  int tail_adam_mode_ = 0;                   // set around enqueue_train_grads (enqueue_pipe)
+  float tail_lr_ = 0.f;
+  bool adam_in_tail(int phase) const { return tail_adam_ && tail_fused(phase) && inv_code_.p != nullptr; }
+  // Split epoch graphs (the pipelined eval-in-forward epoch with the update in the tail): the
+  // training chain is one single-queue graph on st_ (fused forward -> losses -> tower backward ->
+  // tail + Adam) and the evaluation branch another on st2_ (k_wait_count -> evaluation towers ->
+  // losses -> masks -> bookkeeping), launched side by side every epoch with NO graph edge between
+  // them: the evaluation graph waits in-kernel for the fused forward's evaluation recurrences
+  // (esync_ counts), the tail's Adam blocks for the bookkeeping's signal. A cross-queue edge
+  // inside a graph costs ~5-6 us on the chain and a graph that ends on two queues ~12 us at its
+  // boundary (profiles/r5_*timeline*); these cost one poll each.
+  bool split_graphs_ = true;                 // DLAP_SPLIT_GRAPHS
+  int unroll_ = 4;                           // DLAP_UNROLL: body epochs per split-graph launch
+  double host_launch_s_ = 0.0;               // host time in the pipelined body launches ...
+  long host_launch_n_ = 0;                   // ... over this many epochs (fused_info)
+  int* fwd_esig_ = nullptr;                  // set around enqueue_train_grads (enqueue_chain_split)
+  bool split_graphs(int phase) const {
+    return split_graphs_ && adam_in_tail(phase) && b_wait_ == 0 && !side_metrics_ && eval_rnn_in_fwd(phase);
+  }
+  void enqueue_chain_split(int phase, float lr) {
+    tail_metrics_ = true;
+    tail_adam_mode_ = 2;
+    tail_lr_ = lr;
+    fwd_esig_ = esync_.p;
+    enqueue_train_grads(phase, nullptr, true, 0, false, false, true);
+    tail_metrics_ = false;
+    tail_adam_mode_ = 0;
+    fwd_esig_ = nullptr;
+  }
+  void enqueue_eval_split(int phase, int ignore_epoch, float sel) {      // captured on st2_
+    HTRACE("launch_wait_count");
+    launch_wait_count(esync_.p, ne_per_model() * G_, prog_limit_, prog_.p, G_, st2_);
+    enqueue_eval_towers(st2_);
+    enqueue_dropmask(phase, 1, st2_);
+    enqueue_epoch_end(phase, ignore_epoch, sel, st2_, 1);
+  }
   void enqueue_train_tail(int phase) {
     const SplitDev& D = splits_[0];
     if (g_skip & 1) { join_side(); return; }
     const LossJob* lm = tail_metrics_ && phase != 2 ? loss_tab(phase, use_gram(phase)) : nullptr;
     if (tail_fused(phase)) {
       HTRACE("launch_lstm_tail");
-      launch_lstm_tail(as<UpdJob>(j_upd_), as<FinJob>(j_fin_), G_, dd(), md_, D.T, slab_stride(), st_, lm);
+      launch_lstm_tail(as<UpdJob>(j_upd_), as<FinJob>(j_fin_), G_, dd(), md_, D.T, slab_stride(), st_, lm,
+                       tail_adam_mode_, tail_lr_);
       join_side();
       return;
     }
@@ -2041,11 +2140,11 @@ class Engine {
     HTRACE("launch_job_metrics");
     launch_job_metrics(le, n_eval_jobs_, st);
   }
-  void enqueue_epoch_end(int phase, int ignore_epoch, float sel, hipStream_t st) {
+  void enqueue_epoch_end(int phase, int ignore_epoch, float sel, hipStream_t st, int signal = 0) {
     HTRACE("launch_epoch_end");
     if (g_skip & 64) return;
     launch_epoch_end(as<EpochJob>(j_epoch_[phase]), G_, phase, ignore_epoch, sel, md_.residual_factor,
-                     md_.P, st);
+                     md_.P, st, signal);
   }
   // sequential epoch: train step, evaluation, bookkeeping
   void enqueue_epoch(int phase, float lr, int ignore_epoch, float sel) {
@@ -2094,11 +2193,24 @@ class Engine {
       // evaluation branch forks after it: towers, losses, this epoch's train metrics (after its
       // loss pass), the bookkeeping and the next epoch's dropout masks, beside the training
       // backward and its tail
+      const bool ta = adam_in_tail(phase);
       tail_metrics_ = true;
+      tail_adam_mode_ = ta ? 2 : 0;
+      tail_lr_ = lr;
       enqueue_train_grads(phase, nullptr, true, 2, false, false, true);
       tail_metrics_ = false;
+      tail_adam_mode_ = 0;
       HIP_OK(hipStreamWaitEvent(st2_, ev_a_, 0));
       enqueue_eval_towers(st2_);
+      if (ta) {
+        // the next epoch's masks, then the bookkeeping, whose signal releases the tail's update
+        // (both read counters / parameters the update writes)
+        enqueue_dropmask(phase, 1, st2_);
+        enqueue_epoch_end(phase, ignore_epoch, sel, st2_, 1);
+        HIP_OK(hipEventRecord(ev_join_, st2_));
+        HIP_OK(hipStreamWaitEvent(st_, ev_join_, 0));
+        return;
+      }
       enqueue_epoch_end(phase, ignore_epoch, sel, st2_);
       enqueue_dropmask(phase, 1, st2_);
       HIP_OK(hipEventRecord(ev_join_, st2_));
@@ -2179,7 +2291,8 @@ class Engine {
     enqueue_epoch_end(phase, ignore_epoch, sel, st_);
   }
   template <typename F>
-  hipGraphExec_t graph_for(const std::string& key, F&& enqueue) {
+  hipGraphExec_t graph_for(const std::string& key, F&& enqueue, hipStream_t cs = nullptr) {
+    if (!cs) cs = st_;
     auto it = graphs_.find(key);
     if (it != graphs_.end()) return it->second;
     const auto t_cap = std::chrono::steady_clock::now();
@@ -2187,10 +2300,10 @@ class Engine {
     {
       std::lock_guard<std::mutex> g(g_legacy_mu);
       HTRACE("capture %s tid=%ld", key.c_str(), (long)syscall(SYS_gettid));
-      HIP_OK(hipStreamBeginCapture(st_, hipStreamCaptureModeThreadLocal));
+      HIP_OK(hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal));
       enqueue();
       HTRACE("end capture");
-      HIP_OK(hipStreamEndCapture(st_, &graph));
+      HIP_OK(hipStreamEndCapture(cs, &graph));
     }
     HTRACE("instantiate");
     hipGraphExec_t exec;
@@ -2198,7 +2311,7 @@ class Engine {
     HIP_OK(hipGraphDestroy(graph));
     // device-side upload now, not at the first launch (that launch may sit inside a timed or
     // latency-critical region)
-    HIP_OK(hipGraphUpload(exec, st_));
+    HIP_OK(hipGraphUpload(exec, cs));
     graphs_.emplace(key, exec);
     capture_s_ += std::chrono::duration<double>(std::chrono::steady_clock::now() - t_cap).count();
     return exec;

@@ -61,7 +61,7 @@ DLAP_DEV void finalize_block(const FinJob& J, const ModelDesc* __restrict__ md, 
       else if (i >= ppc && i < ppc + md->Dm) col = F + (i - ppc);
       else ok = false;
     }
-    if (wave == 0 && ok) gp(J.grads)[G.w_off + o * G.ld + col] = G.layer > 0 ? v * dscale : v;
+    if (wave == 0 && ok) st_wt(gp(J.grads) + G.w_off + o * G.ld + col, G.layer > 0 ? v * dscale : v);
     return;
   }
   b -= nb_tiles;
@@ -71,7 +71,7 @@ DLAP_DEV void finalize_block(const FinJob& J, const ModelDesc* __restrict__ md, 
     const float v = slab_sum(J.slab + tps * 4096 + ec);     // slice-0 slabs
     const int dst = e < SLAB_EXTRA ? (mom ? md->extra_m[e] : md->extra_s[e]) : -1;
     const bool wo = !mom && e >= DLAP_MAXL * 64 && e < DLAP_MAXL * 64 + 64;   // SDF output row
-    if (wave == 0 && dst >= 0) gp(J.grads)[dst] = wo ? v * dscale : v;
+    if (wave == 0 && dst >= 0) st_wt(gp(J.grads) + dst, wo ? v * dscale : v);
     return;
   }
   b -= nb_extra;

@@ -777,18 +777,26 @@ template <class P, int KS1, int WMB, int HM, bool DPPG, bool SO = false>
 __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd_rnn(const MlpJob* __restrict__ jobs, MlpDims D,
                                                                   const RnnJob* __restrict__ rjobs,
                                                                   const ModelDesc* __restrict__ md, int ne,
-                                                                  int selfproj) {
+                                                                  int selfproj, int* esig) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int w = threadIdx.x >> 6;
   if (blockIdx.x >= 1 && (int)blockIdx.x <= ne) {
     const RnnJob& R = rjobs[gridDim.y + blockIdx.y * ne + (blockIdx.x - 1)];
     float* sx = reinterpret_cast<float*>(smem);
     if (md->nrnn == 0) return;
+    // esig (the split epoch graphs): the recurrence wave, its outputs stored, releases them at
+    // agent scope and counts itself -- the evaluation graph's first launch (k_wait_count) waits
+    // for every evaluation recurrence of the launch
+    auto signal = [&] {
+      if (!esig) return;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(esig, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
     if (selfproj) {
       int* ready = reinterpret_cast<int*>(sx + gls_ready_offset(R.T, md->H));
       for (int i = threadIdx.x; i < (R.T + 15) / 16; i += blockDim.x) ready[i] = 0;
       __syncthreads();
-      if (w == 0) lstm_gls_body<HM, DPPG, false, false>(R, md, sx, nullptr, nullptr, 0, ready);
+      if (w == 0) { lstm_gls_body<HM, DPPG, false, false>(R, md, sx, nullptr, nullptr, 0, ready); signal(); }
       else proj_into_lds(R, md, sx, ready, w - 1, 3);
       return;
     }
@@ -796,7 +804,7 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd_rnn(const MlpJob*
     const int n = R.T * 4 * md->H;
     for (int i = threadIdx.x; i < n; i += blockDim.x) sx[i] = xg[i];
     __syncthreads();
-    if (w == 0) lstm_gls_body<HM, DPPG, false, false>(R, md, sx, nullptr, nullptr, 0);
+    if (w == 0) { lstm_gls_body<HM, DPPG, false, false>(R, md, sx, nullptr, nullptr, 0); signal(); }
     return;
   }
   if (blockIdx.x == 0) {
@@ -1707,7 +1715,7 @@ int mlp_fwd_rnn_capacity(const MlpDims& D0, int KS1, int WMB, int H, int nrnn, i
 
 bool launch_mlp_fwd_rnn(const MlpJob* jobs, const RnnJob* rjobs, const ModelDesc* md, int njobs, int gx,
                         const MlpDims& D0, int KS1, int WMB, int H, int nrnn, int tmax, hipStream_t st, bool so,
-                        int ne, bool selfproj) {
+                        int ne, bool selfproj, int* esig) {
   if (!mlp_fwd_rnn_supported(D0, KS1, WMB, H, nrnn, tmax))
     dlap_throw_hip(hipErrorInvalidValue, "mlp_fwd_rnn: unsupported shape", __FILE__, __LINE__);
   MlpDims D = D0;
@@ -1717,14 +1725,14 @@ bool launch_mlp_fwd_rnn(const MlpJob* jobs, const RnnJob* rjobs, const ModelDesc
   if (so && !D.fp32) {
 #define RS_CASE(K, HM, DP) \
     if (KS1 == K && H == HM) { \
-      hipLaunchKernelGGL((k_mlp_fwd_rnn<PrecBF16, K, 1, HM, DP, true>), grid, block, sh, st, jobs, D, rjobs, md, ne, (int)selfproj); \
+      hipLaunchKernelGGL((k_mlp_fwd_rnn<PrecBF16, K, 1, HM, DP, true>), grid, block, sh, st, jobs, D, rjobs, md, ne, (int)selfproj, esig); \
       HIP_OK(hipGetLastError()); return true; }
     RS_CASE(2, 4, true) RS_CASE(4, 4, true) RS_CASE(2, 8, false) RS_CASE(4, 8, false)
 #undef RS_CASE
   }
 #define R_CASE(PR, K, W, HM, DP) \
   if (KS1 == K && WMB == W && H == HM) { \
-    hipLaunchKernelGGL((k_mlp_fwd_rnn<PR, K, W, HM, DP>), grid, block, sh, st, jobs, D, rjobs, md, ne, (int)selfproj); \
+    hipLaunchKernelGGL((k_mlp_fwd_rnn<PR, K, W, HM, DP>), grid, block, sh, st, jobs, D, rjobs, md, ne, (int)selfproj, esig); \
     HIP_OK(hipGetLastError()); return true; }
 #define R_KW(PR, HM, DP) R_CASE(PR, 2, 1, HM, DP) R_CASE(PR, 2, 2, HM, DP) R_CASE(PR, 2, 4, HM, DP) \
   R_CASE(PR, 4, 1, HM, DP) R_CASE(PR, 4, 2, HM, DP) R_CASE(PR, 4, 4, HM, DP)

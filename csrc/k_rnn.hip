@@ -28,6 +28,7 @@
 #include "lstm_gls.h"
 #include "finalize.h"
 #include "loss_dev.h"
+#include "pack_dev.h"
 
 #define DLAP_MAX_M 1024
 
@@ -434,10 +435,6 @@ __host__ __device__ inline size_t lstm_bwd_scan_floats(int T) { return (size_t)T
 struct LstmBwdLds { size_t cf, h, d, dgs, junk, gpart, M, y, W, N, v, total; };
 // hand-off words of the fused tail (UpdJob::tail_ctr, one 128-byte line each): periods published,
 // gate gradients published, W_ih helper blocks done
-#define TAIL_CNT 0
-#define TAIL_FLAG 32
-#define TAIL_DONE 64
-#define TAIL_WORDS 96
 __host__ __device__ inline LstmBwdLds lstm_bwd_lds(int T, int H, bool scan, bool fused) {
   LstmBwdLds L{};
   const size_t G4 = 4 * (size_t)H, np = (size_t)((T - 1) / 2);
@@ -947,9 +944,9 @@ DLAP_DEV void lstm_bwd_body(const UpdJob& J, const ModelDesc* __restrict__ md, i
         const int col = o >> 4, g = o & 15;
         const int li = 16 * (col >> 2) + g, r = col & 3;
         const float v = ((gpart[li * 4 + r] + gpart[256 + li * 4 + r]) + gpart[512 + li * 4 + r]) + gpart[768 + li * 4 + r];
-        if (col < 4) grads[md->lstm_w_hh[l] + g * 4 + col] = v;
-        else if (col == 4) { grads[md->lstm_b_ih[l] + g] = v; grads[md->lstm_b_hh[l] + g] = v; }
-        else grads[md->lstm_w_ih[l] + g * in_dim + (col - 5)] = v;
+        if (col < 4) st_wt(grads + md->lstm_w_hh[l] + g * 4 + col, v);
+        else if (col == 4) { st_wt(grads + md->lstm_b_ih[l] + g, v); st_wt(grads + md->lstm_b_hh[l] + g, v); }
+        else st_wt(grads + md->lstm_w_ih[l] + g * in_dim + (col - 5), v);
       }
       __syncthreads();
     } else
@@ -982,9 +979,9 @@ DLAP_DEV void lstm_bwd_body(const UpdJob& J, const ModelDesc* __restrict__ md, i
         const int o = idx0 + threadIdx.x, g = o % G4, col = o / G4;
         float v = 0.f;
         for (int q = 0; q < S; ++q) v += gpart[q * nout + o];
-        if (col < H) grads[md->lstm_w_hh[l] + g * H + col] = v;
-        else if (col == H) { grads[md->lstm_b_ih[l] + g] = v; grads[md->lstm_b_hh[l] + g] = v; }
-        else grads[md->lstm_w_ih[l] + g * in_dim + (col - H - 1)] = v;
+        if (col < H) st_wt(grads + md->lstm_w_hh[l] + g * H + col, v);
+        else if (col == H) { st_wt(grads + md->lstm_b_ih[l] + g, v); st_wt(grads + md->lstm_b_hh[l] + g, v); }
+        else st_wt(grads + md->lstm_w_ih[l] + g * in_dim + (col - H - 1), v);
       }
       __syncthreads();
     }
@@ -1102,10 +1099,10 @@ DLAP_DEV void wgrad_block(const UpdJob& J, const ModelDesc* __restrict__ md, int
       if (cc > M) continue;
       if (mom) {
         const PackLayer& L0 = md->m[0];
-        if (cc < M) gp(J.grads)[L0.w_off + (size_t)g * L0.ld + cc] = v[r];
-        else gp(J.grads)[L0.b_off + g] = v[r];
+        if (cc < M) st_wt(gp(J.grads) + L0.w_off + (size_t)g * L0.ld + cc, v[r]);
+        else st_wt(gp(J.grads) + L0.b_off + g, v[r]);
       } else if (cc < M) {
-        gp(J.grads)[md->lstm_w_ih[0] + (size_t)g * M + cc] = v[r];
+        st_wt(gp(J.grads) + md->lstm_w_ih[0] + (size_t)g * M + cc, v[r]);
       }
     }
   }
@@ -1117,61 +1114,130 @@ __global__ __launch_bounds__(256) void k_wgrad(const UpdJob* __restrict__ jobs,
   wgrad_block<GT>(jobs[blockIdx.y], md, phase, blockIdx.x);
 }
 
-// Fused backward tail of phases 1 / 3 (one launch instead of k_finalize -> k_lstm_bwd -> k_wgrad):
-// grid (1 + T + slab blocks + W_ih blocks, models). Block 0 runs the LSTM backward
-// (lstm_bwd_body<4, true>: pre-pass and step matrices first, then it waits for the per-period
-// gradient); blocks 1 .. T form the per-period sums dpp[t] and publish them; the slab blocks sum
-// the weight-gradient slabs; the last (M + 16) / 16 blocks wait for block 0's gate gradients
-// and form the layer-0 W_ih gradient (wgrad_block) while block 0 forms W_hh and the biases.
-// Every block runs the same arithmetic as the separate kernels, so the results are bitwise equal.
-// Blocks 0 and the W_ih blocks are the only ones that wait; the blocks they wait for never wait,
-// and the launch (under 400 blocks at the bench size) is resident at once on an idle device.
-// ljobs (optional): the train split's loss jobs of the step -- one more block per model computes
-// its job metrics (k_job_metrics' body; the loss passes finished before this launch), so the
-// pipelined epoch needs no fork to the evaluation branch for them.
-__global__ __launch_bounds__(256, 2) void k_lstm_tail(const UpdJob* __restrict__ ujobs, const FinJob* __restrict__ fjobs,
-                                                   const ModelDesc* __restrict__ md, int slab_stride, int nslab_blocks,
-                                                   const LossJob* __restrict__ ljobs) {
-  extern __shared__ __attribute__((aligned(16))) float sm[];
-  const UpdJob& U = ujobs[blockIdx.y];
-  if (blockIdx.x == 0) {
-    lstm_bwd_body<4, true>(U, md, 1, sm, blockIdx.y == 0);
-    return;
-  }
-  const FinJob& F = fjobs[blockIdx.y];
-  const int b = blockIdx.x - 1;
-  if (b < U.T) { finalize_block(F, md, 1, slab_stride, nslab_blocks + b, U.tail_ctr + TAIL_CNT); return; }
-  if (b < U.T + nslab_blocks) { finalize_block(F, md, 1, slab_stride, b - U.T); return; }
-  const int nwg = (md->M + 1 + 15) / 16;
-  if (b >= U.T + nslab_blocks + nwg) {            // the train split's job metrics
-    if (ljobs) job_metrics_body<256>(ljobs[blockIdx.y], sm + DLAP_MAX_T, sm);
-    return;
-  }
-  // W_ih helper: k_wgrad's block, its macro operands requested first, then the wait for the gate
-  // gradients (relaxed poll, one agent acquire, barrier) before their loads
-  const int cblk = b - U.T - nslab_blocks;
-  __shared__ int bad;
-  auto wait_dg = [&]() -> bool {
+// Adam in the fused tail (adam = 2): every block, its own work done, arrives on the model's
+// TAIL_ARRIVE count (its write-through stores drained first); the last nadam blocks to arrive
+// become the update's Adam blocks (adam_block, the same arithmetic as k_adam's blocks): each
+// requests its own operands, then waits -- relaxed polls, bounded, one agent acquire -- until
+// every block of the model has arrived and the epoch's evaluation branch has signalled (its
+// bookkeeping reads the parameters, the gradient norm and the step counters this update
+// writes). Both counts only grow (zeroed with the poison records): launch k of the model's
+// tail-Adam launches takes arrivals [k nb, (k + 1) nb) and waits for signal k + 1, so nothing
+// is rearmed. The step counters were read by every block before it arrived (step_pre), so
+// Adam block 0 advances them as soon as it is released. A wait that gives up poisons the model
+// (no update; the host raises). The waiting blocks are the last to arrive, so every block they
+// wait for has been dispatched ahead of them or is next in line.
+DLAP_DEV void tail_adam(const UpdJob& U, const ModelDesc* __restrict__ md, float lr, int nb, int step_pre,
+                        int drop_pre) {
+  __shared__ unsigned s_ord;
+  __shared__ int s_go;
+  __shared__ float red[4];
+  // the gradients / job scalars Adam reads are written through (st_wt): each wave drains its
+  // stores, then one agent-scope add per block
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0)
+    s_ord = __hip_atomic_fetch_add(reinterpret_cast<unsigned*>(U.tail_ctr + TAIL_ARRIVE), 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const unsigned k = s_ord / (unsigned)nb, ord = s_ord - k * (unsigned)nb;
+  const bool tsm = blockIdx.y == 0;
+  RNN_TS(18, tsm && ord == (unsigned)nb - 1);                       // the last arrival
+  const int nadam = (md->P_sdf + ADAM_PB - 1) / ADAM_PB;
+  const int bx = (int)ord - (nb - nadam);
+  if (bx < 0) return;
+  auto wait = [&]() -> bool {
     if (threadIdx.x < 64) {
-      const int* flag = U.tail_ctr + TAIL_FLAG;
-      int v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      unsigned spins = 0;
       bool ok = true;
-      while (v == 0) {
-        if (spins++ >= U.spin_limit) { ok = false; break; }   // block 0 gave up (and poisoned the model)
+      unsigned spins = 0;
+      const unsigned all = (k + 1) * (unsigned)nb;
+      const int* arr = U.tail_ctr + TAIL_ARRIVE;
+      while ((unsigned)__builtin_amdgcn_readfirstlane(__hip_atomic_load(arr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) - all >
+             0x7fffffffu) {                                            // (wrap-safe "count < all")
+        if (spins++ >= U.spin_limit) { ok = false; break; }
         __builtin_amdgcn_s_sleep(2);
-        v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      }
+      const int* gen = U.tail_ctr + TAIL_EVGEN;
+      while (ok && (unsigned)__builtin_amdgcn_readfirstlane(__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) -
+                           (k + 1) > 0x7fffffffu) {
+        if (spins++ >= U.spin_limit) { ok = false; break; }
+        __builtin_amdgcn_s_sleep(2);
       }
       asm volatile("" ::: "memory");
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (threadIdx.x == 0) bad = ok ? 0 : 1;
+      if (threadIdx.x == 0) {
+        if (!ok) atomicAdd(const_cast<int*>(U.prog) + 1, 1);
+        s_go = ok && !prog_poisoned(U.prog);
+      }
     }
     __syncthreads();
-    return bad == 0;
+    RNN_TS(19, tsm && bx == 0);                                      // Adam block 0 released
+    return s_go != 0;
   };
-  wgrad_block<1>(U, md, 1, cblk, U.tail_ctr + TAIL_DONE, nwg, wait_dg);
-  if (blockIdx.y == 0 && cblk == nwg - 1 && threadIdx.x == 0) g_rnn_ts[17] = wall_clock64();
+  adam_block(U, md, 1, lr, bx, nadam, red, wait, step_pre, drop_pre);
+  RNN_TS(20, tsm && bx == nadam - 1);
+}
+
+// Fused backward tail of phases 1 / 3 (one launch instead of k_finalize -> k_lstm_bwd -> k_wgrad
+// [-> k_adam]): grid (1 + T + slab blocks + W_ih blocks [+ 1], models). Block 0 runs the LSTM
+// backward (lstm_bwd_body<4, true>: pre-pass and step matrices first, then it waits for the
+// per-period gradient); blocks 1 .. T form the per-period sums dpp[t] and publish them; the slab
+// blocks sum the weight-gradient slabs; the next (M + 16) / 16 blocks wait for block 0's gate
+// gradients and form the layer-0 W_ih gradient (wgrad_block) while block 0 forms W_hh and the
+// biases. Every block runs the same arithmetic as the separate kernels, so the results are
+// bitwise equal. Blocks 0 and the W_ih blocks wait only for blocks that never wait, and the
+// launch (under 400 blocks per model at the bench size) is resident at once on an idle device.
+// ljobs (optional): the train split's loss jobs of the step -- one more block per model computes
+// its job metrics (k_job_metrics' body; the loss passes finished before this launch), so the
+// pipelined epoch needs no fork to the evaluation branch for them.
+// adam (tail_adam): the clip + Adam update of the step in the launch's last blocks (2: after
+// the evaluation branch's signal; the only mode).
+__global__ __launch_bounds__(256, 2) void k_lstm_tail(const UpdJob* __restrict__ ujobs, const FinJob* __restrict__ fjobs,
+                                                   const ModelDesc* __restrict__ md, int slab_stride, int nslab_blocks,
+                                                   const LossJob* __restrict__ ljobs, int adam, float lr) {
+  extern __shared__ __attribute__((aligned(16))) float sm[];
+  const UpdJob& U = ujobs[blockIdx.y];
+  const FinJob& F = fjobs[blockIdx.y];
+  const int b = (int)blockIdx.x - 1;
+  const int nwg = (md->M + 1 + 15) / 16;
+  __shared__ int s_steps[2];          // (adam) the step counters before this launch's update
+  if (adam && threadIdx.x == 0) { s_steps[0] = gp(U.adam_step)[0]; s_steps[1] = gp(U.drop_step)[0]; }
+  if (b < 0) {
+    lstm_bwd_body<4, true>(U, md, 1, sm, blockIdx.y == 0);
+  } else if (b < U.T) {
+    finalize_block(F, md, 1, slab_stride, nslab_blocks + b, U.tail_ctr + TAIL_CNT);
+  } else if (b < U.T + nslab_blocks) {
+    finalize_block(F, md, 1, slab_stride, b - U.T);
+  } else if (b >= U.T + nslab_blocks + nwg) {      // the train split's job metrics
+    if (ljobs) job_metrics_body<256>(ljobs[blockIdx.y], sm + DLAP_MAX_T, sm);
+  } else {
+    // W_ih helper: k_wgrad's block, its macro operands requested first, then the wait for the
+    // gate gradients (relaxed poll, one agent acquire, barrier) before their loads
+    const int cblk = b - U.T - nslab_blocks;
+    __shared__ int bad;
+    auto wait_dg = [&]() -> bool {
+      if (threadIdx.x < 64) {
+        const int* flag = U.tail_ctr + TAIL_FLAG;
+        int v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        unsigned spins = 0;
+        bool ok = true;
+        while (v == 0) {
+          if (spins++ >= U.spin_limit) { ok = false; break; }   // block 0 gave up (and poisoned the model)
+          __builtin_amdgcn_s_sleep(2);
+          v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        }
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (threadIdx.x == 0) bad = ok ? 0 : 1;
+      }
+      __syncthreads();
+      return bad == 0;
+    };
+    wgrad_block<1>(U, md, 1, cblk, U.tail_ctr + TAIL_DONE, nwg, wait_dg);
+    if (blockIdx.y == 0 && cblk == nwg - 1 && threadIdx.x == 0) g_rnn_ts[17] = wall_clock64();
+  }
+  if (adam) tail_adam(U, md, lr, gridDim.x, s_steps[0], s_steps[1]);
 }
 
 // whether the fused tail applies (single LSTM layer of width 4 on the dense-state BPTT path,
@@ -1185,13 +1251,13 @@ bool lstm_tail_supported(const ModelDesc& mh, int T) {
 }
 int lstm_tail_words() { return TAIL_WORDS; }
 void launch_lstm_tail(const UpdJob* ujobs, const FinJob* fjobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
-                      int T, int slab_stride, hipStream_t st, const LossJob* ljobs) {
+                      int T, int slab_stride, hipStream_t st, const LossJob* ljobs, int adam, float lr) {
   const int nslab_blocks = mh.ntile_s * 64 + (SLAB_EXTRA + 63) / 64;
   const int nwg = (mh.M + 1 + 15) / 16;
   // (the metrics block keeps its scratch in the dynamic LDS: DLAP_MAX_T + 4 floats)
   const size_t sh = std::max(lstm_tail_lds_bytes(T, mh.H), (size_t)(DLAP_MAX_T + 4) * sizeof(float));
   hipLaunchKernelGGL(k_lstm_tail, dim3(1 + T + nslab_blocks + nwg + (ljobs ? 1 : 0), njobs), dim3(256), sh, st,
-                     ujobs, fjobs, md, slab_stride, nslab_blocks, ljobs);
+                     ujobs, fjobs, md, slab_stride, nslab_blocks, ljobs, adam, lr);
   HIP_OK(hipGetLastError());
 }
 

@@ -84,9 +84,9 @@ DLAP_DEV void job_metrics_body(const LossJob& J, float* red, float* ret, long lo
   if (threadIdx.x == 0) {
     float lres = 0.f, inv_b, n1;
     if (J.res_factor > 0.f) residual_stats(J, lres, inv_b, n1);
-    gp(J.scal)[SC_LCOND] = lc;
-    gp(J.scal)[SC_LUNC] = lu;
-    gp(J.scal)[SC_LRES] = lres;
+    st_wt(gp(J.scal) + SC_LCOND, lc);
+    st_wt(gp(J.scal) + SC_LUNC, lu);
+    st_wt(gp(J.scal) + SC_LRES, lres);
   }
   // Sharpe of the weighted training portfolio P (train monitor) and of the L1 portfolio.
   for (int pass = 0; pass < 2; ++pass) {
@@ -105,11 +105,11 @@ DLAP_DEV void job_metrics_body(const LossJob& J, float* red, float* ret, long lo
       const float sd_u = T > 1 ? sqrtf(v / (float)(T - 1)) : __builtin_nanf("");
       const float sharpe = (sd_u < 1e-8f) ? 0.f : mean / sd_u;
       if (pass == 0) {
-        gp(J.scal)[SC_TRAIN_SHARPE] = sharpe;
+        st_wt(gp(J.scal) + SC_TRAIN_SHARPE, sharpe);
       } else {
-        gp(J.scal)[SC_SHARPE] = sharpe;
-        gp(J.scal)[SC_MEAN] = mean;
-        gp(J.scal)[SC_STD] = sqrtf(v / (float)T);
+        st_wt(gp(J.scal) + SC_SHARPE, sharpe);
+        st_wt(gp(J.scal) + SC_MEAN, mean);
+        st_wt(gp(J.scal) + SC_STD, sqrtf(v / (float)T));
       }
     }
     if (pass == 1 && threadIdx.x < 64) {
@@ -146,7 +146,7 @@ DLAP_DEV void job_metrics_body(const LossJob& J, float* red, float* ret, long lo
         mdd = fminf(mdd, (cum - peak) / peak);
       }
       mdd = wave_min(mdd);
-      if (lane == 0) gp(J.scal)[SC_MDD] = mdd;
+      if (lane == 0) st_wt(gp(J.scal) + SC_MDD, mdd);
     }
     __syncthreads();
     MET_TS(2 + pass);

@@ -121,7 +121,7 @@ int mlp_fwd_rnn_capacity(const MlpDims& D, int KS1, int WMB, int H, int nrnn, in
 // bias table -- only when the towers skip the moment network)
 bool launch_mlp_fwd_rnn(const MlpJob* jobs, const RnnJob* rjobs, const ModelDesc* md, int njobs, int gx,
                         const MlpDims& D, int KS1, int WMB, int H, int nrnn, int tmax, hipStream_t st,
-                        bool so = false, int ne = 0, bool selfproj = false);
+                        bool so = false, int ne = 0, bool selfproj = false, int* esig = nullptr);
 void launch_dropmask(const MlpJob* jobs, int njobs, int ntiles, const MlpDims& D, int step_offset,
                      hipStream_t st);
 void launch_mlp_bwd_mom(const MlpJob* jobs, int njobs, int gx, int nslice, int tps, const MlpDims& D,

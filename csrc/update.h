@@ -4,7 +4,16 @@
 
 struct ModelDesc;
 
-#define PACK_FAN 4         // max packed copies of one parameter for k_adam's fused re-pack
+#define PACK_FAN 4
+// hand-off words of the fused backward tail (UpdJob::tail_ctr, 128 bytes apart): the per-period
+// sums published, the gate-gradient flag, the W_ih blocks done, the blocks arrived (Adam in the
+// tail, a running count) and the evaluation branch's signals (a running count)
+#define TAIL_CNT 0
+#define TAIL_FLAG 32
+#define TAIL_DONE 64
+#define TAIL_ARRIVE 96
+#define TAIL_EVGEN 128
+#define TAIL_WORDS 160         // max packed copies of one parameter for k_adam's fused re-pack
 
 struct FinJob {            // one model
   const float* slab;       // first slab of this model (slices contiguous, gx slabs each)
@@ -85,6 +94,8 @@ struct EpochJob {          // one model
   float* snap_sharpe;      // [P]
   int max_ep;              // rows of hist: epochs past the capacity are not recorded
   const int* prog;         // as UpdJob::prog (a poisoned model records NaN epochs, no snapshots)
+  int* eval_gen;           // the model's tail_ctr + TAIL_EVGEN: bookkeeping launches that signal
+                           // (the pipelined epoch's evaluation branch) count here when done
 };
 
 void launch_finalize(const FinJob* jobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
@@ -99,13 +110,22 @@ bool lstm_tail_supported(const ModelDesc& mh, int T);
 int lstm_tail_words();     // ints of UpdJob::tail_ctr (hand-off words, 128 bytes apart)
 struct LossJob;
 // ljobs: the train split's loss jobs whose job metrics one more block per model computes (or nullptr)
+// adam: 0 = none (k_adam follows); 2 = the update runs in the tail (the launch's last blocks,
+// adam_block) after the epoch's evaluation branch signalled (launch_epoch_end)
 void launch_lstm_tail(const UpdJob* ujobs, const FinJob* fjobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
-                      int T, int slab_stride, hipStream_t st, const LossJob* ljobs = nullptr);
+                      int T, int slab_stride, hipStream_t st, const LossJob* ljobs = nullptr, int adam = 0,
+                      float lr = 0.f);
 void launch_pack(float* const* params_unused, const UpdJob* jobs, int njobs, const ModelDesc* md,
                  const ModelDesc& mh, hipStream_t st);
 int pack_total(const ModelDesc& mh);   // packed elements per model (k_pack's element space)
 void pack_index_host(const ModelDesc& mh, int* src);   // packed element -> parameter (-1: padding)
 void launch_set_int(int* p, int v, hipStream_t st);
 void launch_begin_phase(const EpochJob* jobs, int njobs, hipStream_t st);
+// the split epoch graphs' evaluation graph waits (one wave) for `per` more finished evaluation
+// recurrences of the training graph's fused forward than it consumed so far (cnt[0] running
+// count, cnt[32] consumed); giving up poisons the nmodels models (prog records, 48 ints each)
+void launch_wait_count(int* cnt, int per, unsigned limit, int* prog, int nmodels, hipStream_t st);
+// signal: each model's block counts its EpochJob::eval_gen when done (agent release) -- the
+// fused tail's Adam blocks wait for it (launch_lstm_tail, adam 2)
 void launch_epoch_end(const EpochJob* jobs, int njobs, int phase, int ignore_epoch, float sel,
-                      float res_factor, int P, hipStream_t st);
+                      float res_factor, int P, hipStream_t st, int signal = 0);

@@ -163,6 +163,39 @@ def test_fused_backward_tail_equals_separate_kernels(big, monkeypatch):
         _same(ref[s], res[s])
 
 
+def test_adam_in_tail_equals_k_adam(big, monkeypatch):
+    """The pipelined epoch's update in the backward tail's last blocks (waiting in-kernel for
+    every gradient writer and for the evaluation branch's bookkeeping signal, the branches joined
+    only at the graph end) gives the bits of the join + k_adam graphs: parameters, history rows
+    (gradient norms, best-epoch flags) and snapshots, batched models included."""
+    cfg = default_cli_config(178, 46)
+    monkeypatch.setenv("DLAP_SPLIT_GRAPHS", "0")
+    monkeypatch.setenv("DLAP_TAIL_ADAM", "0")
+    e0, ref = _train(big, cfg, [71, 72], 2)
+    assert not e0.eng.fused_info()["adam_in_tail"]
+    monkeypatch.setenv("DLAP_TAIL_ADAM", "1")
+    e1, res = _train(big, cfg, [71, 72], 2)
+    assert e1.eng.fused_info()["adam_in_tail"]
+    for s in (71, 72):
+        _same(ref[s], res[s])
+
+
+def test_split_epoch_graphs_equal_one_graph(big, monkeypatch):
+    """The training chain and the evaluation branch as two graphs on two queues with no graph
+    edge between them (in-kernel waits: the evaluation graph for the fused forward's evaluation
+    recurrences, the tail's Adam blocks for the bookkeeping's signal) give the bits of the
+    one-graph pipelined epoch, batched models included."""
+    cfg = default_cli_config(178, 46)
+    monkeypatch.setenv("DLAP_SPLIT_GRAPHS", "0")
+    e0, ref = _train(big, cfg, [81, 82], 2)
+    assert not e0.eng.fused_info()["split_graphs"]
+    monkeypatch.setenv("DLAP_SPLIT_GRAPHS", "1")
+    e1, res = _train(big, cfg, [81, 82], 2)
+    assert e1.eng.fused_info()["split_graphs"]
+    for s in (81, 82):
+        _same(ref[s], res[s])
+
+
 def test_self_projecting_recurrences_equal_k_proj(big, monkeypatch):
     """The fused forward's recurrences computing their own layer-0 input projections tile by tile
     (spare waves of their workgroups, no k_proj launch) give the bits of k_proj + staged inputs."""

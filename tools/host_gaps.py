@@ -18,6 +18,7 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--adams", type=int, default=21)
     ap.add_argument("--min-api-us", type=float, default=5.0)
+    ap.add_argument("--marker", default="k_adam", help="kernel marking an epoch (k_lstm_tail: update in the tail)")
     a = ap.parse_args()
     kr, hr = [], []
     for f in Path(a.dir).glob("**/*kernel_trace.csv"):
@@ -27,7 +28,7 @@ def main():
     from kernel_stats import demangle
     dm = demangle({r["Kernel_Name"] for r in kr})
     kr.sort(key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(kr) if dm[r["Kernel_Name"]].startswith("k_adam")]
+    idx = [i for i, r in enumerate(kr) if dm[r["Kernel_Name"]].startswith(a.marker)]
     lo = idx[-a.adams - 1] if len(idx) > a.adams else 0
     t0, t1 = int(kr[lo]["Start_Timestamp"]), int(kr[-1]["End_Timestamp"])
     ev = []

@@ -40,6 +40,9 @@ def main():
         if eng.eng.fused_info()["fused_tail"] and ts[16] > ts[9]:    # k_lstm_tail: dpp wait, W_ih
             print(f"    fused tail   : pre-pass->dpp in LDS {us(9, 16):7.1f}  pair maps {us(16, 13):7.1f}  "
                   f"W_hh grads {us(10, 11):7.1f}  last W_ih block done {us(10, 17):7.1f} after the gates")
+        if eng.eng.fused_info().get("adam_in_tail") and pipe and ts[20] > ts[18]:
+            print(f"    tail Adam    : last arrival {us(10, 18):7.1f} after the gates  Adam block 0 released "
+                  f"{us(18, 19):7.1f}  update done {us(19, 20):7.1f} later")
         print(f"  k_proj tile0   : total {us(12, 14):7.1f}")
         m = np.array(mod.Engine.mlp_timestamps(), dtype=np.int64)
         um = lambda a, b: (m[b] - m[a]) / 100.0  # noqa: E731

@@ -16,7 +16,8 @@ sys.path.insert(0, str(Path(__file__).resolve().parent))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("dir")
-    ap.add_argument("--adams", type=int, default=20, help="number of trailing k_adam launches to cover")
+    ap.add_argument("--adams", type=int, default=20, help="number of trailing marker launches to cover")
+    ap.add_argument("--marker", default="k_adam", help="kernel that marks an epoch (k_lstm_tail with the update in the tail)")
     a = ap.parse_args()
     rows = []
     for f in Path(a.dir).glob("**/*kernel_trace.csv"):
@@ -32,7 +33,7 @@ def main():
     for r in rows:
         r["Kernel_Name"] = dm[r["Kernel_Name"]]
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith("k_adam")]
+    idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith(a.marker)]
     lo = idx[-a.adams - 1] if len(idx) > a.adams else 0
     sel = rows[lo:]
     t0 = int(sel[0]["Start_Timestamp"])
