@@ -182,7 +182,6 @@ static int env_int(const char* name, int dflt) {
   const char* v = std::getenv(name);
   return v && *v ? std::atoi(v) : dflt;
 }
-static const int g_skip = env_int("DLAP_SKIP", 0);   // TEMPORARY knock-out timing experiment
 
 static void install_crash_handler();
 // DLAP_TRACE_HOST=1: one stderr line per host-side engine step (crash localisation on boxes
@@ -197,40 +196,16 @@ class Engine {
          float residual, int G, int max_epochs, bool fp32)
       : G_(G), max_epochs_(max_epochs) {
     g_live_engines.fetch_add(1);
-    prio_ = env_int("DLAP_PRIO", 0) != 0;
-    if (prio_) {   // the training chain (critical path) ahead of the evaluation branch
-      int lo = 0, hi = 0;
-      HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-      HIP_OK(hipStreamCreateWithPriority(&st_, hipStreamNonBlocking, hi));
-      HIP_OK(hipStreamCreateWithPriority(&st2_, hipStreamNonBlocking, lo));
-    } else {
-      HIP_OK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
-      const int ncu = env_int("DLAP_EVAL_CUS", 0);     // >0: evaluation branch on a CU subset
-      if (ncu > 0) {
-        hipDeviceProp_t prop;
-        int dev = 0;
-        HIP_OK(hipGetDevice(&dev));
-        HIP_OK(hipGetDeviceProperties(&prop, dev));
-        const int total = prop.multiProcessorCount;
-        std::vector<uint32_t> mask((total + 31) / 32, 0u);
-        // every XCD keeps the same share of its CUs (logical CU ids interleave the XCDs)
-        for (int cu = 0; cu < total; ++cu)
-          if ((long)(cu % 32) * total < (long)ncu * 32) mask[cu / 32] |= 1u << (cu % 32);
-        HIP_OK(hipExtStreamCreateWithCUMask(&st2_, (uint32_t)mask.size(), mask.data()));
-      } else {
-        HIP_OK(hipStreamCreateWithFlags(&st2_, hipStreamNonBlocking));
-      }
-    }
-    HIP_OK(hipStreamCreateWithFlags(&st3_, hipStreamNonBlocking));
+    // (stream priorities and a CU-masked evaluation stream were measured and dropped:
+    // profiles/r5_bench_ab_tail_adam_split_graphs.log, r3 knob logs)
+    HIP_OK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+    HIP_OK(hipStreamCreateWithFlags(&st2_, hipStreamNonBlocking));
     own_st_ = st_;
     HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_gram_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_mid_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_a_, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&ev_m3_, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&ev_b3_, hipEventDisableTiming));
-    HIP_OK(hipEventCreateWithFlags(&ev_f3_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
     // evaluation tower grid cap: the evaluation branch is within a few us of the training chain
@@ -239,18 +214,9 @@ class Engine {
     // job: with G batched models the launch has 2G evaluation jobs, so the per-job grid shrinks
     // with G (see grid_per_model)
     eval_gx_ = env_int("DLAP_EVAL_GX", grid_per_model(384, 96, G));
-    b_wait_ = env_int("DLAP_B_WAIT", 0);
-    // both off: a third graph branch changes how the runtime maps the graph onto its hardware
-    // queues -- the evaluation branch then shared a queue with the training backward and ran
-    // after it (2718 vs 3978 model-epochs/s, profiles/r2_knobs_third_stream.log)
-    side_metrics_ = env_int("DLAP_SIDE_METRICS", 0) != 0;
-    split_tail_ = env_int("DLAP_SPLIT_TAIL", 0) != 0;
-    defer_metrics_ = env_int("DLAP_DEFER_METRICS", 1) != 0;
     zx_eval_ = env_int("DLAP_ZX_EVAL", 1) != 0;
     zx_train_ = env_int("DLAP_ZX_TRAIN", 1) != 0;
     zx_gx_ = std::max(1, env_int("DLAP_ZX_GX", 256));
-    train_first_ = env_int("DLAP_TRAIN_FIRST", 2);
-    eval_after_bwd_ = env_int("DLAP_EVAL_AFTER_BWD", 0) != 0;
     h_cache_ = env_int("DLAP_H_CACHE", 1) != 0;
     gram_on_ = env_int("DLAP_GRAM", 1) != 0;
     rnn_overlap_ = env_int("DLAP_RNN_OVERLAP", 1) != 0;
@@ -264,7 +230,6 @@ class Engine {
     tail_adam_ = env_int("DLAP_TAIL_ADAM", 1) != 0;
     split_graphs_ = env_int("DLAP_SPLIT_GRAPHS", 1) != 0;
     unroll_ = std::max(1, env_int("DLAP_UNROLL", 4));
-    rotate_ = env_int("DLAP_ROTATE", 0) != 0;
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
                residual, fp32);
     // fp32 wide path: layer 0 through k_proj0 + the ZIN towers (the fused-layer-0 k_mlp_fwd_zx
@@ -330,7 +295,6 @@ class Engine {
     HTRACE("~Engine tid=%ld", (long)syscall(SYS_gettid));
     // drain both streams before the graphs, events and (member) buffers go away
     if (st2_) (void)hipStreamSynchronize(st2_);
-    if (st3_) (void)hipStreamSynchronize(st3_);
     if (st_) (void)hipStreamSynchronize(st_);
     if (own_st_ && own_st_ != st_) (void)hipStreamSynchronize(own_st_);
     for (auto& kv : graphs_) retire_graph_exec(kv.second, st_);
@@ -339,9 +303,8 @@ class Engine {
     if (ev_gram_) (void)hipEventDestroy(ev_gram_);
     if (ev_mid_) (void)hipEventDestroy(ev_mid_);
     if (ev_a_) (void)hipEventDestroy(ev_a_);
-    for (hipEvent_t e : {ev_m3_, ev_b3_, ev_f3_, ev_in_, ev_out_}) if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {ev_in_, ev_out_}) if (e) (void)hipEventDestroy(e);
     if (st2_) (void)hipStreamDestroy(st2_);
-    if (st3_) (void)hipStreamDestroy(st3_);
     if (own_st_) (void)hipStreamDestroy(own_st_);
     (void)hipGetLastError();      // (ignored statuses above must not fail the next launch check)
   }
@@ -713,11 +676,6 @@ class Engine {
       for (int e = 0; e < n; ++e) HIP_OK(hipGraphLaunch(g, st_));
       return;
     }
-    // rotated graphs (the eval-in-forward epoch): each graph STARTS with the previous epoch's
-    // Adam and ends at the join of its two branches, so no kernel of the graph waits on the other
-    // branch -- the join coincides with the graph boundary. head = first epoch's training (no
-    // Adam); body = Adam(e-1) | training(e) || evaluation(e-1) + bookkeeping; tail = Adam(last) |
-    // evaluation(last) + bookkeeping. The same kernels in the same dependency order per buffer.
     if (split_graphs(phase)) {
       hipGraphExec_t head = graph_for(graph_key(phase, lr, ignore_epoch, sel, 1), [&] { enqueue_head(phase, lr); });
       // the body epochs in graphs of `unroll_` epochs each (the rest one by one): a graph boundary
@@ -763,16 +721,11 @@ class Engine {
       HIP_OK(hipGraphLaunch(tail, st_));
       return;
     }
-    const bool rot = rotate_ && b_wait_ == 0 && !side_metrics_ && eval_rnn_in_fwd(phase);
-    const int k0 = rot ? 10 : 0;
-    hipGraphExec_t head = graph_for(graph_key(phase, lr, ignore_epoch, sel, k0 + 1),
-                                    [&] { if (rot) enqueue_head_rot(phase); else enqueue_head(phase, lr); });
-    hipGraphExec_t body = graph_for(graph_key(phase, lr, ignore_epoch, sel, k0 + 2),
-                                    [&] { if (rot) enqueue_pipe_rot(phase, lr, ignore_epoch, sel);
-                                          else enqueue_pipe(phase, lr, ignore_epoch, sel); });
-    hipGraphExec_t tail = graph_for(graph_key(phase, lr, ignore_epoch, sel, k0 + 3),
-                                    [&] { if (rot) enqueue_tail_rot(phase, lr, ignore_epoch, sel);
-                                          else enqueue_tail(phase, ignore_epoch, sel); });
+    hipGraphExec_t head = graph_for(graph_key(phase, lr, ignore_epoch, sel, 1), [&] { enqueue_head(phase, lr); });
+    hipGraphExec_t body = graph_for(graph_key(phase, lr, ignore_epoch, sel, 2),
+                                    [&] { enqueue_pipe(phase, lr, ignore_epoch, sel); });
+    hipGraphExec_t tail = graph_for(graph_key(phase, lr, ignore_epoch, sel, 3),
+                                    [&] { enqueue_tail(phase, ignore_epoch, sel); });
     HTRACE("launch head");
     HIP_OK(hipGraphLaunch(head, st_));
     join_eval_gram();                     // the next graphs evaluate
@@ -1059,26 +1012,15 @@ class Engine {
   DevBuf<int> inv_code_;                     // parameter -> packed elements (k_adam's fused re-pack)
   struct FwdTables { DevBuf<char> r, m, l, w; bool built = false; };
   std::map<int, FwdTables> fwd_tables_;      // module-API forward job tables (per split / mode)
-  bool prio_ = false;                        // stream/node priorities (DLAP_PRIO)
   hipStream_t st2_ = nullptr;                // evaluation branch of the pipelined epoch graph
   hipEvent_t ev_fork_ = nullptr, ev_join_ = nullptr, ev_mid_ = nullptr, ev_a_ = nullptr;
-  // third stream: side work of the training chain that nothing on it waits for soon -- the
-  // train split's metrics (read by the epoch bookkeeping) and the weight-gradient slab sums
-  // (read by Adam) -- forked with ev_m3_/ev_b3_ and joined back through ev_f3_
-  hipStream_t st3_ = nullptr;
-  hipEvent_t ev_m3_ = nullptr, ev_b3_ = nullptr, ev_f3_ = nullptr;
   hipEvent_t ev_in_ = nullptr, ev_out_ = nullptr;   // join_from / join_to
   hipEvent_t ev_gram_ = nullptr;                     // deferred evaluation-split Gram builds done
   bool eval_gram_pending_ = false;
-  bool split_tail_ = false;                  // DLAP_SPLIT_TAIL
   int eval_gx_ = 0;                          // cap on the evaluation tower grid (DLAP_EVAL_GX)
-  int b_wait_ = 0;                           // evaluation towers after train towers (DLAP_B_WAIT)
   bool zx_eval_ = true;                      // wide path: fused layer-0 evaluation towers (DLAP_ZX_EVAL)
   bool zx_train_ = true;                     // ... and training forward (DLAP_ZX_TRAIN)
   int zx_gx_ = 256;                          // their workgroups over all evaluation jobs (DLAP_ZX_GX)
-  bool side_metrics_ = false;                // train metrics on the side stream st3_ (DLAP_SIDE_METRICS)
-  bool defer_metrics_ = true;                // pipelined epochs: train metrics on the evaluation branch
-  int train_first_ = 1;                      // capture the training chain before the evaluation branch
                                              // (2: with the evaluation LSTM prologue right behind the training one)
   // Moment cache: the moment net only changes in phase 2, so outside it the moments h of every
   // split are constant (eval mode has no dropout; the train split's only if the moment tower has
@@ -1120,7 +1062,6 @@ class Engine {
   // epoch): fused there in any case -- beside the training chain the spinning tower workgroups
   // of both fused launches compete for the same CUs (profiles/r3_knobs_fused_eval.log)
   bool eval_solo_ = false;
-  bool eval_after_bwd_ = false;              // DLAP_EVAL_AFTER_BWD (see enqueue_pipe)
   int prog_mode_ = 1;                        // DLAP_PROG_MODE (see MlpJob::prog_mode)
   unsigned prog_limit_ = 1u << 22;           // DLAP_PROG_SPIN_LIMIT (see MlpJob::prog_limit)
   bool fused_p2_ = false;                    // DLAP_FUSED_PHASE2: fused training forward in phase 2 too
@@ -1903,22 +1844,18 @@ class Engine {
   bool dropmask_on(int phase) const { return md_.dropout > 0.f && phase != 2; }
   // keep masks of the step *drop_step + offset* (phases 1/3: the SDF tower's dropout)
   void enqueue_dropmask(int phase, int offset, hipStream_t st) {
-    if (!dropmask_on(phase) || (g_skip & 32)) return;
+    if (!dropmask_on(phase)) return;
     HTRACE("launch_dropmask");
     launch_dropmask(as<MlpJob>(j_mlp_train_[phase]), G_, (splits_[0].R + 31) / 32, md_.md, offset, st);
   }
-  // side: if non-null, the train split's Sharpe monitor (not needed by the backward) runs
-  // on that stream after the asset pass; the caller joins it before the bookkeeping copy.
   // premasked: this step's keep masks were generated by the previous epoch graph.
-  // mark: record ev_a_ after the tower backward (1), the tower forward (2) or the wide
-  // layer-0 projection (3);
-  // part1_only: stop before the gradient finalisation (the caller enqueues the tail).
+  // mark: record ev_a_ after the tower forward (2);
   // defer_metrics: the train split's metrics are left to the caller (it records ev_mid_ after the
   // asset pass; the pipelined epoch runs them on the evaluation branch, off the critical chain).
   // eval_rnn: the evaluation splits' projections and recurrences ride in the training prologue
   // and fused forward (eval_rnn_in_fwd; the caller's evaluation branch starts at its towers)
-  void enqueue_train_grads(int phase, hipStream_t side = nullptr, bool premasked = false, int mark = 0,
-                           bool part1_only = false, bool defer_metrics = false, bool eval_rnn = false) {
+  void enqueue_train_grads(int phase, bool premasked = false, int mark = 0, bool defer_metrics = false,
+                           bool eval_rnn = false) {
     const SplitDev& D = splits_[0];
     const bool gram = use_gram(phase);
     const LossJob* lj = loss_tab(phase, gram);
@@ -1941,7 +1878,6 @@ class Engine {
     const bool zx_train = md_.md.wide && zx_train_;
     if (md_.md.wide && !zx_train)
       launch_proj0(as<WideJob>(j_wide_train_[phase]), G_, gx_proj_[0], md_.md, md_.WMB, st_);
-    if (mark == 3) HIP_OK(hipEventRecord(ev_a_, st_));
     if (zx_train)      // layer 0 streamed inside the training towers, z stored for the backward
       launch_mlp_fwd_zx(as<MlpJob>(j_mlp_train_[phase]), G_, std::max(1, zx_gx_ / G_), md_.md, md_.WMB, st_, true);
     else if (eval_rnn)
@@ -1957,8 +1893,8 @@ class Engine {
                      md_.WMB, st_, !train_mom(phase));
     if (mark == 2) HIP_OK(hipEventRecord(ev_a_, st_));
     HTRACE("launch_period_fwd");
-    if (!(g_skip & 128)) launch_period_fwd(lj, G_, D.T, st_);
-    if (g_skip & 128) {} else if (!gram) {
+    launch_period_fwd(lj, G_, D.T, st_);
+    if (!gram) {
       HTRACE("launch_asset");
       launch_asset(lj, G_, D.N, md_.K, st_, asset_full_default());
     } else {
@@ -1971,13 +1907,6 @@ class Engine {
       // the train split's metrics are computed by the backward tail (enqueue_train_tail)
     } else if (defer_metrics && phase != 2) {
       HIP_OK(hipEventRecord(ev_mid_, st_));
-    } else if (side) {
-      HIP_OK(hipEventRecord(ev_mid_, st_));
-      HIP_OK(hipStreamWaitEvent(side, ev_mid_, 0));
-      HTRACE("launch_job_metrics");
-      launch_job_metrics(lj, G_, side);
-      HIP_OK(hipEventRecord(ev_m3_, side));
-      side_open_ = true;
     } else {
       // (k_job_metrics, not the metrics workgroup of k_period_bwd<true>: the same reduction
       // order as the deferred launch of the pipelined epochs, so both schedules are bitwise equal)
@@ -1994,13 +1923,11 @@ class Engine {
         launch_period_bwd(lj, G_, D.T, st_);
       }
       HTRACE("launch_mlp_bwd_sdf");
-      if (!(g_skip & 4)) launch_mlp_bwd_sdf(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_s, md_.tps_s, md_.md, md_.KS1,
+      launch_mlp_bwd_sdf(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_s, md_.tps_s, md_.md, md_.KS1,
                          slab_stride(), fpw_, st_);
     }
     if (md_.md.wide)   // layer-0 weight gradient from the tower's dz fragments
       launch_wgrad0(as<WideJob>(j_wide_bwd_[phase]), G_, dd(), md_.md, phase == 2, md_.WMB, nsplit_, st_);
-    if (mark == 1) HIP_OK(hipEventRecord(ev_a_, st_));
-    if (part1_only) return;
     enqueue_train_tail(phase);
   }
   // k_finalize -> k_lstm_bwd -> k_wgrad as one launch (k_lstm_tail) where it applies
@@ -2010,7 +1937,7 @@ class Engine {
   // the evaluation branch, so the training chain forks only once (after the fused forward)
   bool tail_metrics_ = false;
   bool tail_fused(int phase) const {
-    return fused_tail_ && !split_tail_ && phase != 2 && splits_[0].set && lstm_tail_supported(md_, splits_[0].T);
+    return fused_tail_ && phase != 2 && splits_[0].set && lstm_tail_supported(md_, splits_[0].T);
   }
   // the pipelined eval-in-forward epoch: the clip + Adam update runs in the backward tail's last
   // blocks (k_lstm_tail, adam 2) after the evaluation branch's bookkeeping signalled, so the
@@ -2033,14 +1960,14 @@ class Engine {
   long host_launch_n_ = 0;                   // ... over this many epochs (fused_info)
   int* fwd_esig_ = nullptr;                  // set around enqueue_train_grads (enqueue_chain_split)
   bool split_graphs(int phase) const {
-    return split_graphs_ && adam_in_tail(phase) && b_wait_ == 0 && !side_metrics_ && eval_rnn_in_fwd(phase);
+    return split_graphs_ && adam_in_tail(phase) && eval_rnn_in_fwd(phase);
   }
   void enqueue_chain_split(int phase, float lr) {
     tail_metrics_ = true;
     tail_adam_mode_ = 2;
     tail_lr_ = lr;
     fwd_esig_ = esync_.p;
-    enqueue_train_grads(phase, nullptr, true, 0, false, false, true);
+    enqueue_train_grads(phase, true, 0, false, true);
     tail_metrics_ = false;
     tail_adam_mode_ = 0;
     fwd_esig_ = nullptr;
@@ -2054,45 +1981,20 @@ class Engine {
   }
   void enqueue_train_tail(int phase) {
     const SplitDev& D = splits_[0];
-    if (g_skip & 1) { join_side(); return; }
     const LossJob* lm = tail_metrics_ && phase != 2 ? loss_tab(phase, use_gram(phase)) : nullptr;
     if (tail_fused(phase)) {
       HTRACE("launch_lstm_tail");
       launch_lstm_tail(as<UpdJob>(j_upd_), as<FinJob>(j_fin_), G_, dd(), md_, D.T, slab_stride(), st_, lm,
                        tail_adam_mode_, tail_lr_);
-      join_side();
       return;
     }
     if (lm) launch_job_metrics(lm, G_, st_);
-    if (split_tail_) {
-      // slab sums beside the LSTM backward (which reads only the per-period sums)
-      HIP_OK(hipEventRecord(ev_b3_, st_));
-      HIP_OK(hipStreamWaitEvent(st3_, ev_b3_, 0));
-      HTRACE("launch_finalize");
-      launch_finalize(as<FinJob>(j_fin_), G_, dd(), md_, phase, slab_stride(), D.T, st3_, 1);
-      HTRACE("launch_finalize");
-      launch_finalize(as<FinJob>(j_fin_), G_, dd(), md_, phase, slab_stride(), D.T, st_, 2);
-      HTRACE("launch_lstm_bwd");
-      launch_lstm_bwd(as<UpdJob>(j_upd_), G_, dd(), md_, D.T, phase, st_);
-      side_open_ = true;
-      join_side();
-    } else {
-      HTRACE("launch_finalize");
-      launch_finalize(as<FinJob>(j_fin_), G_, dd(), md_, phase, slab_stride(), D.T, st_);
-      HTRACE("launch_lstm_bwd");
-      launch_lstm_bwd(as<UpdJob>(j_upd_), G_, dd(), md_, D.T, phase, st_);
-      join_side();
-    }
+    HTRACE("launch_finalize");
+    launch_finalize(as<FinJob>(j_fin_), G_, dd(), md_, phase, slab_stride(), D.T, st_);
+    HTRACE("launch_lstm_bwd");
+    launch_lstm_bwd(as<UpdJob>(j_upd_), G_, dd(), md_, D.T, phase, st_);
   }
-  // join whatever was forked onto st3_ back into st_ (required before a graph capture ends)
-  bool side_open_ = false;
   hipStream_t eval_prologue_hook_ = nullptr;   // see enqueue_train_grads
-  void join_side() {
-    if (!side_open_) return;
-    HIP_OK(hipEventRecord(ev_f3_, st3_));
-    HIP_OK(hipStreamWaitEvent(st_, ev_f3_, 0));
-    side_open_ = false;
-  }
   void enqueue_train(int phase, float lr) {
     enqueue_train_grads(phase);
     HTRACE("launch_update");
@@ -2103,14 +2005,14 @@ class Engine {
     enqueue_eval_towers(st);
   }
   void enqueue_eval_prologue(hipStream_t st) {
-    if (n_eval_jobs_ == 0 || (g_skip & 2)) return;
+    if (n_eval_jobs_ == 0) return;
     HTRACE("launch_prologue");
     // fused: the input projections only, the recurrences run inside the tower launch
     if (fused_eval()) launch_proj(as<RnnJob>(j_rnn_eval_), n_eval_jobs_, tmax_eval_, dd(), md_, st, !h_cache_);
     else launch_prologue(as<RnnJob>(j_rnn_eval_), n_eval_jobs_, tmax_eval_, dd(), md_, st, !h_cache_);
   }
   void enqueue_eval_towers(hipStream_t st) {
-    if (n_eval_jobs_ == 0 || (g_skip & 2)) return;
+    if (n_eval_jobs_ == 0) return;
     const int gx = eval_grid();
     if (md_.md.wide && zx_eval_) {     // layer 0 streamed inside the evaluation towers
       HTRACE("launch_mlp_fwd_zx");
@@ -2125,7 +2027,6 @@ class Engine {
       else
         launch_mlp_fwd(as<MlpJob>(j_mlp_eval_), n_eval_jobs_, gx, md_.md, md_.KS1, md_.WMB, st, h_cache_);
     }
-    if (g_skip & 16) return;
     const bool eg = eval_gram_now();
     const LossJob* le = as<LossJob>(eg ? j_loss_eval_ : j_loss_eval_dense_);
     HTRACE("launch_period_fwd");
@@ -2142,7 +2043,6 @@ class Engine {
   }
   void enqueue_epoch_end(int phase, int ignore_epoch, float sel, hipStream_t st, int signal = 0) {
     HTRACE("launch_epoch_end");
-    if (g_skip & 64) return;
     launch_epoch_end(as<EpochJob>(j_epoch_[phase]), G_, phase, ignore_epoch, sel, md_.residual_factor,
                      md_.P, st, signal);
   }
@@ -2160,44 +2060,22 @@ class Engine {
     HTRACE("launch_update");
     launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_, inv_code_.p != nullptr);
   }
-  // rotated pipeline (run_epochs): see there
-  bool rotate_ = true;                       // DLAP_ROTATE
-  void enqueue_head_rot(int phase) {
-    enqueue_train_grads(phase);
-    enqueue_dropmask(phase, 1, st_);                     // masks of the first pipelined epoch
-  }
-  void enqueue_pipe_rot(int phase, float lr, int ignore_epoch, float sel) {
-    HTRACE("launch_update");
-    if (!(g_skip & 8)) launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_, inv_code_.p != nullptr);
-    tail_metrics_ = true;
-    enqueue_train_grads(phase, nullptr, true, 2, false, false, true);
-    tail_metrics_ = false;
-    HIP_OK(hipStreamWaitEvent(st2_, ev_a_, 0));          // after the fused forward (evaluation LSTMs)
-    enqueue_eval_towers(st2_);
-    enqueue_epoch_end(phase, ignore_epoch, sel, st2_);
-    enqueue_dropmask(phase, 1, st2_);
-    HIP_OK(hipEventRecord(ev_join_, st2_));             // (capture end: the branches join here)
-    HIP_OK(hipStreamWaitEvent(st_, ev_join_, 0));
-  }
-  void enqueue_tail_rot(int phase, float lr, int ignore_epoch, float sel) {
-    HTRACE("launch_update");
-    launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_, inv_code_.p != nullptr);
-    { SoloScope solo(eval_solo_); enqueue_eval(st_); }
-    enqueue_epoch_end(phase, ignore_epoch, sel, st_);
-  }
+  // One-graph pipelined epoch (the split graphs' fallback: DLAP_SPLIT_GRAPHS=0, the update outside
+  // the tail, or no fused forward): the training chain on st_, the evaluation branch forked
+  // onto st2_ and joined before the update.
   void enqueue_pipe(int phase, float lr, int ignore_epoch, float sel) {
     HIP_OK(hipEventRecord(ev_fork_, st_));
     HIP_OK(hipStreamWaitEvent(st2_, ev_fork_, 0));
-    if (b_wait_ == 0 && !side_metrics_ && eval_rnn_in_fwd(phase)) {
+    if (eval_rnn_in_fwd(phase)) {
       // the evaluation recurrences run inside this epoch's fused training forward; the
-      // evaluation branch forks after it: towers, losses, this epoch's train metrics (after its
-      // loss pass), the bookkeeping and the next epoch's dropout masks, beside the training
-      // backward and its tail
+      // evaluation branch forks after it: towers, losses, the bookkeeping and the next epoch's
+      // dropout masks, beside the training backward and its tail (which computes the train
+      // split's metrics)
       const bool ta = adam_in_tail(phase);
       tail_metrics_ = true;
       tail_adam_mode_ = ta ? 2 : 0;
       tail_lr_ = lr;
-      enqueue_train_grads(phase, nullptr, true, 2, false, false, true);
+      enqueue_train_grads(phase, true, 2, false, true);
       tail_metrics_ = false;
       tail_adam_mode_ = 0;
       HIP_OK(hipStreamWaitEvent(st2_, ev_a_, 0));
@@ -2213,73 +2091,26 @@ class Engine {
       }
       enqueue_epoch_end(phase, ignore_epoch, sel, st2_);
       enqueue_dropmask(phase, 1, st2_);
-      HIP_OK(hipEventRecord(ev_join_, st2_));
-      HIP_OK(hipStreamWaitEvent(st_, ev_join_, 0));
-      HTRACE("launch_update");
-      if (!(g_skip & 8)) launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_, inv_code_.p != nullptr);
-      return;
-    }
-    if (b_wait_ == 0 && train_first_) {
-      // same graph topology, training-chain nodes first (they land on the graph's first queue)
-      const bool defer = !side_metrics_ && defer_metrics_;
-      const bool inter = train_first_ == 2 && n_eval_jobs_ > 0;
-      if (inter) eval_prologue_hook_ = st2_;
-      // eval_after_bwd_: the evaluation towers wait for the training tower backward, so the
-      // two largest launches of the epoch do not share the CUs; the evaluation then fills the
-      // GPU beside the few-CU serial tail (finalize, BPTT, weight gradient)
-      const int mark = inter && eval_after_bwd_ ? 1 : 0;
-      enqueue_train_grads(phase, side_metrics_ ? st3_ : nullptr, true, mark, false, defer);   // this epoch's fwd/bwd
+    } else {
+      // training-chain nodes first (they land on the graph's first queue); the evaluation
+      // branch's LSTM prologue right behind the training one (eval_prologue_hook_), so its
+      // serial recurrence starts at the epoch start; this epoch's train metrics on the
+      // evaluation branch after the loss pass (ev_mid_), then the bookkeeping and the masks
+      eval_prologue_hook_ = st2_;
+      enqueue_train_grads(phase, true, 0, true);
       eval_prologue_hook_ = nullptr;
-      if (mark && !side_metrics_) {
-        // the work of the evaluation branch that does not need the towers runs beside the
-        // training backward: this epoch's train metrics (after its loss pass) and the next
-        // epoch's dropout masks; then the towers, their losses and the bookkeeping
-        if (defer && phase != 2) {
-          HIP_OK(hipStreamWaitEvent(st2_, ev_mid_, 0));
-          launch_job_metrics(loss_tab(phase, use_gram(phase)), G_, st2_);
-        }
-        enqueue_dropmask(phase, 1, st2_);
-        HIP_OK(hipStreamWaitEvent(st2_, ev_a_, 0));
-        enqueue_eval_towers(st2_);
-        enqueue_epoch_end(phase, ignore_epoch, sel, st2_);
-        HIP_OK(hipEventRecord(ev_join_, st2_));
-        HIP_OK(hipStreamWaitEvent(st_, ev_join_, 0));
-        HTRACE("launch_update");
-        launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_, inv_code_.p != nullptr);
-        return;
-      }
-      if (mark) HIP_OK(hipStreamWaitEvent(st2_, ev_a_, 0));
-      if (inter) enqueue_eval_towers(st2_);               // previous epoch's evaluation
-      else enqueue_eval(st2_);
-      if (side_metrics_) HIP_OK(hipStreamWaitEvent(st2_, ev_m3_, 0));   // train metrics
-      if (defer && phase != 2) {                          // this epoch's train metrics, after its
-        HIP_OK(hipStreamWaitEvent(st2_, ev_mid_, 0));     // asset pass (read by the next bookkeeping)
+      enqueue_eval_towers(st2_);
+      if (phase != 2) {
+        HIP_OK(hipStreamWaitEvent(st2_, ev_mid_, 0));
         launch_job_metrics(loss_tab(phase, use_gram(phase)), G_, st2_);
       }
-      enqueue_epoch_end(phase, ignore_epoch, sel, st2_);  // ... and its bookkeeping
-      enqueue_dropmask(phase, 1, st2_);                   // next epoch's dropout masks
-    } else if (b_wait_ == 0) {
-      // (the bookkeeping is enqueued before the training chain here: train metrics stay on st_)
-      enqueue_eval(st2_);                                 // previous epoch's evaluation
-      enqueue_epoch_end(phase, ignore_epoch, sel, st2_);  // ... and its bookkeeping
-      enqueue_dropmask(phase, 1, st2_);                   // next epoch's dropout masks
-      enqueue_train_grads(phase, nullptr, true);          // this epoch's fwd/bwd
-    } else {
-      // the evaluation towers start once the training towers (b_wait_ 1: backward, 2:
-      // forward) are done, so the wide kernels of the two branches do not contend
-      enqueue_eval_prologue(st2_);
-      enqueue_train_grads(phase, side_metrics_ ? st3_ : nullptr, true, b_wait_, true);
-      HIP_OK(hipStreamWaitEvent(st2_, ev_a_, 0));
-      enqueue_eval_towers(st2_);
-      if (side_metrics_) HIP_OK(hipStreamWaitEvent(st2_, ev_m3_, 0));
       enqueue_epoch_end(phase, ignore_epoch, sel, st2_);
       enqueue_dropmask(phase, 1, st2_);
-      enqueue_train_tail(phase);
     }
-    HIP_OK(hipEventRecord(ev_join_, st2_));               // (train monitor ran on st2_ too)
+    HIP_OK(hipEventRecord(ev_join_, st2_));
     HIP_OK(hipStreamWaitEvent(st_, ev_join_, 0));
     HTRACE("launch_update");
-    if (!(g_skip & 8)) launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_, inv_code_.p != nullptr);
+    launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_, inv_code_.p != nullptr);
   }
   struct SoloScope {
     bool& f;
@@ -2307,7 +2138,7 @@ class Engine {
     }
     HTRACE("instantiate");
     hipGraphExec_t exec;
-    HIP_OK(hipGraphInstantiateWithFlags(&exec, graph, prio_ ? hipGraphInstantiateFlagUseNodePriority : 0));
+    HIP_OK(hipGraphInstantiateWithFlags(&exec, graph, 0));
     HIP_OK(hipGraphDestroy(graph));
     // device-side upload now, not at the first launch (that launch may sit inside a timed or
     // latency-critical region)

@@ -208,18 +208,6 @@ def test_self_projecting_recurrences_equal_k_proj(big, monkeypatch):
         _same(ref[s], res[s])
 
 
-def test_rotated_pipeline_equals_join_before_adam(big, monkeypatch):
-    """The rotated epoch graphs (Adam of the previous epoch at the head of each graph, the two
-    branches joining at the graph boundary) give the bits of the graphs that join before Adam."""
-    cfg = default_cli_config(178, 46)
-    monkeypatch.setenv("DLAP_ROTATE", "0")
-    _, ref = _train(big, cfg, [71, 72], 2)
-    monkeypatch.setenv("DLAP_ROTATE", "1")
-    _, res = _train(big, cfg, [71, 72], 2)
-    for s in (71, 72):
-        _same(ref[s], res[s])
-
-
 def test_fused_phase2_under_the_guarantee_equals_two_launches(big, monkeypatch):
     """Phase 2's fused forward (opt-in, DLAP_FUSED_PHASE2=1) runs on the capped grid and gives the
     same bits as the two-launch path."""
