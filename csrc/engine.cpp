@@ -196,10 +196,24 @@ class Engine {
          float residual, int G, int max_epochs, bool fp32)
       : G_(G), max_epochs_(max_epochs) {
     g_live_engines.fetch_add(1);
-    // (stream priorities and a CU-masked evaluation stream were measured and dropped:
-    // profiles/r5_bench_ab_tail_adam_split_graphs.log, r3 knob logs)
     HIP_OK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
-    HIP_OK(hipStreamCreateWithFlags(&st2_, hipStreamNonBlocking));
+    {
+      // the evaluation stream on a hardware queue of its own: a stream created with a CU mask
+      // (here: every CU) gets a dedicated queue instead of one from the runtime's pool, which
+      // hands out GPU_MAX_HW_QUEUES (4) queues round robin over all streams of the process. The
+      // split epoch graphs wait in-kernel across st_ and st2_; were the two on one queue (a second
+      // engine, torch's / RCCL's streams), a wait would sit in front of the work it waits for
+      // until it gave up.
+      hipDeviceProp_t prop;
+      int dev = 0;
+      HIP_OK(hipGetDevice(&dev));
+      HIP_OK(hipGetDeviceProperties(&prop, dev));
+      std::vector<uint32_t> mask((prop.multiProcessorCount + 31) / 32, 0u);
+      for (int cu = 0; cu < prop.multiProcessorCount; ++cu) mask[cu / 32] |= 1u << (cu % 32);
+      // (measured: no cost against a pooled stream, profiles/r5_eval_queue_ab.log; with a pooled
+      // st2_, two live engines deadlocked until the waits gave up)
+      HIP_OK(hipExtStreamCreateWithCUMask(&st2_, (uint32_t)mask.size(), mask.data()));
+    }
     own_st_ = st_;
     HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
