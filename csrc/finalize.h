@@ -76,7 +76,9 @@ DLAP_DEV void finalize_block(const FinJob& J, const ModelDesc* __restrict__ md, 
   }
   b -= nb_extra;
   // per-period segment sums: one block per period, threads = (column d, row group)
-  const int D = mom ? 64 : (md->nrnn > 0 ? md->Dm : 0);
+  // (phase 2: only the moment layer-0 width of each [R][64] row is live -- the downstream
+  // W_macro / bias gradients read dab[t][g < m[0].out] -- so only those columns are summed)
+  const int D = mom ? md->m[0].out : (md->nrnn > 0 ? md->Dm : 0);
   const int t = b;
   if (D == 0 || t >= J.T) return;
   __shared__ float seg[256];
@@ -84,18 +86,19 @@ DLAP_DEV void finalize_block(const FinJob& J, const ModelDesc* __restrict__ md, 
   while (Dp < D) Dp <<= 1;
   const int nrg = 256 / Dp, d = threadIdx.x % Dp, rg = threadIdx.x / Dp;
   const auto src = gp(mom ? J.v : J.u);
+  const int ld = mom ? 64 : D;                        // row stride of v / u
   const int r0 = gp(J.row_ptr)[t], r1 = gp(J.row_ptr)[t + 1];
   float s = 0.f;
   if (d < D) {
 #pragma unroll 8
-    for (int r = r0 + rg; r < r1; r += nrg) s += src[(size_t)r * D + d];
+    for (int r = r0 + rg; r < r1; r += nrg) s += src[(size_t)r * ld + d];
   }
   seg[threadIdx.x] = s;
   __syncthreads();
   if (rg == 0 && d < D) {
     float tot = 0.f;
     for (int g = 0; g < nrg; ++g) tot += seg[g * Dp + d];
-    if (mom) gp(J.dab)[t * 64 + d] = tot;
+    if (mom) gp(J.dab)[t * 64 + d] = tot;      // (row stride 64)
     else if (ctr) __hip_atomic_store(gp(J.dpp) + t * D + d, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else gp(J.dpp)[t * D + d] = tot;
   }

@@ -114,9 +114,60 @@ DLAP_DEV f32x4 proj_tile(const RnnJob& J, const ModelDesc* md, int t0, int o0) {
 // LDS stores have completed; the recurrence (lstm_gls_body, `ready`) polls a tile's flag (plain
 // LDS reads: no fence -- a wave's LDS operations complete in order) only when it reaches a tile
 // it has not seen ready yet.
+// Fast path (one 16-wide gate tile, MP <= 192: the common LSTM[4]): the weight column fragment is
+// loaded once per wave and the next tile's macro rows are in flight while the MFMAs of the
+// current one run (ping-pong register sets; the fused forward is at its register limit anyway,
+// so the extra set is free) -- a tile every ~memory round trip per wave instead of a round trip
+// plus the MFMA chain; the same operands and MFMA order as proj_tile.
 DLAP_DEV void proj_into_lds(const RnnJob& J, const ModelDesc* __restrict__ md, float* sx, int* ready, int w, int nw) {
   const int T = J.T, G4 = 4 * md->H;
   const int l = threadIdx.x & 63, n = l & 15, kq = l >> 4;
+  constexpr int KC = 48;
+  const int M = md->M, MP = md->proj_mp, NP = md->proj_np;
+  if (G4 == 16 && MP <= 4 * KC) {
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)J.macro, (short)0, T * M * 4, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)J.wproj, (short)0, (MP + 2) * NP * 4, 0x00020000);
+    float b[KC], a0[KC], a1[KC];
+    const int wo = (kq * NP + n) * 4;
+#pragma unroll
+    for (int s = 0; s < KC; ++s) b[s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(wr, wo, 4 * s * NP * 4, 0));
+    const auto wcol = gp(J.wproj) + n;
+    const float bias = wcol[(size_t)MP * NP] + wcol[(size_t)(MP + 1) * NP];
+    auto load_a = [&](int j, float (&a)[KC]) {
+      const int ta = min(16 * j + n, T - 1);
+      const int xo = (ta * M + kq) * 4;
+#pragma unroll
+      for (int s = 0; s < KC; ++s) a[s] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, xo + 16 * s, 0, 0));
+    };
+    auto tile = [&](int j, const float (&a)[KC]) {
+      f32x4 acc = zero4();
+#pragma unroll
+      for (int s = 0; s < KC; ++s) {
+        const int m = 4 * s + kq;
+        acc = __builtin_amdgcn_mfma_f32_16x16x4f32(m < M ? a[s] : 0.f, m < MP ? b[s] : 0.f, acc, 0, 0, 0);
+      }
+      acc = acc + bias;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int t = 16 * j + 4 * kq + r;
+        if (t < T) sx[t * G4 + n] = acc[r];
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (l == 0) __hip_atomic_store(ready + j, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    int j = w;
+    if (j * 16 < T) load_a(j, a0);
+    while (j * 16 < T) {
+      if ((j + nw) * 16 < T) load_a(j + nw, a1);
+      tile(j, a0);
+      j += nw;
+      if (j * 16 >= T) break;
+      if ((j + nw) * 16 < T) load_a(j + nw, a0);
+      tile(j, a1);
+      j += nw;
+    }
+    return;
+  }
   for (int j = w; j * 16 < T; j += nw) {
     for (int o0 = 0; o0 < G4; o0 += 16) {
       const f32x4 acc = proj_tile(J, md, 16 * j, o0);
