@@ -222,12 +222,12 @@ class Engine {
     HIP_OK(hipEventCreateWithFlags(&ev_a_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_out_, hipEventDisableTiming));
-    // evaluation tower grid cap: the evaluation branch is within a few us of the training chain
-    // (profiles/r2_knobs_grids.log); 384 measured best on the round-3 tree (profiles/
-    // r3_knobs_grids_single_model.log: 0.2314-0.2319 vs 0.238 ms per driver-argument epoch). Per
-    // job: with G batched models the launch has 2G evaluation jobs, so the per-job grid shrinks
-    // with G (see grid_per_model)
-    eval_gx_ = env_int("DLAP_EVAL_GX", grid_per_model(384, 96, G));
+    // evaluation tower grid cap: with the split epoch graphs the evaluation branch has slack and
+    // its towers start beside the training chain's loss passes; a narrower grid takes fewer CUs
+    // from them -- 224-256 measured best (phase 3 0.1554 vs 0.164 ms at 384, profiles/
+    // r5_knobs_eval_gx.log; 384 was best on the round-3 tree). Per job: with G batched models the
+    // launch has 2G evaluation jobs, so the per-job grid shrinks with G (see grid_per_model)
+    eval_gx_ = env_int("DLAP_EVAL_GX", grid_per_model(256, 64, G));
     zx_eval_ = env_int("DLAP_ZX_EVAL", 1) != 0;
     zx_train_ = env_int("DLAP_ZX_TRAIN", 1) != 0;
     zx_gx_ = std::max(1, env_int("DLAP_ZX_GX", 256));
