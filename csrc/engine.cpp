@@ -979,14 +979,19 @@ class Engine {
     if (phase < 1 || phase > 3) return;
     plan_tr_[phase] = plan_ev_[phase] = true;
     if (phase == 2 || epochs <= 0 || env_int("DLAP_GRAM_PLAN", 1) == 0) return;
-    const double cb = 7.7e-8, cq = 5e-5, cdt = 1.8e-6, cde = 6.6e-6;
+    // costs in us. The training chain's dense loss (period pass, asset pass, metrics, period
+    // backward) over the Gram one: a T N + b T N K (the conditional loss's moment sums), minus
+    // the quadratic forms' cq T^2 -- calibrated on the split-graph pipeline at 600x3000x46:
+    // Gram saves ~12 us per phase-1 epoch and ~26 us per phase-3 epoch (profiles/
+    // r5_knobs_gramplan.log; the round-4 constants made phase 1 dense)
+    const double cb = 7.7e-8, cq = 5e-5, cta = 2.07e-5, ctb = 2.43e-6, cde = 6.6e-6;
     const double K = md_.K;
     const SplitDev& D0 = splits_[0];
     if (D0.set && D0.T > 0) {
       const bool cond = phase == 3;
       const double T = D0.T, N = D0.N;
       const double build = cb * T * T * N * (cond ? K : 1.0);
-      const double save = cdt * T * N * (cond ? K + 1.0 : 1.0) - cq * T * T;
+      const double save = cta * T * N + (cond ? ctb * T * N * K : 0.0) - cq * T * T;
       plan_tr_[phase] = epochs * save > build;
     }
     double build = 0.0, save = 0.0;
