@@ -60,7 +60,7 @@ DLAP_DEV int opaque_zero() {
 // [0] start, [1] weights staged, [2] first tile done, [3] loop done; [4..7] same, last block.
 // [8..12]: fused LSTM + tower forward, workgroup 0: start, recurrence start / end, LSTM body
 // done, publisher done (k_mlp_fwd_rnn).
-__device__ long long g_mlp_ts[16];
+__device__ long long g_mlp_ts[24];   // [16..]: the last evaluation recurrence (fused forward)
 #define MLP_TS(slot) do { \
     if ((threadIdx.x & 255) == 0 && (bx == 0 || bx == gxw - 1) && J.gbits) \
       g_mlp_ts[(bx == 0 ? 0 : 4) + (slot)] = wall_clock64(); } while (0)
@@ -796,8 +796,11 @@ __global__ __launch_bounds__(256, DLAP_FWD_WPS) void k_mlp_fwd_rnn(const MlpJob*
       int* ready = reinterpret_cast<int*>(sx + gls_ready_offset(R.T, md->H));
       for (int i = threadIdx.x; i < (R.T + 15) / 16; i += blockDim.x) ready[i] = 0;
       __syncthreads();
-      if (w == 0) { lstm_gls_body<HM, DPPG, false, false>(R, md, sx, nullptr, nullptr, 0, ready); signal(); }
-      else proj_into_lds(R, md, sx, ready, w - 1, 3);
+      // (timestamps 13-15: the last evaluation recurrence of model 0 -- the test split)
+      const bool tse = blockIdx.y == 0 && (int)blockIdx.x == ne && jobs[0].gbits;
+      if (tse && threadIdx.x == 0) g_mlp_ts[16] = wall_clock64();
+      if (w == 0) { lstm_gls_body<HM, DPPG, false, false>(R, md, sx, nullptr, tse ? g_mlp_ts : nullptr, 16, ready); signal(); }
+      else proj_into_lds(R, md, sx, ready, w - 1, 3, tse && w == 1 ? g_mlp_ts + 20 : nullptr);
       return;
     }
     const auto xg = gp(R.xg);
@@ -1825,7 +1828,7 @@ void launch_mlp_bwd_mom(const MlpJob* jobs, int njobs, int gx, int nslice, int t
 }
 
 std::vector<long long> mlp_timestamps() {
-  std::vector<long long> v(16);
-  HIP_OK(hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(g_mlp_ts), sizeof(long long) * 16));
+  std::vector<long long> v(24);
+  HIP_OK(hipMemcpyFromSymbol(v.data(), HIP_SYMBOL(g_mlp_ts), sizeof(long long) * 24));
   return v;
 }

@@ -119,7 +119,8 @@ DLAP_DEV f32x4 proj_tile(const RnnJob& J, const ModelDesc* md, int t0, int o0) {
 // current one run (ping-pong register sets; the fused forward is at its register limit anyway,
 // so the extra set is free) -- a tile every ~memory round trip per wave instead of a round trip
 // plus the MFMA chain; the same operands and MFMA order as proj_tile.
-DLAP_DEV void proj_into_lds(const RnnJob& J, const ModelDesc* __restrict__ md, float* sx, int* ready, int w, int nw) {
+DLAP_DEV void proj_into_lds(const RnnJob& J, const ModelDesc* __restrict__ md, float* sx, int* ready, int w, int nw,
+                            long long* ts = nullptr) {
   const int T = J.T, G4 = 4 * md->H;
   const int l = threadIdx.x & 63, n = l & 15, kq = l >> 4;
   constexpr int KC = 48;
@@ -154,7 +155,9 @@ DLAP_DEV void proj_into_lds(const RnnJob& J, const ModelDesc* __restrict__ md, f
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       if (l == 0) __hip_atomic_store(ready + j, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (ts && l == 0 && j == w) ts[0] = wall_clock64();               // (timing: first tile done)
     };
+    if (ts && l == 0) ts[1] = wall_clock64();                           // (timing: weights requested)
     int j = w;
     if (j * 16 < T) load_a(j, a0);
     while (j * 16 < T) {

@@ -53,6 +53,10 @@ def main():
             print(f"  fused fwd blk0 : start->recur {um(8, 9):7.1f}  recur {um(9, 10):7.1f}  flush {um(10, 11):7.1f}  "
                   f"publisher-end {um(8, 12):7.1f}  first tower start {(m[0] - m[8]) / 100.0:7.1f}  "
                   f"last tower end {(max(m[3], m[7]) - m[8]) / 100.0:7.1f}")
+            if len(m) > 20 and m[18] > m[17] > 0:
+                print(f"  fused fwd eval : last evaluation WG start {um(8, 16):7.1f}  first tile {um(16, 20):7.1f} "
+                      f"(weights requested {um(16, 21):7.1f})  recurrence start {um(16, 17):7.1f}  recur {um(17, 18):7.1f}  "
+                      f"end {um(8, 18):7.1f} (from blk0 start)")
         lt = np.array(mod.Engine.loss_timestamps(), dtype=np.int64)
         ul = lambda a, b: (lt[b] - lt[a]) / 100.0  # noqa: E731
         print(f"  k_job_metrics  : losses {ul(0, 1):7.1f}  pass0 {ul(1, 2):7.1f}  pass1 {ul(2, 3):7.1f}")
