@@ -585,6 +585,44 @@ DLAP_DEV void lstm_bwd_body(const UpdJob& J, const ModelDesc* __restrict__ md, i
           }
         }
       }
+      // pair maps: the chain advances two steps per link, y_t = N_t y_{t+2} + v_t for the chain
+      // points t = T-1-2p (p = 1 .. np), N_t = M_{t+1} M_{t+2}, v_t = M_{t+1} (dout_{t+1}, 0) +
+      // (dout_t, 0); one thread per (link, row), fixed summation order. The maps N_t need only
+      // the step matrices, so they are formed before the wait for the incoming gradient (fused
+      // tail: while the period blocks publish it); the offsets v_t after it.
+      __syncthreads();
+      const int npair = (T - 1) / 2;
+      constexpr int PU2 = 2;                           // links per pass, reads hoisted (as above)
+      for (int task0 = threadIdx.x; task0 < npair * 8; task0 += 256 * PU2) {
+        f32x4 a0[PU2], a1[PU2], mb[PU2][16];
+#pragma unroll
+        for (int u = 0; u < PU2; ++u) {
+          const int task = min(task0 + 256 * u, npair * 8 - 1);
+          const int p = 1 + (task >> 3), i = task & 7, t = T - 1 - 2 * p;
+          const f32x4* ra = reinterpret_cast<const f32x4*>(s_M + (t + 1) * 64 + 8 * i);
+          a0[u] = ra[0];
+          a1[u] = ra[1];
+          const f32x4* m4 = reinterpret_cast<const f32x4*>(s_M + (t + 2) * 64);
+#pragma unroll
+          for (int k = 0; k < 16; ++k) mb[u][k] = m4[k];
+        }
+#pragma unroll
+        for (int u = 0; u < PU2; ++u) {
+          const int task = task0 + 256 * u;
+          if (task >= npair * 8) break;
+          const int p = 1 + (task >> 3), i = task & 7;
+          const float a[8] = {a0[u][0], a0[u][1], a0[u][2], a0[u][3], a1[u][0], a1[u][1], a1[u][2], a1[u][3]};
+          f32x4 lo = zero4(), hi = zero4();
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            lo = lo + a[k] * mb[u][2 * k];
+            hi = hi + a[k] * mb[u][2 * k + 1];
+          }
+          f32x4* dn = reinterpret_cast<f32x4*>(s_N + (p - 1) * 64 + 8 * i);
+          dn[0] = lo;
+          dn[1] = hi;
+        }
+      }
       if constexpr (FUSED) {
         // the incoming gradient: every period block of this launch has published dpp[t]
         // (write-through stores, drained, then one agent-scope add each). Wave 0 polls the count
@@ -611,24 +649,15 @@ DLAP_DEV void lstm_bwd_body(const UpdJob& J, const ModelDesc* __restrict__ md, i
         RNN_TS(16, tsm);
       }
       __syncthreads();
-      // pair maps: the chain advances two steps per link, y_t = N_t y_{t+2} + v_t for the chain
-      // points t = T-1-2p (p = 1 .. np), N_t = M_{t+1} M_{t+2}, v_t = M_{t+1} (dout_{t+1}, 0) +
-      // (dout_t, 0); one thread per (link, row), fixed summation order
-      const int npair = (T - 1) / 2;
-      constexpr int PU2 = 2;                           // links per pass, reads hoisted (as above)
+      __syncthreads();
       for (int task0 = threadIdx.x; task0 < npair * 8; task0 += 256 * PU2) {
-        f32x4 a0[PU2], a1[PU2], mb[PU2][16], du[PU2];
+        f32x4 a0[PU2], du[PU2];
         float dt[PU2];
 #pragma unroll
         for (int u = 0; u < PU2; ++u) {
           const int task = min(task0 + 256 * u, npair * 8 - 1);
           const int p = 1 + (task >> 3), i = task & 7, t = T - 1 - 2 * p;
-          const f32x4* ra = reinterpret_cast<const f32x4*>(s_M + (t + 1) * 64 + 8 * i);
-          a0[u] = ra[0];
-          a1[u] = ra[1];
-          const f32x4* m4 = reinterpret_cast<const f32x4*>(s_M + (t + 2) * 64);
-#pragma unroll
-          for (int k = 0; k < 16; ++k) mb[u][k] = m4[k];
+          a0[u] = reinterpret_cast<const f32x4*>(s_M + (t + 1) * 64 + 8 * i)[0];
           du[u] = *reinterpret_cast<const f32x4*>(s_d + (t + 1) * 4);
           dt[u] = s_d[t * 4 + (i & 3)];
         }
@@ -637,17 +666,7 @@ DLAP_DEV void lstm_bwd_body(const UpdJob& J, const ModelDesc* __restrict__ md, i
           const int task = task0 + 256 * u;
           if (task >= npair * 8) break;
           const int p = 1 + (task >> 3), i = task & 7;
-          const float a[8] = {a0[u][0], a0[u][1], a0[u][2], a0[u][3], a1[u][0], a1[u][1], a1[u][2], a1[u][3]};
-          f32x4 lo = zero4(), hi = zero4();
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            lo = lo + a[k] * mb[u][2 * k];
-            hi = hi + a[k] * mb[u][2 * k + 1];
-          }
-          f32x4* dn = reinterpret_cast<f32x4*>(s_N + (p - 1) * 64 + 8 * i);
-          dn[0] = lo;
-          dn[1] = hi;
-          float v = a[0] * du[u][0] + a[1] * du[u][1] + a[2] * du[u][2] + a[3] * du[u][3];
+          float v = a0[u][0] * du[u][0] + a0[u][1] * du[u][1] + a0[u][2] * du[u][2] + a0[u][3] * du[u][3];
           if (i < 4) v += dt[u];
           s_v[(p - 1) * 8 + i] = v;
         }
