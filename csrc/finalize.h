@@ -88,6 +88,41 @@ DLAP_DEV void finalize_block(const FinJob& J, const ModelDesc* __restrict__ md, 
   const auto src = gp(mom ? J.v : J.u);
   const int ld = mom ? 64 : D;                        // row stride of v / u
   const int r0 = gp(J.row_ptr)[t], r1 = gp(J.row_ptr)[t + 1];
+  if (!mom && D == 4) {
+    // (the LSTM[4] per-period inputs) one 16-byte load per row: thread k sums rows r0 + k,
+    // r0 + k + 256, ... in order (every load of the period issued before the first add: one
+    // memory round trip for ~4k rows), then fixed xor trees per wave and the waves in order
+    constexpr int RB = 16;
+    const auto u4 = reinterpret_cast<const f32x4*>(&src[0]);
+    f32x4 acc = zero4();
+    for (int c0 = r0; c0 < r1; c0 += 256 * RB) {
+      f32x4 v[RB];
+#pragma unroll
+      for (int k = 0; k < RB; ++k) {
+        const int r = c0 + threadIdx.x + 256 * k;
+        v[k] = r < r1 ? u4[r] : zero4();
+      }
+#pragma unroll
+      for (int k = 0; k < RB; ++k) acc = acc + v[k];
+    }
+    __shared__ f32x4 wred[4];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[c] += __shfl_xor(acc[c], o, 64);
+    if ((threadIdx.x & 63) == 0) wred[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x < 4) {
+      const float tot = ((wred[0][threadIdx.x] + wred[1][threadIdx.x]) + wred[2][threadIdx.x]) + wred[3][threadIdx.x];
+      if (ctr) __hip_atomic_store(gp(J.dpp) + t * 4 + threadIdx.x, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else gp(J.dpp)[t * 4 + threadIdx.x] = tot;
+    }
+    if (ctr && threadIdx.x < 64) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (threadIdx.x == 0) __hip_atomic_fetch_add(ctr, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
   float s = 0.f;
   if (d < D) {
 #pragma unroll 8
