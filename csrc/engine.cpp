@@ -243,7 +243,7 @@ class Engine {
     self_proj_ = env_int("DLAP_SELF_PROJ", 1) != 0;
     tail_adam_ = env_int("DLAP_TAIL_ADAM", 1) != 0;
     split_graphs_ = env_int("DLAP_SPLIT_GRAPHS", 1) != 0;
-    unroll_ = std::max(1, env_int("DLAP_UNROLL", 4));
+    unroll_ = std::max(1, env_int("DLAP_UNROLL", 8));
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
                residual, fp32);
     // fp32 wide path: layer 0 through k_proj0 + the ZIN towers (the fused-layer-0 k_mlp_fwd_zx
@@ -1974,7 +1974,7 @@ class Engine {
   // inside a graph costs ~5-6 us on the chain and a graph that ends on two queues ~12 us at its
   // boundary (profiles/r5_*timeline*); these cost one poll each.
   bool split_graphs_ = true;                 // DLAP_SPLIT_GRAPHS
-  int unroll_ = 4;                           // DLAP_UNROLL: body epochs per split-graph launch
+  int unroll_ = 8;                           // DLAP_UNROLL: body epochs per split-graph launch
   double host_launch_s_ = 0.0;               // host time in the pipelined body launches ...
   long host_launch_n_ = 0;                   // ... over this many epochs (fused_info)
   int* fwd_esig_ = nullptr;                  // set around enqueue_train_grads (enqueue_chain_split)

@@ -186,11 +186,12 @@ def test_split_epoch_graphs_equal_one_graph(big, monkeypatch):
     recurrences, the tail's Adam blocks for the bookkeeping's signal) give the bits of the
     one-graph pipelined epoch, batched models included."""
     cfg = default_cli_config(178, 46)
+    phases = ((1, 11), (2, 2), (3, 10))      # (9-10 body epochs: the unrolled graphs and singles)
     monkeypatch.setenv("DLAP_SPLIT_GRAPHS", "0")
-    e0, ref = _train(big, cfg, [81, 82], 2)
+    e0, ref = _train(big, cfg, [81, 82], 2, phases=phases)
     assert not e0.eng.fused_info()["split_graphs"]
     monkeypatch.setenv("DLAP_SPLIT_GRAPHS", "1")
-    e1, res = _train(big, cfg, [81, 82], 2)
+    e1, res = _train(big, cfg, [81, 82], 2, phases=phases)
     assert e1.eng.fused_info()["split_graphs"]
     for s in (81, 82):
         _same(ref[s], res[s])
