@@ -1012,10 +1012,6 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
 template <class P, int UB>
 DLAP_DEV void to_rows_k(const typename P::Frag (&pf)[2][(UB + 1) / 2], int blk, const typename P::Frag& s0,
                         const typename P::Frag& s1, typename P::Frag& out) {
-#ifdef DLAP_FAKE_TRANSPOSE      // timing experiment only: wrong results
-  out = (blk & 1) ? pf[1][blk >> 1] : pf[0][blk >> 1];
-  return;
-#endif
   const typename P::Frag sel = (blk & 1) ? s1 : s0;
   out = P::pack(P::mma(pf[0][blk >> 1], sel, zero4()), P::mma(pf[1][blk >> 1], sel, zero4()));
 }
@@ -1023,10 +1019,6 @@ DLAP_DEV void to_rows_k(const typename P::Frag (&pf)[2][(UB + 1) / 2], int blk, 
 template <class P>
 DLAP_DEV void x_rows_k(const typename P::Frag& x0, const typename P::Frag& x1, int blk,
                        const typename P::Frag& s0, const typename P::Frag& s1, typename P::Frag& out) {
-#ifdef DLAP_FAKE_TRANSPOSE
-  out = (blk & 1) ? x1 : x0;
-  return;
-#endif
   const typename P::Frag sel = (blk & 1) ? s1 : s0;
   out = P::pack(P::mma(x0, sel, zero4()), P::mma(x1, sel, zero4()));
 }
