@@ -242,6 +242,7 @@ class Engine {
     fused_tail_ = env_int("DLAP_FUSED_TAIL", 1) != 0;
     self_proj_ = env_int("DLAP_SELF_PROJ", 1) != 0;
     tail_adam_ = env_int("DLAP_TAIL_ADAM", 1) != 0;
+    tail_adam_pipe_ = env_int("DLAP_TAIL_ADAM", 1) == 2;
     split_graphs_ = env_int("DLAP_SPLIT_GRAPHS", 1) != 0;
     unroll_ = std::max(1, env_int("DLAP_UNROLL", 8));
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
@@ -328,7 +329,7 @@ class Engine {
     py::dict d;
     d["P"] = md_.P; d["P_sdf"] = md_.P_sdf; d["KP"] = md_.KP; d["KS1"] = md_.KS1; d["WMB"] = md_.WMB;
     d["Dm"] = md_.Dm; d["blob_frags"] = md_.md.blob_frags; d["aux_floats"] = md_.md.aux_floats;
-    d["ntile_s"] = md_.ntile_s; d["tps_s"] = md_.tps_s; d["ntile_m"] = md_.ntile_m; d["G"] = G_;
+    d["ntile_s"] = md_.ntile_s; d["tps_s"] = md_.tps_s; d["tbwd"] = md_.tbwd; d["ntile_m"] = md_.ntile_m; d["G"] = G_;
     d["wide"] = md_.md.wide; d["KX"] = md_.md.KX; d["nsplit"] = nsplit_; d["fp32"] = md_.md.fp32;
     return d;
   }
@@ -843,8 +844,7 @@ class Engine {
       launch_mlp_bwd_mom(as<MlpJob>(dh ? j_mlp_bwd_dh_ : j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_m, 1, md_.md,
                          md_.KS1, md_.WMB, slab_stride(), fpw_, st_);
     else
-      launch_mlp_bwd_sdf(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_s, md_.tps_s, md_.md, md_.KS1,
-                         slab_stride(), fpw_, st_);
+      launch_sdf_bwd(as<MlpJob>(j_mlp_bwd_[phase]));
     if (md_.md.wide)
       launch_wgrad0(as<WideJob>(j_wide_bwd_[phase]), G_, dd(), md_.md, phase == 2, md_.WMB, nsplit_, st_);
     enqueue_train_tail(phase);
@@ -1166,13 +1166,14 @@ class Engine {
     d["eval_gx_solo"] = fused_grid(eval_grid(), n_eval_jobs_, cap_eval_);
     // pipelined epochs with the evaluation recurrences inside the fused training forward
     d["cap_all"] = cap_all_;
+    d["tail_cap"] = tail_cap_;
     for (int ph = 1; ph <= 3; ph += 2) {
       d[("eval_in_fwd_p" + std::to_string(ph)).c_str()] = eval_rnn_in_fwd(ph);
       d[("all_gx_p" + std::to_string(ph)).c_str()] = eval_rnn_in_fwd(ph) ? fused_all_gx(ph) : 0;
     }
     d["eval_per_model"] = ne_per_model();
     d["fused_tail"] = tail_fused(1);
-    d["adam_in_tail"] = adam_in_tail(1) && pipeline_ && eval_rnn_in_fwd(1);
+    d["adam_in_tail"] = adam_in_tail(1) && pipeline_ && eval_rnn_in_fwd(1) && (split_graphs(1) || tail_adam_pipe_);
     d["split_graphs"] = split_graphs(1) && pipeline_;
     d["host_launch_us_per_epoch"] = host_launch_n_ ? 1e6 * host_launch_s_ / host_launch_n_ : 0.0;
     // backward launch shape: fine slabs per model (R-only partition), fine slabs per workgroup
@@ -1367,6 +1368,10 @@ class Engine {
     const char* tps_env = std::getenv("DLAP_TPS");
     const bool tps2 = (wide || d.KS1 == 2) && d.ntile_s == 2 && tps_env && std::atoi(tps_env) == 2;
     d.tps_s = tps2 ? 2 : 1;
+    // the one-pass backward (k_tbwd.hip) where it is instantiated: every gradient tile in one
+    // slice (DLAP_TBWD=0: the sliced kernel, kept for the fp32 / wide / deep / wide-row shapes)
+    d.tbwd = (env_int("DLAP_TBWD", 1) != 0 && tbwd_supported(D, d.KS1) && d.ntile_s == d.nl_s) ? 1 : 0;
+    if (d.tbwd) d.tps_s = d.ntile_s;
     // at least one slice: slice 0 also produces the bias / output / per-period gradients
     d.nslice_s = std::max(1, (d.ntile_s + d.tps_s - 1) / d.tps_s);
     for (int k = 0; k < d.ntile_s; ++k) d.tile_s[k].slice = k / d.tps_s;
@@ -1397,6 +1402,10 @@ class Engine {
       throw std::invalid_argument("compact panel exceeds 4 GiB on the fused layer-0 path");
   }
   int slab_stride() const { return std::max(md_.tps_s, md_.tps_m) * 4096 + SLAB_EXTRA; }
+  void launch_sdf_bwd(const MlpJob* jobs) {
+    if (md_.tbwd) launch_tbwd_sdf(jobs, G_, gx_bwd_, md_.md, slab_stride(), splits_[0].T, st_);
+    else launch_mlp_bwd_sdf(jobs, G_, gx_bwd_, md_.nslice_s, md_.tps_s, md_.md, md_.KS1, slab_stride(), fpw_, st_);
+  }
 
   void alloc_ws(int s) {
     const SplitDev& D = splits_[s];
@@ -1657,6 +1666,17 @@ class Engine {
 
   void rebuild_jobs() {
     HTRACE("rebuild_jobs");
+    // The tail's Adam hand-off derives its launch index from a running arrival count divided by
+    // the launch's block count, which depends on the train split: with the device
+    // quiescent, rearm the running counts so a new split (or any rebuilt job table) starts them
+    // at launch 0 with the bookkeeping signals.
+    sync();
+    if (st2_) HIP_OK(hipStreamSynchronize(st2_));
+    for (ModelState& S : models_) {
+      HIP_LEGACY(hipMemset(S.tail_ctr.p, 0, S.tail_ctr.n * sizeof(int)));
+      HIP_LEGACY(hipMemset(S.upd_ctr.p, 0, S.upd_ctr.n * sizeof(int)));
+    }
+    tail_cap_ = splits_[0].set && lstm_tail_supported(md_, splits_[0].T) ? lstm_tail_capacity(md_, splits_[0].T) : 0;
     for (auto& kv : graphs_) retire_graph_exec(kv.second, st_);
     graphs_.clear();
     fwd_tables_.clear();
@@ -1669,7 +1689,7 @@ class Engine {
         // reduction: 10.58k vs 10.72k model-epochs/s at G = 9, profiles/r4_bwd_shape.log)
       const int want = env_int("DLAP_BWD_FPW", 1);
       const int tps = std::max(md_.tps_s, md_.tps_m);
-      fpw_ = (want == 4 && mlp_bwd_fpw_fits(md_.md, md_.KS1, slab_stride(), tps, 4)) ? 4 : 1;
+      fpw_ = (want == 4 && !md_.tbwd && mlp_bwd_fpw_fits(md_.md, md_.KS1, slab_stride(), tps, 4)) ? 4 : 1;
       gx_bwd_ = nfine_ / fpw_;
     }
     std::vector<RnnJob> rt, re;
@@ -1942,8 +1962,7 @@ class Engine {
         launch_period_bwd(lj, G_, D.T, st_);
       }
       HTRACE("launch_mlp_bwd_sdf");
-      launch_mlp_bwd_sdf(as<MlpJob>(j_mlp_bwd_[phase]), G_, gx_bwd_, md_.nslice_s, md_.tps_s, md_.md, md_.KS1,
-                         slab_stride(), fpw_, st_);
+      launch_sdf_bwd(as<MlpJob>(j_mlp_bwd_[phase]));
     }
     if (md_.md.wide)   // layer-0 weight gradient from the tower's dz fragments
       launch_wgrad0(as<WideJob>(j_wide_bwd_[phase]), G_, dd(), md_.md, phase == 2, md_.WMB, nsplit_, st_);
@@ -1962,9 +1981,19 @@ class Engine {
   // blocks (k_lstm_tail, adam 2) after the evaluation branch's bookkeeping signalled, so the
   // training chain has no join edge and no k_adam launch (the branches join at the graph end)
   bool tail_adam_ = true;                    // DLAP_TAIL_ADAM
+  bool tail_adam_pipe_ = false;              // DLAP_TAIL_ADAM=2: also in the one-graph fallback
   int tail_adam_mode_ = 0;                   // set around enqueue_train_grads (enqueue_pipe)
   float tail_lr_ = 0.f;
-  bool adam_in_tail(int phase) const { return tail_adam_ && tail_fused(phase) && inv_code_.p != nullptr; }
+  // Co-residency guard: the tail's Adam blocks spin, holding their CU slots, until the
+  // evaluation branch signals; G * nadam of them must leave at least half of the device's tail-sized
+  // slots (occupancy query, tail_cap_) to the evaluation launches they wait for, else the epoch
+  // keeps the join + k_adam update.
+  bool adam_in_tail(int phase) const {
+    if (!(tail_adam_ && tail_fused(phase) && inv_code_.p != nullptr)) return false;
+    const int nadam = (md_.P_sdf + ADAM_PB - 1) / ADAM_PB;
+    return tail_cap_ > 0 && 2 * G_ * nadam <= tail_cap_;
+  }
+  int tail_cap_ = 0;                         // k_lstm_tail workgroups resident at once (rebuild_jobs)
   // Split epoch graphs (the pipelined eval-in-forward epoch with the update in the tail): the
   // training chain is one single-queue graph on st_ (fused forward -> losses -> tower backward ->
   // tail + Adam) and the evaluation branch another on st2_ (k_wait_count -> evaluation towers ->
@@ -2090,7 +2119,10 @@ class Engine {
       // evaluation branch forks after it: towers, losses, the bookkeeping and the next epoch's
       // dropout masks, beside the training backward and its tail (which computes the train
       // split's metrics)
-      const bool ta = adam_in_tail(phase);
+      // (the one-graph fallback keeps the join + k_adam update unless DLAP_TAIL_ADAM=2: an
+      // in-kernel wait across the graph's two branches would rest on the runtime mapping them
+      // to different hardware queues -- ADVICE r5)
+      const bool ta = tail_adam_pipe_ && adam_in_tail(phase);
       tail_metrics_ = true;
       tail_adam_mode_ = ta ? 2 : 0;
       tail_lr_ = lr;
@@ -2289,6 +2321,7 @@ PYBIND11_MODULE(_dlap_hip, m) {
       .def("capture_seconds", [](Engine& e) { return e.capture_seconds(); })
       .def_static("loss_timestamps", []() { return loss_timestamps(); })
       .def_static("mlp_timestamps", []() { return mlp_timestamps(); })
+      .def_static("tbwd_timestamps", []() { return tbwd_timestamps(); })
       .def("forward_split", &Engine::forward_split, py::arg("s"), py::arg("train_mode"), py::arg("do_mom"),
            py::arg("wait") = true)
       .def("train_step", &Engine::train_step)

@@ -50,7 +50,16 @@ DLAP_DEV void finalize_block(const FinJob& J, const ModelDesc* __restrict__ md, 
   if (b < nb_tiles) {
     const int ti = b >> 6, e = ((b & 63) << 6) + lane;
     const GradTile& G = mom ? md->tile_m[ti] : md->tile_s[ti];
-    const int o = e >> 6, i = (e & 63) + 64 * G.chunk;
+    // slab position e of the tile: natural (o, i) = (e >> 6, e & 63), or (the one-pass SDF backward,
+    // k_tbwd.hip) the MFMA accumulator layout -- e = ((4u + v) * 64 + 16 q + n) * 4 + r holds
+    // (o, i) = (16u + 4q + r, 16v + n) -- read lane-contiguously either way
+    int o = e >> 6, i = e & 63;
+    if (!mom && md->tbwd) {
+      const int r = e & 3, l = (e >> 2) & 63, uv = e >> 8;
+      o = 16 * (uv >> 2) + 4 * (l >> 4) + r;
+      i = 16 * (uv & 3) + (l & 15);
+    }
+    i += 64 * G.chunk;
     const int tpos = ti - G.slice * tps;
     const float v = slab_sum(J.slab + (size_t)G.slice * J.nslab * slab_stride + tpos * 4096 + e);
     bool ok = o < G.out && i < G.in;

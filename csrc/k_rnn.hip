@@ -1269,6 +1269,14 @@ bool lstm_tail_supported(const ModelDesc& mh, int T) {
   return lstm_tail_lds_bytes(T, mh.H) + 6400 <= 80 * 1024;   // (+ static LDS) two per CU
 }
 int lstm_tail_words() { return TAIL_WORDS; }
+int lstm_tail_capacity(const ModelDesc& mh, int T) {
+  const size_t sh = std::max(lstm_tail_lds_bytes(T, mh.H), (size_t)(DLAP_MAX_T + 4) * sizeof(float));
+  int per_cu = 0, dev = 0, ncu = 0;
+  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lstm_tail, 256, sh));
+  HIP_OK(hipGetDevice(&dev));
+  HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  return per_cu * ncu;
+}
 void launch_lstm_tail(const UpdJob* ujobs, const FinJob* fjobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
                       int T, int slab_stride, hipStream_t st, const LossJob* ljobs, int adam, float lr) {
   const int nslab_blocks = mh.ntile_s * 64 + (SLAB_EXTRA + 63) / 64;

@@ -56,6 +56,8 @@ struct ModelDesc {
   // gradient reduction tables (phase-specific tower)
   int ntile_s, ntile_m, nslice_s, nslice_m;
   int tps_s, tps_m;        // gradient tiles accumulated per backward slice
+  int tbwd;                 // 1: the SDF backward is the one-pass k_tbwd_sdf (k_tbwd.hip; one slice,
+                            //   tps_s = ntile_s), else the sliced k_mlp_bwd_sdf
   // input-projection matrix re-packed by k_pack for k_proj: wproj[MP + 2][NP] fp32, row m < M =
   // column m of [W_ih(layer 0) ; W_m0[:, :M]], row MP = (b_ih ; b_m0), row MP + 1 = (b_hh ; 0)
   int proj_mp, proj_np;

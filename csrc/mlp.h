@@ -127,4 +127,12 @@ void launch_dropmask(const MlpJob* jobs, int njobs, int ntiles, const MlpDims& D
 void launch_mlp_bwd_mom(const MlpJob* jobs, int njobs, int gx, int nslice, int tps, const MlpDims& D,
                         int KS1, int WMB, int slab_stride, int fpw, hipStream_t st);
 
+// one-pass SDF backward (k_tbwd.hip): every layer's weight gradient from one forward recompute per
+// tile, one wave per SIMD, grid (gx = fine slabs, jobs); the slabs of a one-slice k_mlp_bwd_sdf
+// with tps = nl_sdf, T = the train split's length (its per-period inputs are staged in LDS)
+bool tbwd_supported(const MlpDims& D, int KS1);
+// (weight tiles in the MFMA accumulator layout: k_finalize maps them when ModelDesc::tbwd)
+void launch_tbwd_sdf(const MlpJob* jobs, int njobs, int gx, const MlpDims& D, int slab_stride, int T, hipStream_t st);
+std::vector<long long> tbwd_timestamps();
+
 std::vector<long long> mlp_timestamps();

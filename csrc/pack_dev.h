@@ -190,7 +190,6 @@ DLAP_DEV void pack_store(const UpdJob& J, const ModelDesc* __restrict__ md, cons
 
 
 // ============================================================ clip + Adam ===============
-#define ADAM_PB 1024
 // One Adam block's share of the phase's update (k_adam, and the Adam blocks of the fused
 // backward tail): the clip-by-global-norm scope norm -- reduced in full by every block in a
 // fixed order, so it is the same value in all of them -- then parameters

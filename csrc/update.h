@@ -5,6 +5,7 @@
 struct ModelDesc;
 
 #define PACK_FAN 4
+#define ADAM_PB 1024          // parameters per Adam block (adam_block, k_adam, the tail's Adam blocks)
 // hand-off words of the fused backward tail (UpdJob::tail_ctr, 128 bytes apart): the per-period
 // sums published, the gate-gradient flag, the W_ih blocks done, the blocks arrived (Adam in the
 // tail, a running count) and the evaluation branch's signals (a running count)
@@ -108,6 +109,8 @@ void launch_lstm_bwd(const UpdJob* jobs, int njobs, const ModelDesc* md, const M
 // fused backward tail of phases 1 / 3: k_finalize + k_lstm_bwd + k_wgrad as one launch (k_rnn.hip)
 bool lstm_tail_supported(const ModelDesc& mh, int T);
 int lstm_tail_words();     // ints of UpdJob::tail_ctr (hand-off words, 128 bytes apart)
+// workgroups of k_lstm_tail the device holds at once (occupancy query x CUs) at split length T
+int lstm_tail_capacity(const ModelDesc& mh, int T);
 struct LossJob;
 // ljobs: the train split's loss jobs whose job metrics one more block per model computes (or nullptr)
 // adam: 0 = none (k_adam follows); 2 = the update runs in the tail (the launch's last blocks,

@@ -72,7 +72,9 @@ def variant_path(variant: str) -> Path:
 # runs: k_mlp.hip with "-mllvm -amdgpu-mfma-vgpr-form" (MFMA results in VGPRs instead of the
 # accumulator file: half the v_accvgpr_read moves in the tower backward) ran within noise of
 # the default (3954/3999 vs 3990/3972 model-epochs/s, profiles/README.md).
-FILE_FLAGS: dict = {}
+# k_tbwd.hip: the builtin MFMAs in VGPR form (the forward / chain layer results feed VALU work
+# without accumulator-file moves); its long-lived weight-gradient sums are pinned to AGPRs by asm.
+FILE_FLAGS: dict = {"k_tbwd.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
 def build(force: bool = False, jobs: int = 8, verbose: bool = True, ubsan: bool = False,

@@ -173,7 +173,11 @@ def test_adam_in_tail_equals_k_adam(big, monkeypatch):
     monkeypatch.setenv("DLAP_TAIL_ADAM", "0")
     e0, ref = _train(big, cfg, [71, 72], 2)
     assert not e0.eng.fused_info()["adam_in_tail"]
+    # (the one-graph fallback runs the update in the tail only on request: DLAP_TAIL_ADAM=2)
     monkeypatch.setenv("DLAP_TAIL_ADAM", "1")
+    e1, _ = _train(big, cfg, [71, 72], 2, phases=((1, 2),))
+    assert not e1.eng.fused_info()["adam_in_tail"]
+    monkeypatch.setenv("DLAP_TAIL_ADAM", "2")
     e1, res = _train(big, cfg, [71, 72], 2)
     assert e1.eng.fused_info()["adam_in_tail"]
     for s in (71, 72):
@@ -273,3 +277,86 @@ def test_fused_wait_give_up_poisons_the_model(monkeypatch):
     with pytest.raises(RuntimeError, match="spin wait gave up"):
         train_3phase_gpu(cfg, b, b, b, num_epochs_unc=4, num_epochs_moment=1, num_epochs=2, print_freq=2,
                          ignore_epoch=0, verbose=False, seed=3)
+
+
+def test_tail_adam_handoff_survives_a_new_train_split(big, monkeypatch):
+    """The tail's Adam hand-off derives its launch index from running counts divided by the
+    launch's block count, which depends on the train split: pipelined epochs, then
+    set_data with a shorter train split, then more epochs on the same engine -- the bits of the
+    join + k_adam engine doing the same (no running counts)."""
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import GANEngine
+    cfg = default_cli_config(178, 46)
+    tr, va, te = big
+    tr2 = {k: v[:200].contiguous() for k, v in tr.items()}
+
+    def run(tail_adam):
+        monkeypatch.setenv("DLAP_TAIL_ADAM", tail_adam)
+        eng = GANEngine(AssetPricingGAN(cfg).spec, 2, max_epochs=64)
+        eng.set_data(tr, va, te)
+        for g, s in enumerate((91, 92)):
+            torch.manual_seed(1000 + s)
+            eng.set_model(g, AssetPricingGAN(cfg), s)
+        eng.eng.begin_phase(1)
+        eng.run(1, 11, 1e-3, 1, 1.0, True)
+        eng.set_data(tr2, va, te)
+        eng.eng.begin_phase(1)
+        eng.run(1, 10, 1e-3, 1, 1.0, True)
+        eng.eng.sync()
+        assert eng.eng.prog_timeouts() == 0
+        return eng, [(eng.params(g), np.nan_to_num(eng.history_rows(g), nan=-7.0)) for g in range(2)]
+
+    e1, res = run("1")
+    assert e1.eng.fused_info()["adam_in_tail"]
+    _, ref = run("0")
+    for a, b in zip(res, ref):
+        _same(a, b)
+
+
+def test_concurrent_engines_split_graphs_no_giveups(big):
+    """Three live engines running split-graph epochs at the same time from three threads (the
+    engine releases the GIL) beside a busy torch stream: no in-kernel wait gives up, and every
+    member has the bits of its solo run (the evaluation queue of each engine is its
+    own CU-masked stream, the runtime's queue pooling cannot put one engine's waits in front of
+    the work they wait for)."""
+    import threading
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import GANEngine
+    cfg = default_cli_config(178, 46)
+    seeds = (101, 102, 103)
+    phases = ((1, 9), (3, 9))
+    _, solo = zip(*[_train(big, cfg, [s], 1, phases=phases) for s in seeds])
+    engs = []
+    for s in seeds:
+        eng = GANEngine(AssetPricingGAN(cfg).spec, 1, max_epochs=64)
+        eng.set_data(*big)
+        torch.manual_seed(1000 + s)
+        eng.set_model(0, AssetPricingGAN(cfg), s)
+        assert eng.eng.fused_info()["split_graphs"]
+        engs.append(eng)
+    errs = []
+
+    def work(eng):
+        try:
+            for ph, n in phases:
+                eng.eng.begin_phase(ph)
+                eng.run(ph, n, 1e-3, 1, 1.0, True)
+            eng.eng.sync()
+        except Exception as e:          # pragma: no cover - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(e,)) for e in engs]
+    x = torch.randn(2048, 2048, device="cuda")
+    side = torch.cuda.Stream()
+    for t in th:
+        t.start()
+    with torch.cuda.stream(side):        # a busy torch stream beside the three engines
+        for _ in range(40):
+            x = torch.tanh(x @ x * 1e-3)
+    for t in th:
+        t.join()
+    torch.cuda.synchronize()
+    assert not errs, errs
+    for eng, s, ref in zip(engs, seeds, solo):
+        assert eng.eng.prog_timeouts() == 0
+        out = (eng.params(0), np.nan_to_num(eng.history_rows(0), nan=-7.0), eng.params(0, "sharpe"),
+               eng.params(0, "loss"))
+        _same(ref[s], out)
