@@ -1932,7 +1932,7 @@ class Engine {
                      md_.WMB, st_, !train_mom(phase));
     if (mark == 2) HIP_OK(hipEventRecord(ev_a_, st_));
     HTRACE("launch_period_fwd");
-    launch_period_fwd(lj, G_, D.T, st_);
+    launch_period_fwd(lj, G_, D.T, st_, false);
     if (!gram) {
       HTRACE("launch_asset");
       launch_asset(lj, G_, D.N, md_.K, st_, asset_full_default());
@@ -2078,7 +2078,7 @@ class Engine {
     const bool eg = eval_gram_now();
     const LossJob* le = as<LossJob>(eg ? j_loss_eval_ : j_loss_eval_dense_);
     HTRACE("launch_period_fwd");
-    launch_period_fwd(le, n_eval_jobs_, tmax_eval_, st);
+    launch_period_fwd(le, n_eval_jobs_, tmax_eval_, st, false);
     if (eg) {                        // quadratic-form terms per period (no asset passes)
       HTRACE("launch_period_bwd(eval)");
       launch_period_bwd(le, n_eval_jobs_, tmax_eval_, st);

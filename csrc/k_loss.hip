@@ -32,7 +32,10 @@ __device__ long long g_loss_ts[4];
 // before any use -- one memory round trip instead of one per strided iteration.
 #define PER_NT 512
 #define PER_RB 8
-__global__ __launch_bounds__(PER_NT) void k_period_fwd(const LossJob* __restrict__ jobs) {
+// store_wn: also write the zero-mean weights w' into the dense [T][N] wn (read only by the host-side
+// consumers -- evaluate, the module API, the ensemble export -- never by the epoch's own kernels:
+// the epoch graphs skip the scattered stores)
+__global__ __launch_bounds__(PER_NT) void k_period_fwd(const LossJob* __restrict__ jobs, int store_wn) {
   const LossJob& J = jobs[blockIdx.y];
   const int t = blockIdx.x;
   // the fused forward that produced w has finished (stream order): rearm its progress counter
@@ -72,7 +75,7 @@ __global__ __launch_bounds__(PER_NT) void k_period_fwd(const LossJob* __restrict
     for (int k = 0; k < PER_RB; ++k) {
       if (r0 + (int)threadIdx.x + PER_NT * k >= r1) continue;
       const float v = wv[k] - mu;
-      wn[iv[k]] = v;
+      if (store_wn) wn[iv[k]] = v;
       s_wr += v * rv[k];
       s_abs += fabsf(v);
       s_ww += v * v;
@@ -107,7 +110,7 @@ __global__ __launch_bounds__(PER_NT) void k_period_fwd(const LossJob* __restrict
       for (int k = 0; k < PER_RB; ++k) {
         if (c0 + (int)threadIdx.x + PER_NT * k >= r1) continue;
         const float v = wv[k] - mu;
-        wn[iv[k]] = v;
+        if (store_wn) wn[iv[k]] = v;
         s_wr += v * rv[k];
         s_abs += fabsf(v);
         s_ww += v * v;
@@ -533,8 +536,8 @@ std::vector<long long> loss_timestamps() {
 }
 
 // ---------------------------------------------------------------- launchers ------------
-void launch_period_fwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st) {
-  hipLaunchKernelGGL(k_period_fwd, dim3(tmax, njobs), dim3(PER_NT), 0, st, jobs);
+void launch_period_fwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st, bool store_wn) {
+  hipLaunchKernelGGL(k_period_fwd, dim3(tmax, njobs), dim3(PER_NT), 0, st, jobs, (int)store_wn);
   HIP_OK(hipGetLastError());
 }
 bool asset_full_default() {

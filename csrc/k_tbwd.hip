@@ -405,7 +405,7 @@ template <int NL>
 __global__ __launch_bounds__(256, 1) void k_tbwd_sdf(const MlpJob* __restrict__ jobs, MlpDims D, int slab_stride) {
   using P = PrecBF16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  const MlpJob& J = jobs[blockIdx.y];
+  const MlpJob J = jobs[blockIdx.y];   // (by value: one batch of scalar loads, not one per field)
   bf16x8* lds = reinterpret_cast<bf16x8*>(smem);
   float* aux = aux_lds_ptr(smem, D);
   float* spp = pp_lds_ptr(smem, D);
@@ -429,13 +429,19 @@ __global__ __launch_bounds__(256, 1) void k_tbwd_sdf(const MlpJob* __restrict__ 
   for (int u = 0; u < 4; ++u) { S.gb[u] = zero4(); S.gwo[u] = zero4(); }
   S.gbo = 0.f;
   // prologue: the first two tiles' loads and the step counter in flight with the weight staging
+  // prologue: ONE memory round trip -- the step counter, the first two tiles' loads and their keep
+  // words of both parity halves (the step's half is not known before the counter arrives) are all
+  // in flight with the weight staging, whose drain waits for every one of them; nothing uses the
+  // counter before that
+  // (the counter's load is unconditional -- a null-checked load in a branch would be waited for at
+  // the join -- and its value is first used after the staging)
+  uint32_t stp_raw = *gp(J.step ? reinterpret_cast<const uint32_t*>(J.step)
+                                : reinterpret_cast<const uint32_t*>(J.rowti));
   TileIn<P, 2> s0, s1, s2;
   uint32_t k0[NL], k1[NL], k2[NL];
   if (t0 < ntiles) issue_tile<P, 2, true>(J, t0, s0);
   if (t0 + stride < ntiles) issue_tile<P, 2, true>(J, t0 + stride, s1);
-  // keep words of this step (k_dropmask): the step's parity half is not known before the step
-  // counter arrives, so the first two tiles' words of both halves are in flight with it
-  const bool pre = J.gbits && J.train && J.dropout > 0.f;
+  const bool pre = J.gbits && J.train && J.dropout > 0.f;   // keep words of this step (k_dropmask)
   const DLAP_GLOBAL uint32_t* gb0 = pre ? gp(J.gbits) : nullptr;
   const DLAP_GLOBAL uint32_t* gb1 = pre ? gp(J.gbits) + J.gb_half : nullptr;
   uint32_t a0[NL], a1[NL];
@@ -443,13 +449,14 @@ __global__ __launch_bounds__(256, 1) void k_tbwd_sdf(const MlpJob* __restrict__ 
   tb_issue_kw<NL>(gb0, t0 + stride, ntiles, k1);
   tb_issue_kw<NL>(gb1, t0, ntiles, a0);
   tb_issue_kw<NL>(gb1, t0 + stride, ntiles, a1);
-  const uint32_t stp = load_step(J);
+  stage_weights<P>(J, D, lds, aux, spp);
+  asm volatile("" : "+v"(stp_raw));         // (its wave-uniform copy is taken here, not at the load)
+  const uint32_t stp = J.step ? stp_raw : 0u;
   const DLAP_GLOBAL uint32_t* gbase = (stp & 1u) ? gb1 : gb0;
   if (stp & 1u) {
 #pragma unroll
     for (int l = 0; l < NL; ++l) { k0[l] = a0[l]; k1[l] = a1[l]; }
   }
-  stage_weights<P>(J, D, lds, aux, spp);
   const TbW<NL, kTbRes<NL>> W(lds, D);
   if (tsb) g_tb_ts[tso + 1] = wall_clock64();
   // tile loop: the tile two ahead is issued, then the current one runs; the slots rotate by register

@@ -74,7 +74,8 @@ size_t gram_part_doubles(int T, int njobs);
 // all jobs of one launch share T (one split of every model)
 void launch_gram(const GramJob* jobs, int njobs, int T, int nslice, hipStream_t st);
 
-void launch_period_fwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st);
+// store_wn = false: the epoch graphs (nothing in the epoch reads the dense zero-mean weights)
+void launch_period_fwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st, bool store_wn = true);
 // kmax: the moment count K of the jobs (sizes the output grid of the reduction pass)
 // full: the one-pass k_asset_full (training jobs: fewer launches on the critical chain; the
 // jobs must have been built with asset_full = 1), else k_asset_part + k_asset_red (evaluation
