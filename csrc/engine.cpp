@@ -134,6 +134,7 @@ struct DevBuf {
 struct SplitDev {
   int T = 0, N = 0, R = 0;
   float Nbar = 0.f;
+  float Nnorm = 0.f;                 // cross-sectional sharding: the global stock count (0: N)
   DevBuf<uint16_t> X;
   DevBuf<int> rowti, row_ptr;        // rowti: [R] (t, i) int2
   DevBuf<float> Rm, mask, invNt, Nt, meanR, RR, invT, macro, Rc;
@@ -155,6 +156,7 @@ struct ModelSplitWS {   // per (model, split)
   DevBuf<float> dhx;          // train split, module API: external dL/dh [T*N][K] (lazy)
   DevBuf<double> gram;        // Gram mode: [2][T][T] Gc, Gu of the frozen moments (k_gram.hip)
   DevBuf<double> gpart;       // Gram mode: [T][2] per-period quadratic-form terms
+  DevBuf<float> xs;           // sharded engine: [4][T] per-period partial sums + [2] loss sums
 };
 
 struct ModelState {
@@ -677,7 +679,7 @@ class Engine {
       explicit GramScope(bool& x) : f(x) { f = true; }
       ~GramScope() { f = false; }
     } gram_scope(gram_run_);
-    if (!use_graph) {
+    if (!use_graph || xs_on_) {          // (sharded: the hooks' collectives are enqueued per epoch)
       for (int e = 0; e < n; ++e) enqueue_epoch(phase, lr, ignore_epoch, sel);
       return;
     }
@@ -978,7 +980,7 @@ class Engine {
   void plan_phase(int phase, int epochs) {
     if (phase < 1 || phase > 3) return;
     plan_tr_[phase] = plan_ev_[phase] = true;
-    if (phase == 2 || epochs <= 0 || env_int("DLAP_GRAM_PLAN", 1) == 0) return;
+    if (phase == 2 || epochs <= 0 || xs_on_ || env_int("DLAP_GRAM_PLAN", 1) == 0) return;
     // costs in us. The training chain's dense loss (period pass, asset pass, metrics, period
     // backward) over the Gram one: a T N + b T N K (the conditional loss's moment sums), minus
     // the quadratic forms' cq T^2 -- calibrated on the split-graph pipeline at 600x3000x46:
@@ -1022,6 +1024,55 @@ class Engine {
   }
   uintptr_t stream() const { return (uintptr_t)st_; }
 
+  // ---- cross-sectional sharding on the engine (parallel/xsection.py XSEngine) -------------
+  // The engine holds ONE rank's stocks. At every cross-sectional coupling of the epoch it calls
+  // `hook(what, which, stream)` (GIL taken; the host is enqueueing, nothing waits) so the caller
+  // sums the named rank-local buffers over the ranks, ordered on `stream` (torch.distributed):
+  //   "sums1" / "sums2"  per-period sums of the period pass (ws "xs" rows 0 / 1..3) of the splits
+  //                      in the bitmask `which` (1: train, 6: valid + test, 1 << s: one split);
+  //   "loss"             the dense asset passes' loss sums (ws "xs" [4T, 4T + 2));
+  //   "gram"             the Gram matrices (ws "gram", fp64 [2][T][T]) of split mask `which`;
+  //   "grads"            (which = phase) the flat gradient vector and the per-period input
+  //                      gradients (ws "dpp" [T][Dm], phase 2: "dab" [T][64]) of the train split.
+  // Everything else is computed redundantly from the summed values (replicated parameters, LSTM,
+  // quadratic forms, Adam). Pipelined / split epoch graphs and the fused tail are off; phases 1
+  // and 3 use the Gram-form losses (no per-epoch loss all-reduce at all).
+  void set_xs(py::object hook) {
+    xs_on_ = !hook.is_none();
+    xs_hook_ = hook;
+    if (xs_on_) pipeline_ = false;
+    fwd_tables_.clear();
+    graphs_dirty_ = true;
+  }
+  // the global per-period constants of split s (device float [T] arrays of the caller, read on
+  // the engine stream after join_from): N_t, 1/max(N_t, 1), mean R, sum R^2; Nbar; N (all ranks)
+  void xs_set_globals(int s, uintptr_t Nt, uintptr_t invNt, uintptr_t meanR, uintptr_t RR, float Nbar, float Nnorm) {
+    SplitDev& D = splits_[s];
+    if (!D.set) throw std::runtime_error("split not set");
+    const size_t b = (size_t)D.T * sizeof(float);
+    HIP_OK(hipMemcpyAsync(D.Nt.p, reinterpret_cast<const void*>(Nt), b, hipMemcpyDeviceToDevice, st_));
+    HIP_OK(hipMemcpyAsync(D.invNt.p, reinterpret_cast<const void*>(invNt), b, hipMemcpyDeviceToDevice, st_));
+    HIP_OK(hipMemcpyAsync(D.meanR.p, reinterpret_cast<const void*>(meanR), b, hipMemcpyDeviceToDevice, st_));
+    HIP_OK(hipMemcpyAsync(D.RR.p, reinterpret_cast<const void*>(RR), b, hipMemcpyDeviceToDevice, st_));
+    D.Nbar = Nbar;
+    D.Nnorm = Nnorm;
+    fwd_tables_.clear();
+    graphs_dirty_ = true;
+  }
+  // device pointer + element count of a workspace buffer (the hook's all-reduce operands)
+  py::tuple ws_ptr(int g, int s, const std::string& name) {
+    ModelSplitWS& W = ws(check_g(g), s);
+    if (name == "xs") return py::make_tuple((uintptr_t)W.xs.p, W.xs.n);
+    if (name == "gram") return py::make_tuple((uintptr_t)W.gram.p, W.gram.n);
+    if (name == "dpp") return py::make_tuple((uintptr_t)W.dpp.p, W.dpp.n);
+    if (name == "dab") return py::make_tuple((uintptr_t)W.dab.p, W.dab.n);
+    throw std::invalid_argument("ws_ptr: unknown buffer " + name);
+  }
+  py::tuple grads_ptr(int g) {
+    ModelState& S = models_[check_g(g)];
+    return py::make_tuple((uintptr_t)S.grads.p, S.grads.n);
+  }
+
  private:
   int G_, max_epochs_;
   hipStream_t st_ = nullptr;
@@ -1062,6 +1113,22 @@ class Engine {
   DevBuf<char> j_loss_gram_[4];              // phase training loss jobs in Gram mode (epoch graphs)
   bool gram_valid_[3] = {false, false, false};   // G of split s matches the cached moments
   bool gram_run_ = false;                    // inside run_epochs (epoch graphs use Gram mode)
+  bool xs_on_ = false;                       // cross-sectional sharding hooks (set_xs)
+  py::object xs_hook_;
+  void xs_call(const char* what, int which, hipStream_t st) {
+    if (!xs_on_) return;
+    py::gil_scoped_acquire gil;
+    xs_hook_(std::string(what), which, (uintptr_t)st);
+  }
+  // the period pass, as three launches around the ranks' sums when sharded (loss.h)
+  void period_fwd(const LossJob* lj, int njobs, int tmax, hipStream_t st, bool store_wn, int which) {
+    if (!xs_on_) { launch_period_fwd(lj, njobs, tmax, st, store_wn); return; }
+    launch_period_fwd(lj, njobs, tmax, st, store_wn, 1);
+    xs_call("sums1", which, st);
+    launch_period_fwd(lj, njobs, tmax, st, store_wn, 2);
+    xs_call("sums2", which, st);
+    launch_period_fwd(lj, njobs, tmax, st, store_wn, 3);
+  }
   // Dense or Gram losses per phase (plan_phase): a Gram build pays off only over enough epochs
   int cur_phase_ = 0;                        // phase of the run being enqueued
   bool plan_tr_[4] = {true, true, true, true}, plan_ev_[4] = {true, true, true, true};
@@ -1423,6 +1490,7 @@ class Engine {
       W.pe.alloc((size_t)DLAP_TCH * N * K); W.pu.alloc((size_t)DLAP_TCH * N);
       W.scal.alloc(SC_NSCAL);
       W.gram.alloc((size_t)2 * T * T); W.gpart.alloc((size_t)2 * std::max(T, 1));
+      W.xs.alloc((size_t)4 * T + 8);
       W.h0.alloc((size_t)std::max(md_.nrnn * H, 1)); W.c0.alloc((size_t)std::max(md_.nrnn * H, 1));
       if (s == 0) { W.dh0.alloc((size_t)std::max(md_.nrnn * H, 1)); W.dc0.alloc((size_t)std::max(md_.nrnn * H, 1)); }
       if (s == 0) W.scal_prev.alloc(SC_NSCAL);
@@ -1580,9 +1648,12 @@ class Engine {
     J.normalize = md_.normalize_w; J.weighted = md_.weighted_loss; J.phase = phase;
     J.res_factor = md_.residual_factor;
     J.asset_full = (phase > 0 && asset_full_default()) ? 1 : 0;   // training jobs only
-    const float kn = (float)md_.K * (float)D.N;
+    const float nn = D.Nnorm > 0.f ? D.Nnorm : (float)D.N;   // (sharded: every rank's stocks)
+    const float kn = (float)md_.K * nn;
     J.coef_c = phase == 3 ? 2.f / kn : (phase == 2 ? -2.f / kn : 0.f);
-    J.coef_u = phase == 1 ? 2.f / (float)D.N : 0.f;
+    J.coef_u = phase == 1 ? 2.f / nn : 0.f;
+    J.Nnorm = nn;
+    J.xs = xs_on_ ? W.xs.p : nullptr;
     J.w = W.w.p; J.wn = W.wn.p; J.h = phase == 1 ? nullptr : W.h.p;
     J.P = W.P.p; J.port = phase == 0 ? W.port.p : nullptr; J.sdfv = W.sdf.p;
     J.E = W.E.p; J.Eu = W.Eu.p;
@@ -1654,6 +1725,7 @@ class Engine {
       }
       HTRACE("launch_gram split=%d", s);
       launch_gram(as<GramJob>(j_gram_[s]), G_, D.T, gram_slices(D.T), st);
+      xs_call("gram", 1 << s, st);         // sharded: G summed over every rank's stocks
     }
     if (eval_gram_pending_) HIP_OK(hipEventRecord(ev_gram_, st2_));
   }
@@ -1932,10 +2004,13 @@ class Engine {
                      md_.WMB, st_, !train_mom(phase));
     if (mark == 2) HIP_OK(hipEventRecord(ev_a_, st_));
     HTRACE("launch_period_fwd");
-    launch_period_fwd(lj, G_, D.T, st_, false);
+    period_fwd(lj, G_, D.T, st_, false, 1);
     if (!gram) {
+      if (xs_on_ && phase != 2)
+        throw std::runtime_error("sharded engine: phases 1 / 3 need the Gram-form losses (K % 4 == 0, cached moments)");
       HTRACE("launch_asset");
       launch_asset(lj, G_, D.N, md_.K, st_, asset_full_default());
+      if (xs_on_) { launch_xs_loss_sums(lj, G_, st_); xs_call("loss", 1, st_); }
     } else {
       // Gram mode: the quadratic-form loss terms and dL/dw come from one per-period pass, which
       // the job metrics (the loss values) then read
@@ -1975,7 +2050,7 @@ class Engine {
   // the evaluation branch, so the training chain forks only once (after the fused forward)
   bool tail_metrics_ = false;
   bool tail_fused(int phase) const {
-    return fused_tail_ && phase != 2 && splits_[0].set && lstm_tail_supported(md_, splits_[0].T);
+    return fused_tail_ && !xs_on_ && phase != 2 && splits_[0].set && lstm_tail_supported(md_, splits_[0].T);
   }
   // the pipelined eval-in-forward epoch: the clip + Adam update runs in the backward tail's last
   // blocks (k_lstm_tail, adam 2) after the evaluation branch's bookkeeping signalled, so the
@@ -2039,6 +2114,9 @@ class Engine {
     if (lm) launch_job_metrics(lm, G_, st_);
     HTRACE("launch_finalize");
     launch_finalize(as<FinJob>(j_fin_), G_, dd(), md_, phase, slab_stride(), D.T, st_);
+    // sharded: the rank-local tower gradients and per-period input gradients (dpp, or phase 2's
+    // dab) summed over the ranks before the replicated LSTM backward / moment macro columns
+    xs_call("grads", phase, st_);
     HTRACE("launch_lstm_bwd");
     launch_lstm_bwd(as<UpdJob>(j_upd_), G_, dd(), md_, D.T, phase, st_);
   }
@@ -2078,13 +2156,14 @@ class Engine {
     const bool eg = eval_gram_now();
     const LossJob* le = as<LossJob>(eg ? j_loss_eval_ : j_loss_eval_dense_);
     HTRACE("launch_period_fwd");
-    launch_period_fwd(le, n_eval_jobs_, tmax_eval_, st, false);
+    period_fwd(le, n_eval_jobs_, tmax_eval_, st, false, 6);
     if (eg) {                        // quadratic-form terms per period (no asset passes)
       HTRACE("launch_period_bwd(eval)");
       launch_period_bwd(le, n_eval_jobs_, tmax_eval_, st);
     } else {
       HTRACE("launch_asset");
       launch_asset(le, n_eval_jobs_, nmax_eval_, md_.K, st);
+      if (xs_on_) { launch_xs_loss_sums(le, n_eval_jobs_, st); xs_call("loss", 6, st); }
     }
     HTRACE("launch_job_metrics");
     launch_job_metrics(le, n_eval_jobs_, st);
@@ -2231,8 +2310,9 @@ class Engine {
     launch_prologue(as<RnnJob>(a), G_, D.T, dd(), md_, st_, do_mom);
     if (zx) launch_mlp_fwd_zx(as<MlpJob>(b), G_, std::max(1, zx_gx_ / G_), md_.md, md_.WMB, st_);
     else launch_mlp_fwd(as<MlpJob>(b), G_, gx_fwd_[s], md_.md, md_.KS1, md_.WMB, st_);
-    launch_period_fwd(as<LossJob>(c), G_, D.T, st_);
+    period_fwd(as<LossJob>(c), G_, D.T, st_, true, 1 << s);
     launch_asset(as<LossJob>(c), G_, D.N, md_.K, st_);
+    if (xs_on_) { launch_xs_loss_sums(as<LossJob>(c), G_, st_); xs_call("loss", 1 << s, st_); }
     launch_job_metrics(as<LossJob>(c), G_, st_);
     if (wait) sync();
   }
@@ -2322,6 +2402,10 @@ PYBIND11_MODULE(_dlap_hip, m) {
       .def_static("loss_timestamps", []() { return loss_timestamps(); })
       .def_static("mlp_timestamps", []() { return mlp_timestamps(); })
       .def_static("tbwd_timestamps", []() { return tbwd_timestamps(); })
+      .def("set_xs", &Engine::set_xs)
+      .def("xs_set_globals", &Engine::xs_set_globals)
+      .def("ws_ptr", &Engine::ws_ptr)
+      .def("grads_ptr", &Engine::grads_ptr)
       .def("forward_split", &Engine::forward_split, py::arg("s"), py::arg("train_mode"), py::arg("do_mom"),
            py::arg("wait") = true)
       .def("train_step", &Engine::train_step)

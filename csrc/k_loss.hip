@@ -35,27 +35,60 @@ __device__ long long g_loss_ts[4];
 // store_wn: also write the zero-mean weights w' into the dense [T][N] wn (read only by the host-side
 // consumers -- evaluate, the module API, the ensemble export -- never by the epoch's own kernels:
 // the epoch graphs skip the scattered stores)
-__global__ __launch_bounds__(PER_NT) void k_period_fwd(const LossJob* __restrict__ jobs, int store_wn) {
+// stage: 0 the whole pass; sharded jobs (LossJob::xs) run it as three launches around the ranks'
+// sums (loss.h launch_period_fwd): 1 local sum w, 2 local sums of w' (mu from the global sum),
+// 3 P / SDF / portfolio / residual statistics from the global sums.
+__global__ __launch_bounds__(PER_NT) void k_period_fwd(const LossJob* __restrict__ jobs, int store_wn, int stage) {
   const LossJob& J = jobs[blockIdx.y];
   const int t = blockIdx.x;
   // the fused forward that produced w has finished (stream order): rearm its progress counter
-  if (J.prog_reset && t == 0 && threadIdx.x == 0) gp(J.prog_reset)[0] = 0;
+  if (stage <= 1 && J.prog_reset && t == 0 && threadIdx.x == 0) gp(J.prog_reset)[0] = 0;
   if (t >= J.T) return;
   __shared__ float red[PER_NT / 64];
   const int N = J.N;
+  const float invN = gp(J.invNt)[t];
+  auto finish = [&](float s_wr, float s_abs, float s_ww) {     // (thread 0)
+    const float p = J.weighted ? s_wr * invN * J.Nbar : s_wr;
+    gp(J.P)[t] = p;
+    gp(J.sdfv)[t] = 1.f + p;
+    if (gp(J.port)) gp(J.port)[t] = s_wr / fmaxf(s_abs, 1e-8f);
+    if (gp(J.rstat)) {
+      gp(J.rstat)[4 * t + 0] = s_ww;
+      gp(J.rstat)[4 * t + 1] = s_wr;
+    }
+  };
+  if (stage == 3) {
+    if (threadIdx.x == 0) {
+      const auto xs = gp(J.xs);
+      finish(xs[J.T + t], xs[2 * J.T + t], xs[3 * J.T + t]);
+    }
+    return;
+  }
   const int r0 = gp(J.row_ptr)[t], r1 = gp(J.row_ptr)[t + 1];   // this period's compact rows
   DLAP_ASSERT(0 <= r0 && r0 <= r1 && r1 <= J.R);
   const auto w = gp(J.w);
   const auto Rc = gp(J.Rc);
   const auto rowti = gp(J.rowti);
-  const float invN = gp(J.invNt)[t];
   float* wn = gp(J.wn) + (size_t)t * N;
   float s_wr = 0.f, s_abs = 0.f, s_ww = 0.f, mu = 0.f;
+  // mu from the period's weight sum: the local rows' (stage 0), published for the ranks' sum
+  // (stage 1: nothing else to do), or the ranks' sum (stage 2)
+  auto mean_of = [&](float sw) -> bool {
+    if (stage == 2) { mu = J.normalize ? gp(J.xs)[t] * invN : 0.f; return true; }
+    const float tot = J.normalize ? block_sum<PER_NT>(sw, red) : 0.f;
+    if (stage == 1) {
+      if (threadIdx.x == 0) gp(J.xs)[t] = tot;
+      return false;
+    }
+    mu = tot * invN;
+    return true;
+  };
   // A period without valid stocks has no compact rows: r0 == r1, possibly == R (the last
   // period of the split), so the clamped `rr = r0` below would read one element past the end of
   // w / Rc / rowti (and then index wn with a garbage stock). Its sums are all zero.
   if (r1 == r0) {
     // (block-uniform: every thread takes this branch; no barrier is skipped by some threads)
+    if (!mean_of(0.f)) return;
   } else if (r1 - r0 <= PER_NT * PER_RB) {
     float wv[PER_RB], rv[PER_RB];
     int iv[PER_RB];
@@ -65,12 +98,10 @@ __global__ __launch_bounds__(PER_NT) void k_period_fwd(const LossJob* __restrict
       const int rr = r < r1 ? r : r0;
       wv[k] = w[rr]; rv[k] = Rc[rr]; iv[k] = rowti[rr].y;
     }
-    if (J.normalize) {
-      float sw = 0.f;
+    float sw = 0.f;
 #pragma unroll
-      for (int k = 0; k < PER_RB; ++k) sw += (r0 + (int)threadIdx.x + PER_NT * k < r1) ? wv[k] : 0.f;
-      mu = block_sum<PER_NT>(sw, red) * invN;
-    }
+    for (int k = 0; k < PER_RB; ++k) sw += (r0 + (int)threadIdx.x + PER_NT * k < r1) ? wv[k] : 0.f;
+    if (!mean_of(sw)) return;
 #pragma unroll
     for (int k = 0; k < PER_RB; ++k) {
       if (r0 + (int)threadIdx.x + PER_NT * k >= r1) continue;
@@ -83,8 +114,8 @@ __global__ __launch_bounds__(PER_NT) void k_period_fwd(const LossJob* __restrict
   } else {          // very wide period: two passes in chunks of PER_NT * PER_RB rows, each
                     // chunk's loads issued before use (the chunk is L2-hot for the second pass)
     constexpr int CH = PER_NT * PER_RB;
-    if (J.normalize) {
-      float sw = 0.f;
+    float sw = 0.f;
+    if (J.normalize && stage != 2) {
       for (int c0 = r0; c0 < r1; c0 += CH) {
         float wv[PER_RB];
 #pragma unroll
@@ -95,8 +126,8 @@ __global__ __launch_bounds__(PER_NT) void k_period_fwd(const LossJob* __restrict
 #pragma unroll
         for (int k = 0; k < PER_RB; ++k) sw += (c0 + (int)threadIdx.x + PER_NT * k < r1) ? wv[k] : 0.f;
       }
-      mu = block_sum<PER_NT>(sw, red) * invN;
     }
+    if (!mean_of(sw)) return;
     for (int c0 = r0; c0 < r1; c0 += CH) {
       float wv[PER_RB], rv[PER_RB];
       int iv[PER_RB];
@@ -120,16 +151,29 @@ __global__ __launch_bounds__(PER_NT) void k_period_fwd(const LossJob* __restrict
   if (threadIdx.x == 0) gp(J.mu)[t] = mu;
   s_wr = block_sum<PER_NT>(s_wr, red);
   s_abs = block_sum<PER_NT>(s_abs, red);
-  if (gp(J.rstat)) s_ww = block_sum<PER_NT>(s_ww, red);
+  if (gp(J.rstat) || stage == 2) s_ww = block_sum<PER_NT>(s_ww, red);
   if (threadIdx.x == 0) {
-    const float p = J.weighted ? s_wr * invN * J.Nbar : s_wr;
-    gp(J.P)[t] = p;
-    gp(J.sdfv)[t] = 1.f + p;
-    if (gp(J.port)) gp(J.port)[t] = s_wr / fmaxf(s_abs, 1e-8f);
-    if (gp(J.rstat)) {
-      gp(J.rstat)[4 * t + 0] = s_ww;
-      gp(J.rstat)[4 * t + 1] = s_wr;
+    if (stage == 2) {
+      const auto xs = gp(J.xs);
+      xs[J.T + t] = s_wr;
+      xs[2 * J.T + t] = s_abs;
+      xs[3 * J.T + t] = s_ww;
+    } else {
+      finish(s_wr, s_abs, s_ww);
     }
+  }
+}
+
+// Sharded jobs: the local loss sums of the dense asset passes -> xs[4T], xs[4T + 1] (summed over
+// the ranks by the engine's hook before k_job_metrics reads them).
+__global__ __launch_bounds__(256) void k_xs_loss_sums(const LossJob* __restrict__ jobs) {
+  const LossJob& J = jobs[blockIdx.x];
+  __shared__ float red[4];
+  float a, b;
+  local_loss_sums<256>(J, a, b, red);
+  if (threadIdx.x == 0) {
+    gp(J.xs)[4 * J.T] = a;
+    gp(J.xs)[4 * J.T + 1] = b;
   }
 }
 
@@ -486,7 +530,11 @@ __global__ __launch_bounds__(PER_NT) void k_period_bwd(const LossJob* __restrict
   }
   const float mu = gp(J.mu)[t];
   float gres_mean = 0.f;
-  if (rcoef != 0.f && J.normalize) {
+  if (rcoef != 0.f && J.normalize && J.xs) {
+    // sharded: the period's sum over every rank's stocks, sum (R_i - beta w'_i) = N_t mean R
+    // (the zero-mean weights sum to 0)
+    gres_mean = rcoef * gp(J.meanR)[t];
+  } else if (rcoef != 0.f && J.normalize) {
     float sg = 0.f;
     for (int rr = r0 + threadIdx.x; rr < r1; rr += PER_NT) sg += Rc[rr] - beta * (gp(J.w)[rr] - mu);
     sg = block_sum<PER_NT>(sg, red);
@@ -536,8 +584,12 @@ std::vector<long long> loss_timestamps() {
 }
 
 // ---------------------------------------------------------------- launchers ------------
-void launch_period_fwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st, bool store_wn) {
-  hipLaunchKernelGGL(k_period_fwd, dim3(tmax, njobs), dim3(PER_NT), 0, st, jobs, (int)store_wn);
+void launch_period_fwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st, bool store_wn, int stage) {
+  hipLaunchKernelGGL(k_period_fwd, dim3(tmax, njobs), dim3(PER_NT), 0, st, jobs, (int)store_wn, stage);
+  HIP_OK(hipGetLastError());
+}
+void launch_xs_loss_sums(const LossJob* jobs, int njobs, hipStream_t st) {
+  hipLaunchKernelGGL(k_xs_loss_sums, dim3(njobs), dim3(256), 0, st, jobs);
   HIP_OK(hipGetLastError());
 }
 bool asset_full_default() {

@@ -58,6 +58,13 @@ struct LossJob {
   double* gpart;         // [T][2] per-period s_t (G s)_t of Gc and Gu
   int* prog_reset;       // train jobs: the fused forward's progress counter of this (model, split),
                          //   zeroed by k_period_fwd (it follows every fused forward; nullptr: none)
+  // Cross-sectional sharding (parallel/xsection.py, the engine path): this engine holds one rank's
+  // stocks. Every cross-sectional sum is formed locally, summed over the ranks between launches
+  // (the engine's hook) and consumed from here; the per-period constants (N_t, mean R, Nbar) are
+  // the global ones and Nnorm is the global stock count of the loss means.
+  float* xs;             // [4][T] per-period partial sums (nullptr: not sharded), then [2] the
+                         //   phase-2 / dense-evaluation loss sums
+  float Nnorm;           // N of the loss normalisation (J.N unless sharded)
 };
 
 // One (model, split) of the Gram build (k_gram.hip).
@@ -75,7 +82,15 @@ size_t gram_part_doubles(int T, int njobs);
 void launch_gram(const GramJob* jobs, int njobs, int T, int nslice, hipStream_t st);
 
 // store_wn = false: the epoch graphs (nothing in the epoch reads the dense zero-mean weights)
-void launch_period_fwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st, bool store_wn = true);
+// stage (sharded jobs, LossJob::xs): 1 the local sum of the raw weights per period -> xs[0]; 2 with
+// the global sum back in xs[0]: the zero-mean weights' local sums sum w'R, sum |w'|, sum w'^2 ->
+// xs[1..3]; 3 with those global: P, SDF, the L1 portfolio return, the residual statistics.
+// 0: all of it from the local rows (one launch).
+void launch_period_fwd(const LossJob* jobs, int njobs, int tmax, hipStream_t st, bool store_wn = true,
+                       int stage = 0);
+// sharded jobs: the local loss sums of the asset passes (sum E^2 over k, i and sum E_u^2) ->
+// xs[4 T], xs[4 T + 1]; once summed over the ranks k_job_metrics takes them from there
+void launch_xs_loss_sums(const LossJob* jobs, int njobs, hipStream_t st);
 // kmax: the moment count K of the jobs (sizes the output grid of the reduction pass)
 // full: the one-pass k_asset_full (training jobs: fewer launches on the critical chain; the
 // jobs must have been built with asset_full = 1), else k_asset_part + k_asset_red (evaluation

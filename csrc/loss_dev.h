@@ -48,6 +48,16 @@ DLAP_DEV double block_sum_d(double v, double* red) {
 template <int NT>
 DLAP_DEV double block_sum_d(double v, double* red);
 
+// (the local loss sums of the dense asset passes, before the division by K N / N)
+template <int NT>
+DLAP_DEV void local_loss_sums(const LossJob& J, float& a, float& b, float* red) {
+  const int nblk = asset_red_blocks(J);
+  a = 0.f; b = 0.f;
+  for (int k = threadIdx.x; k < nblk; k += NT) { a += gp(J.part)[2 * k]; b += gp(J.part)[2 * k + 1]; }
+  a = block_sum<NT>(a, red);
+  b = block_sum<NT>(b, red);
+}
+
 template <int NT>
 DLAP_DEV void final_losses(const LossJob& J, float& lc, float& lu, float* red) {
   if (J.gram) {        // fixed-order fp64 sum of the per-period quadratic-form terms
@@ -56,17 +66,19 @@ DLAP_DEV void final_losses(const LossJob& J, float& lc, float& lu, float* red) {
     for (int t = threadIdx.x; t < J.T; t += NT) { a += gp(J.gpart)[2 * t]; b += gp(J.gpart)[2 * t + 1]; }
     a = block_sum_d<NT>(a, redd);
     b = block_sum_d<NT>(b, redd);
-    lc = J.h ? (float)(a / ((double)J.K * (double)J.N)) : 0.f;
-    lu = (float)(b / (double)J.N);
+    lc = J.h ? (float)(a / ((double)J.K * (double)J.Nnorm)) : 0.f;
+    lu = (float)(b / (double)J.Nnorm);
     return;
   }
-  const int nblk = asset_red_blocks(J);
-  float a = 0.f, b = 0.f;
-  for (int k = threadIdx.x; k < nblk; k += NT) { a += gp(J.part)[2 * k]; b += gp(J.part)[2 * k + 1]; }
-  a = block_sum<NT>(a, red);
-  b = block_sum<NT>(b, red);
-  lc = J.h ? a / ((float)J.K * (float)J.N) : 0.f;
-  lu = b / (float)J.N;
+  float a, b;
+  if (J.xs) {          // sharded: the loss sums of every rank's stocks (launch_xs_loss_sums + hook)
+    a = gp(J.xs)[4 * J.T];
+    b = gp(J.xs)[4 * J.T + 1];
+  } else {
+    local_loss_sums<NT>(J, a, b, red);
+  }
+  lc = J.h ? a / ((float)J.K * J.Nnorm) : 0.f;
+  lu = b / J.Nnorm;
 }
 
 // ts: in-kernel timestamps (k_job_metrics' g_loss_ts), or nullptr

@@ -215,7 +215,8 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
                      print_freq=128, save_dir=None, ignore_epoch=64, seed=None,
                      precision="bf16", selection_sign=1.0, verbose=True, n_models=1,
                      models=None, seeds=None, save_dirs=None, lrs=None, dropouts=None, resume=False,
-                     resume_path=None, nan_policy="warn", stop_after=None, final_weights_device=False):
+                     resume_path=None, nan_policy="warn", stop_after=None, final_weights_device=False,
+                     engine_setup=None):
     """GPU executor of the 3-phase schedule; with ``n_models > 1`` trains an ensemble batch.
 
     Returns ``(model, history)`` for a single model, or ``(models, histories)`` when
@@ -234,6 +235,8 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
                      (used to test interruption; the resume record is written first).
     ``final_weights_device``: the final evaluation's L1-normalised weights stay on the GPU
     (``engine_final_eval[s]["weights"]`` is then a CUDA tensor; the ensemble all-gathers them).
+    ``engine_setup``: called with the ``GANEngine`` once data and parameters are set, before the
+    first epoch (the cross-sectional sharding installs its collectives there, parallel/xsection.py).
     """
     from ..models.gan import AssetPricingGAN
     from ..utils import checkpoint as ckpt
@@ -270,6 +273,8 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
                 eng.eng.set_lr(g, float(lrs[g]))
             if dropouts is not None:
                 eng.eng.set_dropout(g, float(dropouts[g]))
+        if engine_setup is not None:
+            engine_setup(eng)
         eng.eng.sync()
     template = AssetPricingGAN(config)
     t_start = time.time()

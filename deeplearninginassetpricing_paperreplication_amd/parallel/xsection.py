@@ -600,6 +600,154 @@ def train_3phase_xsection(config: Dict, train_data: Dict, valid_data: Dict, test
                                  model=model, train_fn=train_epoch, eval_fn=evaluate)
 
 
+class _DevView:
+    """A typed 1-D view of engine device memory (``torch.as_tensor`` reads the interface)."""
+
+    def __init__(self, ptr: int, n: int, typestr: str):
+        self.__cuda_array_interface__ = {"shape": (int(n),), "typestr": typestr, "data": (int(ptr), False),
+                                         "version": 2}
+
+
+class XSEngine:
+    """Cross-sectional sharding INSIDE the native epoch engine: every rank's ``Engine`` holds the
+    rank's stocks of the three splits and runs the whole epoch itself (towers, losses, backward,
+    BPTT, Adam); at each cross-sectional coupling it calls back (``Engine.set_xs``) and the
+    rank-local sums are all-reduced on the engine stream, one collective per coupling:
+
+      sums1  [T]  Σ w of every period (the zero mean),             per split, before the P pass
+      sums2  [3T] Σ w'R, Σ |w'|, Σ w'^2 (P_t, the L1 portfolio, the residual loss)
+      gram   [2T²] fp64 Gram matrices (once per moment refresh: the phase-1/3 losses and dL/dSDF_t
+             are quadratic forms of them, so a training epoch needs NO loss all-reduce)
+      loss   [2]  the dense asset passes' loss sums (phase 2, dense evaluations)
+      grads  [P + T Dm (+ 64 T)] the flat gradient and the per-period input gradients of the
+             replicated LSTM, after the tower backward -- the only backward collective.
+
+    Reference math: `/root/reference/src/model.py:271-279` (zero mean), `:346-433` (losses);
+    the per-period constants N_t, mean R, Σ R², N̄ and the loss normaliser N are the global ones
+    (``Engine.xs_set_globals``). Replicated parameters stay bit-identical (every rank applies the
+    same summed gradient). With one rank the callbacks return at once."""
+
+    def __init__(self, eng, shards: Sequence[Optional[Dict]], dist: comm.Dist):
+        self.ge, self.d = eng, dist
+        self.dev = torch.device("cuda", torch.cuda.current_device())
+        self.T = {s: int(b["returns"].shape[0]) for s, b in enumerate(shards) if b is not None}
+        self._views: Dict = {}
+        self._streams: Dict[int, torch.cuda.ExternalStream] = {}
+        self.n_calls = 0
+        if self.d.active:
+            for s, b in enumerate(shards):
+                if b is not None:
+                    self._set_globals(s, b)
+        self.ge.eng.set_xs(self._hook)
+
+    def _set_globals(self, s: int, b: Dict):
+        m = b["mask"].to(self.dev).bool()
+        r = torch.where(m, b["returns"].to(self.dev, torch.float64), torch.zeros((), dtype=torch.float64,
+                                                                                 device=self.dev))
+        st = torch.stack([m.sum(1).double(), r.sum(1), (r * r).sum(1)])        # [3, T]
+        tdist.all_reduce(st)
+        nc = st[0].clamp_min(1.0)
+        Nt, invNt = st[0].float().contiguous(), (1.0 / nc).float().contiguous()
+        meanR, RR = (st[1] / nc).float().contiguous(), st[2].float().contiguous()
+        nbar = float(nc.mean()) if nc.numel() else 1.0
+        n_total = int(b["n_total"]) if "n_total" in b else self._sum_int(m.shape[1])
+        ts = torch.cuda.current_stream(self.dev).cuda_stream
+        self.ge.eng.join_from(ts)
+        self.ge.eng.xs_set_globals(s, Nt.data_ptr(), invNt.data_ptr(), meanR.data_ptr(), RR.data_ptr(),
+                                   nbar, float(n_total))
+        self.ge.eng.sync()                          # (the temporaries are read)
+
+    def _sum_int(self, v: int) -> int:
+        t = torch.tensor([float(v)], dtype=torch.float64, device=self.dev)
+        tdist.all_reduce(t)
+        return int(t.item())
+
+    def _view(self, key, ptr: int, n: int, typestr: str) -> torch.Tensor:
+        v = self._views.get(key)
+        if v is None or v[0] != ptr:
+            v = (ptr, torch.as_tensor(_DevView(ptr, n, typestr), device=self.dev))
+            self._views[key] = v
+        return v[1]
+
+    def _ws(self, s: int, name: str, typestr: str = "<f4") -> torch.Tensor:
+        ptr, n = self.ge.eng.ws_ptr(0, s, name)
+        return self._view((s, name), ptr, n, typestr)
+
+    def _bufs(self, what: str, which: int) -> list:
+        splits = [s for s in sorted(self.T) if which & (1 << s)]
+        if what == "grads":
+            ptr, n = self.ge.eng.grads_ptr(0)
+            out = [self._view("grads", ptr, n, "<f4"), self._ws(0, "dpp")]
+            if which == 2:
+                out.append(self._ws(0, "dab"))
+            return out
+        if what == "gram":
+            return [self._ws(s, "gram", "<f8") for s in splits]
+        rows = {"sums1": (0, 1), "sums2": (1, 4)}
+        out = []
+        for s in splits:
+            T, xs = self.T[s], self._ws(s, "xs")
+            if what == "loss":
+                out.append(xs[4 * T:4 * T + 2])
+            else:
+                a, b = rows[what]
+                out.append(xs[a * T:b * T])
+        return out
+
+    def _hook(self, what: str, which: int, stream: int):
+        self.n_calls += 1
+        if not self.d.active:
+            return
+        bufs = [b for b in self._bufs(what, which) if b.numel()]
+        st = self._streams.get(stream)
+        if st is None:
+            st = self._streams[stream] = torch.cuda.ExternalStream(stream, device=self.dev)
+        with torch.cuda.stream(st):
+            if len(bufs) == 1:
+                tdist.all_reduce(bufs[0])
+                return
+            flat = torch.cat([b.reshape(-1) for b in bufs])      # one collective per coupling
+            tdist.all_reduce(flat)
+            o = 0
+            for b in bufs:
+                b.copy_(flat[o:o + b.numel()])
+                o += b.numel()
+
+
+def train_3phase_xsection_engine(config: Dict, train_data: Dict, valid_data: Dict, test_data: Optional[Dict],
+                                 dist: comm.Dist, device=None, seed: int = 42, verbose: bool = True,
+                                 save_dir: Optional[str] = None, **kw):
+    """``train_3phase`` over stock shards with the whole epoch on the native engine (``XSEngine``).
+    ``*_data``: FULL split dicts or this rank's shards (carrying ``n_total``). Returns
+    ``(model, history)`` on every rank; ``model.engine_final_eval[s]`` holds the GLOBAL metrics
+    (the weights are the rank's stocks). ``kw``: the schedule / optimiser arguments of
+    ``engine.runner.train_3phase_gpu``."""
+    from ..engine.runner import train_3phase_gpu
+    device = torch.device(device or dist.device)
+    sh = [None if b is None else (b if "n_total" in b else shard_batch(b, dist.rank, dist.world))
+          for b in (train_data, valid_data, test_data)]
+    sh = [None if b is None else {k: (v.to(device) if isinstance(v, torch.Tensor) else v) for k, v in b.items()}
+          for b in sh]
+    torch.manual_seed(seed)                      # identical initial parameters on every rank
+    model = AssetPricingGAN(config)
+    salt = dist.rank + 1 if dist.active else 0
+    holder = {}
+
+    def setup(eng):
+        eng.eng.set_tower_salt(0, salt)          # independent tower dropout masks per rank
+        holder["xs"] = XSEngine(eng, sh, dist)
+
+    main = dist.rank == 0
+    quiet = contextlib.redirect_stdout(io.StringIO()) if not main else contextlib.nullcontext()
+    with quiet:
+        out = train_3phase_gpu(config, *[None if b is None else {k: v for k, v in b.items() if k != "n_total"}
+                                         for b in sh],
+                               device=device, seed=seed, models=[model], seeds=[seed], verbose=verbose and main,
+                               save_dir=save_dir if main else None, engine_setup=setup, **kw)
+    train_3phase_xsection_engine.last_xs = holder.get("xs")
+    return out
+
+
 def load_shards(args, d: comm.Dist) -> Dict[str, Dict]:
     """Each rank's stocks of every split: from ``--data_dir`` (each rank reads the files and keeps
     its slice) or a ``--synthetic`` panel generated identically on every rank."""
@@ -622,6 +770,9 @@ def main(argv: Optional[Sequence[str]] = None):
     ap.add_argument("--save_dir", default=None)
     ap.add_argument("--cpu", action="store_true")
     ap.add_argument("--torch_towers", action="store_true", help="local towers as PyTorch ops instead of the engine")
+    ap.add_argument("--mode", choices=("engine", "towers"), default="engine",
+                    help="engine: the whole epoch on the native engine with all-reduce callbacks (GPU); "
+                         "towers: engine (or --torch_towers) towers under eager torch losses")
     ap.add_argument("--out", default=None)
     args = ap.parse_args(argv)
     d = comm.init(use_gpu=False if args.cpu else None)
@@ -630,12 +781,20 @@ def main(argv: Optional[Sequence[str]] = None):
     cfg = default_cli_config(tr["macro_features"].shape[1] if tr.get("macro_features") is not None else 0,
                              tr["individual_features"].shape[2])
     t0 = time.time()
-    model, hist = train_3phase_xsection(cfg, b["train"], b["valid"], b["test"], d, num_epochs_unc=args.epochs[0],
-                                        num_epochs_moment=args.epochs[1], num_epochs=args.epochs[2], lr=args.lr,
-                                        print_freq=args.print_freq, save_dir=args.save_dir,
-                                        ignore_epoch=args.ignore_epoch, seed=args.seed,
-                                        engine=False if args.torch_towers else None)
-    ev = {k: evaluate(model, b[k], d.device) for k in SPLITS}
+    if args.mode == "engine" and d.device.type == "cuda" and not args.torch_towers:
+        model, hist = train_3phase_xsection_engine(cfg, b["train"], b["valid"], b["test"], d,
+                                                   num_epochs_unc=args.epochs[0], num_epochs_moment=args.epochs[1],
+                                                   num_epochs=args.epochs[2], lr=args.lr,
+                                                   print_freq=args.print_freq, save_dir=args.save_dir,
+                                                   ignore_epoch=args.ignore_epoch, seed=args.seed)
+        ev = {k: model.engine_final_eval[i] for i, k in enumerate(SPLITS)}
+    else:
+        model, hist = train_3phase_xsection(cfg, b["train"], b["valid"], b["test"], d, num_epochs_unc=args.epochs[0],
+                                            num_epochs_moment=args.epochs[1], num_epochs=args.epochs[2], lr=args.lr,
+                                            print_freq=args.print_freq, save_dir=args.save_dir,
+                                            ignore_epoch=args.ignore_epoch, seed=args.seed,
+                                            engine=False if args.torch_towers else None)
+        ev = {k: evaluate(model, b[k], d.device) for k in SPLITS}
     wall = time.time() - t0
     n_ep = sum(args.epochs)
     res = {"world_size": d.world, "n_stocks": tr["n_total"], "wall_s": wall, "epochs": n_ep,

@@ -186,3 +186,84 @@ def test_tower_dropout_independent_across_ranks():
     assert torch.equal(a, b)
     frac = float((a != c).float().mean())
     assert frac > 0.5, frac                # different masks change (almost) every row's output
+
+
+# ---- the whole epoch on the engine (XSEngine: all-reduce callbacks between the engine's passes)
+_SCHED = dict(num_epochs_unc=4, num_epochs_moment=3, num_epochs=4, print_freq=100, ignore_epoch=0,
+              precision="fp32", verbose=False)
+
+
+def _full_splits(dev):
+    full = _shards(dev)
+    return [{k: v for k, v in b.items() if k != "n_total"} for b in full]
+
+
+def _plain_run(dev):
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import flatten_state, train_3phase_gpu
+    from deeplearninginassetpricing_paperreplication_amd.models.gan import AssetPricingGAN
+    cfg = default_cli_config(8, 46, dropout=0.0)
+    torch.manual_seed(42)
+    model = AssetPricingGAN(cfg)
+    m, hist = train_3phase_gpu(cfg, *_full_splits(dev), device=dev, seed=42, models=[model], seeds=[42], **_SCHED)
+    return flatten_state(m, m.spec), hist, m.engine_final_eval
+
+
+def test_xs_engine_one_rank_matches_engine():
+    """One rank: the sharded epoch (staged period passes, Gram losses, unfused tail, eager epochs)
+    trains the same model as the production engine (fp32: rounding-level differences only)."""
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import flatten_state
+    dev = torch.device("cuda:0")
+    ref, href, fref = _plain_run(dev)
+    cfg = default_cli_config(8, 46, dropout=0.0)
+    m, hist = X.train_3phase_xsection_engine(cfg, *_full_splits(dev), comm.Dist(device=dev), device=dev, seed=42,
+                                             **_SCHED)
+    assert X.train_3phase_xsection_engine.last_xs.n_calls > 0        # the callbacks fired
+    got = flatten_state(m, m.spec)
+    np.testing.assert_allclose(got, ref, rtol=1e-4, atol=2e-6)
+    np.testing.assert_allclose(hist["train_loss"], href["train_loss"], rtol=1e-4)
+    np.testing.assert_allclose(hist["valid_sharpe"], href["valid_sharpe"], rtol=1e-3, atol=1e-4)
+    for s in fref:
+        assert abs(m.engine_final_eval[s]["sharpe"] - fref[s]["sharpe"]) < 1e-3
+
+
+def _xs_rank_worker(rank, world, port, out_path):
+    import json
+    import os
+    os.environ.update(WORLD_SIZE=str(world), RANK=str(rank), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), DLAP_SHARE_GPU="1")
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import flatten_state
+    d = comm.init(backend="gloo", use_gpu=True, timeout_s=120)
+    dev = d.device
+    cfg = default_cli_config(8, 46, dropout=0.0)
+    m, hist = X.train_3phase_xsection_engine(cfg, *_full_splits(dev), d, device=dev, seed=42, **_SCHED)
+    p = flatten_state(m, m.spec)
+    allp = [torch.zeros_like(torch.from_numpy(p)) for _ in range(world)]
+    torch.distributed.all_gather(allp, torch.from_numpy(p))
+    if d.rank == 0:
+        with open(out_path, "w") as f:
+            json.dump({"params": p.tolist(), "replicas_equal": all(torch.equal(allp[0], q) for q in allp),
+                       "train_loss": hist["train_loss"], "valid_sharpe": hist["valid_sharpe"],
+                       "sharpe": {str(s): float(v["sharpe"]) for s, v in m.engine_final_eval.items()}}, f)
+    comm.shutdown(d)
+
+
+def test_xs_engine_two_ranks_equal_unsharded(tmp_path):
+    """Two ranks (gloo, sharing the GPU), half the stocks each, the whole 3-phase schedule on the
+    engine with the all-reduce callbacks: the replicas stay bit-identical and train the unsharded
+    model (fp32; the cross-rank sums only reorder fp32 additions)."""
+    import json
+    import socket
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    out = tmp_path / "r0.json"
+    mp.start_processes(_xs_rank_worker, args=(2, port, str(out)), nprocs=2, join=True, start_method="spawn")
+    res = json.loads(out.read_text())
+    dev = torch.device("cuda:0")
+    ref, href, fref = _plain_run(dev)
+    assert res["replicas_equal"]
+    np.testing.assert_allclose(np.asarray(res["params"], dtype=np.float32), ref, rtol=1e-4, atol=5e-6)
+    np.testing.assert_allclose(res["train_loss"], href["train_loss"], rtol=2e-4)
+    for s, v in res["sharpe"].items():
+        assert abs(v - fref[int(s)]["sharpe"]) < 2e-3
