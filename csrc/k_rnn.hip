@@ -458,11 +458,12 @@ __host__ __device__ inline LstmBwdLds lstm_bwd_lds(int T, int H, bool scan, bool
   return L;
 }
 
-// FUSED (the tail launch k_lstm_tail, single layer, H = 4, dense-state path): the incoming
-// gradient dpp is produced by the period blocks of the same launch -- the block waits for their
+// FUSED (the tail launch k_lstm_tail): the incoming gradient dpp is produced by the period blocks
+// of the same launch. Single layer of width 4 (the dense-state path): the block waits for their
 // count (J.tail_ctr) only right before the pair maps, after the pre-pass and the step matrices;
-// the step matrices go to global scratch (LDS map above); the layer-0 W_ih gradient (k_wgrad's
-// sum, same order) is formed here from the gate gradients in LDS.
+// the step matrices go to global scratch (LDS map above). Any other shape (H = 8, stacked layers)
+// runs k_lstm_bwd's serial chain in k_lstm_bwd's LDS map and waits after the top layer's pre-pass.
+// The layer-0 W_ih gradient (k_wgrad's sum, same order) is handed to the launch's helper blocks.
 template <int HM, bool FUSED>
 DLAP_DEV void lstm_bwd_body(const UpdJob& J, const ModelDesc* __restrict__ md, int scan, float* sm, bool tsm) {
   if (md->nrnn == 0) return;
@@ -475,7 +476,9 @@ DLAP_DEV void lstm_bwd_body(const UpdJob& J, const ModelDesc* __restrict__ md, i
   const auto params = gp(J.params);
   const auto grads = gp(J.grads);
   RNN_TS(8, tsm);
-  const LstmBwdLds LL = lstm_bwd_lds(T, H, HM == 4 && H == 4 && scan, FUSED);
+  // the dense-state BPTT: k_lstm_bwd with `scan` at H = 4; the fused tail for one layer of width 4
+  const bool dense = HM == 4 && H == 4 && (FUSED ? md->nrnn == 1 : scan != 0);
+  const LstmBwdLds LL = lstm_bwd_lds(T, H, dense && !FUSED, FUSED && dense);
   float* s_cf = sm + LL.cf;                    // [T][6][H] BPTT coefficients (pre-pass)
   float* s_h = sm + LL.h;                      // [T][H]  layer outputs
   float* s_d = sm + LL.d;                      // [T][H]  incoming gradient
@@ -484,8 +487,33 @@ DLAP_DEV void lstm_bwd_body(const UpdJob& J, const ModelDesc* __restrict__ md, i
   __shared__ int s_bad;                        // FUSED: the wait for dpp gave up
   if (FUSED && threadIdx.x == 0) s_bad = 0;
   if (FUSED) __syncthreads();
-  for (int l = FUSED ? 0 : md->nrnn - 1; l >= 0; --l) {
+  // FUSED: the incoming gradient: every period block of this launch has published dpp[t]
+  // (write-through stores, drained, then one agent-scope add each). Wave 0 polls the count
+  // (relaxed, s_sleep between polls, bounded), ONE agent acquire; false: gave up (block-uniform)
+  auto wait_dpp = [&]() -> bool {
+    if (threadIdx.x < 64) {
+      const int* ctr = J.tail_ctr;
+      int v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      unsigned spins = 0;
+      while (v < T) {
+        if (spins++ >= J.spin_limit) {         // never on a resident grid: poison the model
+          if (threadIdx.x == 0) { atomicAdd(const_cast<int*>(J.prog) + 1, 1); s_bad = 1; }
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+        v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      }
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    return s_bad == 0;
+  };
+  for (int l = md->nrnn - 1; l >= 0; --l) {
     const auto dout = l == md->nrnn - 1 ? gp(J.dpp) : gp(J.dx);
+    // (FUSED: the top layer's incoming gradient is loaded after the wait)
+    const bool late_d = FUSED && l == md->nrnn - 1;
     const auto sgg = gp(J.sg) + (size_t)l * T * G4;
     const auto scg = gp(J.sc) + (size_t)l * T * H;
     const auto shg = gp(J.sh) + (size_t)l * T * H;
@@ -510,7 +538,7 @@ DLAP_DEV void lstm_bwd_body(const UpdJob& J, const ModelDesc* __restrict__ md, i
         c[u] = scg[i];
         cp[u] = t > 0 ? scg[i - H] : (J.c0 ? gp(J.c0)[l * H + k] : 0.f);
         hv[u] = shg[i];
-        dv[u] = FUSED ? 0.f : dout[i];
+        dv[u] = late_d ? 0.f : dout[i];
       }
 #pragma unroll
       for (int u = 0; u < PU; ++u) {
@@ -526,13 +554,18 @@ DLAP_DEV void lstm_bwd_body(const UpdJob& J, const ModelDesc* __restrict__ md, i
         q[4 * H] = tc * go[u] * (1.f - go[u]);
         q[5 * H] = gf[u];
         s_h[i] = hv[u];
-        if (!FUSED) s_d[i] = dv[u];
+        if (!late_d) s_d[i] = dv[u];
       }
     }
     __syncthreads();
     if (l == 0) RNN_TS(9, tsm);
     if (wave == 0) __builtin_amdgcn_s_setprio(3);     // serial chain: see k_lstm_gls
-    if (FUSED || (HM == 4 && H == 4 && scan)) {
+    if (late_d && !dense) {
+      if (!wait_dpp()) return;
+      for (int i = threadIdx.x; i < T * H; i += 256) s_d[i] = dout[i];
+      __syncthreads();
+    }
+    if (dense) {
       // ---- dense-state BPTT (header comment): step matrices, chain on wave 0, gate gradients
       float* s_M = FUSED ? gp(J.mscr) : sm + LL.M;   // [T][64] step matrices
       float* s_y = sm + LL.y;
@@ -624,27 +657,7 @@ DLAP_DEV void lstm_bwd_body(const UpdJob& J, const ModelDesc* __restrict__ md, i
         }
       }
       if constexpr (FUSED) {
-        // the incoming gradient: every period block of this launch has published dpp[t]
-        // (write-through stores, drained, then one agent-scope add each). Wave 0 polls the count
-        // (relaxed, s_sleep between polls, bounded), ONE agent acquire, then every wave loads.
-        if (threadIdx.x < 64) {
-          const int* ctr = J.tail_ctr;
-          int v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-          unsigned spins = 0;
-          while (v < T) {
-            if (spins++ >= J.spin_limit) {         // never on a resident grid: poison the model
-              if (threadIdx.x == 0) { atomicAdd(const_cast<int*>(J.prog) + 1, 1); s_bad = 1; }
-              break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-            v = __builtin_amdgcn_readfirstlane(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-          }
-          asm volatile("" ::: "memory");
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        __syncthreads();
-        if (s_bad) return;                           // block-uniform; nothing written
+        if (!wait_dpp()) return;                     // block-uniform; nothing written
         for (int i = threadIdx.x; i < T * H; i += 256) s_d[i] = dout[i];
         RNN_TS(16, tsm);
       }
@@ -773,7 +786,7 @@ DLAP_DEV void lstm_bwd_body(const UpdJob& J, const ModelDesc* __restrict__ md, i
         d[8] = dc * q[12 + k];
         d[12] = dh * q[16 + k];
       }
-    } else if (!FUSED && wave == 0 && HM == 4 && H == 4) {
+    } else if (wave == 0 && HM == 4 && H == 4) {
       // Gate-per-lane BPTT (H = 4): lane L (mod 16) owns gate row L = 4q + k and keeps the
       // recurrent state of unit k replicated, so d_L = (q == 3 ? dh : dc) * coef is lane-local
       // and dh_next_j = sum_L W_hh[L][j] d_L is ONE reduce-scatter over the 16 lanes: two DPP
@@ -840,7 +853,7 @@ DLAP_DEV void lstm_bwd_body(const UpdJob& J, const ModelDesc* __restrict__ md, i
       }
       // dL/d(initial state) of the layer: the gradients carried past t = 0
       if (J.dh0 && lane < 4) { gp(J.dh0)[l * 4 + lane] = dh_next; gp(J.dc0)[l * 4 + lane] = dc_next; }
-    } else if (!FUSED && wave == 0) {
+    } else if (wave == 0) {
       const int k = lane < H ? lane : 0;
       const bool act = lane < H;
       const auto Whh = params + md->lstm_w_hh[l];
@@ -932,7 +945,7 @@ DLAP_DEV void lstm_bwd_body(const UpdJob& J, const ModelDesc* __restrict__ md, i
     const int nout = G4 * ncol;
     const int S = max(1, min(LSTM_GSEG, 256 / max(nout, 1)));
     float* gpart = sm + LL.gpart;                     // [S][nout] (after the gate gradients)
-    if (FUSED || (HM == 4 && H == 4)) {
+    if (HM == 4 && H == 4) {
       // H = 4: [ncol x 16 gates] = sum_t x[t][col] dG[t][g] on v_mfma_f32_16x16x4f32 (exact
       // fp32 products) -- x = (h_{t-1} (the initial state at t = 0), 1 for the biases, the layer
       // input of a deeper layer). Wave w takes the 4-period k-steps w, w + 4, ...; the four
@@ -1004,7 +1017,7 @@ DLAP_DEV void lstm_bwd_body(const UpdJob& J, const ModelDesc* __restrict__ md, i
       }
       __syncthreads();
     }
-    if (!FUSED && l > 0) {
+    if (l > 0) {
       const auto Wih = params + md->lstm_w_ih[l];
       const auto dx = gp(J.dx);
       for (int idx = threadIdx.x; idx < T * H; idx += 256) {
@@ -1199,8 +1212,8 @@ DLAP_DEV void tail_adam(const UpdJob& U, const ModelDesc* __restrict__ md, float
 
 // Fused backward tail of phases 1 / 3 (one launch instead of k_finalize -> k_lstm_bwd -> k_wgrad
 // [-> k_adam]): grid (1 + T + slab blocks + W_ih blocks [+ 1], models). Block 0 runs the LSTM
-// backward (lstm_bwd_body<4, true>: pre-pass and step matrices first, then it waits for the
-// per-period gradient); blocks 1 .. T form the per-period sums dpp[t] and publish them; the slab
+// backward (lstm_bwd_body<HM, true>: the pre-pass (and, dense-state path, the step matrices)
+// first, then it waits for the per-period gradient; every layer of a stacked LSTM); blocks 1 .. T form the per-period sums dpp[t] and publish them; the slab
 // blocks sum the weight-gradient slabs; the next (M + 16) / 16 blocks wait for block 0's gate
 // gradients and form the layer-0 W_ih gradient (wgrad_block) while block 0 forms W_hh and the
 // biases. Every block runs the same arithmetic as the separate kernels, so the results are
@@ -1211,6 +1224,7 @@ DLAP_DEV void tail_adam(const UpdJob& U, const ModelDesc* __restrict__ md, float
 // pipelined epoch needs no fork to the evaluation branch for them.
 // adam (tail_adam): the clip + Adam update of the step in the launch's last blocks (2: after
 // the evaluation branch's signal; the only mode).
+template <int HM>
 __global__ __launch_bounds__(256, 2) void k_lstm_tail(const UpdJob* __restrict__ ujobs, const FinJob* __restrict__ fjobs,
                                                    const ModelDesc* __restrict__ md, int slab_stride, int nslab_blocks,
                                                    const LossJob* __restrict__ ljobs, int adam, float lr) {
@@ -1222,7 +1236,7 @@ __global__ __launch_bounds__(256, 2) void k_lstm_tail(const UpdJob* __restrict__
   __shared__ int s_steps[2];          // (adam) the step counters before this launch's update
   if (adam && threadIdx.x == 0) { s_steps[0] = gp(U.adam_step)[0]; s_steps[1] = gp(U.drop_step)[0]; }
   if (b < 0) {
-    lstm_bwd_body<4, true>(U, md, 1, sm, blockIdx.y == 0);
+    lstm_bwd_body<HM, true>(U, md, 1, sm, blockIdx.y == 0);
   } else if (b < U.T) {
     finalize_block(F, md, 1, slab_stride, nslab_blocks + b, U.tail_ctr + TAIL_CNT);
   } else if (b < U.T + nslab_blocks) {
@@ -1253,26 +1267,38 @@ __global__ __launch_bounds__(256, 2) void k_lstm_tail(const UpdJob* __restrict__
       __syncthreads();
       return bad == 0;
     };
-    wgrad_block<1>(U, md, 1, cblk, U.tail_ctr + TAIL_DONE, nwg, wait_dg);
+    wgrad_block<HM == 4 ? 1 : 2>(U, md, 1, cblk, U.tail_ctr + TAIL_DONE, nwg, wait_dg);   // 4H gates
     if (blockIdx.y == 0 && cblk == nwg - 1 && threadIdx.x == 0) g_rnn_ts[17] = wall_clock64();
   }
   if (adam) tail_adam(U, md, lr, gridDim.x, s_steps[0], s_steps[1]);
 }
 
-// whether the fused tail applies (single LSTM layer of width 4 on the dense-state BPTT path,
-// phases 1 / 3); its LDS bytes
-size_t lstm_tail_lds_bytes(int T, int H) { return lstm_bwd_lds(T, H, true, true).total * sizeof(float); }
+// whether the fused tail applies (phases 1 / 3; LSTM widths up to 8, any depth); its LDS bytes:
+// the dense-state map for one layer of width 4, else k_lstm_bwd's
+static bool tail_dense(const ModelDesc& mh) { return mh.nrnn == 1 && mh.H == 4; }
+size_t lstm_tail_lds_bytes(const ModelDesc& mh, int T) {
+  return lstm_bwd_lds(T, mh.H, false, tail_dense(mh)).total * sizeof(float);
+}
 bool lstm_tail_supported(const ModelDesc& mh, int T) {
-  if (mh.nrnn != 1 || mh.H != 4 || mh.M <= 0 || T < 2) return false;
+  if (mh.nrnn < 1 || mh.H > 8 || mh.M <= 0 || T < 2) return false;
   const char* scan_env = std::getenv("DLAP_LSTM_SCAN");
-  if (scan_env && std::atoi(scan_env) == 0) return false;
-  return lstm_tail_lds_bytes(T, mh.H) + 6400 <= 80 * 1024;   // (+ static LDS) two per CU
+  if (tail_dense(mh) && scan_env && std::atoi(scan_env) == 0) return false;
+  // (+ static LDS) two per CU for the dense map; one per CU otherwise (H = 8: ~100 KB at T = 240).
+  // Residency is not required: the only in-kernel waits are on lower-numbered blocks (the LSTM
+  // block waits for the period blocks dispatched right after it) or, for Adam, the last arrivals
+  const size_t lim = tail_dense(mh) ? 80 * 1024 : 160 * 1024;
+  return lstm_tail_lds_bytes(mh, T) + 6400 <= lim;
 }
 int lstm_tail_words() { return TAIL_WORDS; }
+static size_t tail_dyn_lds(const ModelDesc& mh, int T) {
+  // (the metrics block keeps its scratch in the dynamic LDS: DLAP_MAX_T + 4 floats)
+  return std::max(lstm_tail_lds_bytes(mh, T), (size_t)(DLAP_MAX_T + 4) * sizeof(float));
+}
 int lstm_tail_capacity(const ModelDesc& mh, int T) {
-  const size_t sh = std::max(lstm_tail_lds_bytes(T, mh.H), (size_t)(DLAP_MAX_T + 4) * sizeof(float));
+  const size_t sh = tail_dyn_lds(mh, T);
   int per_cu = 0, dev = 0, ncu = 0;
-  HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lstm_tail, 256, sh));
+  if (mh.H <= 4) HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lstm_tail<4>, 256, sh));
+  else HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_lstm_tail<8>, 256, sh));
   HIP_OK(hipGetDevice(&dev));
   HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
   return per_cu * ncu;
@@ -1281,10 +1307,12 @@ void launch_lstm_tail(const UpdJob* ujobs, const FinJob* fjobs, int njobs, const
                       int T, int slab_stride, hipStream_t st, const LossJob* ljobs, int adam, float lr) {
   const int nslab_blocks = mh.ntile_s * 64 + (SLAB_EXTRA + 63) / 64;
   const int nwg = (mh.M + 1 + 15) / 16;
-  // (the metrics block keeps its scratch in the dynamic LDS: DLAP_MAX_T + 4 floats)
-  const size_t sh = std::max(lstm_tail_lds_bytes(T, mh.H), (size_t)(DLAP_MAX_T + 4) * sizeof(float));
-  hipLaunchKernelGGL(k_lstm_tail, dim3(1 + T + nslab_blocks + nwg + (ljobs ? 1 : 0), njobs), dim3(256), sh, st,
-                     ujobs, fjobs, md, slab_stride, nslab_blocks, ljobs, adam, lr);
+  const size_t sh = tail_dyn_lds(mh, T);
+  const dim3 grid(1 + T + nslab_blocks + nwg + (ljobs ? 1 : 0), njobs);
+  if (mh.H <= 4)
+    hipLaunchKernelGGL(k_lstm_tail<4>, grid, dim3(256), sh, st, ujobs, fjobs, md, slab_stride, nslab_blocks, ljobs, adam, lr);
+  else
+    hipLaunchKernelGGL(k_lstm_tail<8>, grid, dim3(256), sh, st, ujobs, fjobs, md, slab_stride, nslab_blocks, ljobs, adam, lr);
   HIP_OK(hipGetLastError());
 }
 

@@ -22,14 +22,22 @@ dL/dθ = Σ_r (local paths). The replicated clip + Adam then keep the replicas b
 Collectives per training step: 3 forward ([2,T], [2,T], [K]; +[4,T] with a residual loss), their 3 backward mirrors and one
 flat gradient all-reduce (~12k floats) — all latency-bound, a few µs each over xGMI.
 
-Local towers on a GPU run on the native engine (``EngineTowers``; one engine per rank holding
-the rank's three split shards): the LSTM, the SDF tower and the moment network are the engine's
-fused MFMA kernels, and the cross-sectional remainder (zero mean, P_t, E, losses: [T]- and
-[N_r, K]-sized tensors) stays in torch around the all-reduces. Autograd enters the engine at
-two points -- the raw SDF weights w[t, i] and the moment sums E[k, i] = Σ_t h q / T_i (the only
-way the moments reach any loss) -- and leaves through ``Engine.xs_backward``, which recomputes
-the rank's forward and runs the engine's tower backward from the external dL/dw or
-(dL/dE, global SDF_t). On CPU (or ``engine=False``) the towers are PyTorch ops.
+Two executors:
+
+* ``train_3phase_xsection_engine`` (GPU production path, ``XSEngine``): the WHOLE epoch runs in
+  the native engine of each rank -- towers, loss passes, tower backward, BPTT, clip + Adam, the
+  evaluations and the bookkeeping -- and the engine calls back at each cross-sectional coupling
+  so the rank-local sums are all-reduced on the engine stream, one collective per coupling.
+  Phases 1 / 3 use the Gram-form losses, so a training epoch exchanges only the period sums
+  ([T] + [3T] per split) and one packed gradient vector; the Gram matrices are all-reduced once
+  per moment refresh.
+* ``train_3phase_xsection`` (any device): the CPU trainer's loop over ``XSectionGAN``, whose local
+  towers run on the native engine (``EngineTowers``) or as PyTorch ops, with the cross-sectional
+  remainder (zero mean, P_t, E, losses: [T]- and [N_r, K]-sized tensors) in torch around the
+  all-reduces. Autograd enters the engine at two points -- the raw SDF weights w[t, i] and the
+  moment sums E[k, i] = Σ_t h q / T_i -- and leaves through ``Engine.xs_backward``, which
+  recomputes the rank's forward and runs the engine's tower backward from the external dL/dw or
+  (dL/dE, global SDF_t). On CPU (or ``engine=False``) the towers are PyTorch ops.
 """
 from __future__ import annotations
 

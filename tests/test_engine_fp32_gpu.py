@@ -104,6 +104,13 @@ BRANCHES = {
     "no_lstm_raw_macro": {"use_rnn": False},
     "lstm_2_layers": {"num_units_rnn": [3, 4]},
     "moment_hidden": {"hidden_dim_moment": [16]},
+    # the paper grid's axes (`parallel/sweep.py` GRID): SDF depth 3 / 4 at width
+    # 64, SMV = 8 LSTM units, 32 moment conditions, a 32-wide moment hidden layer
+    "paper_hl3": {"hidden_dim": [64] * 3, "num_layers": 3},
+    "paper_hl4": {"hidden_dim": [64] * 4, "num_layers": 4},
+    "paper_smv8": {"num_units_rnn": [8], "num_layers_rnn": 1},
+    "paper_cm32": {"num_condition_moment": 32},
+    "paper_moment_hidden32": {"hidden_dim_moment": [32], "num_layers_moment": 1},
 }
 
 

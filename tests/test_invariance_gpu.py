@@ -163,6 +163,34 @@ def test_fused_backward_tail_equals_separate_kernels(big, monkeypatch):
         _same(ref[s], res[s])
 
 
+@pytest.mark.parametrize("rnn", [[8], [4, 4], [8, 8]])
+def test_fused_backward_tail_other_lstm_shapes(big, monkeypatch, rnn):
+    """The fused tail beyond one layer of width 4 (the paper grid's SMV = 8 and
+    stacked LSTMs): k_lstm_bwd's serial chain inside the tail launch -- bits of the separate
+    kernels -- and the split epoch graphs with the update in the tail on top of it."""
+    cfg = default_cli_config(178, 46, rnn_dim=rnn, dropout=0.05)
+    ph = ((1, 3), (2, 2), (3, 3))
+    monkeypatch.setenv("DLAP_FUSED_TAIL", "0")
+    e0, ref = _train(big, cfg, [61, 62], 2, phases=ph)
+    assert not e0.eng.fused_info()["fused_tail"]
+    monkeypatch.setenv("DLAP_FUSED_TAIL", "1")
+    monkeypatch.setenv("DLAP_SPLIT_GRAPHS", "0")
+    monkeypatch.setenv("DLAP_TAIL_ADAM", "0")
+    e1, res = _train(big, cfg, [61, 62], 2, phases=ph)
+    info = e1.eng.fused_info()
+    assert info["fused_tail"] and not info["adam_in_tail"], info
+    for s in (61, 62):
+        _same(ref[s], res[s])
+    monkeypatch.setenv("DLAP_SPLIT_GRAPHS", "1")
+    monkeypatch.setenv("DLAP_TAIL_ADAM", "1")
+    e2, res2 = _train(big, cfg, [61, 62], 2, phases=ph)
+    info = e2.eng.fused_info()
+    if rnn[0] == 8 and len(rnn) == 1:        # the paper grid's SMV = 8 runs the production pipeline
+        assert info["split_graphs"] and info["adam_in_tail"], info
+    for s in (61, 62):
+        _same(ref[s], res2[s])
+
+
 def test_adam_in_tail_equals_k_adam(big, monkeypatch):
     """The pipelined epoch's update in the backward tail's last blocks (waiting in-kernel for
     every gradient writer and for the evaluation branch's bookkeeping signal, the branches joined
