@@ -246,6 +246,8 @@ class Engine {
     tail_adam_ = env_int("DLAP_TAIL_ADAM", 1) != 0;
     tail_adam_pipe_ = env_int("DLAP_TAIL_ADAM", 1) == 2;
     split_graphs_ = env_int("DLAP_SPLIT_GRAPHS", 1) != 0;
+    mom_tail_ = env_int("DLAP_MOM_TAIL", 1) != 0;
+    p2_lstm_cache_ = env_int("DLAP_P2_LSTM_CACHE", 1) != 0;
     unroll_ = std::max(1, env_int("DLAP_UNROLL", 8));
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
                residual, fp32);
@@ -674,6 +676,17 @@ class Engine {
     cur_phase_ = phase;
     if (phase == 2) h_valid_ = false;
     else ensure_moments(true, pipe && use_graph);
+    // phase 2: the frozen SDF's LSTM state (no inter-layer dropout) is the same every epoch --
+    // computed once here, the epochs project only the moment network's bias table
+    if (phase == 2 && p2_lstm_cached()) {
+      HTRACE("launch_prologue(phase-2 LSTM, once)");
+      launch_prologue(as<RnnJob>(j_rnn_train_), G_, splits_[0].T, dd(), md_, st_, false, true);
+      lstm_once_ = true;
+    }
+    struct OnceScope {
+      bool& f;
+      ~OnceScope() { f = false; }
+    } once_scope{lstm_once_};
     struct GramScope {                    // epoch graphs run the loss in Gram mode
       bool& f;
       explicit GramScope(bool& x) : f(x) { f = true; }
@@ -688,7 +701,7 @@ class Engine {
     // host ~one epoch, and the wait is not per executor, profiles/r4_hostgaps_short.txt -- and
     // unrolling several pipelined epochs into one graph: both 2-5% slower.)
     if (!pipe) {
-      hipGraphExec_t g = graph_for(graph_key(phase, lr, ignore_epoch, sel, 200),
+      hipGraphExec_t g = graph_for(graph_key(phase, lr, ignore_epoch, sel, 200 + 10 * (int)lstm_once_ + (int)mom_tail_on(phase)),
                                    [&] { enqueue_epoch(phase, lr, ignore_epoch, sel); });
       for (int e = 0; e < n; ++e) HIP_OK(hipGraphLaunch(g, st_));
       return;
@@ -1240,6 +1253,8 @@ class Engine {
     }
     d["eval_per_model"] = ne_per_model();
     d["fused_tail"] = tail_fused(1);
+    d["mom_tail"] = mom_tail_on(2);
+    d["p2_lstm_cached"] = p2_lstm_cached();
     d["adam_in_tail"] = adam_in_tail(1) && pipeline_ && eval_rnn_in_fwd(1) && (split_graphs(1) || tail_adam_pipe_);
     d["split_graphs"] = split_graphs(1) && pipeline_;
     d["host_launch_us_per_epoch"] = host_launch_n_ ? 1e6 * host_launch_s_ / host_launch_n_ : 0.0;
@@ -1981,6 +1996,7 @@ class Engine {
     if (selfproj) {}
     else if (eval_rnn) launch_proj(as<RnnJob>(j_rnn_all_), G_ + n_eval_jobs_, tmax_fwd_all(), dd(), md_, st_, train_mom(phase));
     else if (fused) launch_proj(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_, train_mom(phase));
+    else if (phase == 2 && lstm_once_) launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_, true, false);
     else launch_prologue(as<RnnJob>(j_rnn_train_), G_, D.T, dd(), md_, st_, train_mom(phase));
     // pipelined epoch, train_first_ == 2: the evaluation branch's LSTM prologue is enqueued right
     // behind the training one, so its (serial, few-CU) recurrence starts at the epoch start
@@ -2017,7 +2033,7 @@ class Engine {
       HTRACE("launch_period_bwd(gram)");
       launch_period_bwd(lj, G_, D.T, st_);
     }
-    if (tail_metrics_ && phase != 2) {
+    if ((tail_metrics_ && phase != 2) || mom_tail(phase)) {
       // the train split's metrics are computed by the backward tail (enqueue_train_tail)
     } else if (defer_metrics && phase != 2) {
       HIP_OK(hipEventRecord(ev_mid_, st_));
@@ -2049,6 +2065,22 @@ class Engine {
   // (one more block of k_lstm_tail; a launch after the tail where it is not fused) instead of on
   // the evaluation branch, so the training chain forks only once (after the fused forward)
   bool tail_metrics_ = false;
+  // Phase 2 (enqueue_epoch): k_finalize -> k_wgrad -> k_adam and the train metrics as ONE launch
+  // (k_lstm_tail, phase 2: the per-period sums relayed to the W_macro helpers, the moment
+  // network's clip + Adam in the last blocks), DLAP_MOM_TAIL
+  bool mom_tail_ = true;
+  bool mom_adam_ = false;                    // set around enqueue_train_grads (enqueue_epoch)
+  bool mom_tail_on(int phase) const {
+    return phase == 2 && mom_tail_ && !xs_on_ && inv_code_.p != nullptr && splits_[0].set &&
+           mom_tail_supported(md_, splits_[0].T);
+  }
+  bool mom_tail(int phase) const { return mom_adam_ && mom_tail_on(phase); }
+  // phase 2: the LSTM recurrence once per run_epochs call (DLAP_P2_LSTM_CACHE)
+  bool p2_lstm_cache_ = true;
+  bool lstm_once_ = false;
+  bool p2_lstm_cached() const {
+    return p2_lstm_cache_ && md_.nrnn > 0 && (md_.nrnn == 1 || md_.dropout == 0.f) && !xs_on_;
+  }
   bool tail_fused(int phase) const {
     return fused_tail_ && !xs_on_ && phase != 2 && splits_[0].set && lstm_tail_supported(md_, splits_[0].T);
   }
@@ -2104,6 +2136,12 @@ class Engine {
   }
   void enqueue_train_tail(int phase) {
     const SplitDev& D = splits_[0];
+    if (mom_tail(phase)) {
+      HTRACE("launch_lstm_tail(phase 2)");
+      launch_lstm_tail(as<UpdJob>(j_upd_), as<FinJob>(j_fin_), G_, dd(), md_, D.T, slab_stride(), st_,
+                       loss_tab(2, false), 1, tail_lr_, 2);
+      return;
+    }
     const LossJob* lm = tail_metrics_ && phase != 2 ? loss_tab(phase, use_gram(phase)) : nullptr;
     if (tail_fused(phase)) {
       HTRACE("launch_lstm_tail");
@@ -2175,9 +2213,15 @@ class Engine {
   }
   // sequential epoch: train step, evaluation, bookkeeping
   void enqueue_epoch(int phase, float lr, int ignore_epoch, float sel) {
+    const bool mt = mom_tail_on(phase);
+    mom_adam_ = mt;
+    tail_lr_ = lr;
     enqueue_train_grads(phase);
-    HTRACE("launch_update");
-    launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_, inv_code_.p != nullptr);
+    mom_adam_ = false;
+    if (!mt) {
+      HTRACE("launch_update");
+      launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_, inv_code_.p != nullptr);
+    }
     if (phase != 2) { SoloScope solo(eval_solo_); enqueue_eval(st_); }
     enqueue_epoch_end(phase, ignore_epoch, sel, st_);
   }

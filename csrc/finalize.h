@@ -142,7 +142,8 @@ DLAP_DEV void finalize_block(const FinJob& J, const ModelDesc* __restrict__ md, 
   if (rg == 0 && d < D) {
     float tot = 0.f;
     for (int g = 0; g < nrg; ++g) tot += seg[g * Dp + d];
-    if (mom) gp(J.dab)[t * 64 + d] = tot;      // (row stride 64)
+    if (mom && ctr) __hip_atomic_store(gp(J.dab) + t * 64 + d, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if (mom) gp(J.dab)[t * 64 + d] = tot;      // (row stride 64)
     else if (ctr) __hip_atomic_store(gp(J.dpp) + t * D + d, tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else gp(J.dpp)[t * D + d] = tot;
   }

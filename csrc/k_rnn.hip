@@ -1060,10 +1060,11 @@ __global__ __launch_bounds__(256) void k_lstm_bwd(const UpdJob* __restrict__ job
 // and before any gate-gradient load (the fused tail's helpers wait for the hand-off there, with
 // their constant operands already in flight); returns false to abandon the block (block-uniform).
 struct NoWait { DLAP_DEV bool operator()() const { return true; } };
+// red: [4][GT][64] f32x4 of LDS (the fused tail passes its dynamic LDS)
 template <int GT, typename BeforeDG = NoWait>
-DLAP_DEV void wgrad_block(const UpdJob& J, const ModelDesc* __restrict__ md, int phase, int cblk,
+DLAP_DEV void wgrad_block(const UpdJob& J, const ModelDesc* __restrict__ md, int phase, int cblk, f32x4* red_,
                           int* done = nullptr, int ndone = 0, BeforeDG before_dg = NoWait{}) {
-  __shared__ f32x4 red[4][GT][64];
+  auto red = reinterpret_cast<f32x4 (*)[GT][64]>(red_);
   const int T = J.T, M = md->M;
   const bool mom = phase == 2;
   const int G = mom ? md->m[0].out : 4 * md->H;
@@ -1143,7 +1144,8 @@ DLAP_DEV void wgrad_block(const UpdJob& J, const ModelDesc* __restrict__ md, int
 template <int GT>
 __global__ __launch_bounds__(256) void k_wgrad(const UpdJob* __restrict__ jobs,
                                                const ModelDesc* __restrict__ md, int phase) {
-  wgrad_block<GT>(jobs[blockIdx.y], md, phase, blockIdx.x);
+  __shared__ f32x4 red[4][GT][64];
+  wgrad_block<GT>(jobs[blockIdx.y], md, phase, blockIdx.x, &red[0][0][0]);
 }
 
 // Adam in the fused tail (adam = 2): every block, its own work done, arrives on the model's
@@ -1159,7 +1161,7 @@ __global__ __launch_bounds__(256) void k_wgrad(const UpdJob* __restrict__ jobs,
 // (no update; the host raises). The waiting blocks are the last to arrive, so every block they
 // wait for has been dispatched ahead of them or is next in line.
 DLAP_DEV void tail_adam(const UpdJob& U, const ModelDesc* __restrict__ md, float lr, int nb, int step_pre,
-                        int drop_pre) {
+                        int drop_pre, int phase, bool evgen) {
   __shared__ unsigned s_ord;
   __shared__ int s_go;
   __shared__ float red[4];
@@ -1168,13 +1170,13 @@ DLAP_DEV void tail_adam(const UpdJob& U, const ModelDesc* __restrict__ md, float
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0)
-    s_ord = __hip_atomic_fetch_add(reinterpret_cast<unsigned*>(U.tail_ctr + TAIL_ARRIVE), 1u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+    s_ord = __hip_atomic_fetch_add(reinterpret_cast<unsigned*>(U.tail_ctr + (phase == 2 ? TAIL_ARRIVE2 : TAIL_ARRIVE)),
+                                   1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   const unsigned k = s_ord / (unsigned)nb, ord = s_ord - k * (unsigned)nb;
   const bool tsm = blockIdx.y == 0;
   RNN_TS(18, tsm && ord == (unsigned)nb - 1);                       // the last arrival
-  const int nadam = (md->P_sdf + ADAM_PB - 1) / ADAM_PB;
+  const int nadam = ((phase == 2 ? md->P - md->P_sdf : md->P_sdf) + ADAM_PB - 1) / ADAM_PB;
   const int bx = (int)ord - (nb - nadam);
   if (bx < 0) return;
   auto wait = [&]() -> bool {
@@ -1182,14 +1184,14 @@ DLAP_DEV void tail_adam(const UpdJob& U, const ModelDesc* __restrict__ md, float
       bool ok = true;
       unsigned spins = 0;
       const unsigned all = (k + 1) * (unsigned)nb;
-      const int* arr = U.tail_ctr + TAIL_ARRIVE;
+      const int* arr = U.tail_ctr + (phase == 2 ? TAIL_ARRIVE2 : TAIL_ARRIVE);
       while ((unsigned)__builtin_amdgcn_readfirstlane(__hip_atomic_load(arr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) - all >
              0x7fffffffu) {                                            // (wrap-safe "count < all")
         if (spins++ >= U.spin_limit) { ok = false; break; }
         __builtin_amdgcn_s_sleep(2);
       }
       const int* gen = U.tail_ctr + TAIL_EVGEN;
-      while (ok && (unsigned)__builtin_amdgcn_readfirstlane(__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) -
+      while (ok && evgen && (unsigned)__builtin_amdgcn_readfirstlane(__hip_atomic_load(gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) -
                            (k + 1) > 0x7fffffffu) {
         if (spins++ >= U.spin_limit) { ok = false; break; }
         __builtin_amdgcn_s_sleep(2);
@@ -1206,7 +1208,7 @@ DLAP_DEV void tail_adam(const UpdJob& U, const ModelDesc* __restrict__ md, float
     RNN_TS(19, tsm && bx == 0);                                      // Adam block 0 released
     return s_go != 0;
   };
-  adam_block(U, md, 1, lr, bx, nadam, red, wait, step_pre, drop_pre);
+  adam_block(U, md, phase, lr, bx, nadam, red, wait, step_pre, drop_pre);
   RNN_TS(20, tsm && bx == nadam - 1);
 }
 
@@ -1227,20 +1229,46 @@ DLAP_DEV void tail_adam(const UpdJob& U, const ModelDesc* __restrict__ md, float
 template <int HM>
 __global__ __launch_bounds__(256, 2) void k_lstm_tail(const UpdJob* __restrict__ ujobs, const FinJob* __restrict__ fjobs,
                                                    const ModelDesc* __restrict__ md, int slab_stride, int nslab_blocks,
-                                                   const LossJob* __restrict__ ljobs, int adam, float lr) {
+                                                   const LossJob* __restrict__ ljobs, int adam, float lr, int phase) {
   extern __shared__ __attribute__((aligned(16))) float sm[];
   const UpdJob& U = ujobs[blockIdx.y];
   const FinJob& F = fjobs[blockIdx.y];
   const int b = (int)blockIdx.x - 1;
   const int nwg = (md->M + 1 + 15) / 16;
+  const bool mom = phase == 2;
   __shared__ int s_steps[2];          // (adam) the step counters before this launch's update
-  if (adam && threadIdx.x == 0) { s_steps[0] = gp(U.adam_step)[0]; s_steps[1] = gp(U.drop_step)[0]; }
-  if (b < 0) {
+  if (adam && threadIdx.x == 0) { s_steps[0] = gp(U.adam_step)[mom ? 1 : 0]; s_steps[1] = gp(U.drop_step)[0]; }
+  if (b < 0 && mom) {
+    // phase 2 (no BPTT): relay the per-period blocks' count to the W_macro helpers -- wait for all
+    // T (relaxed polls, bounded, one agent acquire), rearm the count, raise the flag
+    __shared__ int bad;
+    if (threadIdx.x < 64) {
+      const int* ctr = U.tail_ctr + TAIL_CNT;
+      unsigned spins = 0;
+      bool ok = true;
+      while (__builtin_amdgcn_readfirstlane(__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) < U.T) {
+        if (spins++ >= U.spin_limit) { ok = false; break; }
+        __builtin_amdgcn_s_sleep(2);
+      }
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (threadIdx.x == 0) {
+        bad = ok ? 0 : 1;
+        if (!ok) atomicAdd(const_cast<int*>(U.prog) + 1, 1);      // poison: no update, the host raises
+        else {
+          __hip_atomic_store(U.tail_ctr + TAIL_CNT, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+          __hip_atomic_store(U.tail_ctr + TAIL_FLAG, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+    __syncthreads();
+  } else if (b < 0) {
     lstm_bwd_body<HM, true>(U, md, 1, sm, blockIdx.y == 0);
   } else if (b < U.T) {
-    finalize_block(F, md, 1, slab_stride, nslab_blocks + b, U.tail_ctr + TAIL_CNT);
+    finalize_block(F, md, phase, slab_stride, nslab_blocks + b, U.tail_ctr + TAIL_CNT);
   } else if (b < U.T + nslab_blocks) {
-    finalize_block(F, md, 1, slab_stride, b - U.T);
+    finalize_block(F, md, phase, slab_stride, b - U.T);
   } else if (b >= U.T + nslab_blocks + nwg) {      // the train split's job metrics
     if (ljobs) job_metrics_body<256>(ljobs[blockIdx.y], sm + DLAP_MAX_T, sm);
   } else {
@@ -1267,10 +1295,14 @@ __global__ __launch_bounds__(256, 2) void k_lstm_tail(const UpdJob* __restrict__
       __syncthreads();
       return bad == 0;
     };
-    wgrad_block<HM == 4 ? 1 : 2>(U, md, 1, cblk, U.tail_ctr + TAIL_DONE, nwg, wait_dg);   // 4H gates
+    f32x4* red = reinterpret_cast<f32x4*>(sm);
+    const int G = mom ? md->m[0].out : 4 * md->H;         // gate / moment layer-0 columns
+    if (G <= 16) wgrad_block<1>(U, md, phase, cblk, red, U.tail_ctr + TAIL_DONE, nwg, wait_dg);
+    else if (G <= 32) wgrad_block<2>(U, md, phase, cblk, red, U.tail_ctr + TAIL_DONE, nwg, wait_dg);
+    else wgrad_block<4>(U, md, phase, cblk, red, U.tail_ctr + TAIL_DONE, nwg, wait_dg);
     if (blockIdx.y == 0 && cblk == nwg - 1 && threadIdx.x == 0) g_rnn_ts[17] = wall_clock64();
   }
-  if (adam) tail_adam(U, md, lr, gridDim.x, s_steps[0], s_steps[1]);
+  if (adam) tail_adam(U, md, lr, gridDim.x, s_steps[0], s_steps[1], phase, adam == 2);
 }
 
 // whether the fused tail applies (phases 1 / 3; LSTM widths up to 8, any depth); its LDS bytes:
@@ -1290,9 +1322,14 @@ bool lstm_tail_supported(const ModelDesc& mh, int T) {
   return lstm_tail_lds_bytes(mh, T) + 6400 <= lim;
 }
 int lstm_tail_words() { return TAIL_WORDS; }
-static size_t tail_dyn_lds(const ModelDesc& mh, int T) {
-  // (the metrics block keeps its scratch in the dynamic LDS: DLAP_MAX_T + 4 floats)
-  return std::max(lstm_tail_lds_bytes(mh, T), (size_t)(DLAP_MAX_T + 4) * sizeof(float));
+static size_t tail_dyn_lds(const ModelDesc& mh, int T, int phase = 1) {
+  // (the metrics block keeps its scratch in the dynamic LDS: DLAP_MAX_T + 4 floats; the W_ih /
+  // W_macro helpers their [4][GT][64] f32x4 partial tiles, GT <= 4)
+  const size_t small = std::max((size_t)(DLAP_MAX_T + 4) * sizeof(float), (size_t)4 * 4 * 64 * 16);
+  return phase == 2 ? small : std::max(lstm_tail_lds_bytes(mh, T), small);
+}
+bool mom_tail_supported(const ModelDesc& mh, int T) {
+  return mh.M > 0 && mh.m[0].out <= 64 && T >= 1;
 }
 int lstm_tail_capacity(const ModelDesc& mh, int T) {
   const size_t sh = tail_dyn_lds(mh, T);
@@ -1304,15 +1341,17 @@ int lstm_tail_capacity(const ModelDesc& mh, int T) {
   return per_cu * ncu;
 }
 void launch_lstm_tail(const UpdJob* ujobs, const FinJob* fjobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
-                      int T, int slab_stride, hipStream_t st, const LossJob* ljobs, int adam, float lr) {
-  const int nslab_blocks = mh.ntile_s * 64 + (SLAB_EXTRA + 63) / 64;
+                      int T, int slab_stride, hipStream_t st, const LossJob* ljobs, int adam, float lr, int phase) {
+  const int nslab_blocks = (phase == 2 ? mh.ntile_m : mh.ntile_s) * 64 + (SLAB_EXTRA + 63) / 64;
   const int nwg = (mh.M + 1 + 15) / 16;
-  const size_t sh = tail_dyn_lds(mh, T);
+  const size_t sh = tail_dyn_lds(mh, T, phase);
   const dim3 grid(1 + T + nslab_blocks + nwg + (ljobs ? 1 : 0), njobs);
   if (mh.H <= 4)
-    hipLaunchKernelGGL(k_lstm_tail<4>, grid, dim3(256), sh, st, ujobs, fjobs, md, slab_stride, nslab_blocks, ljobs, adam, lr);
+    hipLaunchKernelGGL(k_lstm_tail<4>, grid, dim3(256), sh, st, ujobs, fjobs, md, slab_stride, nslab_blocks, ljobs, adam, lr,
+                       phase);
   else
-    hipLaunchKernelGGL(k_lstm_tail<8>, grid, dim3(256), sh, st, ujobs, fjobs, md, slab_stride, nslab_blocks, ljobs, adam, lr);
+    hipLaunchKernelGGL(k_lstm_tail<8>, grid, dim3(256), sh, st, ujobs, fjobs, md, slab_stride, nslab_blocks, ljobs, adam, lr,
+                       phase);
   HIP_OK(hipGetLastError());
 }
 

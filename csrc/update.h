@@ -14,7 +14,8 @@ struct ModelDesc;
 #define TAIL_DONE 64
 #define TAIL_ARRIVE 96
 #define TAIL_EVGEN 128
-#define TAIL_WORDS 160         // max packed copies of one parameter for k_adam's fused re-pack
+#define TAIL_ARRIVE2 160       // (phase-2 tail launches: their own running arrival count)
+#define TAIL_WORDS 192         // max packed copies of one parameter for k_adam's fused re-pack
 
 struct FinJob {            // one model
   const float* slab;       // first slab of this model (slices contiguous, gx slabs each)
@@ -114,10 +115,15 @@ int lstm_tail_capacity(const ModelDesc& mh, int T);
 struct LossJob;
 // ljobs: the train split's loss jobs whose job metrics one more block per model computes (or nullptr)
 // adam: 0 = none (k_adam follows); 2 = the update runs in the tail (the launch's last blocks,
-// adam_block) after the epoch's evaluation branch signalled (launch_epoch_end)
+// adam_block) after the epoch's evaluation branch signalled (launch_epoch_end); 1 = the same
+// without that signal (phase 2: nothing else reads the parameters during the epoch)
+// phase 2: the moment network's tail -- k_finalize + k_wgrad (the macro columns of moment layer
+// 0) [+ k_adam]; block 0 relays the per-period sums' count to the W_macro helpers (no BPTT)
 void launch_lstm_tail(const UpdJob* ujobs, const FinJob* fjobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
                       int T, int slab_stride, hipStream_t st, const LossJob* ljobs = nullptr, int adam = 0,
-                      float lr = 0.f);
+                      float lr = 0.f, int phase = 1);
+// whether the phase-2 tail applies (macro columns in moment layer 0)
+bool mom_tail_supported(const ModelDesc& mh, int T);
 void launch_pack(float* const* params_unused, const UpdJob* jobs, int njobs, const ModelDesc* md,
                  const ModelDesc& mh, hipStream_t st);
 int pack_total(const ModelDesc& mh);   // packed elements per model (k_pack's element space)

@@ -191,6 +191,28 @@ def test_fused_backward_tail_other_lstm_shapes(big, monkeypatch, rnn):
         _same(ref[s], res2[s])
 
 
+@pytest.mark.parametrize("rnn,mom_hidden", [([4], []), ([8], [32]), ([4, 4], [])])
+def test_phase2_tail_and_lstm_once_equal_separate_kernels(big, monkeypatch, rnn, mom_hidden):
+    """Phase 2 as [k_proj (moment bias table)] -> towers -> losses -> moment backward -> ONE tail
+    launch (per-period sums, the W_macro gradient, the train metrics and the moment network's
+    clip + Adam) with the frozen SDF's LSTM state computed once per run instead of every epoch:
+    the bits of k_finalize -> k_wgrad -> k_adam with the recurrence in every epoch."""
+    cfg = default_cli_config(178, 46, rnn_dim=rnn, hidden_dim_moment=mom_hidden, dropout=0.05)
+    ph = ((1, 2), (2, 5), (3, 2))
+    monkeypatch.setenv("DLAP_MOM_TAIL", "0")
+    monkeypatch.setenv("DLAP_P2_LSTM_CACHE", "0")
+    e0, ref = _train(big, cfg, [91, 92], 2, phases=ph)
+    info = e0.eng.fused_info()
+    assert not info["mom_tail"] and not info["p2_lstm_cached"], info
+    monkeypatch.setenv("DLAP_MOM_TAIL", "1")
+    monkeypatch.setenv("DLAP_P2_LSTM_CACHE", "1")
+    e1, res = _train(big, cfg, [91, 92], 2, phases=ph)
+    info = e1.eng.fused_info()
+    assert info["mom_tail"] and info["p2_lstm_cached"] == (len(rnn) == 1), info
+    for s in (91, 92):
+        _same(ref[s], res[s])
+
+
 def test_adam_in_tail_equals_k_adam(big, monkeypatch):
     """The pipelined epoch's update in the backward tail's last blocks (waiting in-kernel for
     every gradient writer and for the evaluation branch's bookkeeping signal, the branches joined
