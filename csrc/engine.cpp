@@ -241,6 +241,7 @@ class Engine {
     prog_limit_ = (unsigned)env_int("DLAP_PROG_SPIN_LIMIT", 1 << 22);
     fused_p2_ = env_int("DLAP_FUSED_PHASE2", 0) != 0;
     eval_in_fwd_ = env_int("DLAP_EVAL_IN_FWD", 1) != 0;
+    eval_sep_ = env_int("DLAP_EVAL_SEP", 0) != 0;
     fused_tail_ = env_int("DLAP_FUSED_TAIL", 1) != 0;
     self_proj_ = env_int("DLAP_SELF_PROJ", 1) != 0;
     tail_adam_ = env_int("DLAP_TAIL_ADAM", 1) != 0;
@@ -768,6 +769,20 @@ class Engine {
     HTRACE("run_epochs done");
   }
   void set_pipeline(bool on) { pipeline_ = on; }
+  // Safe mode (the runner's fallback after a spin wait gave up): no in-kernel
+  // wait on work of another launch or queue -- no fused LSTM + tower forward, no split epoch
+  // graphs, no Adam in the tail (waits inside one launch on lower-numbered, already dispatched
+  // blocks stay). The graphs are rebuilt.
+  void set_safe_mode(bool on) {
+    safe_mode_ = on;
+    rnn_overlap_ = on ? false : env_int("DLAP_RNN_OVERLAP", 1) != 0;
+    split_graphs_ = on ? false : env_int("DLAP_SPLIT_GRAPHS", 1) != 0;
+    tail_adam_ = on ? false : env_int("DLAP_TAIL_ADAM", 1) != 0;
+    // the waits left (inside one launch, on blocks dispatched ahead) get the default patience
+    if (on) prog_limit_ = std::max(prog_limit_, 1u << 22);
+    graphs_dirty_ = true;
+  }
+  bool safe_mode_ = false;
   // job tables (and the fused launches' co-residency capacities) current
   void ensure_jobs() { if (graphs_dirty_) { rebuild_jobs(); graphs_dirty_ = false; } }
 
@@ -1192,7 +1207,8 @@ class Engine {
   }
   int train_fwd_grid(int phase) const { return phase == 2 ? gx_fwd_[0] : gx_fwd13_; }
   bool fused_eval() const {
-    return rnn_overlap_ && (rnn_overlap_eval_ || eval_solo_) && md_.nrnn > 0 && !md_.md.wide && n_eval_jobs_ > 0 &&
+    return rnn_overlap_ && (rnn_overlap_eval_ || eval_solo_ || eval_sep_now_) && md_.nrnn > 0 && !md_.md.wide &&
+           n_eval_jobs_ > 0 &&
            mlp_fwd_rnn_supported(md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, tmax_eval_) &&
            fused_grid(eval_grid(), n_eval_jobs_, cap_eval_) > 0;
   }
@@ -1257,6 +1273,7 @@ class Engine {
     d["p2_lstm_cached"] = p2_lstm_cached();
     d["adam_in_tail"] = adam_in_tail(1) && pipeline_ && eval_rnn_in_fwd(1) && (split_graphs(1) || tail_adam_pipe_);
     d["split_graphs"] = split_graphs(1) && pipeline_;
+    d["eval_sep"] = split_graphs(1) && pipeline_ && sep_eval(1);
     d["host_launch_us_per_epoch"] = host_launch_n_ ? 1e6 * host_launch_s_ / host_launch_n_ : 0.0;
     // backward launch shape: fine slabs per model (R-only partition), fine slabs per workgroup
     d["bwd_nfine"] = nfine_; d["bwd_fpw"] = fpw_;
@@ -1675,7 +1692,9 @@ class Engine {
     J.dE = (phase == 2 || phase == 3) ? W.dE.p : nullptr;
     J.dEu = phase == 1 ? W.dEu.p : nullptr;
     J.part = W.part.p; J.pe = W.pe.p; J.pu = W.pu.p; J.dw = W.dw.p; J.rstat = W.rstat.p; J.scal = W.scal.p;
-    if (s == 0 && phase > 0) J.prog_reset = prog_ptr(g, 0);
+    // the fused forward's progress counter of the (model, split), rearmed by the period pass that
+    // follows it (train split; evaluation splits: the fused evaluation forward)
+    if ((s == 0 && phase > 0) || s > 0) J.prog_reset = prog_ptr(g, s);
     if (gram) {
       J.gram = 1; J.G = W.gram.p; J.gpart = W.gpart.p;
       J.asset_full = 0;
@@ -2115,22 +2134,51 @@ class Engine {
   long host_launch_n_ = 0;                   // ... over this many epochs (fused_info)
   int* fwd_esig_ = nullptr;                  // set around enqueue_train_grads (enqueue_chain_split)
   bool split_graphs(int phase) const {
-    return split_graphs_ && adam_in_tail(phase) && eval_rnn_in_fwd(phase);
+    return split_graphs_ && adam_in_tail(phase) && (sep_eval(phase) || eval_rnn_in_fwd(phase));
+  }
+  // Split epoch graphs with the evaluation recurrences on the evaluation queue (DLAP_EVAL_SEP):
+  // the training chain's fused forward runs the train recurrence only; the evaluation graph waits
+  // for the previous update (k_wait_gen) and runs its own fused LSTM + tower forward (the
+  // recurrences project their inputs, the towers trail the published periods). Bitwise equal to
+  // the default; measured slower on the bench panel (0.153 vs 0.142 ms steady,
+  // profiles/r6_eval_sep_ab.txt: the train-only fused forward still takes ~42 us, so it was not
+  // bound by the evaluation recurrences, and the evaluation graph's own fused launch contends
+  // with the chain) -- off by default.
+  bool eval_sep_ = false;
+  bool eval_sep_now_ = false;                // set around enqueue_eval_split (fused_eval)
+  bool eval_selfproj_ = false;
+  bool sep_eval(int phase) const {
+    if (!eval_sep_ || phase == 2 || n_eval_jobs_ == 0 || !fused_fwd(phase) || md_.nrnn == 0 || md_.md.wide) return false;
+    return mlp_fwd_rnn_supported(md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, tmax_eval_) &&
+           fused_grid(eval_grid(), n_eval_jobs_, cap_eval_) > 0;
   }
   void enqueue_chain_split(int phase, float lr) {
     tail_metrics_ = true;
     tail_adam_mode_ = 2;
     tail_lr_ = lr;
-    fwd_esig_ = esync_.p;
-    enqueue_train_grads(phase, true, 0, false, true);
+    const bool sep = sep_eval(phase);
+    fwd_esig_ = sep ? nullptr : esync_.p;
+    enqueue_train_grads(phase, true, 0, false, !sep);
     tail_metrics_ = false;
     tail_adam_mode_ = 0;
     fwd_esig_ = nullptr;
   }
   void enqueue_eval_split(int phase, int ignore_epoch, float sel) {      // captured on st2_
-    HTRACE("launch_wait_count");
-    launch_wait_count(esync_.p, ne_per_model() * G_, prog_limit_, prog_.p, G_, st2_);
-    enqueue_eval_towers(st2_);
+    if (sep_eval(phase)) {
+      HTRACE("launch_wait_gen");
+      launch_wait_gen(as<UpdJob>(j_upd_), G_, prog_limit_, st2_);
+      eval_sep_now_ = true;
+      // the recurrences project their own inputs when the towers skip the moment network (cached
+      // moments); else k_proj first (gate projections + the moment bias table)
+      eval_selfproj_ = self_proj_ && h_cache_;
+      if (!eval_selfproj_) launch_proj(as<RnnJob>(j_rnn_eval_), n_eval_jobs_, tmax_eval_, dd(), md_, st2_, !h_cache_);
+      enqueue_eval_towers(st2_);
+      eval_sep_now_ = eval_selfproj_ = false;
+    } else {
+      HTRACE("launch_wait_count");
+      launch_wait_count(esync_.p, ne_per_model() * G_, prog_limit_, prog_.p, G_, st2_);
+      enqueue_eval_towers(st2_);
+    }
     enqueue_dropmask(phase, 1, st2_);
     enqueue_epoch_end(phase, ignore_epoch, sel, st2_, 1);
   }
@@ -2187,7 +2235,7 @@ class Engine {
       HTRACE("launch_mlp_fwd");
       if (fused_eval())
         launch_mlp_fwd_rnn(as<MlpJob>(j_mlp_eval_), as<RnnJob>(j_rnn_eval_), dd(), n_eval_jobs_, fused_eval_gx(),
-                           md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, tmax_eval_, st, h_cache_);
+                           md_.md, md_.KS1, md_.WMB, md_.H, md_.nrnn, tmax_eval_, st, h_cache_, 0, eval_selfproj_);
       else
         launch_mlp_fwd(as<MlpJob>(j_mlp_eval_), n_eval_jobs_, gx, md_.md, md_.KS1, md_.WMB, st, h_cache_);
     }
@@ -2230,6 +2278,8 @@ class Engine {
     enqueue_dropmask(phase, 1, st_);                     // masks of the first pipelined epoch
     HTRACE("launch_update");
     launch_update(as<UpdJob>(j_upd_), G_, dd(), md_, phase, lr, st_, inv_code_.p != nullptr);
+    // (k_adam does not count as a tail update: the first evaluation graph's wait passes)
+    if (split_graphs(phase) && sep_eval(phase)) launch_gen_sync(as<UpdJob>(j_upd_), G_, st_);
   }
   // One-graph pipelined epoch (the split graphs' fallback: DLAP_SPLIT_GRAPHS=0, the update outside
   // the tail, or no fused forward): the training chain on st_, the evaluation branch forked
@@ -2430,6 +2480,7 @@ PYBIND11_MODULE(_dlap_hip, m) {
       .def("history", &Engine::history)
       .def("run_epochs", &Engine::run_epochs, py::call_guard<py::gil_scoped_release>())
       .def("set_pipeline", &Engine::set_pipeline)
+      .def("set_safe_mode", &Engine::set_safe_mode)
       .def("plan_phase", &Engine::plan_phase)
       .def("gram_plan", &Engine::gram_plan)
       .def("set_lr", &Engine::set_lr)

@@ -476,8 +476,9 @@ DLAP_DEV void lstm_bwd_body(const UpdJob& J, const ModelDesc* __restrict__ md, i
   const auto params = gp(J.params);
   const auto grads = gp(J.grads);
   RNN_TS(8, tsm);
-  // the dense-state BPTT: k_lstm_bwd with `scan` at H = 4; the fused tail for one layer of width 4
-  const bool dense = HM == 4 && H == 4 && (FUSED ? md->nrnn == 1 : scan != 0);
+  // the dense-state BPTT at H = 4: k_lstm_bwd with `scan`, the fused tail always (every layer; the
+  // same path and summation order as k_lstm_bwd, so both give the same bits)
+  const bool dense = HM == 4 && H == 4 && (FUSED || scan != 0);
   const LstmBwdLds LL = lstm_bwd_lds(T, H, dense && !FUSED, FUSED && dense);
   float* s_cf = sm + LL.cf;                    // [T][6][H] BPTT coefficients (pre-pass)
   float* s_h = sm + LL.h;                      // [T][H]  layer outputs
@@ -656,7 +657,7 @@ DLAP_DEV void lstm_bwd_body(const UpdJob& J, const ModelDesc* __restrict__ md, i
           dn[1] = hi;
         }
       }
-      if constexpr (FUSED) {
+      if (FUSED && late_d) {
         if (!wait_dpp()) return;                     // block-uniform; nothing written
         for (int i = threadIdx.x; i < T * H; i += 256) s_d[i] = dout[i];
         RNN_TS(16, tsm);
@@ -1029,6 +1030,12 @@ DLAP_DEV void lstm_bwd_body(const UpdJob& J, const ModelDesc* __restrict__ md, i
       }
       __threadfence_block();
     }
+    // (fused tail, stacked layers: the next layer rewrites the global step-matrix scratch this one
+    // read -- drop this CU's cached copies of it; the layer input gradient dx is read back, too)
+    if (FUSED && l > 0) {
+      __syncthreads();
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+    }
   }
   __syncthreads();
   if constexpr (FUSED) {
@@ -1209,6 +1216,18 @@ DLAP_DEV void tail_adam(const UpdJob& U, const ModelDesc* __restrict__ md, float
     return s_go != 0;
   };
   adam_block(U, md, phase, lr, bx, nadam, red, wait, step_pre, drop_pre);
+  if (evgen) {
+    // the update is complete once all nadam Adam blocks of the launch are: each counts itself
+    // (acq_rel: its stores released, the earlier counts' acquired); the last of the launch advances
+    // the model's update generation (release) -- the evaluation graph's k_wait_gen waits for it
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned prev = __hip_atomic_fetch_add(reinterpret_cast<unsigned*>(U.tail_ctr + TAIL_ADONE), 1u,
+                                                   __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if ((prev + 1u) % (unsigned)nadam == 0u)
+        __hip_atomic_fetch_add(U.tail_ctr + TAIL_UPDGEN, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
   RNN_TS(20, tsm && bx == nadam - 1);
 }
 
@@ -1307,7 +1326,7 @@ __global__ __launch_bounds__(256, 2) void k_lstm_tail(const UpdJob* __restrict__
 
 // whether the fused tail applies (phases 1 / 3; LSTM widths up to 8, any depth); its LDS bytes:
 // the dense-state map for one layer of width 4, else k_lstm_bwd's
-static bool tail_dense(const ModelDesc& mh) { return mh.nrnn == 1 && mh.H == 4; }
+static bool tail_dense(const ModelDesc& mh) { return mh.H == 4; }
 size_t lstm_tail_lds_bytes(const ModelDesc& mh, int T) {
   return lstm_bwd_lds(T, mh.H, false, tail_dense(mh)).total * sizeof(float);
 }

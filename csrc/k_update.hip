@@ -103,6 +103,48 @@ void launch_wait_count(int* cnt, int per, unsigned limit, int* prog, int nmodels
   HIP_OK(hipGetLastError());
 }
 
+// One wave; lane g (per 64 models) polls model g's update generation until it is one past what the
+// evaluation graph consumed (wrap-safe), then ONE agent acquire and the consumed counts advance.
+// Relaxed polls with s_sleep, bounded; a give-up poisons every model still waiting.
+__global__ __launch_bounds__(64) void k_wait_gen(const UpdJob* __restrict__ jobs, int njobs, unsigned limit) {
+  for (int g0 = 0; g0 < njobs; g0 += 64) {
+    const int g = g0 + (int)threadIdx.x;
+    const bool mine = g < njobs;
+    int* ctr = mine ? jobs[g].tail_ctr : nullptr;
+    const int want = mine ? gp(ctr)[TAIL_UPDSEEN] + 1 : 0;
+    unsigned spins = 0;
+    bool ok = true;
+    while (true) {
+      const bool done = !mine || __hip_atomic_load(ctr + TAIL_UPDGEN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want >= 0;
+      if (__all(done)) break;
+      if (spins++ >= limit) { ok = done; break; }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    asm volatile("" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    if (mine) {
+      gp(ctr)[TAIL_UPDSEEN] = want;
+      if (!ok) atomicAdd(const_cast<int*>(jobs[g].prog) + 1, 1);
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void k_gen_sync(const UpdJob* __restrict__ jobs, int njobs) {
+  const int g = blockIdx.x * 64 + threadIdx.x;
+  if (g >= njobs) return;
+  int* ctr = jobs[g].tail_ctr;
+  gp(ctr)[TAIL_UPDSEEN] = __hip_atomic_load(ctr + TAIL_UPDGEN, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - 1;
+}
+
+void launch_wait_gen(const UpdJob* jobs, int njobs, unsigned limit, hipStream_t st) {
+  hipLaunchKernelGGL(k_wait_gen, dim3(1), dim3(64), 0, st, jobs, njobs, limit);
+  HIP_OK(hipGetLastError());
+}
+void launch_gen_sync(const UpdJob* jobs, int njobs, hipStream_t st) {
+  hipLaunchKernelGGL(k_gen_sync, dim3((njobs + 63) / 64), dim3(64), 0, st, jobs, njobs);
+  HIP_OK(hipGetLastError());
+}
+
 // One int written on the stream (module API: the dropout stream position of a model), so the
 // host never touches device memory synchronously between calls. The store sits under a lane
 // test (a vector store, not a scalar one).

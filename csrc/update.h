@@ -15,7 +15,10 @@ struct ModelDesc;
 #define TAIL_ARRIVE 96
 #define TAIL_EVGEN 128
 #define TAIL_ARRIVE2 160       // (phase-2 tail launches: their own running arrival count)
-#define TAIL_WORDS 192         // max packed copies of one parameter for k_adam's fused re-pack
+#define TAIL_ADONE 192         // tail Adam blocks finished (running count)
+#define TAIL_UPDGEN 224        // tail updates finished (running count; the last Adam block of a launch)
+#define TAIL_UPDSEEN 256       // updates the evaluation graph has consumed (k_wait_gen)
+#define TAIL_WORDS 288         // max packed copies of one parameter for k_adam's fused re-pack
 
 struct FinJob {            // one model
   const float* slab;       // first slab of this model (slices contiguous, gx slabs each)
@@ -134,6 +137,12 @@ void launch_begin_phase(const EpochJob* jobs, int njobs, hipStream_t st);
 // recurrences of the training graph's fused forward than it consumed so far (cnt[0] running
 // count, cnt[32] consumed); giving up poisons the nmodels models (prog records, 48 ints each)
 void launch_wait_count(int* cnt, int per, unsigned limit, int* prog, int nmodels, hipStream_t st);
+// the split epoch graphs with the evaluation recurrences on the evaluation queue: the evaluation
+// graph's first launch waits (one wave) until every model's previous update is complete (the
+// tail's TAIL_UPDGEN one past TAIL_UPDSEEN), then consumes it; giving up poisons the models.
+// launch_gen_sync (after the head epoch's k_adam, which does not count): the next wait passes.
+void launch_wait_gen(const UpdJob* jobs, int njobs, unsigned limit, hipStream_t st);
+void launch_gen_sync(const UpdJob* jobs, int njobs, hipStream_t st);
 // signal: each model's block counts its EpochJob::eval_gen when done (agent release) -- the
 // fused tail's Adam blocks wait for it (launch_lstm_tail, adam 2)
 void launch_epoch_end(const EpochJob* jobs, int njobs, int phase, int ignore_epoch, float sel,

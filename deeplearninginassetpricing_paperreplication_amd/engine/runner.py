@@ -216,7 +216,7 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
                      precision="bf16", selection_sign=1.0, verbose=True, n_models=1,
                      models=None, seeds=None, save_dirs=None, lrs=None, dropouts=None, resume=False,
                      resume_path=None, nan_policy="warn", stop_after=None, final_weights_device=False,
-                     engine_setup=None):
+                     engine_setup=None, wait_fallback=True):
     """GPU executor of the 3-phase schedule; with ``n_models > 1`` trains an ensemble batch.
 
     Returns ``(model, history)`` for a single model, or ``(models, histories)`` when
@@ -237,6 +237,10 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
     (``engine_final_eval[s]["weights"]`` is then a CUDA tensor; the ensemble all-gathers them).
     ``engine_setup``: called with the ``GANEngine`` once data and parameters are set, before the
     first epoch (the cross-sectional sharding installs its collectives there, parallel/xsection.py).
+    ``wait_fallback``: when an in-kernel spin wait gives up (a fused launch or the split epoch
+    graphs could not make progress -- e.g. the GPU shared with other work), the models are restored
+    to the start of that print interval and the interval is re-run in the engine's safe mode (no
+    cross-launch waits; bitwise the same results), instead of stopping the run.
     """
     from ..models.gan import AssetPricingGAN
     from ..utils import checkpoint as ckpt
@@ -283,6 +287,7 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
     if resume_path is None and n_models == 1 and save_dirs[0]:
         resume_path = os.path.join(save_dirs[0], ckpt.RESUME_FILE)
     monitor = NonFiniteMonitor(n_models, HIST, nan_policy)
+    fallback = {"safe": False, "reruns": 0}
     start = (1, 0)                  # (phase, epochs done in it) to continue from
     run_fp = ckpt.run_fingerprint(lr, ignore_epoch, selection_sign,
                                   ckpt.data_fingerprint(train_data, valid_data, test_data)) if resume_path else None
@@ -333,10 +338,28 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
             k = mk + 1 - done
             if k <= 0:
                 continue
+            saved = None
+            if wait_fallback and not fallback["safe"]:
+                lr_of = (lambda g: lrs[g]) if lrs is not None else (lambda g: None)
+                saved = [ckpt.capture_model(eng.eng, g, seeds[g], lr_of(g)) for g in range(n_models)]
             t0 = time.time()
             with trace_range(f"phase{phase}-epochs", timers):
                 eng.run(phase, k, lr, ignore_epoch, selection_sign)
                 eng.eng.sync()
+            if saved is not None and eng.eng.prog_timeouts():
+                # a spin wait gave up (its model is poisoned: no update, NaN epochs): back to the
+                # interval's start, the rest of the run without cross-launch waits
+                say(f"[engine] an in-kernel wait gave up in phase {phase}; re-running epochs "
+                    f"{done + 1}-{mk + 1} in safe mode")
+                eng.eng.reset_prog_errors()
+                for g in range(n_models):
+                    ckpt.restore_model(eng.eng, g, saved[g])
+                eng.eng.set_safe_mode(True)
+                fallback["safe"] = True
+                fallback["reruns"] += 1
+                with trace_range(f"phase{phase}-epochs", timers):
+                    eng.run(phase, k, lr, ignore_epoch, selection_sign)
+                    eng.eng.sync()
             dt = (time.time() - t0) / k
             done = mk + 1
             # first: a fused forward that gave up a wait poisons its model on the device (no
@@ -425,6 +448,7 @@ def train_3phase_gpu(config, train_data, valid_data, test_data=None, device=None
     # host time of the graph captures (inside the first run of every phase's epoch ranges)
     train_3phase_gpu.last_capture_s = float(eng.eng.capture_seconds())
     train_3phase_gpu.last_nonfinite = monitor.nonfinite_models
+    train_3phase_gpu.last_wait_fallback = dict(fallback)
     if n_models == 1:
         return out_models[0], hists[0]
     return out_models, hists

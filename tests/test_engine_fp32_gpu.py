@@ -156,7 +156,8 @@ def _check_trajectory(branch, splits, cfg_update, wide=None):
     ref64 = _cpu_trajectory(m64, _double(splits[0]), SCHED, lr)
     e_gpu = np.abs(got - ref64) / np.abs(ref64)
     e_cpu = np.abs(ref - ref64) / np.abs(ref64)
-    assert e_gpu.max() <= 2 * e_cpu.max() + 1e-6, (branch, e_gpu.max(), e_cpu.max())
+    assert e_gpu.max() <= 2 * e_cpu.max() + 1e-6, (branch, e_gpu.max(), e_cpu.max(), rel.max(axis=0), worst,
+                                                    errs[worst])
     sd64 = {k: v for k, v in m64.state_dict().items()}
     sdg = eng.state_dict(0)
     for k, v in model.state_dict().items():

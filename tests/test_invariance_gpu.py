@@ -185,7 +185,9 @@ def test_fused_backward_tail_other_lstm_shapes(big, monkeypatch, rnn):
     monkeypatch.setenv("DLAP_TAIL_ADAM", "1")
     e2, res2 = _train(big, cfg, [61, 62], 2, phases=ph)
     info = e2.eng.fused_info()
-    if rnn[0] == 8 and len(rnn) == 1:        # the paper grid's SMV = 8 runs the production pipeline
+    # (SMV = 8 on this panel: the fused forward's LDS cannot hold the 300-step test recurrence at
+    # width 8, so the epochs run the one-graph pipeline with the update after the join)
+    if rnn == [4, 4]:
         assert info["split_graphs"] and info["adam_in_tail"], info
     for s in (61, 62):
         _same(ref[s], res2[s])
@@ -248,6 +250,25 @@ def test_split_epoch_graphs_equal_one_graph(big, monkeypatch):
     e1, res = _train(big, cfg, [81, 82], 2, phases=phases)
     assert e1.eng.fused_info()["split_graphs"]
     for s in (81, 82):
+        _same(ref[s], res[s])
+
+
+def test_eval_recurrences_on_the_eval_queue_equal_in_training_launch(big, monkeypatch):
+    """Split epoch graphs with the evaluation splits' recurrences in the evaluation graph's own
+    fused LSTM + tower forward (after an in-kernel wait for the previous update, k_wait_gen)
+    instead of inside the training chain's fused forward: the bits of the round-5 split graphs,
+    batched models included."""
+    cfg = default_cli_config(178, 46)
+    phases = ((1, 11), (2, 2), (3, 10))
+    monkeypatch.setenv("DLAP_EVAL_SEP", "0")
+    e0, ref = _train(big, cfg, [83, 84], 2, phases=phases)
+    info = e0.eng.fused_info()
+    assert info["split_graphs"] and not info["eval_sep"], info
+    monkeypatch.setenv("DLAP_EVAL_SEP", "1")
+    e1, res = _train(big, cfg, [83, 84], 2, phases=phases)
+    info = e1.eng.fused_info()
+    assert info["split_graphs"] and info["eval_sep"], info
+    for s in (83, 84):
         _same(ref[s], res[s])
 
 
@@ -326,7 +347,38 @@ def test_fused_wait_give_up_poisons_the_model(monkeypatch):
     assert eng.eng.prog_timeouts() == 0
     with pytest.raises(RuntimeError, match="spin wait gave up"):
         train_3phase_gpu(cfg, b, b, b, num_epochs_unc=4, num_epochs_moment=1, num_epochs=2, print_freq=2,
-                         ignore_epoch=0, verbose=False, seed=3)
+                         ignore_epoch=0, verbose=False, seed=3, wait_fallback=False)
+
+
+def test_wait_give_up_falls_back_to_safe_mode(monkeypatch):
+    """a spin wait that gives up no longer ends the run -- the GPU trainer
+    restores the models to the start of the print interval and re-runs it (and the rest of the
+    run) without cross-launch waits. Forced here with a zero spin limit for the first interval:
+    the final state, history and snapshots are the bits of an undisturbed run."""
+    from deeplearninginassetpricing_paperreplication_amd.data.synthetic import generate_panel_fast
+    from deeplearninginassetpricing_paperreplication_amd.engine.runner import train_3phase_gpu
+    ret, feats, mask, mac = generate_panel_fast(96, 600, 46, 8, seed=1)
+    mac = (mac - mac.mean(0)) / (mac.std(0, unbiased=False) + 1e-8)
+    b = {"returns": ret, "individual_features": feats, "mask": mask, "macro_features": mac}
+    cfg = default_cli_config(8, 46)
+    kw = dict(num_epochs_unc=6, num_epochs_moment=2, num_epochs=6, print_freq=3, ignore_epoch=0, verbose=False,
+              seed=3)
+
+    def run():
+        torch.manual_seed(0)
+        m, h = train_3phase_gpu(cfg, b, b, b, **kw)
+        e = train_3phase_gpu.last_engine
+        return (e.params(0), e.params(0, "sharpe"), e.params(0, "loss"), np.asarray(h["valid_sharpe"])), \
+            dict(train_3phase_gpu.last_wait_fallback)
+
+    ref, fb0 = run()
+    assert fb0["reruns"] == 0
+    monkeypatch.setenv("DLAP_PROG_SPIN_LIMIT", "0")
+    got, fb1 = run()
+    assert fb1["reruns"] == 1 and fb1["safe"], fb1
+    assert train_3phase_gpu.last_engine.eng.prog_timeouts() == 0
+    for x, y in zip(ref, got):
+        np.testing.assert_array_equal(x, y)
 
 
 def test_tail_adam_handoff_survives_a_new_train_split(big, monkeypatch):

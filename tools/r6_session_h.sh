@@ -7,7 +7,7 @@ tag=${1:-r6h}
 rc=0
 $T 900 python -u -m pytest --maxfail=8 -v --timeout 300 --timeout-method thread tests/test_xsection_gpu.py \
   "tests/test_invariance_gpu.py::test_fused_backward_tail_other_lstm_shapes" \
-  "tests/test_invariance_gpu.py::test_fused_backward_tail_equals_separate_kernels" "tests/test_invariance_gpu.py::test_phase2_tail_and_lstm_once_equal_separate_kernels" \
+  "tests/test_invariance_gpu.py::test_fused_backward_tail_equals_separate_kernels" "tests/test_invariance_gpu.py::test_phase2_tail_and_lstm_once_equal_separate_kernels" "tests/test_invariance_gpu.py::test_wait_give_up_falls_back_to_safe_mode" "tests/test_invariance_gpu.py::test_fused_wait_give_up_poisons_the_model" \
   tests/test_engine_fp32_gpu.py -k "paper or default or xsection or sweep or tail" tests/test_sweep_gpu.py \
   > gpurun_out/${tag}_tests.log 2>&1 || rc=$?
 tail -30 gpurun_out/${tag}_tests.log
