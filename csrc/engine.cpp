@@ -2154,9 +2154,9 @@ class Engine {
   }
   void enqueue_chain_split(int phase, float lr) {
     tail_metrics_ = true;
-    tail_adam_mode_ = 2;
-    tail_lr_ = lr;
     const bool sep = sep_eval(phase);
+    tail_adam_mode_ = sep ? 3 : 2;
+    tail_lr_ = lr;
     fwd_esig_ = sep ? nullptr : esync_.p;
     enqueue_train_grads(phase, true, 0, false, !sep);
     tail_metrics_ = false;

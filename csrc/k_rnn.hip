@@ -1168,7 +1168,7 @@ __global__ __launch_bounds__(256) void k_wgrad(const UpdJob* __restrict__ jobs,
 // (no update; the host raises). The waiting blocks are the last to arrive, so every block they
 // wait for has been dispatched ahead of them or is next in line.
 DLAP_DEV void tail_adam(const UpdJob& U, const ModelDesc* __restrict__ md, float lr, int nb, int step_pre,
-                        int drop_pre, int phase, bool evgen) {
+                        int drop_pre, int phase, bool evgen, bool gen) {
   __shared__ unsigned s_ord;
   __shared__ int s_go;
   __shared__ float red[4];
@@ -1216,7 +1216,7 @@ DLAP_DEV void tail_adam(const UpdJob& U, const ModelDesc* __restrict__ md, float
     return s_go != 0;
   };
   adam_block(U, md, phase, lr, bx, nadam, red, wait, step_pre, drop_pre);
-  if (evgen) {
+  if (gen) {
     // the update is complete once all nadam Adam blocks of the launch are: each counts itself
     // (acq_rel: its stores released, the earlier counts' acquired); the last of the launch advances
     // the model's update generation (release) -- the evaluation graph's k_wait_gen waits for it
@@ -1321,7 +1321,7 @@ __global__ __launch_bounds__(256, 2) void k_lstm_tail(const UpdJob* __restrict__
     else wgrad_block<4>(U, md, phase, cblk, red, U.tail_ctr + TAIL_DONE, nwg, wait_dg);
     if (blockIdx.y == 0 && cblk == nwg - 1 && threadIdx.x == 0) g_rnn_ts[17] = wall_clock64();
   }
-  if (adam) tail_adam(U, md, lr, gridDim.x, s_steps[0], s_steps[1], phase, adam == 2);
+  if (adam) tail_adam(U, md, lr, gridDim.x, s_steps[0], s_steps[1], phase, adam >= 2, adam == 3);
 }
 
 // whether the fused tail applies (phases 1 / 3; LSTM widths up to 8, any depth); its LDS bytes:

@@ -119,7 +119,8 @@ struct LossJob;
 // ljobs: the train split's loss jobs whose job metrics one more block per model computes (or nullptr)
 // adam: 0 = none (k_adam follows); 2 = the update runs in the tail (the launch's last blocks,
 // adam_block) after the epoch's evaluation branch signalled (launch_epoch_end); 1 = the same
-// without that signal (phase 2: nothing else reads the parameters during the epoch)
+// without that signal (phase 2: nothing else reads the parameters during the epoch); 3 = as 2, and
+// the launch's last Adam block advances the model's update generation (k_wait_gen, DLAP_EVAL_SEP)
 // phase 2: the moment network's tail -- k_finalize + k_wgrad (the macro columns of moment layer
 // 0) [+ k_adam]; block 0 relays the per-period sums' count to the W_macro helpers (no BPTT)
 void launch_lstm_tail(const UpdJob* ujobs, const FinJob* fjobs, int njobs, const ModelDesc* md, const ModelDesc& mh,
