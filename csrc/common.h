@@ -242,10 +242,15 @@ DLAP_DEV bool dropout_keep(uint32_t key, uint32_t row, uint32_t unit, uint32_t t
   return (h >> 8) >= thr;
 }
 // Two decisions from one hash for the unit pair (2*pair, 2*pair+1): 16-bit thresholds
-// thr16 = round(p * 2^16) (p = 0.05 -> 0.050003). rowmix = row * 0xcc9e2d51 ^ (row >> 16)
-// is hoisted per row by the caller. Branch-free: evaluated for every element.
-DLAP_DEV uint32_t dropout_pair(uint32_t key, uint32_t rowmix, uint32_t pair) {
-  return fmix32(key ^ rowmix ^ (pair * 0x27d4eb2fu));
+// thr16 = round(p * 2^16) (p = 0.05 -> 0.050003). One full mix per (stream key, dense row)
+// (row_key; rowmix = row * 0xcc9e2d51 ^ (row >> 16)), then per unit pair a Weyl step and one
+// xorshift-multiply-xorshift round (one integer multiply instead of fmix32's two: the keep-word
+// generation is integer-multiply bound). Branch-free: evaluated for every element.
+DLAP_DEV uint32_t row_key(uint32_t key, uint32_t rowmix) { return fmix32(key ^ rowmix); }
+DLAP_DEV uint32_t pair_hash(uint32_t rk, uint32_t pair) {
+  uint32_t h = rk + pair * 0x9E3779B9u;
+  h ^= h >> 16; h *= 0x7feb352du; h ^= h >> 15;
+  return h;
 }
 DLAP_DEV uint32_t row_mix(uint32_t row) { return row * 0xcc9e2d51u ^ (row >> 16); }
 // Keep word of lane group q (split layout, see "packed bf16 element ops" below) for UB unit
@@ -255,18 +260,20 @@ template <int UB>
 DLAP_DEV uint32_t keep_word(uint32_t key, const uint32_t (&rowmix)[2], uint32_t thr16, int q) {
   uint32_t w = 0;
 #pragma unroll
-  for (int b = 0; b < 2; ++b)
+  for (int b = 0; b < 2; ++b) {
+    const uint32_t rk = row_key(key, rowmix[b]);
 #pragma unroll
     for (int u = 0; u < UB; ++u) {
       const uint32_t pair0 = (uint32_t)(8 * u + 2 * q);
-      const uint32_t h0 = dropout_pair(key, rowmix[b], pair0);
-      const uint32_t h1 = dropout_pair(key, rowmix[b], pair0 + 1);
+      const uint32_t h0 = pair_hash(rk, pair0);
+      const uint32_t h1 = pair_hash(rk, pair0 + 1);
       const int p = 8 * b + 2 * u;          // element e = 4u + r -> bit (r & 1) * 16 + 8b + (e >> 1)
       w |= ((h0 & 0xFFFFu) >= thr16 ? 1u : 0u) << p;
       w |= ((h0 >> 16) >= thr16 ? 1u : 0u) << (16 + p);
       w |= ((h1 & 0xFFFFu) >= thr16 ? 1u : 0u) << (p + 1);
       w |= ((h1 >> 16) >= thr16 ? 1u : 0u) << (16 + p + 1);
     }
+  }
   return w;
 }
 

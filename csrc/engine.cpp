@@ -220,6 +220,7 @@ class Engine {
     HIP_OK(hipEventCreateWithFlags(&ev_fork_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_join_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_gram_, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&ev_trgram_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_mid_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_a_, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&ev_in_, hipEventDisableTiming));
@@ -248,6 +249,7 @@ class Engine {
     tail_adam_pipe_ = env_int("DLAP_TAIL_ADAM", 1) == 2;
     split_graphs_ = env_int("DLAP_SPLIT_GRAPHS", 1) != 0;
     mom_tail_ = env_int("DLAP_MOM_TAIL", 1) != 0;
+    train_gram_side_ = env_int("DLAP_TRAIN_GRAM_SIDE", 1) != 0;
     p2_lstm_cache_ = env_int("DLAP_P2_LSTM_CACHE", 1) != 0;
     unroll_ = std::max(1, env_int("DLAP_UNROLL", 8));
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
@@ -708,7 +710,6 @@ class Engine {
       return;
     }
     if (split_graphs(phase)) {
-      hipGraphExec_t head = graph_for(graph_key(phase, lr, ignore_epoch, sel, 1), [&] { enqueue_head(phase, lr); });
       // the body epochs in graphs of `unroll_` epochs each (the rest one by one): a graph boundary
       // costs ~5-9 us (the last node's system-scope release, the first one's acquire); inside a
       // graph consecutive kernels of one queue follow each other directly
@@ -728,7 +729,7 @@ class Engine {
       }
       hipGraphExec_t tail = graph_for(graph_key(phase, lr, ignore_epoch, sel, 3),
                                       [&] { enqueue_tail(phase, ignore_epoch, sel); });
-      HIP_OK(hipGraphLaunch(head, st_));
+      launch_head(phase, lr, ignore_epoch, sel);
       join_eval_gram();
       // the evaluation graphs follow the head on st2_ (its masks / step counters, its weights)
       HIP_OK(hipEventRecord(ev_fork_, st_));
@@ -752,13 +753,12 @@ class Engine {
       HIP_OK(hipGraphLaunch(tail, st_));
       return;
     }
-    hipGraphExec_t head = graph_for(graph_key(phase, lr, ignore_epoch, sel, 1), [&] { enqueue_head(phase, lr); });
     hipGraphExec_t body = graph_for(graph_key(phase, lr, ignore_epoch, sel, 2),
                                     [&] { enqueue_pipe(phase, lr, ignore_epoch, sel); });
     hipGraphExec_t tail = graph_for(graph_key(phase, lr, ignore_epoch, sel, 3),
                                     [&] { enqueue_tail(phase, ignore_epoch, sel); });
     HTRACE("launch head");
-    HIP_OK(hipGraphLaunch(head, st_));
+    launch_head(phase, lr, ignore_epoch, sel);
     join_eval_gram();                     // the next graphs evaluate
     const auto t_l = std::chrono::steady_clock::now();
     for (int e = 1; e < n; ++e) HIP_OK(hipGraphLaunch(body, st_));
@@ -1749,19 +1749,56 @@ class Engine {
       if (cur_phase_ >= 1 && cur_phase_ <= 3 && !(s == 0 ? plan_tr_[cur_phase_] : plan_ev_[cur_phase_])) continue;
       gram_valid_[s] = true;
       hipStream_t st = st_;
-      if (s > 0 && defer) {
-        if (!eval_gram_pending_) {
+      if ((s > 0 || train_gram_side_) && defer) {
+        if (!eval_gram_pending_ && !train_gram_pending_) {
           HIP_OK(hipEventRecord(ev_fork_, st_));
           HIP_OK(hipStreamWaitEvent(st2_, ev_fork_, 0));
         }
-        eval_gram_pending_ = true;
+        if (s > 0) eval_gram_pending_ = true;
         st = st2_;
       }
       HTRACE("launch_gram split=%d", s);
       launch_gram(as<GramJob>(j_gram_[s]), G_, D.T, gram_slices(D.T), st);
       xs_call("gram", 1 << s, st);         // sharded: G summed over every rank's stocks
+      if (s == 0 && st == st2_) {
+        HIP_OK(hipEventRecord(ev_trgram_, st2_));
+        train_gram_pending_ = true;
+      }
     }
     if (eval_gram_pending_) HIP_OK(hipEventRecord(ev_gram_, st2_));
+  }
+  // st_ waits for the train split's deferred refresh + Gram build (no-op when none is pending)
+  void join_train_gram() {
+    if (!train_gram_pending_) return;
+    HIP_OK(hipStreamWaitEvent(st_, ev_trgram_, 0));
+    train_gram_pending_ = false;
+  }
+  bool train_gram_side_ = true;              // DLAP_TRAIN_GRAM_SIDE
+  bool train_gram_pending_ = false;
+  hipEvent_t ev_trgram_ = nullptr;
+  int tg_part_ = 0;                          // enqueue_train_grads: 1 forward only, 2 the rest
+  // The head epoch of a pipelined run. With the train split's moment refresh / Gram build deferred
+  // to the evaluation stream, two graphs: the forward (dropout masks, LSTM + towers) overlaps the
+  // build, then st_ waits for it and the losses, backward and update follow.
+  void launch_head(int phase, float lr, int ig, float sel) {
+    if (!train_gram_pending_) {
+      hipGraphExec_t head = graph_for(graph_key(phase, lr, ig, sel, 1), [&] { enqueue_head(phase, lr); });
+      HIP_OK(hipGraphLaunch(head, st_));
+      return;
+    }
+    hipGraphExec_t a = graph_for(graph_key(phase, lr, ig, sel, 11), [&] {
+      tg_part_ = 1;
+      enqueue_train_grads(phase);
+      tg_part_ = 0;
+    });
+    hipGraphExec_t b = graph_for(graph_key(phase, lr, ig, sel, 12), [&] {
+      tg_part_ = 2;
+      enqueue_head(phase, lr);
+      tg_part_ = 0;
+    });
+    HIP_OK(hipGraphLaunch(a, st_));
+    join_train_gram();
+    HIP_OK(hipGraphLaunch(b, st_));
   }
   // st_ waits for deferred evaluation-split Gram builds (no-op when none is pending)
   void join_eval_gram() {
@@ -1962,8 +1999,11 @@ class Engine {
       HIP_OK(hipStreamWaitEvent(st2_, ev_fork_, 0));
       eval_gram_pending_ = true;
       HTRACE("launch_prologue (moments, split)");
-      launch_prologue(as<RnnJob>(j_rnn_mom_), n_mom_tr_, tmax_mom_tr_, dd(), md_, st_, true, false);
-      launch_mlp_fwd(as<MlpJob>(j_mlp_mom_), n_mom_tr_, gx_mom_, md_.md, md_.KS1, md_.WMB, st_);
+      // (train_gram_side_: the train split's refresh and Gram build too, ahead of the evaluation
+      // splits' -- the head epoch's forward needs neither, its loss pass waits, launch_head)
+      hipStream_t sm = train_gram_side_ ? st2_ : st_;
+      launch_prologue(as<RnnJob>(j_rnn_mom_), n_mom_tr_, tmax_mom_tr_, dd(), md_, sm, true, false);
+      launch_mlp_fwd(as<MlpJob>(j_mlp_mom_), n_mom_tr_, gx_mom_, md_.md, md_.KS1, md_.WMB, sm);
       launch_prologue(as<RnnJob>(j_rnn_mom_) + n_mom_tr_, n_ev, tmax_mom_ev_, dd(), md_, st2_, true, false);
       launch_mlp_fwd(as<MlpJob>(j_mlp_mom_) + n_mom_tr_, n_ev, gx_mom_, md_.md, md_.KS1, md_.WMB, st2_);
       h_valid_ = true;
@@ -2004,6 +2044,8 @@ class Engine {
     const SplitDev& D = splits_[0];
     const bool gram = use_gram(phase);
     const LossJob* lj = loss_tab(phase, gram);
+    // (tg_part_: the head epoch split around the wait for a deferred train Gram build, launch_head)
+    if (tg_part_ != 2) {
     if (!premasked) enqueue_dropmask(phase, 0, st_);
     // the latency-bound LSTM first, before the streaming projection loads the memory system
     // (fused: only its input projection here, the recurrence runs inside the tower launch)
@@ -2038,6 +2080,8 @@ class Engine {
       launch_mlp_fwd(as<MlpJob>(j_mlp_train_[phase]), G_, phase == 2 ? gx_fwd_[0] : gx_fwd13_, md_.md, md_.KS1,
                      md_.WMB, st_, !train_mom(phase));
     if (mark == 2) HIP_OK(hipEventRecord(ev_a_, st_));
+    }
+    if (tg_part_ == 1) return;
     HTRACE("launch_period_fwd");
     period_fwd(lj, G_, D.T, st_, false, 1);
     if (!gram) {

@@ -60,12 +60,17 @@ def dropout_key(seed, step, layer):
 
 
 def tower_keep(seed, step, layer, rows, width, p):
-    """keep[row, unit] of relu_dropout / k_dropmask: one hash per unit pair, 16-bit halves."""
+    """keep[row, unit] of relu_dropout / k_dropmask: a row key, one hash round per unit pair,
+    16-bit halves."""
     key = dropout_key(seed, step, layer)
     r = np.asarray(rows, dtype=np.uint64)[:, None]
     rowmix = ((r * 0xCC9E2D51) & M32) ^ (r >> 16)
     n = np.arange(width, dtype=np.uint64)[None, :]
-    h = fmix32(np.uint64(key) ^ rowmix ^ (((n >> 1) * 0x27D4EB2F) & M32))
+    rk = fmix32(np.uint64(key) ^ rowmix)                     # row_key
+    h = (rk + (n >> 1) * 0x9E3779B9) & M32                    # pair_hash
+    h ^= h >> 16
+    h = (h * 0x7FEB352D) & M32
+    h ^= h >> 15
     half = (h >> (16 * (n & 1))) & 0xFFFF
     thr16 = int(p * 65536.0 + 0.5)
     return half >= thr16

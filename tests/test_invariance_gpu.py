@@ -272,6 +272,20 @@ def test_eval_recurrences_on_the_eval_queue_equal_in_training_launch(big, monkey
         _same(ref[s], res[s])
 
 
+def test_train_gram_on_eval_stream_equals_in_chain(big, monkeypatch):
+    """The train split's moment refresh and Gram build at a phase start on the evaluation stream,
+    the head epoch's forward beside them and its loss pass waiting for them (two head graphs):
+    the bits of the build on the training stream ahead of the head."""
+    cfg = default_cli_config(178, 46)
+    phases = ((1, 4), (2, 2), (3, 4), (3, 3))
+    monkeypatch.setenv("DLAP_TRAIN_GRAM_SIDE", "0")
+    _, ref = _train(big, cfg, [85, 86], 2, phases=phases)
+    monkeypatch.setenv("DLAP_TRAIN_GRAM_SIDE", "1")
+    _, res = _train(big, cfg, [85, 86], 2, phases=phases)
+    for s in (85, 86):
+        _same(ref[s], res[s])
+
+
 def test_self_projecting_recurrences_equal_k_proj(big, monkeypatch):
     """The fused forward's recurrences computing their own layer-0 input projections tile by tile
     (spare waves of their workgroups, no k_proj launch) give the bits of k_proj + staged inputs."""

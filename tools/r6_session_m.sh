@@ -1,0 +1,18 @@
+# cheaper dropout hash: dropout tests, invariance subset, bench short + steady, kernel trace
+set -o pipefail
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+T="timeout -k 10"
+tag=${1:-r6m}
+rc=0
+$T 600 python -u -m pytest --maxfail=5 -v --timeout 300 --timeout-method thread tests/test_dropout_gpu.py tests/test_tbwd_gpu.py \
+  tests/test_invariance_gpu.py -k "not nine_seeds and not per_member and not member_is" > gpurun_out/${tag}_tests.log 2>&1 || rc=$?
+grep -E "FAILED|ERROR|passed|failed" gpurun_out/${tag}_tests.log | tail -12
+[ $rc -le 1 ] || exit $rc
+for a in "--steps 20 --warmup 5" "--steps 210 --warmup 21"; do
+  $T 300 python bench.py $a --no-ensemble9 > gpurun_out/${tag}_bench.log 2>&1 || { tail -20 gpurun_out/${tag}_bench.log; exit 1; }
+  tail -1 gpurun_out/${tag}_bench.log | grep -o '"ms_per_step": [0-9.]*\|"ms_per_epoch_phase": \[[^]]*\]'
+done
+$T 300 rocprofv3 --kernel-trace -d gpurun_out/${tag}_prof -o run -- python3 bench.py --steps 20 --warmup 5 --no-ensemble9 > gpurun_out/${tag}_prof.log 2>&1 || { tail -5 gpurun_out/${tag}_prof.log; exit 1; }
+python3 tools/run_timeline.py gpurun_out/${tag}_prof --adams 2 --marker k_begin_phase > gpurun_out/${tag}_timeline.txt || true
+grep -m3 k_dropmask gpurun_out/${tag}_timeline.txt
