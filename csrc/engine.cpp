@@ -249,7 +249,7 @@ class Engine {
     tail_adam_pipe_ = env_int("DLAP_TAIL_ADAM", 1) == 2;
     split_graphs_ = env_int("DLAP_SPLIT_GRAPHS", 1) != 0;
     mom_tail_ = env_int("DLAP_MOM_TAIL", 1) != 0;
-    train_gram_side_ = env_int("DLAP_TRAIN_GRAM_SIDE", 1) != 0;
+    train_gram_side_ = env_int("DLAP_TRAIN_GRAM_SIDE", 0) != 0;
     p2_lstm_cache_ = env_int("DLAP_P2_LSTM_CACHE", 1) != 0;
     unroll_ = std::max(1, env_int("DLAP_UNROLL", 8));
     build_desc(F, M, nrnn, H, raw_macro_sdf, hidden, mom_hidden, K, dropout, normalize_w, weighted,
@@ -1773,7 +1773,7 @@ class Engine {
     HIP_OK(hipStreamWaitEvent(st_, ev_trgram_, 0));
     train_gram_pending_ = false;
   }
-  bool train_gram_side_ = true;              // DLAP_TRAIN_GRAM_SIDE
+  bool train_gram_side_ = false;             // DLAP_TRAIN_GRAM_SIDE
   bool train_gram_pending_ = false;
   hipEvent_t ev_trgram_ = nullptr;
   int tg_part_ = 0;                          // enqueue_train_grads: 1 forward only, 2 the rest
