@@ -1033,6 +1033,10 @@ class Engine {
       save += cde * T * N * (K + 1.0) - cq * T * T;
     }
     plan_ev_[phase] = epochs * save > build;
+    // (A/B of the plan: DLAP_GRAM_PLAN=2 dense evaluation splits, 3 dense train split)
+    const int force = env_int("DLAP_GRAM_PLAN", 1);
+    if (force == 2) plan_ev_[phase] = false;
+    if (force == 3) plan_tr_[phase] = false;
   }
   py::tuple gram_plan(int phase) const {
     const int p = (phase >= 1 && phase <= 3) ? phase : 1;
@@ -1741,8 +1745,9 @@ class Engine {
   // to the evaluation stream st2_ (after the moment refresh queued so far) and
   // eval_gram_pending_ is set: the caller joins ev_gram_ into st_ before the first graph that
   // evaluates (the pipelined head trains only, so they overlap it).
-  void build_gram(bool defer = false) {
+  void build_gram(bool defer = false, int smask = 7) {
     for (int s = 0; s < 3; ++s) {
+      if (!((smask >> s) & 1)) continue;
       const SplitDev& D = splits_[s];
       if (!D.set || D.T == 0 || gram_valid_[s]) continue;
       // only what the current run's plan reads (run_epochs sets cur_phase_; 0: everything)
@@ -2004,10 +2009,11 @@ class Engine {
       hipStream_t sm = train_gram_side_ ? st2_ : st_;
       launch_prologue(as<RnnJob>(j_rnn_mom_), n_mom_tr_, tmax_mom_tr_, dd(), md_, sm, true, false);
       launch_mlp_fwd(as<MlpJob>(j_mlp_mom_), n_mom_tr_, gx_mom_, md_.md, md_.KS1, md_.WMB, sm);
+      for (bool& v : gram_valid_) v = false;
+      if (train_gram_side_) build_gram(true, 1);          // (the head's loss pass waits for it first)
       launch_prologue(as<RnnJob>(j_rnn_mom_) + n_mom_tr_, n_ev, tmax_mom_ev_, dd(), md_, st2_, true, false);
       launch_mlp_fwd(as<MlpJob>(j_mlp_mom_) + n_mom_tr_, n_ev, gx_mom_, md_.md, md_.KS1, md_.WMB, st2_);
       h_valid_ = true;
-      for (bool& v : gram_valid_) v = false;
       build_gram(true);
       return;
     }

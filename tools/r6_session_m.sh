@@ -5,8 +5,8 @@ export TMPDIR=/tmp
 T="timeout -k 10"
 tag=${1:-r6m}
 rc=0
-$T 600 python -u -m pytest --maxfail=5 -v --timeout 300 --timeout-method thread tests/test_dropout_gpu.py tests/test_tbwd_gpu.py \
-  tests/test_invariance_gpu.py -k "not nine_seeds and not per_member and not member_is" > gpurun_out/${tag}_tests.log 2>&1 || rc=$?
+$T 600 python -u -m pytest --maxfail=5 -v --timeout 300 --timeout-method thread tests/test_gram_gpu.py \
+  tests/test_invariance_gpu.py -k "train_gram or split_epoch or adam_in_tail" > gpurun_out/${tag}_tests.log 2>&1 || rc=$?
 grep -E "FAILED|ERROR|passed|failed" gpurun_out/${tag}_tests.log | tail -12
 [ $rc -le 1 ] || exit $rc
 for side in 0 1; do
