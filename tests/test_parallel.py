@@ -181,9 +181,9 @@ def test_sweep_lpt_balances_8_ranks(tmp_path):
     """The paper's 384-config grid (48 architecture buckets) over 8 gloo ranks: every rank derives
     the same longest-processing-time-first assignment from the bucket cost table (the measured
     per-architecture epoch times, parallel/sweep_costs.json, tools/sweep_costs.py on an MI355X),
-    each bucket is owned exactly once, the predicted per-rank load is within 1.05x, and the
-    busiest rank carries strictly less than under round-robin dealing (measured table: LPT
-    1.02x vs round-robin 1.79x)."""
+    each bucket is owned exactly once, the busiest rank is within LPT's bound (the mean load plus
+    the costliest bucket; the round-6 table's largest bucket, HL 4 / SMV 8 / K 32, is ~40% of a
+    rank's load, so the spread is 1.09x) and carries strictly less than under round-robin dealing."""
     from deeplearninginassetpricing_paperreplication_amd.config import ModelSpec
     assert sweep._load_costs(), "parallel/sweep_costs.json (measured bucket costs) is missing"
     r = _run("sweep_plan", tmp_path, world=8)
@@ -192,10 +192,11 @@ def test_sweep_lpt_balances_8_ranks(tmp_path):
     owned = np.array(r[0]["owned"])
     assert owned.shape == (8, r[0]["n"]) and (owned.sum(axis=0) == 1).all()
     loads = np.array(r[0]["loads"])
-    assert loads.max() / loads.min() <= 1.05, loads
     entries = sweep.paper_grid(178, 46)
     bks = sweep.buckets(entries)
     costs = [sweep.bucket_cost(ModelSpec.from_config(entries[b[0]][0]), len(b)) for b in bks]
+    assert loads.max() <= loads.mean() + max(costs) + 1e-9, loads
+    assert loads.max() / loads.min() <= 1.15, loads
     rr = [sum(costs[i] for i in range(k, len(costs), 8)) for k in range(8)]
     assert loads.max() < max(rr) - 1e-9, (loads.max(), max(rr))
 
