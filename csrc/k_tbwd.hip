@@ -485,7 +485,9 @@ __global__ __launch_bounds__(256, 1) void k_tbwd_sdf(const MlpJob* __restrict__ 
 // LDS image always fits -- blob <= 42 KiB, staged per-period inputs <= 38 KiB (T <= 600, Dm <= 16),
 // the transpose images 48 KiB -- and is checked at launch)
 bool tbwd_supported(const MlpDims& D, int KS1) {
-  return !D.fp32 && !D.wide && KS1 == 2 && D.nl_sdf >= 1 && D.nl_sdf <= 3 && D.Dm <= 16;
+  // (HL = 4: spill-free as well; its 8-member paper-grid bucket 1.44 -> 1.02 ms per epoch against
+  // the sliced kernel, profiles/r6_tbwd_hl4_ab.txt)
+  return !D.fp32 && !D.wide && KS1 == 2 && D.nl_sdf >= 1 && D.nl_sdf <= 4 && D.Dm <= 16;
 }
 
 void launch_tbwd_sdf(const MlpJob* jobs, int njobs, int gx, const MlpDims& D0, int slab_stride, int T,
@@ -499,7 +501,7 @@ void launch_tbwd_sdf(const MlpJob* jobs, int njobs, int gx, const MlpDims& D0, i
     dlap_throw_hip(hipErrorInvalidValue, "tbwd_sdf: slab stride too small", __FILE__, __LINE__);
   dim3 grid(gx, njobs), block(256);
 #define TB_CASE(N) if (D.nl_sdf == N) { hipLaunchKernelGGL(k_tbwd_sdf<N>, grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
-  TB_CASE(1) TB_CASE(2) TB_CASE(3)
+  TB_CASE(1) TB_CASE(2) TB_CASE(3) TB_CASE(4)
 #undef TB_CASE
 }
 

@@ -55,6 +55,7 @@ CASES = [
     ([64], [8], 0.05),           # SMV = 8 of the paper grid, one hidden layer
     ([64, 64, 64], [4], 0.05),   # HL = 3
     ([48, 32], [2, 2], 0.0),     # narrow layers (zero-padded units), two-layer LSTM of width 2
+    ([64] * 4, [4], 0.05),       # HL = 4 (the paper grid's deepest SDF)
 ]
 
 

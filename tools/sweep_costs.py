@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--grid", choices=["paper", "baseline", "both"], default="both")
     ap.add_argument("--epochs", type=int, default=12)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--only", default=None, help="architectures whose key contains this string")
     a = ap.parse_args()
     from bench import make_panel
     from deeplearninginassetpricing_paperreplication_amd.config import ModelSpec
@@ -45,6 +46,8 @@ def main():
     out = {}
     n = a.epochs
     for key, cfg in seen.items():
+        if a.only and a.only not in key:
+            continue
         spec = ModelSpec.from_config(cfg)
         t0 = time.perf_counter()
         eng = GANEngine(spec, n_models=8, max_epochs=4 * n + 16)
