@@ -1472,7 +1472,7 @@ class Engine {
     const bool tps2 = (wide || d.KS1 == 2) && d.ntile_s == 2 && tps_env && std::atoi(tps_env) == 2;
     d.tps_s = tps2 ? 2 : 1;
     // the one-pass backward (k_tbwd.hip) where it is instantiated: every gradient tile in one
-    // slice (DLAP_TBWD=0: the sliced kernel, kept for the fp32 / wide / wide-row shapes)
+    // slice, the wide path included (DLAP_TBWD=0: the sliced kernel, kept for the fp32 / wide-row shapes)
     d.tbwd = (env_int("DLAP_TBWD", 1) != 0 && tbwd_supported(D, d.KS1) && d.ntile_s == d.nl_s) ? 1 : 0;
     if (d.tbwd) d.tps_s = d.ntile_s;
     // at least one slice: slice 0 also produces the bias / output / per-period gradients

@@ -1,6 +1,7 @@
 // One-pass SDF tower backward (phases 1 / 3 and the module API's SDF backward) for the production
 // shapes: bf16 towers, fused layer 0 over a 64-column panel row (F + per-period inputs <= 64),
-// 1..4 hidden layers of <= 64 units. Replaces, for those shapes, the sliced k_mlp_bwd_sdf
+// 1..4 hidden layers of <= 64 units; and the wide layer-0 path (layer 0 from the stored z, see
+// tb_tile). Replaces, for those shapes, the sliced k_mlp_bwd_sdf
 // (k_mlp.hip), which recomputed the forward once per weight-gradient tile (one slice per layer)
 // to fit two waves per SIMD and still spilled.
 //
@@ -25,6 +26,7 @@
 //    (slab v owns tiles 4v + w + k * 4 * nslab) is k_mlp_bwd_sdf's, a function of R only, so a
 //    model's gradient bits never depend on how many models share the launch.
 #include <algorithm>
+#include <type_traits>
 #include "common.h"
 #include "layout.h"
 #include "mlp.h"
@@ -68,6 +70,21 @@ struct ImgMap {
                //   4u + (n & 3) (half e: rows + 4e, + 512 e -- f and g do not change) and receives
                //   column 16u + n of rows 8q + 4e .. +3 (fragment elements 4e .. 4e + 3)
 };
+
+// Wide path (ZIN): the layer-0 dz goes to k_wgrad0 in the row order of the sliced kernel's
+// selector transposes (and of the k_xt_build panel fragments) -- lane (q, n) holds column 16u + n
+// of rows 4q .. 4q + 3 (elements 0..3) and 16 + 4q .. +3 (elements 4..7): the same transposed read
+// with lane (q, n) supplying row 4q + (n >> 2) (second half: + 16 rows = + 2048 bytes; rows + 16
+// keep bits 0, 1, 3, so the swizzle is unchanged).
+DLAP_DEV bf16x8 img_get_sliced(const char* img, int u) {
+  const int l = lane_id(), q = l >> 4, n = l & 15;
+  const int off = img_off(4 * q + (n >> 2), 4 * u + (n & 3));
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS3 s16x4*)(const_cast<char*>(img) + off));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((LDS3 s16x4*)(const_cast<char*>(img) + off + 2048));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  const s16x8 v{lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
 
 DLAP_DEV ImgMap img_map() {
   ImgMap m;
@@ -223,9 +240,12 @@ struct TbState {
 };
 
 // One 32-row tile: forward recompute, output gradient, backward chain, every weight gradient.
-template <int NL>
+// ZIN (wide path): the tile input is the stored layer-0 pre-activation z (k_mlp_fwd_zx), layer 0's
+// gradient tile covers only the per-period input columns W0[:, F:F+Dm] (the panel columns are
+// k_wgrad0's), and the layer-0 dz is stored for k_wgrad0 (J.dz_out [tile][4][64]).
+template <int NL, bool ZIN, class TI>
 DLAP_DEV void tb_tile(const MlpJob& J, const MlpDims& D, const TbW<NL, kTbRes<NL>>& W, const float* aux, const float* spp,
-                      char* img, const ImgMap& im, int tile, TileIn<PrecBF16, 2>& in, const uint32_t (&kw)[NL],
+                      char* img, const ImgMap& im, int tile, TI& in, const uint32_t (&kw)[NL],
                       TbState<NL>& S) {
   using P = PrecBF16;
   using Frag = bf16x8;
@@ -235,22 +255,34 @@ DLAP_DEV void tb_tile(const MlpJob& J, const MlpDims& D, const TbW<NL, kTbRes<NL
   char* aimg = img + kImg;
   char* zimg = img + 2 * kImg;
   Frag xf[2][2];
-  tb_finish(J, D, tile, in, xf, spp);                  // per-period columns inserted; dw = 0 beyond R
-  img_put_x(ximg, im, xf);
-  __builtin_amdgcn_sched_barrier(0);
-  // ---- forward recompute (the train blob: dropout scale folded into layers >= 1) ----
   f32x4 a[2][4];
+  if constexpr (ZIN) {
+    const RowInfo ri = finish_ztile<1>(J, tile, in);       // dw = 0 beyond R
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const f32x4 bias = ld4(auxt + D.a_sb + 16 * u + 4 * q);
-    f32x4 c0 = bias, c1 = bias;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const Frag w = W.w0(2 * u + s);
-      c0 = P::mma(w, xf[0][s], c0);
-      c1 = P::mma(w, xf[1][s], c1);
+    for (int b = 0; b < 2; ++b) {
+      xf[b][0] = pp_xfrag<P>(spp, D.ppst, ri.t[b], 0, D);   // Dm <= 16: k-step 0 only
+      xf[b][1] = P::zero();
     }
-    a[0][u] = c0; a[1][u] = c1;
+    img_put_x(ximg, im, xf);
+    __builtin_amdgcn_sched_barrier(0);
+    zin_sdf0(in.zs, ri, spp, D.ppst, auxt, D, a);
+  } else {
+    tb_finish(J, D, tile, in, xf, spp);                  // per-period columns inserted; dw = 0 beyond R
+    img_put_x(ximg, im, xf);
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- forward recompute (the train blob: dropout scale folded into layers >= 1) ----
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const f32x4 bias = ld4(auxt + D.a_sb + 16 * u + 4 * q);
+      f32x4 c0 = bias, c1 = bias;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const Frag w = W.w0(2 * u + s);
+        c0 = P::mma(w, xf[0][s], c0);
+        c1 = P::mma(w, xf[1][s], c1);
+      }
+      a[0][u] = c0; a[1][u] = c1;
+    }
   }
   Frag act[NL][2][2];
   act_tile<P, 4, true>(a, kw[0], act[0]);
@@ -302,9 +334,17 @@ DLAP_DEV void tb_tile(const MlpJob& J, const MlpDims& D, const TbW<NL, kTbRes<NL
     }
 #pragma unroll
     for (int v = 0; v < 4; ++v) {
+      if (ZIN && j == 0 && v > 0) break;                 // per-period columns: block 0 only
       const Frag aN = img_get(j > 0 ? aimg : ximg, im, v);
 #pragma unroll
       for (int u = 0; u < 4; ++u) mma_acc(S.dW[j][u][v], dzN[u], aN);
+    }
+    if constexpr (ZIN) {
+      if (j == 0) {                                      // layer-0 dz for k_wgrad0
+        const auto dzo = gp(reinterpret_cast<bf16x8*>(J.dz_out)) + (size_t)tile * 4 * 64 + lane_id();
+#pragma unroll
+        for (int u = 0; u < 4; ++u) dzo[u * 64] = img_get_sliced(zimg, u);
+      }
     }
     __builtin_amdgcn_sched_barrier(0);
     if (j > 0) {
@@ -401,7 +441,7 @@ DLAP_DEV void tb_reduce_store(const MlpJob& J, char* smem, int slab_stride, TbSt
     slab[NL * 4096 + x] = (red[x] + red[SLAB_EXTRA + x]) + (red[2 * SLAB_EXTRA + x] + red[3 * SLAB_EXTRA + x]);
 }
 
-template <int NL>
+template <int NL, bool ZIN>
 __global__ __launch_bounds__(256, 1) void k_tbwd_sdf(const MlpJob* __restrict__ jobs, MlpDims D, int slab_stride) {
   using P = PrecBF16;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -437,10 +477,15 @@ __global__ __launch_bounds__(256, 1) void k_tbwd_sdf(const MlpJob* __restrict__ 
   // the join -- and its value is first used after the staging)
   uint32_t stp_raw = *gp(J.step ? reinterpret_cast<const uint32_t*>(J.step)
                                 : reinterpret_cast<const uint32_t*>(J.rowti));
-  TileIn<P, 2> s0, s1, s2;
+  using TI = std::conditional_t<ZIN, ZTile<1>, TileIn<P, 2>>;
+  auto issue = [&](int t, TI& in) {
+    if constexpr (ZIN) issue_ztile<1, true>(J, D, t, in, true, false);
+    else issue_tile<P, 2, true>(J, t, in);
+  };
+  TI s0, s1, s2;
   uint32_t k0[NL], k1[NL], k2[NL];
-  if (t0 < ntiles) issue_tile<P, 2, true>(J, t0, s0);
-  if (t0 + stride < ntiles) issue_tile<P, 2, true>(J, t0 + stride, s1);
+  if (t0 < ntiles) issue(t0, s0);
+  if (t0 + stride < ntiles) issue(t0 + stride, s1);
   const bool pre = J.gbits && J.train && J.dropout > 0.f;   // keep words of this step (k_dropmask)
   const DLAP_GLOBAL uint32_t* gb0 = pre ? gp(J.gbits) : nullptr;
   const DLAP_GLOBAL uint32_t* gb1 = pre ? gp(J.gbits) + J.gb_half : nullptr;
@@ -463,9 +508,9 @@ __global__ __launch_bounds__(256, 1) void k_tbwd_sdf(const MlpJob* __restrict__ 
   // copies (unrolling the loop by the three slots instead lets the compiler interleave the bodies,
   // which spills)
   for (int t = t0; t < ntiles; t += stride) {
-    if (t + 2 * stride < ntiles) issue_tile<P, 2, true>(J, t + 2 * stride, s2);
+    if (t + 2 * stride < ntiles) issue(t + 2 * stride, s2);
     tb_issue_kw<NL>(gbase, t + 2 * stride, ntiles, k2);
-    tb_tile<NL>(J, D, W, aux, spp, img, im, t, s0, k0, S);
+    tb_tile<NL, ZIN>(J, D, W, aux, spp, img, im, t, s0, k0, S);
     s0 = s1;
     s1 = s2;
 #pragma unroll
@@ -484,10 +529,13 @@ __global__ __launch_bounds__(256, 1) void k_tbwd_sdf(const MlpJob* __restrict__ 
 // (1..3 layers: at four the weight sums fill the accumulator file and the tile loop spills; the
 // LDS image always fits -- blob <= 42 KiB, staged per-period inputs <= 38 KiB (T <= 600, Dm <= 16),
 // the transpose images 48 KiB -- and is checked at launch)
+// Wide path (ZIN): layer 0 from the stored z, the per-period input columns as layer 0's gradient
+// tile -- needs an LSTM (Dm >= 1: one layer-0 tile, so ntile_s == nl_sdf).
 bool tbwd_supported(const MlpDims& D, int KS1) {
   // (HL = 4: spill-free as well; its 8-member paper-grid bucket 1.44 -> 1.02 ms per epoch against
   // the sliced kernel, profiles/r6_tbwd_hl4_ab.txt)
-  return !D.fp32 && !D.wide && KS1 == 2 && D.nl_sdf >= 1 && D.nl_sdf <= 4 && D.Dm <= 16;
+  if (D.wide) return !D.fp32 && D.nl_sdf >= 1 && D.nl_sdf <= 4 && D.Dm >= 1 && D.Dm <= 16;
+  return !D.fp32 && KS1 == 2 && D.nl_sdf >= 1 && D.nl_sdf <= 4 && D.Dm <= 16;
 }
 
 void launch_tbwd_sdf(const MlpJob* jobs, int njobs, int gx, const MlpDims& D0, int slab_stride, int T,
@@ -500,7 +548,10 @@ void launch_tbwd_sdf(const MlpJob* jobs, int njobs, int gx, const MlpDims& D0, i
   if (slab_stride < D.nl_sdf * 4096 + SLAB_EXTRA)
     dlap_throw_hip(hipErrorInvalidValue, "tbwd_sdf: slab stride too small", __FILE__, __LINE__);
   dim3 grid(gx, njobs), block(256);
-#define TB_CASE(N) if (D.nl_sdf == N) { hipLaunchKernelGGL(k_tbwd_sdf<N>, grid, block, sh, st, jobs, D, slab_stride); HIP_OK(hipGetLastError()); return; }
+#define TB_CASE(N) if (D.nl_sdf == N) { \
+    if (D.wide) hipLaunchKernelGGL((k_tbwd_sdf<N, true>), grid, block, sh, st, jobs, D, slab_stride); \
+    else hipLaunchKernelGGL((k_tbwd_sdf<N, false>), grid, block, sh, st, jobs, D, slab_stride); \
+    HIP_OK(hipGetLastError()); return; }
   TB_CASE(1) TB_CASE(2) TB_CASE(3) TB_CASE(4)
 #undef TB_CASE
 }

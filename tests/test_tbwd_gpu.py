@@ -108,3 +108,37 @@ def test_one_pass_backward_matches_fp32_autograd(monkeypatch):
     # (bf16 GEMM operands: ~5% whole-scope L2 error on this panel, the sliced kernel's too -- the two
     # agree to 1e-4 above)
     assert err < 0.08 and cos > 0.998, (err, cos)
+
+
+WIDE_CASES = [
+    ([64, 64], [4], 0.05, 46),   # the scaled panel's architecture (wide path forced)
+    ([64], [4], 0.0, 46),
+    ([64, 64, 64], [4], 0.05, 46),
+    ([48, 32], [2, 2], 0.0, 46),
+    ([64] * 4, [4], 0.05, 46),
+    ([64, 64], [4], 0.05, 200),  # F + LSTM columns > 128: wide by size
+]
+
+
+@pytest.mark.parametrize("hidden,rnn,dropout,F", WIDE_CASES)
+@pytest.mark.parametrize("phase", [1, 3])
+def test_one_pass_backward_wide_path_equals_sliced_kernel(monkeypatch, hidden, rnn, dropout, F, phase):
+    """Wide layer-0 path (ZIN): the one-pass backward starts from the stored layer-0 pre-activations
+    (k_mlp_fwd_zx), its layer-0 gradient tile is the per-period input columns only, and the layer-0
+    dz it stores (in the sliced kernel's row order) feeds k_wgrad0 -- so the whole SDF gradient,
+    the streamed panel columns of W0 included, must agree with the sliced kernel to fp32 rounding."""
+    monkeypatch.setenv("DLAP_WIDE", "1")
+    cfg = default_cli_config(8, F, hidden_dim=hidden, rnn_dim=rnn, dropout=dropout)
+    b = _batch(F=F, seed=5)
+    (ref,), P_sdf = _grads(cfg, b, False, phase, monkeypatch=monkeypatch)
+    (got,), _ = _grads(cfg, b, True, phase, monkeypatch=monkeypatch)
+    assert np.isfinite(got[:P_sdf]).all()
+    assert np.abs(ref[:P_sdf]).max() > 0
+    # every SDF parameter, and layer 0's weight (k_wgrad0 from the stored dz) on its own
+    lay = dict(AssetPricingGAN(cfg).spec.param_layout())
+    o0 = sum(int(np.prod(shp)) for k, shp in AssetPricingGAN(cfg).spec.param_layout()
+             if k.startswith("sdf_net.macro_lstm"))
+    w0 = slice(o0, o0 + int(np.prod(lay["sdf_net.fc_layers.0.weight"])))
+    for sl in (slice(0, P_sdf), w0):
+        assert _rel(got[sl], ref[sl]) < 1e-4, _rel(got[sl], ref[sl])
+        np.testing.assert_allclose(got[sl], ref[sl], rtol=2e-3, atol=1e-6 * np.abs(ref[sl]).max())
