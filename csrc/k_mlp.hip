@@ -463,13 +463,17 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
       const auto row = gp(J.X) + (size_t)r * rstride;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const int ks = 4 * ch + s;
-        x[b][s] = ks < KSX ? row[4 * ks + q] : zero8();
+        // (unconditional: a k-step past KSX re-reads the last one, and the MFMAs skip it)
+        x[b][s] = row[4 * min(4 * ch + s, KSX - 1) + q];
       }
     }
   };
-  // panel chunks streamed two ahead (xn, xn2): 16 KiB per wave in flight
-  bf16x8 xc[2][4], xn[2][4], xn2[2][4];
+  // panel chunks streamed two ahead: three register slots that rotate by unrolling the chunk loop
+  // three times (a register copy of a slot whose load is in flight would wait for that load, so a
+  // copy rotation keeps only the current chunk's MFMAs between a load and its use). Every chunk
+  // load is issued -- past the wave's last tile it re-reads the last tile -- so the in-order load
+  // counter is the same on every path. 16 KiB per wave in flight.
+  bf16x8 xa[2][4], xb[2][4], xd[2][4];
   f32x4 acc[2][NU];
 #pragma unroll
   for (int b = 0; b < 2; ++b)
@@ -477,7 +481,7 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
     for (int u = 0; u < NU; ++u) acc[b][u] = zero4();
   int2 ti[2];
   issue_rowti(J, tile, ti);
-  issue(tile, 0, xc);
+  issue(tile, 0, xa);
   int ch = 0;
   auto advance = [&](int tl, int c, int& t2, int& c2) {
     t2 = tl; c2 = c + 1;
@@ -486,12 +490,13 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
   int ntl, nc;
   advance(tile, ch, ntl, nc);
   bool more = ntl < ntiles;
-  if (more) issue(ntl, nc, xn);
-  for (;;) {
+  issue(min(ntl, ntiles - 1), nc, xb);
+  // one chunk: the chunk two ahead goes into xn2, the current one (xc) runs; false after the last
+  auto step = [&](const bf16x8 (&xc)[2][4], bf16x8 (&xn2)[2][4]) __attribute__((always_inline)) -> bool {
     int ntl2, nc2;
     advance(ntl, nc, ntl2, nc2);
     const bool more2 = more && ntl2 < ntiles;
-    if (more2) issue(ntl2, nc2, xn2);
+    issue(min(ntl2, ntiles - 1), nc2, xn2);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int ks = 4 * ch + s;
@@ -568,6 +573,11 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
         };
         mom_forward_tile<PrecBF16, WMB>(lds, aux, D, J, dc, ri, l0m);
       }
+      // drain the vector-memory counter once per tile: the tile's stores (w_out, z) sit between
+      // loads and their uses in the vmcnt order, and a store may complete before an older load
+      // (measured: without this wait the evaluation outputs of the unrolled loop were
+      // nondeterministic, tools/wide_det_probe.py); the chunk prefetch inside a tile is untouched
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
       for (int b = 0; b < 2; ++b) {
 #pragma unroll
@@ -575,19 +585,15 @@ __global__ __launch_bounds__(512, 1) void k_mlp_fwd_zx(const MlpJob* __restrict_
         if (more) ti[b] = tn[b];
       }
     }
-    if (!more) break;
+    if (!more) return false;
     tile = ntl;
     ch = nc;
     ntl = ntl2;
     nc = nc2;
     more = more2;
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        xc[b][s] = xn[b][s];
-        xn[b][s] = xn2[b][s];
-      }
+    return true;
+  };
+  while (step(xa, xd) && step(xb, xa) && step(xd, xb)) {
   }
 }
 
