@@ -1746,6 +1746,7 @@ class Engine {
   // eval_gram_pending_ is set: the caller joins ev_gram_ into st_ before the first graph that
   // evaluates (the pipelined head trains only, so they overlap it).
   void build_gram(bool defer = false, int smask = 7) {
+    bool forked = false;
     for (int s = 0; s < 3; ++s) {
       if (!((smask >> s) & 1)) continue;
       const SplitDev& D = splits_[s];
@@ -1755,9 +1756,14 @@ class Engine {
       gram_valid_[s] = true;
       hipStream_t st = st_;
       if ((s > 0 || train_gram_side_) && defer) {
-        if (!eval_gram_pending_ && !train_gram_pending_) {
+        // the builds read the cached moments: st2_ waits for everything queued on st_ so far --
+        // on the wide path the moment refresh itself runs on st_ (ensure_moments), so a build
+        // deferred while an earlier one is still pending must fork again, or it reads moments
+        // the refresh is still writing (run-to-run differences, profiles/r6_wide_determinism.txt)
+        if (!forked) {
           HIP_OK(hipEventRecord(ev_fork_, st_));
           HIP_OK(hipStreamWaitEvent(st2_, ev_fork_, 0));
+          forked = true;
         }
         if (s > 0) eval_gram_pending_ = true;
         st = st2_;
