@@ -18,7 +18,7 @@ mac = (mac - mac.mean(0)) / (mac.std(0, unbiased=False) + 1e-8)
 b = {"returns": ret, "individual_features": feats, "mask": mask, "macro_features": mac}
 cfg = default_cli_config(8, 46, dropout=0.05)
 out = []
-for _ in range(2):
+for _ in range(int(sys.argv[1]) if len(sys.argv) > 1 else 2):
     eng = GANEngine(AssetPricingGAN(cfg).spec, 1, max_epochs=8)
     assert int(eng.desc["tbwd"]) == 1
     eng.set_data(b, b, b)
@@ -37,3 +37,7 @@ print("differing history entries (epoch, column):", sorted({int(r) for r, c in d
       "max|d|", float(np.abs(out[0][1] - out[1][1]).max()))
 print("rows", int(mask.sum()), "grads bitwise equal", np.array_equal(out[0][0], out[1][0]),
       "history equal", np.array_equal(out[0][1], out[1][1]), "params equal", np.array_equal(out[0][2], out[1][2]))
+
+for i in range(2, len(out)):
+    print(f"engine 1 vs engine {i + 1}: history equal", np.array_equal(out[1][1], out[i][1]),
+          "| engine 0 vs engine", i + 1, np.array_equal(out[0][1], out[i][1]))
